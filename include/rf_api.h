@@ -1,0 +1,209 @@
+/*
+ * rf_api.h — C ABI of the MI355X-native RecommendFlow hot path (librf.so).
+ *
+ * The reference (mechsihao/RecommendFlow) has no native boundary: its hot path is
+ * Keras operators. Each entry point below replaces one reference operator; the
+ * operator it replaces is cited next to it (paths relative to the reference root).
+ * The Python mirror of the reference operator API (recommendflow_amd/backend/...)
+ * is the only in-tree caller; INTEGRATION.md shows the ctypes binding.
+ *
+ * Conventions
+ *  - All data pointers are caller-owned DEVICE buffers (hipMalloc / torch CUDA
+ *    tensors). The library allocates nothing, frees nothing, never synchronises.
+ *  - `stream` is a hipStream_t passed as void* (0 = default stream). All work is
+ *    stream-ordered and asynchronous; entry points are reentrant.
+ *  - Return value: RF_OK (0) or a negative RF_E* code; rf_last_error() returns a
+ *    thread-local message for the last failing call on this thread.
+ *  - Table rows are row-major [rows][dim], element type RF_DTYPE_*.
+ *  - No C++ exceptions cross this boundary.
+ */
+#ifndef RF_API_H
+#define RF_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RF_ABI_VERSION 1
+
+/* error codes */
+#define RF_OK 0
+#define RF_EINVAL (-1) /* bad argument (shape, dtype, combiner, alignment) */
+#define RF_EHIP (-2)   /* a HIP runtime call failed (launch error) */
+#define RF_EOOB (-3)   /* a computed row index falls outside the table */
+
+/* element types */
+#define RF_DTYPE_F32 0
+#define RF_DTYPE_BF16 1
+#define RF_DTYPE_F16 2
+
+/* pooling combiners, EmbeddingBag.get_combiner (backend/layers/preprocess_layers.py:44-64) */
+#define RF_COMB_SUM 0
+#define RF_COMB_AVG 1
+#define RF_COMB_MAX 2
+#define RF_COMB_MIN 3
+#define RF_COMB_FIRST 4 /* position 0 of each example (deviation D-first-last; `cls` aliases it) */
+#define RF_COMB_LAST 5  /* position Lmax-1 of each example (deviation D-first-last) */
+#define RF_COMB_NULL 6  /* no pooling: [Lmax, D] per table, concatenated along the sequence axis */
+
+/* flags for rf_fused_hash_embed_fwd */
+#define RF_FLAG_MASK_PADDING 0x1 /* exclude padding positions (mask_zero intent); default OFF = reference parity:
+                                    padded positions gather row 0 and count in sum/avg/max/min
+                                    (dataloader.py:32-33 pads with b"" which Hashing maps to bin 0) */
+#define RF_FLAG_EMIT_IDX 0x2     /* also write the two bucket ids of every token to idx_out[2*t + k] */
+
+/*
+ * One hashed feature ("slot") of a fused multi-slot table.
+ * Reference: DoubleHashingEmbedding.__init__ (backend/layers/preprocess_layers.py:82-92) builds
+ * two Keras Hashing layers (salt seeds[0], seeds[1]) and two Embedding tables of num_bins rows;
+ * here the two tables are two segments [row_base[k], row_base[k] + num_bins) of ONE fused table.
+ */
+typedef struct rf_slot_desc {
+    int64_t row_base[2]; /* first fused-table row of table k (k = 0: seeds[0], k = 1: seeds[1]) */
+    int64_t num_bins;    /* Keras Hashing num_bins (>= 1) */
+    uint64_t salt[2];    /* SipHash key for table k is (salt[k], salt[k]) (Keras Hashing int salt) */
+    int64_t out_off;     /* element offset of this slot's [2*D] (or [2*Lmax*D] for NULL) in an output row */
+    int32_t dim;         /* embedding dim D (must equal the launch's dim) */
+    int32_t combiner;    /* RF_COMB_* */
+    int32_t mask_empty;  /* 1: Hashing(mask_value="") — b"" -> bin 0, others 1 + h mod (N-1) */
+    int32_t reserved;    /* must be 0 */
+} rf_slot_desc;          /* 64 bytes */
+
+/* ---- version / errors ------------------------------------------------------------- */
+int32_t rf_abi_version(void);
+const char* rf_last_error(void);
+
+/*
+ * Keras Hashing(num_bins, mask_value="" | None, salt=s) over a batch of byte strings.
+ * Replaces: tf.keras.layers.Hashing -> tf.strings.to_hash_bucket_strong, called at
+ * backend/layers/preprocess_layers.py:89-90,95.
+ * tokens: tok_bytes[tok_off[t] .. tok_off[t+1]) for t in [0, n_tok); out: int64 [n_tok].
+ * bucket = mask_empty && len == 0 ? 0
+ *        : mask_empty && num_bins > 1 ? 1 + SipHash24((k0,k1), tok) mod (num_bins - 1)
+ *        : SipHash24((k0,k1), tok) mod num_bins
+ */
+int rf_siphash_bucket(const uint8_t* tok_bytes, const int32_t* tok_off, int64_t n_tok, uint64_t k0,
+                      uint64_t k1, int64_t num_bins, int32_t mask_empty, int64_t* out, void* stream);
+
+/*
+ * Fused multi-slot  hash -> gather -> pool -> concat  (one launch for every slot of a tower).
+ * Replaces, per hashing feature f of get_preprocess_layers (backend/utils/preprocess_utils.py:7-20):
+ *   DoubleHashingEmbedding.call (preprocess_layers.py:94-97) = Hashing x2 -> EmbeddingBag x2
+ *   (Embedding gather :67 + combiner :44-64) -> tf.concat(axis=1) :97,
+ * over the padded [B, Lmax_f] string tensor produced by parse_example (dataloader.py:32-33,86).
+ *
+ * Input batch (CSR, example-major):
+ *   bag_off[b*n_slots + s] .. bag_off[b*n_slots + s + 1]  token range of (example b, slot s)
+ *   tok_off[t] .. tok_off[t+1]                             byte range of token t in tok_bytes
+ *   lmax[s]                                                batch max list length of slot s (Lmax_f)
+ * d_slots: DEVICE array of n_slots rf_slot_desc, all with .dim == dim.
+ * table: fused [table_rows][dim] (table_dtype F32 or BF16).
+ * out: [batch][out_stride] (out_dtype F32 or BF16); slot s writes
+ *   out[b, out_off + k*dim + d]          (k = 0,1; pooled combiners)
+ *   out[b, out_off + (k*Lmax + l)*dim + d] (RF_COMB_NULL)
+ * Accumulation is fp32, sequential over positions l = 0 .. Lmax-1 (deterministic).
+ * idx_out (optional, RF_FLAG_EMIT_IDX): int64 [n_tok][2] bucket ids (before row_base).
+ */
+int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                            const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                            int32_t batch, const void* table, int32_t table_dtype, int64_t table_rows,
+                            int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
+                            int64_t* idx_out, void* stream);
+
+/*
+ * EmbeddingBag over dense integer ids [batch][len] (every position pooled, as Keras does).
+ * Replaces: EmbeddingBag.call (backend/layers/preprocess_layers.py:66-68) when its input ids come
+ * from StringLookup/IntegerLookup/Discretization (LookupEmbedding :157-160, DiscreteEmbedding :189-191).
+ * ids are rows of `table` (row_base added); out [batch][out_stride] at out_off (pooled: D
+ * elements; NULL: len*D elements).
+ */
+int rf_embedding_bag_fwd(const int64_t* ids, int32_t batch, int32_t len, int64_t row_base,
+                         const void* table, int32_t table_dtype, int64_t table_rows, int32_t dim,
+                         int32_t combiner, void* out, int32_t out_dtype, int64_t out_stride,
+                         int64_t out_off, void* stream);
+
+/*
+ * Counter-based table init, identical for any sharding: fused global row g = row0 + r*row_stride
+ *   T[r][d] = lo + (hi - lo) * ((splitmix64(seed ^ (g*dim + d)) >> 40) * 2^-24)
+ * (Keras Embedding 'uniform' initializer is U(-0.05, 0.05), preprocess_layers.py:24,31-39).
+ */
+int rf_table_init_uniform(void* table, int32_t dtype, int64_t rows, int32_t dim, int64_t row0,
+                          int64_t row_stride, uint64_t seed, float lo, float hi, void* stream);
+
+/*
+ * ESIM local inference + composition pooling, one fused launch.
+ * Replaces: SoftAttention.__call__ (backend/layers/attention_layers.py:15-30, _attention :33-47,
+ * _soft_alignment :56-74) followed by the Esim.call combine (models/ranking/esim.py:79-84):
+ *   E[i,j]   = sum_k a[i,k] q[j,k]           (x0 = q, x1 = a; [L1, L0])
+ *   S        = softmax_j(E)                  (max-subtracted, fp32)
+ *   att_q    = S @ q,  att_a = S @ a         (L0 == L1 == L)
+ *   m_q      = [q; att_q; q-att_q; q*att_q] (4L rows), m_a likewise
+ *   pooled   = [avg(m_q), max(m_q), avg(m_a), max(m_a), avg_q-avg_a, max_q-max_a]   [6d]
+ * q, a: [batch][L][d] (dtype BF16 or F16), row stride ld (elements) between positions, example
+ * stride ex_stride (elements). out: F32 [batch][out_stride], pooled written at out_off.
+ * Optional att_out (F32 [batch][2][L][d], may be NULL): att_q then att_a, for tests.
+ * Constraints: 1 <= L <= 128, d in {64, 128}.
+ */
+int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L,
+                               int32_t d, int64_t ex_stride, int64_t ld, float* out, int64_t out_stride,
+                               int64_t out_off, float* att_out, void* stream);
+
+/* activations for rf_linear_fwd */
+#define RF_ACT_NONE 0
+#define RF_ACT_GELU 1 /* exact erf gelu (tf.keras.activations.gelu, approximate=False) */
+#define RF_ACT_RELU 2
+#define RF_ACT_SELU 3
+#define RF_ACT_SOFTMAX 4 /* row softmax over the N outputs (Dense(units, activation='softmax')) */
+
+/*
+ * Row normalisation feeding a Dense layer (the `normalization_layer` of create_mlp,
+ * backend/blocks/mlp.py:4-15):
+ *   mode 0 LayerNormalization(eps): y = (x - mean) / sqrt(var + eps) * gamma + beta
+ *   mode 1 BatchNormalization(eps), inference: y = (x - mean[c]) / sqrt(var[c] + eps) * gamma + beta
+ * x: F32 [rows][cols] (row stride ldx); y: [rows][cols] in y_dtype (BF16 or F32), row stride ldy.
+ * mode 1 reads running mean/var from `mean`/`var` (per column); mode 0 ignores them.
+ */
+int rf_norm_fwd(const float* x, int64_t rows, int32_t cols, int64_t ldx, int32_t mode, float eps,
+                const float* gamma, const float* beta, const float* mean, const float* var, void* y,
+                int32_t y_dtype, int64_t ldy, void* stream);
+
+/*
+ * Dense layer  y = act(x @ W + b)  (tf.keras.layers.Dense, mlp.py:12; esim.py:53,88; dssm.py:25-26).
+ * x: [M][K] (x_dtype BF16 -> bf16 MFMA, or F32 -> exact-fp32 MFMA), row stride ldx.
+ * W: [N][K] row-major (i.e. the Keras kernel transposed), same dtype as x. b: F32 [N] (may be NULL).
+ * y: F32 [M][N] with row stride ldy. fp32 accumulate. RF_ACT_SOFTMAX requires N <= 64.
+ */
+int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,
+                  int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream);
+
+/*
+ * Masked scaled-dot-product attention (backend/layers/layer_utils.py:4-24):
+ *   logits = q k^T / sqrt(depth); logits[i, :] = -4294967295 where mask[i] == 0 (QUERY rows, as the
+ *   reference's [..., Lq, 1] mask broadcasts); softmax over keys (fp32); out = P v.
+ * q,k,v: [BH][Lq|Lk][depth] (dtype F16 or BF16, contiguous); mask: F32 [BH][Lq] (may be NULL).
+ * out: F32 [BH][Lq][depth]. Constraints: Lk <= 256, depth in {32, 64, 128}.
+ */
+int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int32_t BH, int32_t Lq,
+                int32_t Lk, int32_t depth, const float* mask, float* out, void* stream);
+
+/*
+ * Row-sharded tables: route fused-table rows to their owner rank (owner = g mod P, local = g div P).
+ * Stage 1 of the sharded lookup: for n global rows, write counts[P] (int32) and a
+ * stable owner-major permutation perm[n] (int32) with local_rows[n] (int64) in permuted order.
+ * ws must hold rf_bucketize_ws_bytes(n, P) bytes.
+ */
+size_t rf_bucketize_ws_bytes(int64_t n, int32_t nranks);
+int rf_bucketize_owner(const int64_t* rows, int64_t n, int32_t nranks, int32_t* counts, int32_t* perm,
+                       int64_t* local_rows, void* ws, size_t ws_bytes, void* stream);
+
+/* Gather whole rows: out[i] = table[rows[i]] (owner side of the sharded lookup). */
+int rf_gather_rows(const int64_t* rows, int64_t n, const void* table, int32_t dtype, int64_t table_rows,
+                   int32_t dim, void* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RF_API_H */

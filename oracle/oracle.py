@@ -1,0 +1,279 @@
+"""CPU oracle for the RecommendFlow hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module; the product (``recommendflow_amd``) never does. It restates the reference semantics:
+
+* integer / byte work (hash, gather, pool) in plain C: ``oracle/rf_oracle.c`` (ctypes below);
+* the dense floating-point stages in float64 numpy, each function citing the reference lines it
+  follows (backend/layers/attention_layers.py, layer_utils.py, backend/blocks/mlp.py,
+  models/ranking/esim.py, models/matching/dssm.py).
+
+Parity pins: see ``tests/test_oracle_kats.py`` (SipHash-2-4 reference vectors, CPython's siphash24,
+TF/Keras docstring KATs) and ``tests/golden/`` (config-parser fixtures generated from the reference's
+own parser, see tests/golden/make_config_golden.py). The dense stages (ESIM, MLP, SDPA) are restated
+from the reference source lines cited; no reference output pins them ("parity unpinned" for those
+stages).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "librf_oracle.so")
+_lib = None
+
+# rf_slot_desc (include/rf_api.h), 64 bytes
+SLOT_DTYPE = np.dtype(
+    [
+        ("row_base", "<i8", (2,)),
+        ("num_bins", "<i8"),
+        ("salt", "<u8", (2,)),
+        ("out_off", "<i8"),
+        ("dim", "<i4"),
+        ("combiner", "<i4"),
+        ("mask_empty", "<i4"),
+        ("reserved", "<i4"),
+    ]
+)
+assert SLOT_DTYPE.itemsize == 64
+
+COMB = {"sum": 0, "avg": 1, "max": 2, "min": 3, "first": 4, "last": 5, "null": 6}
+DT_F32, DT_BF16 = 0, 1
+FLAG_MASK_PADDING, FLAG_EMIT_IDX = 1, 2
+
+
+def build(force: bool = False) -> str:
+    """Compile oracle/rf_oracle.c (gcc) into oracle/build/librf_oracle.so."""
+    src = os.path.join(_HERE, "rf_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE] + (["-B"] if force else []))
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u64, i64, i32, vp = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p
+        L.orf_siphash24.restype = u64
+        L.orf_siphash24.argtypes = [u64, u64, ctypes.c_char_p, i64]
+        L.orf_hash_bucket.restype = i64
+        L.orf_hash_bucket.argtypes = [u64, u64, ctypes.c_char_p, i64, i64, i32]
+        L.orf_hash_tokens.restype = None
+        L.orf_hash_tokens.argtypes = [vp, vp, i64, u64, u64, i64, i32, vp]
+        L.orf_table_value.restype = ctypes.c_float
+        L.orf_table_value.argtypes = [u64, i64, i32, i32, ctypes.c_float, ctypes.c_float]
+        L.orf_table_init_uniform.restype = None
+        L.orf_table_init_uniform.argtypes = [vp, i32, i64, i32, i64, i64, u64, ctypes.c_float, ctypes.c_float]
+        L.orf_fused_hash_embed_fwd.restype = ctypes.c_int
+        L.orf_fused_hash_embed_fwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i32, i64, i32, vp, i32, i64, i32, vp, i32]
+        L.orf_embedding_bag_fwd.restype = ctypes.c_int
+        L.orf_embedding_bag_fwd.argtypes = [vp, i32, i32, i64, vp, i32, i64, i32, i32, vp, i32, i64, i64]
+        L.orf_bucketize_owner.restype = None
+        L.orf_bucketize_owner.argtypes = [vp, i64, i32, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ----------------------------------------------------------------------------------------------
+# integer / byte work (C)
+# ----------------------------------------------------------------------------------------------
+def siphash24(k0: int, k1: int, msg: bytes) -> int:
+    return lib().orf_siphash24(k0, k1, msg, len(msg))
+
+
+def hash_bucket(token: bytes, num_bins: int, salt: int, mask_empty: bool = True) -> int:
+    """keras.layers.Hashing(num_bins, mask_value="" if mask_empty else None, salt=salt)(token)."""
+    return lib().orf_hash_bucket(salt, salt, token, len(token), num_bins, int(mask_empty))
+
+
+def hash_tokens(tok_bytes: np.ndarray, tok_off: np.ndarray, k0: int, k1: int, num_bins: int, mask_empty: bool) -> np.ndarray:
+    tok_bytes = np.ascontiguousarray(tok_bytes, dtype=np.uint8)
+    tok_off = np.ascontiguousarray(tok_off, dtype=np.int32)
+    n = len(tok_off) - 1
+    out = np.empty(n, dtype=np.int64)
+    lib().orf_hash_tokens(_p(tok_bytes), _p(tok_off), n, k0, k1, num_bins, int(mask_empty), _p(out))
+    return out
+
+
+def table_init_uniform(rows: int, dim: int, dtype: int = DT_F32, seed: int = 0, row0: int = 0, row_stride: int = 1,
+                       lo: float = -0.05, hi: float = 0.05) -> np.ndarray:
+    out = np.empty((rows, dim), dtype=np.float32 if dtype == DT_F32 else np.uint16)
+    lib().orf_table_init_uniform(_p(out), dtype, rows, dim, row0, row_stride, seed, lo, hi)
+    return out
+
+
+def fused_hash_embed(slots: np.ndarray, tok_bytes: np.ndarray, tok_off: np.ndarray, bag_off: np.ndarray,
+                     lmax: np.ndarray, batch: int, table: np.ndarray, dim: int, out_stride: int,
+                     out_dtype: int = DT_F32, flags: int = 0, emit_idx: bool = False, n_threads: int = 0):
+    """Restatement of rf_fused_hash_embed_fwd; returns (out, idx or None)."""
+    slots = np.ascontiguousarray(slots, dtype=SLOT_DTYPE)
+    tok_bytes = np.ascontiguousarray(tok_bytes, dtype=np.uint8)
+    if tok_bytes.size == 0:
+        tok_bytes = np.zeros(1, np.uint8)
+    tok_off = np.ascontiguousarray(tok_off, dtype=np.int32)
+    bag_off = np.ascontiguousarray(bag_off, dtype=np.int32)
+    lmax = np.ascontiguousarray(lmax, dtype=np.int32)
+    table = np.ascontiguousarray(table)
+    tdt = DT_F32 if table.dtype == np.float32 else DT_BF16
+    out = np.zeros((batch, out_stride), dtype=np.float32 if out_dtype == DT_F32 else np.uint16)
+    n_tok = len(tok_off) - 1
+    idx = np.zeros((max(n_tok, 1), 2), dtype=np.int64) if emit_idx else None
+    if emit_idx:
+        flags |= FLAG_EMIT_IDX
+    rc = lib().orf_fused_hash_embed_fwd(_p(slots), len(slots), _p(tok_bytes), _p(tok_off), _p(bag_off), _p(lmax),
+                                        batch, _p(table), tdt, table.shape[0], dim, _p(out), out_dtype, out_stride,
+                                        flags, _p(idx) if emit_idx else None, n_threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle fused_hash_embed failed rc={rc}")
+    return out, (idx[:n_tok] if emit_idx else None)
+
+
+def embedding_bag(ids: np.ndarray, table: np.ndarray, combiner: str, row_base: int = 0, out_dtype: int = DT_F32):
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    B, L = ids.shape
+    table = np.ascontiguousarray(table)
+    D = table.shape[1]
+    tdt = DT_F32 if table.dtype == np.float32 else DT_BF16
+    width = L * D if combiner == "null" else D
+    out = np.zeros((B, width), dtype=np.float32 if out_dtype == DT_F32 else np.uint16)
+    rc = lib().orf_embedding_bag_fwd(_p(ids), B, L, row_base, _p(table), tdt, table.shape[0], D, COMB[combiner],
+                                     _p(out), out_dtype, width, 0)
+    if rc != 0:
+        raise RuntimeError(f"oracle embedding_bag failed rc={rc}")
+    return out
+
+
+def bucketize_owner(rows: np.ndarray, nranks: int):
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    counts = np.zeros(nranks, np.int32)
+    perm = np.zeros(len(rows), np.int32)
+    local = np.zeros(len(rows), np.int64)
+    lib().orf_bucketize_owner(_p(rows), len(rows), nranks, _p(counts), _p(perm), _p(local))
+    return counts, perm, local
+
+
+def bf16_to_f32(u16: np.ndarray) -> np.ndarray:
+    return (np.asarray(u16, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def f32_to_bf16(x: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even f32 -> bf16 bits (NaN stays NaN)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    r[nan] = ((u[nan] >> 16) | 0x40).astype(np.uint16)
+    return r
+
+
+# ----------------------------------------------------------------------------------------------
+# dense floating-point stages (float64 numpy)
+# ----------------------------------------------------------------------------------------------
+def soft_attention(x0: np.ndarray, x1: np.ndarray):
+    """SoftAttention.__call__ (attention_layers.py:15-30): inputs [x0, x1] = [q, a].
+
+    _attention (:44-47): batch_dot(x0, x1^T) -> [B, L0, L1], permuted -> E[n, i, j] = x1[n,i].x0[n,j].
+    _soft_alignment (:69-74): S = exp(E - max_j E) / sum_j;  align_0 = S @ x0, align_1 = S @ x1.
+    """
+    x0 = np.asarray(x0, np.float64)
+    x1 = np.asarray(x1, np.float64)
+    E = np.einsum("bjk,bik->bij", x0, x1)
+    e = np.exp(E - E.max(axis=-1, keepdims=True))
+    S = e / e.sum(axis=-1, keepdims=True)
+    return S @ x0, S @ x1
+
+
+def esim_pool(q: np.ndarray, a: np.ndarray) -> np.ndarray:
+    """Esim.call combine (esim.py:78-82): [avg_q, max_q, avg_a, max_a, avg_q-avg_a, max_q-max_a] -> [B, 6d]."""
+    att_q, att_a = soft_attention(q, a)
+    q = np.asarray(q, np.float64)
+    a = np.asarray(a, np.float64)
+    m_q = np.concatenate([q, att_q, q - att_q, q * att_q], axis=1)
+    m_a = np.concatenate([a, att_a, a - att_a, a * att_a], axis=1)
+    avg_q, max_q = m_q.mean(axis=1), m_q.max(axis=1)
+    avg_a, max_a = m_a.mean(axis=1), m_a.max(axis=1)
+    return np.concatenate([avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a], axis=1)
+
+
+def gelu(x):
+    """tf.keras.activations.gelu (approximate=False): 0.5 x (1 + erf(x / sqrt 2))."""
+    from scipy.special import erf
+
+    return 0.5 * x * (1.0 + erf(x / math.sqrt(2.0)))
+
+
+def selu(x):
+    alpha, scale = 1.6732632423543772848170429916717, 1.0507009873554804934193349852946
+    return scale * np.where(x > 0, x, alpha * (np.exp(np.minimum(x, 0)) - 1.0))
+
+
+def activation(x, act: str):
+    if act in (None, "none", "linear"):
+        return x
+    if act == "gelu":
+        return gelu(x)
+    if act == "relu":
+        return np.maximum(x, 0)
+    if act == "selu":
+        return selu(x)
+    if act == "softmax":
+        e = np.exp(x - x.max(axis=-1, keepdims=True))
+        return e / e.sum(axis=-1, keepdims=True)
+    raise ValueError(act)
+
+
+def layer_norm(x, gamma, beta, eps=1e-6):
+    """tf.keras.layers.LayerNormalization(epsilon) over the last axis."""
+    x = np.asarray(x, np.float64)
+    mu = x.mean(axis=-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(axis=-1, keepdims=True)
+    return (x - mu) / np.sqrt(var + eps) * gamma + beta
+
+
+def batch_norm_infer(x, gamma, beta, mean, var, eps=1e-6):
+    """tf.keras.layers.BatchNormalization(epsilon) at inference."""
+    return (np.asarray(x, np.float64) - mean) / np.sqrt(var + eps) * gamma + beta
+
+
+def mlp(x, layers, act: str, norm: str = "ln", eps: float = 1e-6):
+    """create_mlp (mlp.py:4-15): per layer  x = act(Norm(x) @ W + b); Dropout = identity at inference.
+
+    layers: list of dicts {W: [K, N], b: [N], gamma, beta, (mean, var for BN)} — one norm per layer
+    (deviation D-shared-norm).
+    """
+    x = np.asarray(x, np.float64)
+    for p in layers:
+        if norm == "ln":
+            x = layer_norm(x, p["gamma"], p["beta"], eps)
+        elif norm == "bn":
+            x = batch_norm_infer(x, p["gamma"], p["beta"], p["mean"], p["var"], eps)
+        x = activation(x @ np.asarray(p["W"], np.float64) + p["b"], act)
+    return x
+
+
+def sdpa(q, k, v, mask=None):
+    """scaled_dot_product_attention (layer_utils.py:4-24): mask [.., Lq] zero => whole QUERY row filled
+    with -4294967295 (the [..., Lq, 1] mask broadcasts over keys), softmax over keys, @ v."""
+    q, k, v = (np.asarray(t, np.float64) for t in (q, k, v))
+    logits = q @ np.swapaxes(k, -1, -2) / math.sqrt(k.shape[-1])
+    if mask is not None:
+        m = np.asarray(mask)[..., :, None]
+        logits = np.where(m == 0, -4294967295.0, logits)
+    e = np.exp(logits - logits.max(axis=-1, keepdims=True))
+    return (e / e.sum(axis=-1, keepdims=True)) @ v
+
+
+def l2_normalize(x, eps=1e-12):
+    """K.l2_normalize (dssm.py:35-36): x / sqrt(max(sum x^2, eps))."""
+    x = np.asarray(x, np.float64)
+    return x / np.sqrt(np.maximum((x * x).sum(axis=-1, keepdims=True), eps))
