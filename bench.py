@@ -1,0 +1,186 @@
+"""Benchmark: BASELINE.json metric "examples/sec at 1/2/4/8 GPU + achieved HBM GB/s on embedding gather".
+
+Workload (BASELINE.json configs[1]): the sparse hot path of base_recall_sdpa.yaml —
+229 hashing slots (68+1 user incl. slot 0 by deviation D-ellipsis, 160 ad; 30 ArrayType multi-valued),
+double hashing (seeds 2022/2023) -> gather -> sum pool -> concat, over ONE fused 10,000,000 x 64 fp32
+table (458 segments x 21,834 rows), B = 4096 examples per GPU, synthetic Zipf(1.1) tokens
+f"s{slot:03d}:{id}" (runtime/batch.synthetic_batch). A step = one rf_fused_hash_embed_fwd over one
+resident CSR batch (inputs in HBM when the timed region starts).
+
+Multi-GPU: one process per GPU (torchrun); each rank holds a replica of the 2.56 GB table and its own
+batches (the reference mirrors tables per GPU, gpu_utils.py:13-14): no data-path collective, weak
+scaling; value = examples of all ranks / max-over-ranks time.
+
+Also reported: roofline of the fused kernel (algorithmic bytes / HIP-event kernel time vs 8 TB/s),
+PMC-measured HBM traffic when profiles/ holds it for this workload, and the CPU baseline (the C
+oracle — the "port" of the reference semantics — on a bounded sample, rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "examples/sec at 1/2/4/8 GPU + achieved HBM GB/s on embedding gather"
+HBM_PEAK_GBS = 8000.0
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch", type=int, default=4096)
+    p.add_argument("--batches", type=int, default=4, help="distinct resident batches cycled through")
+    p.add_argument("--table-rows", type=int, default=10_000_000)
+    p.add_argument("--dim", type=int, default=64)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
+    p.add_argument("--uniform", action="store_true", help="uniform ids instead of Zipf(1.1)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
+    from recommendflow_amd.config_parser.configuration import Configuration
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "base_recall_sdpa.yaml"))
+    feats = conf.features.hashing_features
+    S = len(feats)
+    n_bins = args.table_rows // (2 * S)
+    specs = [SlotSpec(f.name, n_bins, tuple(f.hash_seeds), f.pooling.value) for f in feats]
+    enc = FusedSparseEncoder(specs, args.dim, table_dtype=torch.float32, seed=2023)
+    multi = [bool(f.multivalued) for f in feats]
+    host = [synthetic_batch(args.batch, multi, seed=1234 + rank * 1000 + i, uniform=args.uniform)
+            for i in range(args.batches)]
+    dev = [h.to("cuda") for h in host]
+    out = torch.empty((args.batch, enc.out_width), dtype=torch.float32, device="cuda")
+    algo_bytes = [enc.algorithmic_bytes(h) for h in host]
+    torch.cuda.synchronize()
+
+    def step(i):
+        enc(dev[i % len(dev)], out=out)
+
+    for i in range(args.warmup):
+        step(i)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record()
+        step(i)
+        ends[i].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+    bytes_per_launch = sum(algo_bytes[i % len(algo_bytes)] for i in range(args.steps)) / args.steps
+    achieved = bytes_per_launch / avg_kern_s / 1e9
+    n_tok = sum(h.n_tokens for h in host) / len(host)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        tr = json.load(open(TRAFFIC_FILE))
+        if tr.get("batch") == args.batch and tr.get("table_rows") == args.table_rows and tr.get("dim") == args.dim:
+            traffic = tr.get("hbm_bytes_per_launch")
+
+    cpu = None
+    if world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(enc, host[0], args.cpu_seconds)
+
+    value = args.batch * world * args.steps / elapsed
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "examples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": "cfg2 base_recall_sdpa.yaml sparse encoder: hash x2 -> gather -> sum pool -> concat",
+            "global_batch": args.batch * world,
+            "batch_per_gpu": args.batch,
+            "slots": S,
+            "table": f"{enc.table_rows}x{args.dim} fp32 fused ({2 * S} segments x {n_bins})",
+            "tokens_per_example": round(n_tok / args.batch, 2),
+            "ids": "uniform" if args.uniform else "zipf1.1",
+            "parallelism": f"replicas{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "fused_hash_embed_kernel",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "kernel_ms": round(avg_kern_s * 1e3, 4),
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(enc, hb, budget_s):
+    """The C oracle (OpenMP) on the same batch; examples/s over ~budget_s seconds of repeated runs."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    threads = min(16, os.cpu_count() or 1)
+    table = enc.table.cpu().numpy()
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        O.fused_hash_embed(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, hb.batch, table, enc.dim,
+                           enc.out_width, n_threads=threads)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(n * hb.batch / el, 1), "unit": "examples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x one {hb.batch}-example cfg2 batch through oracle/rf_oracle.c "
+                      f"(orf_fused_hash_embed_fwd, OpenMP {threads} threads, gcc -O3) in {el:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

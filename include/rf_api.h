@@ -180,14 +180,17 @@ int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t 
                   int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream);
 
 /*
- * Masked scaled-dot-product attention (backend/layers/layer_utils.py:4-24):
- *   logits = q k^T / sqrt(depth); logits[i, :] = -4294967295 where mask[i] == 0 (QUERY rows, as the
- *   reference's [..., Lq, 1] mask broadcasts); softmax over keys (fp32); out = P v.
- * q,k,v: [BH][Lq|Lk][depth] (dtype F16 or BF16, contiguous); mask: F32 [BH][Lq] (may be NULL).
- * out: F32 [BH][Lq][depth]. Constraints: Lk <= 256, depth in {32, 64, 128}.
+ * Masked scaled-dot-product attention over heads (backend/layers/layer_utils.py:4-24, with the
+ * split_heads / merge transposes of MultiHeadAttention.call, attention_layers.py:159-167, folded
+ * into the addressing):
+ *   logits = q k^T / sqrt(depth); logits[i, :] = -4294967295 where mask[b, i] == 0 (QUERY rows, as
+ *   the reference's [..., Lq, 1] mask broadcasts over keys); softmax over keys (fp32); out = P v.
+ * q: [batch][Lq][heads*depth], k, v: [batch][Lk][heads*depth] (dtype F16 or BF16, contiguous; head h
+ * owns columns [h*depth, (h+1)*depth)); mask: F32 [batch][Lq] (NULL = no mask).
+ * out: F32 [batch][Lq][heads*depth]. Constraints: 1 <= Lq, Lk <= 256, depth in {32, 64, 128}.
  */
-int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int32_t BH, int32_t Lq,
-                int32_t Lk, int32_t depth, const float* mask, float* out, void* stream);
+int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int32_t batch, int32_t heads,
+                int32_t Lq, int32_t Lk, int32_t depth, const float* mask, float* out, void* stream);
 
 /*
  * Row-sharded tables: route fused-table rows to their owner rank (owner = g mod P, local = g div P).

@@ -1,0 +1,160 @@
+"""Fused multi-slot sparse encoder: every hashing feature of a tower in ONE kernel launch.
+
+Replaces the per-feature loop the reference runs inside a model: for each hashing feature f of
+get_preprocess_layers (backend/utils/preprocess_utils.py:10-20), DoubleHashingEmbedding.call
+(backend/layers/preprocess_layers.py:94-97) = 2 x Hashing + 2 x (Embedding gather + combiner) + concat,
+i.e. 2 string-hash ops + 2 gathers + 2 reductions per feature per step (456 + 456 + 456 TF ops for
+base_recall_sdpa.yaml). Here all slots of a tower share one fused table; slot s owns two segments
+[row_base[k], row_base[k] + N_s) (k = seeds[0], seeds[1]); its output [pool(T1) | pool(T2)] lands at
+a fixed column offset of one [B, sum_s 2*D] tensor (the concat of the reference's per-feature outputs
+in feature order).
+"""
+from __future__ import annotations
+
+import zlib
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ...runtime import lib as L
+from ...runtime.batch import SparseBatch
+
+# rf_slot_desc (include/rf_api.h), 64 bytes
+SLOT_DTYPE = np.dtype(
+    [
+        ("row_base", "<i8", (2,)),
+        ("num_bins", "<i8"),
+        ("salt", "<u8", (2,)),
+        ("out_off", "<i8"),
+        ("dim", "<i4"),
+        ("combiner", "<i4"),
+        ("mask_empty", "<i4"),
+        ("reserved", "<i4"),
+    ]
+)
+assert SLOT_DTYPE.itemsize == 64
+
+POOLED = ("sum", "avg", "max", "min", "first", "last")
+
+
+def normalize_seeds(seeds) -> Tuple[int, int]:
+    """DoubleHashingEmbedding seeds: [s0, s1]; an int s means [s, s + 7] (preprocess_layers.py:88; the
+    reference then indexes the raw int and crashes — deviation D-int-seed keeps the stated intent)."""
+    if seeds is None:
+        raise ValueError("DoubleHashingEmbedding needs hash seeds (Keras Hashing without a salt uses FarmHash64, "
+                         "which this build does not implement)")
+    if isinstance(seeds, (int, np.integer)):
+        return int(seeds), int(seeds) + 7
+    s = list(seeds)
+    if len(s) < 2:
+        raise ValueError(f"seeds must hold two salts, got {seeds}")
+    return int(s[0]), int(s[1])
+
+
+def name_seed(name: str, base: int = 0) -> int:
+    return (zlib.crc32(name.encode()) ^ (base * 0x9E3779B1)) & 0xFFFFFFFF
+
+
+@dataclass
+class SlotSpec:
+    name: str
+    num_bins: int
+    seeds: Tuple[int, int]
+    combiner: str = "sum"
+    mask_empty: bool = True  # get_preprocess_layers builds Hashing with mask_value="" (preprocess_utils.py:15)
+
+
+def init_table(table: torch.Tensor, row0: int = 0, row_stride: int = 1, seed: int = 0, lo: float = -0.05,
+               hi: float = 0.05, stream=None) -> torch.Tensor:
+    """Counter-based U(lo, hi) init on the GPU (rf_table_init_uniform): identical rows for any sharding."""
+    L.require_gpu()
+    rows, dim = table.shape
+    L.call("rf_table_init_uniform", L.ptr(table), L.torch_dtype_code(table.dtype), rows, dim, row0, row_stride,
+           seed, lo, hi, L.stream_ptr(stream))
+    return table
+
+
+class FusedSparseEncoder(torch.nn.Module):
+    """All hashing slots of one tower -> [B, sum_s 2*D] with one rf_fused_hash_embed_fwd launch."""
+
+    def __init__(self, slots: Sequence[SlotSpec], dim: int, table_dtype=torch.float32, out_dtype=None,
+                 seed: int = 0, mask_padding: bool = False, device="cuda", init_range=(-0.05, 0.05),
+                 table: Optional[torch.Tensor] = None, row_base0: int = 0):
+        super().__init__()
+        if not slots:
+            raise ValueError("FusedSparseEncoder needs at least one slot")
+        self.slots = list(slots)
+        self.dim = int(dim)
+        self.table_dtype = table_dtype
+        self.out_dtype = out_dtype or table_dtype
+        self.mask_padding = bool(mask_padding)
+        self.seed = int(seed)
+        desc = np.zeros(len(self.slots), SLOT_DTYPE)
+        base = int(row_base0)
+        for i, sp in enumerate(self.slots):
+            if sp.num_bins is None or sp.num_bins <= 0:
+                raise ValueError("`num_bins` cannot be `None` or non-positive values.")
+            if sp.num_bins >= 2 ** 31:
+                raise ValueError("num_bins must be < 2^31")
+            if sp.combiner not in POOLED:
+                raise ValueError(f"Do not support combiner = '{sp.combiner}' in a fused encoder, supported: "
+                                 f"[{', '.join(POOLED)}] (null pooling runs per feature)")
+            desc[i]["row_base"] = (base, base + sp.num_bins)
+            desc[i]["num_bins"] = sp.num_bins
+            desc[i]["salt"] = (sp.seeds[0] & (2 ** 64 - 1), sp.seeds[1] & (2 ** 64 - 1))
+            desc[i]["out_off"] = i * 2 * self.dim
+            desc[i]["dim"] = self.dim
+            desc[i]["combiner"] = L.COMB[sp.combiner]
+            desc[i]["mask_empty"] = int(sp.mask_empty)
+            base += 2 * sp.num_bins
+        self.host_desc = desc
+        self.table_rows = base
+        self.out_width = 2 * self.dim * len(self.slots)
+        L.load()
+        L.require_gpu()
+        self.register_buffer("desc", torch.from_numpy(desc.view(np.uint8).copy()).to(device), persistent=False)
+        if table is None:
+            table = torch.empty((self.table_rows, self.dim), dtype=table_dtype, device=device)
+            init_table(table, 0, 1, self.seed, *init_range)
+        elif table.shape[0] < self.table_rows or table.shape[1] != self.dim:
+            raise ValueError(f"shared table {tuple(table.shape)} too small for {self.table_rows} x {self.dim}")
+        self.table = table
+
+    def slot_offsets(self) -> List[Tuple[str, int, int]]:
+        return [(sp.name, i * 2 * self.dim, (i + 1) * 2 * self.dim) for i, sp in enumerate(self.slots)]
+
+    def forward(self, batch: SparseBatch, out: Optional[torch.Tensor] = None, out_col: int = 0,
+                emit_idx: bool = False, stream=None):
+        if batch.n_slots != len(self.slots):
+            raise ValueError(f"batch has {batch.n_slots} slots, encoder {len(self.slots)}")
+        if not batch.is_device():
+            batch = batch.to(self.table.device)
+        B = batch.batch
+        if out is None:
+            out = torch.empty((B, self.out_width), dtype=self.out_dtype, device=self.table.device)
+            out_col = 0
+        if out_col:
+            raise ValueError("out_col is reserved; pass a column slice through the descriptors instead")
+        flags = (L.FLAG_MASK_PADDING if self.mask_padding else 0) | (L.FLAG_EMIT_IDX if emit_idx else 0)
+        idx = torch.empty((max(batch.n_tokens, 1), 2), dtype=torch.int64, device=self.table.device) if emit_idx else None
+        L.call("rf_fused_hash_embed_fwd", L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes),
+               L.ptr(batch.tok_off), L.ptr(batch.bag_off), L.ptr(batch.lmax), B, L.ptr(self.table),
+               L.torch_dtype_code(self.table.dtype), self.table.shape[0], self.dim, L.ptr(out),
+               L.torch_dtype_code(out.dtype), out.stride(0), flags, L.ptr(idx), L.stream_ptr(stream))
+        if emit_idx:
+            return out, idx[: batch.n_tokens]
+        return out
+
+    def algorithmic_bytes(self, batch: SparseBatch) -> int:
+        """HBM bytes one forward must move: rows read (every occurrence, padding positions
+        included as one pad-row read per table when Lmax > len), pooled output written, token bytes +
+        i32 offsets read."""
+        h = batch.numpy()
+        esz = torch.tensor([], dtype=self.table_dtype).element_size()
+        osz = torch.tensor([], dtype=self.out_dtype).element_size()
+        lens = np.diff(h.bag_off).reshape(h.batch, h.n_slots)
+        rows = int(lens.sum()) if self.mask_padding else int(lens.sum() + ((lens < h.lmax[None, :]).sum()))
+        return 2 * rows * self.dim * esz + h.batch * self.out_width * osz + int(len(h.tok_bytes)) + 4 * (h.n_tokens + 1) \
+            + 4 * (h.batch * h.n_slots + 1)

@@ -1,0 +1,100 @@
+"""Dense and normalisation layers on librf.so (the building blocks of create_mlp, backend/blocks/mlp.py).
+
+Dense(units, activation)  tf.keras.layers.Dense: y = act(x @ W + b); W kept as [N][K] (transposed Keras
+                          kernel) in the compute dtype (bf16 -> bf16 MFMA, fp32 -> exact fp32 MFMA);
+                          glorot_uniform kernel, zero bias (Keras defaults), deterministic by seed.
+LayerNormalization(eps)   tf.keras.layers.LayerNormalization over the last axis (gamma 1, beta 0).
+BatchNormalization(eps)   tf.keras.layers.BatchNormalization at inference (running mean 0, var 1).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ...runtime import lib as L
+
+
+def act_name(activation) -> Optional[str]:
+    if activation is None:
+        return None
+    if isinstance(activation, str):
+        name = activation.lower()
+    else:
+        name = getattr(activation, "__name__", str(activation)).lower()
+    if name not in L.ACT:
+        raise ValueError(f"unsupported activation {activation!r}")
+    return name
+
+
+class Dense(torch.nn.Module):
+    def __init__(self, in_features: int, units: int, activation=None, use_bias: bool = True, dtype=torch.bfloat16,
+                 seed: int = 0, device="cuda", weight: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None):
+        super().__init__()
+        self.in_features, self.units = int(in_features), int(units)
+        self.activation = act_name(activation)
+        self.dtype = dtype
+        L.load()
+        L.require_gpu()
+        if weight is None:
+            g = torch.Generator().manual_seed(int(seed))
+            lim = math.sqrt(6.0 / (self.in_features + self.units))
+            weight = (torch.rand((self.units, self.in_features), generator=g) * 2 - 1) * lim
+        self.weight = weight.to(device=device, dtype=dtype).contiguous()  # [N][K]
+        if bias is None and use_bias:
+            bias = torch.zeros(self.units)
+        self.bias = None if bias is None else bias.to(device=device, dtype=torch.float32).contiguous()
+
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        if x.dtype != self.dtype:
+            x = x.to(self.dtype)
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty((M, self.units), dtype=torch.float32, device=self.weight.device)
+        L.call("rf_linear_fwd", L.ptr(x), L.torch_dtype_code(self.dtype), M, self.in_features, x.stride(0),
+               L.ptr(self.weight), self.units, L.ptr(self.bias), L.ACT[self.activation], L.ptr(out), out.stride(0),
+               L.stream_ptr(stream))
+        return out
+
+
+class LayerNormalization:
+    mode = 0
+
+    def __init__(self, epsilon: float = 1e-3, name: Optional[str] = None):
+        self.epsilon = float(epsilon)
+        self.name = name
+
+
+class BatchNormalization:
+    mode = 1
+
+    def __init__(self, epsilon: float = 1e-3, name: Optional[str] = None):
+        self.epsilon = float(epsilon)
+        self.name = name
+
+
+class Norm(torch.nn.Module):
+    """One normalisation instance with its own parameters (deviation D-shared-norm: the reference appends
+    the SAME Keras layer before every Dense, mlp.py:10-11, which only works when all widths match)."""
+
+    def __init__(self, spec, width: int, device="cuda"):
+        super().__init__()
+        self.mode, self.eps, self.width = spec.mode, spec.epsilon, int(width)
+        self.gamma = torch.ones(width, device=device)
+        self.beta = torch.zeros(width, device=device)
+        self.mean = torch.zeros(width, device=device) if self.mode == 1 else None
+        self.var = torch.ones(width, device=device) if self.mode == 1 else None
+
+    def forward(self, x: torch.Tensor, out_dtype=torch.bfloat16, stream=None) -> torch.Tensor:
+        x = x.float()
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        M = x.shape[0]
+        y = torch.empty((M, self.width), dtype=out_dtype, device=x.device)
+        L.call("rf_norm_fwd", L.ptr(x), M, self.width, x.stride(0), self.mode, self.eps, L.ptr(self.gamma),
+               L.ptr(self.beta), L.ptr(self.mean), L.ptr(self.var), L.ptr(y), L.torch_dtype_code(out_dtype),
+               y.stride(0), L.stream_ptr(stream))
+        return y

@@ -1,0 +1,436 @@
+// rf_attn.hip — attention stages on gfx950 MFMA (v_mfma_f32_16x16x32_{bf16,f16}, fp32 accumulate).
+//   rf_esim_soft_attention_fwd  SoftAttention + ESIM combine/pool  (attention_layers.py:15-74, esim.py:78-84)
+//   rf_sdpa_fwd                 masked multi-head SDPA             (layer_utils.py:4-38, attention_layers.py:153-168)
+//
+// Both kernels keep one example (or one (example, head)) per workgroup of 4 waves:
+//   * the [L, d] operand images sit in LDS with a 16-byte row pad (conflict-free ds_read_b128 for the
+//     16x16x32 A/B fragments, 8-byte aligned rows for ds_read_b64_tr_b16);
+//   * each wave owns 16-row stripes of the score matrix; scores stay in registers (never HBM), the
+//     row softmax runs in fp32 with 16-lane xor shuffles, P is rounded once to the MFMA dtype into a
+//     per-wave LDS stripe;
+//   * P @ V takes V's B fragments with the hardware transpose read (ds_read_b64_tr_b16, guide T10),
+//     so V is staged once, row-major, straight from HBM.
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cmath>
+
+#include "rf_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <bool F16>
+struct Mfma;
+
+template <>
+struct Mfma<false> {  // bf16
+    using frag = bf16x8;
+    static __device__ __forceinline__ f4 mma(frag a, frag b, f4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ float to_f(uint16_t h) { return bf16_bits_to_f32(h); }
+    static __device__ __forceinline__ uint16_t from_f(float f) { return (uint16_t)f32_to_bf16_bits(f); }
+};
+
+template <>
+struct Mfma<true> {  // f16
+    using frag = f16x8;
+    static __device__ __forceinline__ f4 mma(frag a, frag b, f4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ float to_f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
+    static __device__ __forceinline__ uint16_t from_f(float f) { return __half_as_ushort(__float2half_rn(f)); }
+};
+
+template <typename frag>
+__device__ __forceinline__ frag lds_frag(const uint16_t* p) {  // 16-byte aligned LDS address -> ds_read_b128
+    return *reinterpret_cast<const frag*>(p);
+}
+
+__device__ __forceinline__ s4v tr_read(const uint16_t* p) {  // ds_read_b64_tr_b16
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(p));
+}
+
+// B fragment of the 16x16x32 MFMA for B[k][n] = V[k0 + k][n0 + n] (V row-major in LDS, row stride rs):
+// lane l needs V[k0 + 8*(l>>4) + j][n0 + (l&15)], j = 0..7 — two transposed 4-row reads.
+template <typename frag>
+__device__ __forceinline__ frag v_frag_tr(const uint16_t* V, int rs, int k0, int n0, int lane) {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+    const uint16_t* base = V + (k0 + 8 * g + qq) * rs + n0 + 4 * p;
+    const s4v lo = tr_read(base);
+    const s4v hi = tr_read(base + 4 * rs);
+    const s8v x = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(frag, x);
+}
+
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// ESIM: one workgroup per example
+// ---------------------------------------------------------------------------------------------
+template <bool F16, int D>
+__global__ __launch_bounds__(256) void esim_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ a, int L,
+                                                   int64_t ex_stride, int64_t ld, float* __restrict__ out,
+                                                   int64_t out_stride, int64_t out_off, float* __restrict__ att_out) {
+    using M = Mfma<F16>;
+    using frag = typename M::frag;
+    constexpr int RS = D + 8;       // LDS row stride (elements) of the q / a images
+    constexpr int DK = D / 32;      // k-steps of the score product
+    constexpr int NT = D / 16;      // n-tiles of the P @ V product (per side)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int64_t b = blockIdx.x;
+    const int Lk = (L + 31) & ~31;  // k extent of P @ V (zero rows past L)
+    const int nt = (L + 15) >> 4;   // 16-wide tiles over positions
+    const int SS = Lk + 8;          // row stride of a wave's P stripe
+    uint16_t* qs = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* as = qs + Lk * RS;
+    uint16_t* pbuf = as + Lk * RS;
+    float* st = reinterpret_cast<float*>(pbuf + 4 * 16 * SS);  // [wave][stat 6][side*D + n]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+
+    // stage q and a (rows >= L zero), 16-byte chunks
+    constexpr int CPR = D / 8;
+    for (int c = tid; c < 2 * Lk * CPR; c += 256) {
+        const int m = c / (Lk * CPR), rem = c - m * Lk * CPR, r = rem / CPR, ch = rem - r * CPR;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (r < L) v = *reinterpret_cast<const uint4*>((m ? a : q) + b * ex_stride + (int64_t)r * ld + ch * 8);
+        *reinterpret_cast<uint4*>((m ? as : qs) + r * RS + ch * 8) = v;
+    }
+    for (int i = tid; i < 4 * 6 * 2 * D; i += 256) st[i] = ((i / (2 * D)) % 6) < 3 ? 0.0f : -INFINITY;
+    __syncthreads();
+
+    float* wst = st + wave * 6 * 2 * D;
+    uint16_t* pw = pbuf + wave * 16 * SS;
+    for (int sp = wave; sp < nt; sp += 4) {
+        // E[i, j] = sum_k a[i, k] q[j, k] for the stripe's 16 rows i (attention_layers.py:44-47)
+        frag af[DK];
+#pragma unroll
+        for (int kk = 0; kk < DK; ++kk) af[kk] = lds_frag<frag>(as + (sp * 16 + lr) * RS + kk * 32 + lg * 8);
+        f4 e[8];
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) {
+            e[jt] = f4{0.f, 0.f, 0.f, 0.f};
+            if (jt < nt) {
+#pragma unroll
+                for (int kk = 0; kk < DK; ++kk)
+                    e[jt] = M::mma(af[kk], lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8), e[jt]);
+            }
+        }
+        // row softmax over j < L (max-subtracted, attention_layers.py:69-72), fp32
+        float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt)
+            if (jt < nt) {
+                const bool valid = jt * 16 + lr < L;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (!valid) e[jt][r] = -INFINITY;
+                    mx[r] = fmaxf(mx[r], e[jt][r]);
+                }
+            }
+        float sm[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            mx[r] = group16_max(mx[r]);
+            sm[r] = 0.f;
+        }
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt)
+            if (jt < nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    e[jt][r] = expf(e[jt][r] - mx[r]);
+                    sm[r] += e[jt][r];
+                }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm[r] = 1.0f / group16_sum(sm[r]);
+        // P stripe -> LDS (MFMA dtype), zero past the valid tiles up to Lk
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt)
+            if (jt * 16 < Lk)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    pw[(lg * 4 + r) * SS + jt * 16 + lr] = jt < nt ? M::from_f(e[jt][r] * sm[r]) : (uint16_t)0;
+        wave_lds_sync();
+
+        // att_side = P @ side (attention_layers.py:74), then the ESIM combine statistics (esim.py:79-82)
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const uint16_t* V = side ? as : qs;
+            f4 acc[NT];
+#pragma unroll
+            for (int nn = 0; nn < NT; ++nn) acc[nn] = f4{0.f, 0.f, 0.f, 0.f};
+            for (int kt = 0; kt < Lk; kt += 32) {
+                const frag pa = lds_frag<frag>(pw + lr * SS + kt + lg * 8);
+#pragma unroll
+                for (int nn = 0; nn < NT; ++nn) acc[nn] = M::mma(pa, v_frag_tr<frag>(V, RS, kt, nn * 16, lane), acc[nn]);
+            }
+#pragma unroll
+            for (int nn = 0; nn < NT; ++nn) {
+                const int n = nn * 16 + lr;
+                float s_att = 0.f, s_dif = 0.f, s_mul = 0.f, m_att = -INFINITY, m_dif = -INFINITY, m_mul = -INFINITY;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = sp * 16 + lg * 4 + r;
+                    if (row < L) {
+                        const float x = M::to_f(V[row * RS + n]);
+                        const float at = acc[nn][r];
+                        const float df = x - at, ml = x * at;
+                        s_att += at; s_dif += df; s_mul += ml;
+                        m_att = fmaxf(m_att, at); m_dif = fmaxf(m_dif, df); m_mul = fmaxf(m_mul, ml);
+                        if (att_out) att_out[((b * 2 + side) * L + row) * D + n] = at;
+                    }
+                }
+#pragma unroll
+                for (int o = 16; o < 64; o <<= 1) {
+                    s_att += __shfl_xor(s_att, o, 64); s_dif += __shfl_xor(s_dif, o, 64); s_mul += __shfl_xor(s_mul, o, 64);
+                    m_att = fmaxf(m_att, __shfl_xor(m_att, o, 64)); m_dif = fmaxf(m_dif, __shfl_xor(m_dif, o, 64));
+                    m_mul = fmaxf(m_mul, __shfl_xor(m_mul, o, 64));
+                }
+                if (lg == 0) {
+                    float* w = wst + side * D + n;
+                    w[0 * 2 * D] += s_att; w[1 * 2 * D] += s_dif; w[2 * 2 * D] += s_mul;
+                    w[3 * 2 * D] = fmaxf(w[3 * 2 * D], m_att); w[4 * 2 * D] = fmaxf(w[4 * 2 * D], m_dif);
+                    w[5 * 2 * D] = fmaxf(w[5 * 2 * D], m_mul);
+                }
+            }
+        }
+        wave_lds_sync();
+    }
+    __syncthreads();
+
+    // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84)
+    for (int n = tid; n < D; n += 256) {
+        float avg[2], mxv[2];
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const uint16_t* V = side ? as : qs;
+            float sx = 0.f, mxx = -INFINITY;
+            for (int i = 0; i < L; ++i) {
+                const float x = M::to_f(V[i * RS + n]);
+                sx += x;
+                mxx = fmaxf(mxx, x);
+            }
+            float s3 = 0.f, m3 = mxx;
+            for (int w = 0; w < 4; ++w) {
+                const float* ws = st + w * 6 * 2 * D + side * D + n;
+                s3 += ws[0] + ws[2 * D] + ws[4 * D];
+                m3 = fmaxf(m3, fmaxf(ws[6 * D], fmaxf(ws[8 * D], ws[10 * D])));
+            }
+            avg[side] = (sx + s3) / (float)(4 * L);
+            mxv[side] = m3;
+        }
+        float* o = out + b * out_stride + out_off + n;
+        o[0] = avg[0];
+        o[D] = mxv[0];
+        o[2 * D] = avg[1];
+        o[3 * D] = mxv[1];
+        o[4 * D] = avg[0] - avg[1];
+        o[5 * D] = mxv[0] - mxv[1];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// masked multi-head SDPA: one workgroup per (example, head)
+// ---------------------------------------------------------------------------------------------
+template <bool F16, int DEP>
+__global__ __launch_bounds__(256) void sdpa_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ k,
+                                                   const uint16_t* __restrict__ v, int heads, int Lq, int Lk,
+                                                   const float* __restrict__ mask, float* __restrict__ out) {
+    using M = Mfma<F16>;
+    using frag = typename M::frag;
+    constexpr int RS = DEP + 8, DK = DEP / 32, NT = DEP / 16, MAXT = 16;  // up to 256 keys
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int64_t b = blockIdx.x / heads;
+    const int h = blockIdx.x - (int)(b * heads);
+    const int64_t rowstride = (int64_t)heads * DEP;
+    const int Lkp = (Lk + 31) & ~31, nt = (Lk + 15) >> 4, SS = Lkp + 8;
+    uint16_t* ks = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* vs = ks + Lkp * RS;
+    uint16_t* pbuf = vs + Lkp * RS;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    constexpr int CPR = DEP / 8;
+    for (int c = tid; c < 2 * Lkp * CPR; c += 256) {
+        const int m = c / (Lkp * CPR), rem = c - m * Lkp * CPR, r = rem / CPR, ch = rem - r * CPR;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (r < Lk) x = *reinterpret_cast<const uint4*>((m ? v : k) + (b * Lk + r) * rowstride + h * DEP + ch * 8);
+        *reinterpret_cast<uint4*>((m ? vs : ks) + r * RS + ch * 8) = x;
+    }
+    __syncthreads();
+    const float scale = 1.0f / sqrtf((float)DEP);
+    uint16_t* pw = pbuf + wave * 16 * SS;
+    const int ntq = (Lq + 15) >> 4;
+    for (int sp = wave; sp < ntq; sp += 4) {
+        const int qrow = sp * 16 + lr;
+        frag af[DK];
+#pragma unroll
+        for (int kk = 0; kk < DK; ++kk) {
+            if (qrow < Lq)
+                af[kk] = *reinterpret_cast<const frag*>(q + (b * Lq + qrow) * rowstride + h * DEP + kk * 32 + lg * 8);
+            else
+                af[kk] = __builtin_bit_cast(frag, s8v{0, 0, 0, 0, 0, 0, 0, 0});
+        }
+        f4 e[MAXT];
+#pragma unroll
+        for (int jt = 0; jt < MAXT; ++jt) {
+            e[jt] = f4{0.f, 0.f, 0.f, 0.f};
+            if (jt < nt) {
+#pragma unroll
+                for (int kk = 0; kk < DK; ++kk)
+                    e[jt] = M::mma(af[kk], lds_frag<frag>(ks + (jt * 16 + lr) * RS + kk * 32 + lg * 8), e[jt]);
+            }
+        }
+        // rows of this lane: sp*16 + lg*4 + r ; query-row mask replaces the whole row (layer_utils.py:13-14)
+        bool masked[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = sp * 16 + lg * 4 + r;
+            masked[r] = mask != nullptr && row < Lq && mask[b * Lq + row] == 0.0f;
+        }
+        float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int jt = 0; jt < MAXT; ++jt)
+            if (jt < nt) {
+                const bool valid = jt * 16 + lr < Lk;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float x = e[jt][r] * scale;
+                    if (masked[r]) x = -4294967295.0f;
+                    if (!valid) x = -INFINITY;
+                    e[jt][r] = x;
+                    mx[r] = fmaxf(mx[r], x);
+                }
+            }
+        float sm[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            mx[r] = group16_max(mx[r]);
+            sm[r] = 0.f;
+        }
+#pragma unroll
+        for (int jt = 0; jt < MAXT; ++jt)
+            if (jt < nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    e[jt][r] = expf(e[jt][r] - mx[r]);
+                    sm[r] += e[jt][r];
+                }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm[r] = 1.0f / group16_sum(sm[r]);
+#pragma unroll
+        for (int jt = 0; jt < MAXT; ++jt)
+            if (jt * 16 < Lkp)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    pw[(lg * 4 + r) * SS + jt * 16 + lr] = jt < nt ? M::from_f(e[jt][r] * sm[r]) : (uint16_t)0;
+        wave_lds_sync();
+        f4 acc[NT];
+#pragma unroll
+        for (int nn = 0; nn < NT; ++nn) acc[nn] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < Lkp; kt += 32) {
+            const frag pa = lds_frag<frag>(pw + lr * SS + kt + lg * 8);
+#pragma unroll
+            for (int nn = 0; nn < NT; ++nn) acc[nn] = M::mma(pa, v_frag_tr<frag>(vs, RS, kt, nn * 16, lane), acc[nn]);
+        }
+#pragma unroll
+        for (int nn = 0; nn < NT; ++nn)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = sp * 16 + lg * 4 + r;
+                if (row < Lq) out[(b * Lq + row) * rowstride + h * DEP + nn * 16 + lr] = acc[nn][r];
+            }
+        wave_lds_sync();
+    }
+}
+
+template <typename K>
+int launch_big_lds(K kernel, int grid, size_t lds, hipStream_t st, const char* name) {
+    (void)kernel;
+    (void)grid;
+    (void)st;
+    if (lds > 160 * 1024) return rf_set_error(RF_EINVAL, "%s: needs %zu bytes of LDS (> 160 KiB)", name, lds);
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: hipFuncSetAttribute: %s", name, hipGetErrorString(e));
+    }
+    return RF_OK;
+}
+
+}  // namespace
+
+extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                                          int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
+                                          float* att_out, void* stream) {
+    RF_REQUIRE(dtype == RF_DTYPE_BF16 || dtype == RF_DTYPE_F16, "rf_esim_soft_attention_fwd: dtype must be BF16 or F16");
+    RF_REQUIRE(L >= 1 && L <= 128, "rf_esim_soft_attention_fwd: need 1 <= L <= 128 (got %d)", L);
+    RF_REQUIRE(d == 64 || d == 128, "rf_esim_soft_attention_fwd: d must be 64 or 128 (got %d)", d);
+    RF_REQUIRE(batch >= 0, "rf_esim_soft_attention_fwd: batch < 0");
+    RF_REQUIRE(ld % 8 == 0 && ex_stride % 8 == 0 && ld >= d, "rf_esim_soft_attention_fwd: ld/ex_stride must be multiples of 8 elements (16-byte rows)");
+    RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)a & 15) == 0, "rf_esim_soft_attention_fwd: q/a must be 16-byte aligned");
+    if (batch == 0) return RF_OK;
+    RF_REQUIRE(q && a && out, "rf_esim_soft_attention_fwd: null pointer");
+    const int Lk = (L + 31) & ~31;
+    const size_t lds = (size_t)2 * Lk * (d + 8) * 2 + (size_t)4 * 16 * (Lk + 8) * 2 + (size_t)4 * 6 * 2 * d * 4;
+    hipStream_t st = rf_stream(stream);
+#define RF_ESIM_LAUNCH(F16, D)                                                                                     \
+    {                                                                                                              \
+        auto kern = esim_kernel<F16, D>;                                                                           \
+        int rc = launch_big_lds(kern, batch, lds, st, "esim_kernel");                                              \
+        if (rc) return rc;                                                                                         \
+        hipLaunchKernelGGL(kern, dim3(batch), dim3(256), lds, st, (const uint16_t*)q, (const uint16_t*)a, L,       \
+                           ex_stride, ld, out, out_stride, out_off, att_out);                                      \
+    }
+    if (dtype == RF_DTYPE_BF16) {
+        if (d == 64) RF_ESIM_LAUNCH(false, 64) else RF_ESIM_LAUNCH(false, 128)
+    } else {
+        if (d == 64) RF_ESIM_LAUNCH(true, 64) else RF_ESIM_LAUNCH(true, 128)
+    }
+#undef RF_ESIM_LAUNCH
+    return rf_check_launch("esim_kernel");
+}
+
+extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int32_t batch, int32_t heads,
+                           int32_t Lq, int32_t Lk, int32_t depth, const float* mask, float* out, void* stream) {
+    RF_REQUIRE(dtype == RF_DTYPE_BF16 || dtype == RF_DTYPE_F16, "rf_sdpa_fwd: dtype must be BF16 or F16");
+    RF_REQUIRE(depth == 32 || depth == 64 || depth == 128, "rf_sdpa_fwd: depth must be 32, 64 or 128 (got %d)", depth);
+    RF_REQUIRE(Lq >= 1 && Lq <= 4096 && Lk >= 1 && Lk <= 256, "rf_sdpa_fwd: need 1 <= Lk <= 256 and Lq >= 1");
+    RF_REQUIRE(batch >= 0 && heads >= 1, "rf_sdpa_fwd: batch >= 0, heads >= 1");
+    RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)k & 15) == 0 && ((uintptr_t)v & 15) == 0, "rf_sdpa_fwd: q/k/v must be 16-byte aligned");
+    if (batch == 0) return RF_OK;
+    RF_REQUIRE(q && k && v && out, "rf_sdpa_fwd: null pointer");
+    const int Lkp = (Lk + 31) & ~31;
+    const size_t lds = (size_t)2 * Lkp * (depth + 8) * 2 + (size_t)4 * 16 * (Lkp + 8) * 2;
+    hipStream_t st = rf_stream(stream);
+    const int grid = batch * heads;
+#define RF_SDPA_LAUNCH(F16, DEP)                                                                                    \
+    {                                                                                                               \
+        auto kern = sdpa_kernel<F16, DEP>;                                                                          \
+        int rc = launch_big_lds(kern, grid, lds, st, "sdpa_kernel");                                                \
+        if (rc) return rc;                                                                                          \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, (const uint16_t*)q, (const uint16_t*)k,            \
+                           (const uint16_t*)v, heads, Lq, Lk, mask, out);                                          \
+    }
+    if (dtype == RF_DTYPE_BF16) {
+        if (depth == 32) RF_SDPA_LAUNCH(false, 32) else if (depth == 64) RF_SDPA_LAUNCH(false, 64) else RF_SDPA_LAUNCH(false, 128)
+    } else {
+        if (depth == 32) RF_SDPA_LAUNCH(true, 32) else if (depth == 64) RF_SDPA_LAUNCH(true, 64) else RF_SDPA_LAUNCH(true, 128)
+    }
+#undef RF_SDPA_LAUNCH
+    return rf_check_launch("sdpa_kernel");
+}

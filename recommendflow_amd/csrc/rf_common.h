@@ -1,0 +1,178 @@
+// rf_common.h — shared device/host helpers of librf.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rf_api.h"
+
+// ---------------------------------------------------------------------------------------------
+// error state (thread-local message, see rf_last_error)
+// ---------------------------------------------------------------------------------------------
+int rf_set_error(int code, const char* fmt, ...);
+int rf_check_launch(const char* what);  // hipGetLastError -> RF_EHIP with message
+
+#define RF_REQUIRE(cond, ...)                                 \
+    do {                                                      \
+        if (!(cond)) return rf_set_error(RF_EINVAL, __VA_ARGS__); \
+    } while (0)
+
+static inline hipStream_t rf_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------------------------------------
+// wave helpers
+// ---------------------------------------------------------------------------------------------
+// Orders this wave's LDS writes before its later LDS reads by other lanes of the same wave.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16 <-> f32 (bit exact with oracle/rf_oracle.c)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float bf16_bits_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+__device__ __forceinline__ uint32_t f32_to_bf16_bits(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return ((u >> 16) | 0x40u) & 0xffffu;  // quiet NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SipHash-2-4 on 64-bit lanes (the compiler splits into 32-bit pairs; rotations -> v_alignbit_b32).
+// Reads the token with aligned dword loads: a dword that holds at least one byte of the token never
+// crosses a page boundary past the token, so no read faults beyond the caller's buffer.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+
+#define RF_SIPROUND                                                          \
+    do {                                                                     \
+        v0 += v1; v1 = rotl64(v1, 13); v1 ^= v0; v0 = rotl64(v0, 32);        \
+        v2 += v3; v3 = rotl64(v3, 16); v3 ^= v2;                             \
+        v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;                             \
+        v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);        \
+    } while (0)
+
+__device__ __forceinline__ uint64_t siphash24_dev(uint64_t k0, uint64_t k1, const uint8_t* p, int n) {
+    uint64_t v0 = 0x736f6d6570736575ULL ^ k0;
+    uint64_t v1 = 0x646f72616e646f6dULL ^ k1;
+    uint64_t v2 = 0x6c7967656e657261ULL ^ k0;
+    uint64_t v3 = 0x7465646279746573ULL ^ k1;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a - sh);
+    const int nwords = n > 0 ? (int)((sh + (uint32_t)n + 3) >> 2) : 0;  // aligned dwords holding token bytes
+    // message dword j = token bytes [4j, 4j+4) = aligned words j, j+1 shifted by sh bytes
+    auto msg32 = [&](int j) -> uint32_t {
+        uint32_t lo = j < nwords ? w[j] : 0u;
+        uint32_t hi = (j + 1) < nwords ? w[j + 1] : 0u;
+        return sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    };
+    const int nb = n >> 3;
+    for (int i = 0; i < nb; ++i) {
+        uint64_t m = (uint64_t)msg32(2 * i) | ((uint64_t)msg32(2 * i + 1) << 32);
+        v3 ^= m;
+        RF_SIPROUND;
+        RF_SIPROUND;
+        v0 ^= m;
+    }
+    const int r = n & 7;
+    uint64_t tail = 0;
+    if (r) {
+        tail = (uint64_t)msg32(2 * nb) | ((uint64_t)msg32(2 * nb + 1) << 32);
+        tail &= (~0ULL) >> (64 - 8 * r);
+    }
+    uint64_t bl = ((uint64_t)(uint32_t)n << 56) | tail;
+    v3 ^= bl;
+    RF_SIPROUND;
+    RF_SIPROUND;
+    v0 ^= bl;
+    v2 ^= 0xff;
+    RF_SIPROUND;
+    RF_SIPROUND;
+    RF_SIPROUND;
+    RF_SIPROUND;
+    return v0 ^ v1 ^ v2 ^ v3;
+}
+
+// Keras Hashing bucket (see rf_siphash_bucket in include/rf_api.h)
+__device__ __forceinline__ int64_t hash_bucket_dev(uint64_t k0, uint64_t k1, const uint8_t* p, int n,
+                                                   int64_t num_bins, int mask_empty) {
+    if (mask_empty) {
+        if (n == 0) return 0;
+        if (num_bins > 1) return 1 + (int64_t)(siphash24_dev(k0, k1, p, n) % (uint64_t)(num_bins - 1));
+    }
+    return (int64_t)(siphash24_dev(k0, k1, p, n) % (uint64_t)num_bins);
+}
+
+// Two SipHash-2-4 states over ONE read of the token: keys (s0,s0) and (s1,s1) — the two Hashing
+// layers of DoubleHashingEmbedding (preprocess_layers.py:89-90) hash the same bytes.
+__device__ __forceinline__ void siphash24x2_dev(uint64_t s0, uint64_t s1, const uint8_t* p, int n, uint64_t& h0,
+                                                uint64_t& h1) {
+    uint64_t a0 = 0x736f6d6570736575ULL ^ s0, a1 = 0x646f72616e646f6dULL ^ s0;
+    uint64_t a2 = 0x6c7967656e657261ULL ^ s0, a3 = 0x7465646279746573ULL ^ s0;
+    uint64_t b0 = 0x736f6d6570736575ULL ^ s1, b1 = 0x646f72616e646f6dULL ^ s1;
+    uint64_t b2 = 0x6c7967656e657261ULL ^ s1, b3 = 0x7465646279746573ULL ^ s1;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a - sh);
+    const int nwords = n > 0 ? (int)((sh + (uint32_t)n + 3) >> 2) : 0;
+    auto msg32 = [&](int j) -> uint32_t {
+        uint32_t lo = j < nwords ? w[j] : 0u;
+        uint32_t hi = (j + 1) < nwords ? w[j + 1] : 0u;
+        return sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    };
+#define RF_SIPROUND2                                                                                 \
+    do {                                                                                             \
+        uint64_t v0 = a0, v1 = a1, v2 = a2, v3 = a3;                                                 \
+        RF_SIPROUND;                                                                                 \
+        a0 = v0; a1 = v1; a2 = v2; a3 = v3;                                                          \
+        v0 = b0; v1 = b1; v2 = b2; v3 = b3;                                                          \
+        RF_SIPROUND;                                                                                 \
+        b0 = v0; b1 = v1; b2 = v2; b3 = v3;                                                          \
+    } while (0)
+    const int nb = n >> 3;
+    for (int i = 0; i < nb; ++i) {
+        const uint64_t m = (uint64_t)msg32(2 * i) | ((uint64_t)msg32(2 * i + 1) << 32);
+        a3 ^= m; b3 ^= m;
+        RF_SIPROUND2;
+        RF_SIPROUND2;
+        a0 ^= m; b0 ^= m;
+    }
+    const int r = n & 7;
+    uint64_t tail = 0;
+    if (r) {
+        tail = (uint64_t)msg32(2 * nb) | ((uint64_t)msg32(2 * nb + 1) << 32);
+        tail &= (~0ULL) >> (64 - 8 * r);
+    }
+    const uint64_t bl = ((uint64_t)(uint32_t)n << 56) | tail;
+    a3 ^= bl; b3 ^= bl;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+    a0 ^= bl; b0 ^= bl;
+    a2 ^= 0xff; b2 ^= 0xff;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+#undef RF_SIPROUND2
+    h0 = a0 ^ a1 ^ a2 ^ a3;
+    h1 = b0 ^ b1 ^ b2 ^ b3;
+}
+
+__device__ __forceinline__ int64_t bucket_from_hash(uint64_t h, int n, int64_t num_bins, int mask_empty) {
+    if (mask_empty) {
+        if (n == 0) return 0;
+        if (num_bins > 1) return 1 + (int64_t)(h % (uint64_t)(num_bins - 1));
+    }
+    return (int64_t)(h % (uint64_t)num_bins);
+}
+
+__device__ __forceinline__ uint64_t splitmix64_dev(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}

@@ -1,0 +1,307 @@
+// rf_dense.hip — the interaction-MLP scorer on gfx950 (create_mlp, backend/blocks/mlp.py:4-15):
+//   rf_norm_fwd    LayerNormalization / BatchNormalization(inference) -> bf16 (or f32) GEMM operand
+//   rf_linear_fwd  Dense: y = act(x @ W + b)
+//       * bf16 x/W: v_mfma_f32_16x16x32_bf16, 128x128x64 block tile, 4 waves of 64x64, double-buffered LDS
+//       * f32  x/W: v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate), 128x128x32 tile
+//       * N <= 16 or softmax heads (Dense(2, softmax), esim.py:53): one wave per row, fp32 dot + row softmax
+//     bias + activation (gelu(erf) / relu / selu / softmax) fused in the epilogue.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "rf_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float act_apply(int act, float x) {
+    switch (act) {
+        case RF_ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+        case RF_ACT_RELU: return x > 0.f ? x : 0.f;
+        case RF_ACT_SELU: {
+            const float alpha = 1.6732632423543772848170429916717f, scale = 1.0507009873554804934193349852946f;
+            return x > 0.f ? scale * x : scale * alpha * (expf(x) - 1.0f);
+        }
+        default: return x;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// row normalisation: one wave per row
+// ---------------------------------------------------------------------------------------------
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void norm_kernel(const float* __restrict__ x, int64_t rows, int cols, int64_t ldx,
+                                                   int mode, float eps, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, const float* __restrict__ mean,
+                                                   const float* __restrict__ var, void* __restrict__ y, int64_t ldy) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + row * ldx;
+    float mu = 0.f, rstd = 1.f;
+    if (mode == 0) {
+        float s = 0.f;
+        for (int c = lane; c < cols; c += 64) s += xr[c];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        mu = s / (float)cols;
+        float v = 0.f;
+        for (int c = lane; c < cols; c += 64) {
+            const float dlt = xr[c] - mu;
+            v += dlt * dlt;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        rstd = 1.0f / sqrtf(v / (float)cols + eps);
+    }
+    for (int c = lane; c < cols; c += 64) {
+        float o;
+        if (mode == 0)
+            o = (xr[c] - mu) * rstd * (gamma ? gamma[c] : 1.f) + (beta ? beta[c] : 0.f);
+        else
+            o = (xr[c] - mean[c]) / sqrtf(var[c] + eps) * (gamma ? gamma[c] : 1.f) + (beta ? beta[c] : 0.f);
+        if constexpr (OUT_BF16)
+            reinterpret_cast<uint16_t*>(y)[row * ldy + c] = (uint16_t)f32_to_bf16_bits(o);
+        else
+            reinterpret_cast<float*>(y)[row * ldy + c] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// GEMM y[M,N] = act(x[M,K] W[N,K]^T + b)
+// ---------------------------------------------------------------------------------------------
+constexpr int BM = 128, BN = 128;
+
+// bf16: BK = 64 (128-byte rows), LDS rows padded to 72 elements (144 B): conflict-free ds_read_b128
+// for the 16 rows a 16-lane group reads.
+constexpr int BKH = 64, RSH = BKH + 8;
+// f32: BK = 32 (128-byte rows), rows padded to 36 floats (144 B).
+constexpr int BKF = 32, RSF = BKF + 4;
+
+template <bool BF16>
+struct GemmCfg {
+    static constexpr int BK = BF16 ? BKH : BKF;
+    static constexpr int RS = BF16 ? RSH : RSF;          // elements
+    static constexpr int ESZ = BF16 ? 2 : 4;
+    static constexpr int EPC = 16 / ESZ;                  // elements per 16-byte chunk
+    static constexpr int CPR = BK / EPC;                  // chunks per tile row (8)
+    static constexpr int CHUNKS = BM * CPR;               // per operand tile (1024)
+    static constexpr int PER_THREAD = CHUNKS / 256;       // 4
+};
+
+template <bool BF16>
+__device__ __forceinline__ void load_tile(uint4 (&rg)[2][GemmCfg<BF16>::PER_THREAD], const char* __restrict__ x,
+                                          const char* __restrict__ w, int64_t M, int N, int K, int64_t ldx, int64_t m0,
+                                          int n0, int k0, int tid) {
+    using C = GemmCfg<BF16>;
+#pragma unroll
+    for (int i = 0; i < C::PER_THREAD; ++i) {
+        const int c = tid + i * 256;
+        const int r = c / C::CPR, ch = c - r * C::CPR;
+        const int kk = k0 + ch * C::EPC;
+        uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+        if (m0 + r < M && kk < K) va = *reinterpret_cast<const uint4*>(x + ((m0 + r) * ldx + kk) * C::ESZ);
+        if (n0 + r < N && kk < K) vb = *reinterpret_cast<const uint4*>(w + ((int64_t)(n0 + r) * K + kk) * C::ESZ);
+        rg[0][i] = va;
+        rg[1][i] = vb;
+    }
+}
+
+template <bool BF16>
+__device__ __forceinline__ void store_tile(char* __restrict__ As, char* __restrict__ Bs,
+                                           const uint4 (&rg)[2][GemmCfg<BF16>::PER_THREAD], int tid) {
+    using C = GemmCfg<BF16>;
+#pragma unroll
+    for (int i = 0; i < C::PER_THREAD; ++i) {
+        const int c = tid + i * 256;
+        const int r = c / C::CPR, ch = c - r * C::CPR;
+        *reinterpret_cast<uint4*>(As + (r * C::RS + ch * C::EPC) * C::ESZ) = rg[0][i];
+        *reinterpret_cast<uint4*>(Bs + (r * C::RS + ch * C::EPC) * C::ESZ) = rg[1][i];
+    }
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
+                                                   const float* __restrict__ bias, float* __restrict__ y, int64_t M,
+                                                   int N, int K, int64_t ldx, int64_t ldy, int act) {
+    using C = GemmCfg<BF16>;
+    __shared__ __attribute__((aligned(16))) char smem[2][2][BM * C::RS * C::ESZ];
+    const char* x = reinterpret_cast<const char*>(xv);
+    const char* w = reinterpret_cast<const char*>(wv);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-aware tile order: consecutive tiles of one M row-panel on one XCD (guide T1)
+    const int tiles_n = (N + BN - 1) / BN;
+    const int64_t tid_lin = blockIdx.x;
+    const int64_t m0 = (tid_lin / tiles_n) * BM;
+    const int n0 = (int)(tid_lin % tiles_n) * BN;
+    f4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    uint4 rg[2][C::PER_THREAD];
+    const int nk = (K + C::BK - 1) / C::BK;
+    load_tile<BF16>(rg, x, w, M, N, K, ldx, m0, n0, 0, tid);
+    store_tile<BF16>(smem[0][0], smem[0][1], rg, tid);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) load_tile<BF16>(rg, x, w, M, N, K, ldx, m0, n0, (kt + 1) * C::BK, tid);
+        const char* As = smem[cur][0];
+        const char* Bs = smem[cur][1];
+        if constexpr (BF16) {
+#pragma unroll
+            for (int ks = 0; ks < C::BK; ks += 32) {
+                bf16x8 af[4], bfr[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    af[i] = *reinterpret_cast<const bf16x8*>(As + ((wm * 64 + i * 16 + lr) * C::RS + ks + lg * 8) * 2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ((wn * 64 + j * 16 + lr) * C::RS + ks + lg * 8) * 2);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+            // 16x16x4 f32: lane (lr, lg) supplies A[lr][k], B[k][lr] for k = lg*8 + s at step s (the k order is
+            // permuted consistently for A and B, so the dot product is over all 32 k of the tile)
+            f4 a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float* p = reinterpret_cast<const float*>(As) + (wm * 64 + i * 16 + lr) * C::RS + lg * 8;
+                a0[i] = *reinterpret_cast<const f4*>(p);
+                a1[i] = *reinterpret_cast<const f4*>(p + 4);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float* p = reinterpret_cast<const float*>(Bs) + (wn * 64 + j * 16 + lr) * C::RS + lg * 8;
+                b0[j] = *reinterpret_cast<const f4*>(p);
+                b1[j] = *reinterpret_cast<const f4*>(p + 4);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float av = s < 4 ? a0[i][s] : a1[i][s - 4];
+                        const float bv = s < 4 ? b0[j][s] : b1[j][s - 4];
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
+                    }
+        }
+        if (kt + 1 < nk) store_tile<BF16>(smem[cur ^ 1][0], smem[cur ^ 1][1], rg, tid);
+        __syncthreads();
+    }
+    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + lr;
+        if (col >= N) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * 64 + i * 16 + lg * 4 + r;
+                if (row < M) y[row * ldy + col] = act_apply(act, acc[i][j][r] + bv);
+            }
+    }
+}
+
+// small-N head: one wave per row, fp32 dot products, optional row softmax (N <= 64)
+template <bool BF16>
+__global__ __launch_bounds__(256) void small_n_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
+                                                      const float* __restrict__ bias, float* __restrict__ y, int64_t M,
+                                                      int N, int K, int64_t ldx, int64_t ldy, int act) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    float outv[64];
+    float mx = -INFINITY;
+    for (int n = 0; n < N && n < 64; ++n) {
+        float s = 0.f;
+        for (int k = lane; k < K; k += 64) {
+            float xv_, wv_;
+            if constexpr (BF16) {
+                xv_ = bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(xv)[row * ldx + k]);
+                wv_ = bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(wv)[(int64_t)n * K + k]);
+            } else {
+                xv_ = reinterpret_cast<const float*>(xv)[row * ldx + k];
+                wv_ = reinterpret_cast<const float*>(wv)[(int64_t)n * K + k];
+            }
+            s = fmaf(xv_, wv_, s);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        s += bias ? bias[n] : 0.f;
+        outv[n] = act == RF_ACT_SOFTMAX ? s : act_apply(act, s);
+        mx = fmaxf(mx, outv[n]);
+    }
+    if (act == RF_ACT_SOFTMAX) {
+        float sum = 0.f;
+        for (int n = 0; n < N; ++n) {
+            outv[n] = expf(outv[n] - mx);
+            sum += outv[n];
+        }
+        for (int n = 0; n < N; ++n) outv[n] /= sum;
+    }
+    if (lane == 0)
+        for (int n = 0; n < N; ++n) y[row * ldy + n] = outv[n];
+}
+
+}  // namespace
+
+extern "C" int rf_norm_fwd(const float* x, int64_t rows, int32_t cols, int64_t ldx, int32_t mode, float eps,
+                           const float* gamma, const float* beta, const float* mean, const float* var, void* y,
+                           int32_t y_dtype, int64_t ldy, void* stream) {
+    RF_REQUIRE(mode == 0 || mode == 1, "rf_norm_fwd: mode must be 0 (LayerNorm) or 1 (BatchNorm)");
+    RF_REQUIRE(y_dtype == RF_DTYPE_BF16 || y_dtype == RF_DTYPE_F32, "rf_norm_fwd: y dtype must be BF16 or F32");
+    RF_REQUIRE(rows >= 0 && cols > 0 && ldx >= cols && ldy >= cols, "rf_norm_fwd: bad shape");
+    RF_REQUIRE(mode == 0 || (mean && var), "rf_norm_fwd: BatchNorm needs running mean/var");
+    if (rows == 0) return RF_OK;
+    RF_REQUIRE(x && y, "rf_norm_fwd: null pointer");
+    const unsigned grid = (unsigned)((rows + 3) / 4);
+    if (y_dtype == RF_DTYPE_BF16)
+        hipLaunchKernelGGL(norm_kernel<true>, dim3(grid), dim3(256), 0, rf_stream(stream), x, rows, cols, ldx, mode,
+                           eps, gamma, beta, mean, var, y, ldy);
+    else
+        hipLaunchKernelGGL(norm_kernel<false>, dim3(grid), dim3(256), 0, rf_stream(stream), x, rows, cols, ldx, mode,
+                           eps, gamma, beta, mean, var, y, ldy);
+    return rf_check_launch("norm_kernel");
+}
+
+extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,
+                             int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream) {
+    RF_REQUIRE(x_dtype == RF_DTYPE_BF16 || x_dtype == RF_DTYPE_F32, "rf_linear_fwd: x dtype must be BF16 or F32");
+    RF_REQUIRE(act >= RF_ACT_NONE && act <= RF_ACT_SOFTMAX, "rf_linear_fwd: unknown activation %d", act);
+    RF_REQUIRE(M >= 0 && K > 0 && N > 0 && ldx >= K && ldy >= N, "rf_linear_fwd: bad shape");
+    RF_REQUIRE(act != RF_ACT_SOFTMAX || N <= 64, "rf_linear_fwd: softmax head needs N <= 64");
+    const int epc = x_dtype == RF_DTYPE_BF16 ? 8 : 4;
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && W && y, "rf_linear_fwd: null pointer");
+    hipStream_t st = rf_stream(stream);
+    const bool bf = x_dtype == RF_DTYPE_BF16;
+    if (N <= 16 || act == RF_ACT_SOFTMAX) {
+        const unsigned grid = (unsigned)((M + 3) / 4);
+        if (bf)
+            hipLaunchKernelGGL(small_n_kernel<true>, dim3(grid), dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+        else
+            hipLaunchKernelGGL(small_n_kernel<false>, dim3(grid), dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+        return rf_check_launch("small_n_kernel");
+    }
+    RF_REQUIRE(K % epc == 0 && ldx % epc == 0, "rf_linear_fwd: K and ldx must be multiples of %d (16-byte rows)", epc);
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0, "rf_linear_fwd: x/W must be 16-byte aligned");
+    const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_linear_fwd: too many tiles");
+    if (bf)
+        hipLaunchKernelGGL(gemm_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+    else
+        hipLaunchKernelGGL(gemm_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+    return rf_check_launch("gemm_kernel");
+}

@@ -1,0 +1,112 @@
+"""ctypes binding of librf.so (include/rf_api.h).
+
+The product path has NO fallback: if the library is missing or no GPU is visible, every operator
+raises. Build the library with ``python -c "import __graft_entry__ as g; g.build()"`` (or
+``make -C recommendflow_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "librf.so"))
+
+RF_OK, RF_EINVAL, RF_EHIP, RF_EOOB = 0, -1, -2, -3
+DT_F32, DT_BF16, DT_F16 = 0, 1, 2
+COMB = {"sum": 0, "avg": 1, "max": 2, "min": 3, "first": 4, "last": 5, "null": 6, "cls": 4}
+FLAG_MASK_PADDING, FLAG_EMIT_IDX = 0x1, 0x2
+ACT = {None: 0, "none": 0, "linear": 0, "gelu": 1, "relu": 2, "selu": 3, "softmax": 4}
+
+_lock = threading.Lock()
+_lib = None
+
+_i32, _i64, _u64, _vp, _f32 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_float
+_SIGS = {
+    "rf_abi_version": (_i32, []),
+    "rf_last_error": (ctypes.c_char_p, []),
+    "rf_siphash_bucket": (ctypes.c_int, [_vp, _vp, _i64, _u64, _u64, _i64, _i32, _vp, _vp]),
+    "rf_fused_hash_embed_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i32, _i64, _i32, _vp, _i32, _i64, _i32, _vp, _vp]),
+    "rf_embedding_bag_fwd": (ctypes.c_int, [_vp, _i32, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _vp, _i32, _i64, _i64, _vp]),
+    "rf_table_init_uniform": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _u64, _f32, _f32, _vp]),
+    "rf_esim_soft_attention_fwd": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
+    "rf_norm_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _vp]),
+    "rf_linear_fwd": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
+    "rf_sdpa_fwd": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "rf_bucketize_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
+    "rf_bucketize_owner": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "rf_gather_rows": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i64, _i32, _vp, _vp]),
+}
+EXPORTED = tuple(_SIGS)
+
+
+class RFError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load librf.so (no GPU needed to load). Raises RFError if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RFError(f"librf.so not found at {path}: build it first (make -C recommendflow_amd/csrc)")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.rf_abi_version() != 1:
+            raise RFError(f"librf.so ABI version {lib.rf_abi_version()} != 1")
+        _lib = lib
+        return lib
+
+
+def require_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        raise RFError("recommendflow_amd operators need a ROCm GPU (torch.cuda.is_available() is False); "
+                      "there is no CPU fallback")
+
+
+def check(rc: int, what: str):
+    if rc != RF_OK:
+        msg = load().rf_last_error().decode(errors="replace")
+        kind = {RF_EINVAL: "invalid argument", RF_EHIP: "HIP error", RF_EOOB: "out of range"}.get(rc, str(rc))
+        if rc == RF_EINVAL:
+            raise ValueError(f"{what}: {kind}: {msg}")
+        raise RFError(f"{what}: {kind}: {msg}")
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    return None if t is None else int(t.data_ptr())
+
+
+def call(name: str, *args):
+    fn = getattr(load(), name)
+    rc = fn(*args)
+    check(rc, name)
+    return rc
+
+
+def torch_dtype_code(dtype) -> int:
+    import torch
+
+    if dtype == torch.float32:
+        return DT_F32
+    if dtype == torch.bfloat16:
+        return DT_BF16
+    if dtype == torch.float16:
+        return DT_F16
+    raise ValueError(f"unsupported dtype {dtype}")

@@ -1,0 +1,119 @@
+"""GPU parity of the dense stages (ESIM soft attention + pooling, Dense/LN/BN MLP, masked SDPA) against
+the float64 numpy oracle. Tolerances (stated per test) follow from the MFMA operand rounding:
+bf16 operands carry 2^-8 relative error, f16 2^-11; exact-fp32 MFMA ~1e-6 relative."""
+import numpy as np
+import pytest
+import torch
+
+from recommendflow_amd.backend.blocks.mlp import create_mlp
+from recommendflow_amd.backend.layers.attention_layers import MultiHeadAttention, SoftAttention, esim_soft_attention_pool
+from recommendflow_amd.backend.layers.core import BatchNormalization, Dense, LayerNormalization
+from recommendflow_amd.backend.layers.layer_utils import scaled_dot_product_attention
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(shape, seed, scale=1.0, dtype=torch.bfloat16):
+    g = torch.Generator().manual_seed(seed)
+    return ((torch.rand(shape, generator=g) * 2 - 1) * scale).to(dtype)
+
+
+@pytest.mark.parametrize("L,d", [(1, 64), (7, 64), (16, 128), (33, 128), (100, 128), (128, 64)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_esim_pool_vs_oracle(O, cuda, L, d, dt):
+    B = 9
+    # embedding-like magnitudes (pooled hash embeddings sum 2 rows of U(-0.05, 0.05)) and a larger case
+    for scale in (0.1, 2.0):
+        q, a = rnd((B, L, d), L * 7 + d, scale, dt), rnd((B, L, d), L * 11 + d + 1, scale, dt)
+        att = torch.empty((B, 2, L, d), device="cuda")
+        got = esim_soft_attention_pool(q.cuda(), a.cuda(), att_out=att).cpu().numpy()
+        want = O.esim_pool(q.float().numpy(), a.float().numpy())
+        aq, aa = O.soft_attention(q.float().numpy(), a.float().numpy())
+        # P is rounded once to the MFMA dtype: |d att| <= 2^-8 * max|v| (bf16), sums of 4L terms / 4L
+        tol = (2 ** -7 if dt == torch.bfloat16 else 2 ** -10) * scale
+        np.testing.assert_allclose(att[:, 0].cpu().numpy(), aq, atol=tol, rtol=0)
+        np.testing.assert_allclose(att[:, 1].cpu().numpy(), aa, atol=tol, rtol=0)
+        np.testing.assert_allclose(got, want, atol=tol * (scale + 1), rtol=0)
+
+
+def test_esim_strided_views(O, cuda):
+    """q and a as slices of one [B, 200, 128] token tensor (cfg3: 100 user + 100 ad slots)."""
+    x = rnd((6, 200, 128), 5, 0.1).cuda()
+    got = esim_soft_attention_pool(x[:, :100], x[:, 100:]).cpu().numpy()
+    xf = x.float().cpu().numpy()
+    want = O.esim_pool(xf[:, :100], xf[:, 100:])
+    np.testing.assert_allclose(got, want, atol=2e-3, rtol=0)
+
+
+def test_soft_attention_api(O, cuda):
+    q, a = rnd((3, 10, 64), 1, 0.5), rnd((3, 10, 64), 2, 0.5)
+    aq, aa = SoftAttention()([q.cuda(), a.cuda()])
+    wq, wa = O.soft_attention(q.float().numpy(), a.float().numpy())
+    np.testing.assert_allclose(aq.cpu().numpy(), wq, atol=4e-3)
+    np.testing.assert_allclose(aa.cpu().numpy(), wa, atol=4e-3)
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 16, 256), (129, 64, 130), (256, 1280, 1024), (300, 512, 2), (64, 8704, 48)])
+@pytest.mark.parametrize("act", [None, "gelu", "relu", "selu", "softmax"])
+def test_dense_bf16(O, cuda, M, K, N, act):
+    if act == "softmax" and N > 64:
+        pytest.skip("softmax head needs N <= 64")
+    x = rnd((M, K), M + K, 1.0)
+    dense = Dense(K, N, activation=act, dtype=torch.bfloat16, seed=N)
+    y = dense(x.cuda()).cpu().numpy()
+    W = dense.weight.float().cpu().numpy()
+    want = O.activation(x.float().numpy().astype(np.float64) @ W.T.astype(np.float64) + dense.bias.cpu().numpy(), act)
+    # operands are exact in bf16; only fp32 accumulation error remains: ~K * 2^-24 * sum|xw|
+    bound = 1e-5 * np.abs(x.float().numpy()) @ np.abs(W.T) + 1e-6
+    np.testing.assert_array_less(np.abs(y - want), bound * 4 + 1e-5)
+
+
+@pytest.mark.parametrize("M,K,N", [(100, 32, 64), (257, 8704, 1024), (64, 20480, 256)])
+def test_dense_fp32_exact_mfma(O, cuda, M, K, N):
+    """cfg2 towers run in fp32 (the reference's dtype): rtol 1e-5 / atol 1e-6 vs float64."""
+    x = rnd((M, K), K, 0.5, torch.float32)
+    dense = Dense(K, N, activation="selu", dtype=torch.float32, seed=1)
+    y = dense(x.cuda()).cpu().numpy()
+    W = dense.weight.cpu().numpy().astype(np.float64)
+    want = O.activation(x.numpy().astype(np.float64) @ W.T, "selu")
+    np.testing.assert_allclose(y, want, rtol=1e-5, atol=1e-6 * np.sqrt(K))
+
+
+@pytest.mark.parametrize("norm", ["ln", "bn"])
+def test_create_mlp(O, cuda, norm):
+    spec = LayerNormalization(epsilon=1e-6) if norm == "ln" else BatchNormalization(epsilon=1e-6)
+    mlp = create_mlp([256, 128], 0.3, "gelu" if norm == "ln" else "selu", spec, in_features=200,
+                     dtype=torch.float32, seed=3)
+    x = rnd((50, 200), 9, 1.0, torch.float32)
+    y = mlp(x.cuda()).cpu().numpy()
+    layers = []
+    for nm, dn in zip(mlp.norms, mlp.denses):
+        layers.append({"W": dn.weight.cpu().numpy().T, "b": dn.bias.cpu().numpy(), "gamma": nm.gamma.cpu().numpy(),
+                       "beta": nm.beta.cpu().numpy(), "mean": None if nm.mean is None else nm.mean.cpu().numpy(),
+                       "var": None if nm.var is None else nm.var.cpu().numpy()})
+    want = O.mlp(x.numpy(), layers, "gelu" if norm == "ln" else "selu", norm)
+    np.testing.assert_allclose(y, want, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("Lq,Lk,depth,heads", [(10, 10, 64, 2), (100, 100, 32, 4), (37, 200, 128, 1), (1, 5, 64, 3)])
+def test_sdpa_masked_rows(O, cuda, Lq, Lk, depth, heads):
+    B = 3
+    q, k, v = (rnd((B, L_, heads * depth), s, 1.0, torch.float16) for s, L_ in ((1, Lq), (2, Lk), (3, Lk)))
+    mask = (torch.rand(B, Lq, generator=torch.Generator().manual_seed(4)) > 0.3).float()
+    got = scaled_dot_product_attention(q.cuda(), k.cuda(), v.cuda(), mask.cuda(), heads=heads).cpu().numpy()
+    qs = q.float().numpy().reshape(B, Lq, heads, depth).transpose(0, 2, 1, 3)
+    ks = k.float().numpy().reshape(B, Lk, heads, depth).transpose(0, 2, 1, 3)
+    vs = v.float().numpy().reshape(B, Lk, heads, depth).transpose(0, 2, 1, 3)
+    m = np.broadcast_to(mask.numpy()[:, None, :], (B, heads, Lq))
+    want = O.sdpa(qs, ks, vs, m).transpose(0, 2, 1, 3).reshape(B, Lq, heads * depth)
+    np.testing.assert_allclose(got, want, atol=3e-3, rtol=0)
+    # fully masked query rows are uniform over the keys (the -4294967295 fill, A.9)
+    b, i = np.argwhere(mask.numpy() == 0)[0]
+    np.testing.assert_allclose(got[b, i], vs[b].mean(axis=1).reshape(-1), atol=2e-3)
+
+
+def test_multi_head_attention_api(O, cuda):
+    mha = MultiHeadAttention(128, 4, seed=2)
+    x = rnd((2, 20, 128), 8, 1.0, torch.float32).cuda()
+    out = mha.call(x, x, x, None)
+    assert tuple(out.shape) == (2, 20, 128) and torch.isfinite(out).all()
