@@ -16,308 +16,10 @@
 #include <algorithm>
 #include <cmath>
 
-#include "rf_common.h"
+#include "rf_fused.h"
 
 namespace {
-
-constexpr int kWaves = 4;    // waves per workgroup
-constexpr int kCap = 256;    // tokens per wave item kept in the LDS index bucket
-constexpr int kUnits = 64;   // (example, slot) units per wave item
-
-template <typename T>
-struct Elem {
-    static constexpr int EPV = 16 / (int)sizeof(T);  // elements per 16-byte chunk
-};
-
-template <typename TT>
-__device__ __forceinline__ void unpack16(const uint4& v, float* f) {
-    if constexpr (sizeof(TT) == 4) {
-        f[0] = __uint_as_float(v.x);
-        f[1] = __uint_as_float(v.y);
-        f[2] = __uint_as_float(v.z);
-        f[3] = __uint_as_float(v.w);
-    } else {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            f[2 * i] = bf16_bits_to_f32(w[i] & 0xffffu);
-            f[2 * i + 1] = bf16_bits_to_f32(w[i] >> 16);
-        }
-    }
-}
-
-template <typename OT, int EPV>
-__device__ __forceinline__ void store_chunk(OT* dst, const float* f) {
-    if constexpr (sizeof(OT) == 4) {
-#pragma unroll
-        for (int i = 0; i < EPV; i += 4)
-            *reinterpret_cast<float4*>(dst + i) = make_float4(f[i], f[i + 1], f[i + 2], f[i + 3]);
-    } else {
-        uint32_t w[EPV / 2];
-#pragma unroll
-        for (int i = 0; i < EPV / 2; ++i) w[i] = f32_to_bf16_bits(f[2 * i]) | (f32_to_bf16_bits(f[2 * i + 1]) << 16);
-        if constexpr (EPV == 4)
-            *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
-        else
-            *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-}
-
-__device__ __forceinline__ uint4 nan_chunk() {
-    const uint32_t q = 0x7fc07fc0u;  // NaN as f32 and as a bf16 pair
-    return make_uint4(q, q, q, q);
-}
-
-template <typename TT>
-__device__ __forceinline__ uint4 load_chunk(const TT* __restrict__ table, int64_t row, int64_t table_rows, int dim,
-                                            int c) {
-    constexpr int EPV = Elem<TT>::EPV;
-    if (row < 0 || row >= table_rows) return nan_chunk();
-    return *reinterpret_cast<const uint4*>(table + row * (int64_t)dim + (int64_t)c * EPV);
-}
-
-__device__ __forceinline__ float comb_init(int comb) {
-    return comb == RF_COMB_MAX ? -INFINITY : comb == RF_COMB_MIN ? INFINITY : 0.0f;
-}
-
-__device__ __forceinline__ float comb_step(int comb, float a, float v) {
-    // sum/avg: one fp32 add per position in order (no fma, no reassociation)
-    return comb == RF_COMB_MAX ? (v > a ? v : a) : comb == RF_COMB_MIN ? (v < a ? v : a) : __fadd_rn(a, v);
-}
-
-// ---------------------------------------------------------------------------------------------
-// fused multi-slot hash -> gather -> pool
-// ---------------------------------------------------------------------------------------------
-template <int LPR, int CPL, typename TT, typename OT>
-__global__ __launch_bounds__(kWaves * 64) void fused_hash_embed_kernel(
-    const rf_slot_desc* __restrict__ slots, int n_slots, const uint8_t* __restrict__ tok_bytes,
-    const int32_t* __restrict__ tok_off, const int32_t* __restrict__ bag_off, const int32_t* __restrict__ lmax,
-    int64_t n_units, const TT* __restrict__ table, int64_t table_rows, int dim, OT* __restrict__ out,
-    int64_t out_stride, int flags, int64_t* __restrict__ idx_out) {
-    constexpr int EPV = Elem<TT>::EPV;
-    constexpr int TEAMS = 64 / LPR;
-    constexpr int KPT = kUnits / TEAMS;  // units per team per item
-    __shared__ int32_t s_bin[kWaves][2][kCap];
-    __shared__ int32_t s_bag[kWaves][kUnits + 1];
-
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int team = lane / LPR, tl = lane % LPR;
-    const int nchunks = dim / EPV;
-    const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
-    const bool emit = (flags & RF_FLAG_EMIT_IDX) != 0 && idx_out != nullptr;
-    const int64_t n_items = (n_units + kUnits - 1) / kUnits;
-
-    for (int64_t item = (int64_t)blockIdx.x * kWaves + wave; item < n_items; item += (int64_t)gridDim.x * kWaves) {
-        const int64_t u0 = item * kUnits;
-        const int nu = (int)min((int64_t)kUnits, n_units - u0);
-        for (int i = lane; i <= nu; i += 64) s_bag[wave][i] = bag_off[u0 + i];
-        wave_lds_sync();
-        const int t0 = s_bag[wave][0];
-        const int ntok = s_bag[wave][nu] - t0;
-        const int nh = min(ntok, kCap);
-
-        // ---- phase 1: lane-per-token double hashing into the LDS bucket ----
-        for (int i = lane; i < nh; i += 64) {
-            const int t = t0 + i;
-            int lo = 0, hi = nu - 1;  // unit of token t: last j with s_bag[j] <= t
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (s_bag[wave][mid] <= t) lo = mid; else hi = mid - 1;
-            }
-            const int s = (int)((u0 + lo) % n_slots);
-            const rf_slot_desc* sd = slots + s;
-            const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
-            uint64_t h0, h1;
-            siphash24x2_dev(sd->salt[0], sd->salt[1], tok_bytes + b0, n, h0, h1);
-            const int64_t i0 = bucket_from_hash(h0, n, sd->num_bins, sd->mask_empty);
-            const int64_t i1 = bucket_from_hash(h1, n, sd->num_bins, sd->mask_empty);
-            s_bin[wave][0][i] = (int32_t)i0;
-            s_bin[wave][1][i] = (int32_t)i1;
-            if (emit) {
-                idx_out[2 * (int64_t)t] = i0;
-                idx_out[2 * (int64_t)t + 1] = i1;
-            }
-        }
-        wave_lds_sync();
-
-        // ---- phase 2: team-per-unit gather + pool ----
-        for (int kk = 0; kk < KPT; ++kk) {
-            const int j = team * KPT + kk;
-            if (j >= nu) break;
-            const int64_t u = u0 + j;
-            const int s = (int)(u % n_slots);
-            const int64_t b = u / n_slots;
-            const rf_slot_desc* sd = slots + s;
-            const int comb = sd->combiner;
-            const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1];
-            const int64_t nbins = sd->num_bins;
-            const int mask_empty = sd->mask_empty;
-            const int tb = s_bag[wave][j] - t0, len = s_bag[wave][j + 1] - s_bag[wave][j];
-            const int lm = lmax[s];
-            const int L = mask_pad ? len : max(lm, len);
-            OT* orow = out + b * out_stride + sd->out_off;
-            // poison rather than fault if the descriptor does not fit the table
-            const bool bad = rb0 < 0 || rb1 < 0 || rb0 + nbins > table_rows || rb1 + nbins > table_rows;
-            const int64_t trows = bad ? -1 : table_rows;
-
-            // token position -> fused-table row of table k
-            auto row_of = [&](int k, int l) -> int64_t {
-                const int i = tb + l;
-                int64_t bin;
-                if (i < kCap) {
-                    bin = s_bin[wave][k][i];
-                } else {  // bucket overflow (very long bags): hash inline
-                    const int t = t0 + i;
-                    const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
-                    uint64_t h0, h1;
-                    siphash24x2_dev(sd->salt[0], sd->salt[1], tok_bytes + b0, n, h0, h1);
-                    bin = bucket_from_hash(k ? h1 : h0, n, nbins, mask_empty);
-                    if (emit && tl == 0) idx_out[2 * (int64_t)t + k] = bin;
-                }
-                return (k ? rb1 : rb0) + bin;
-            };
-            // padded position (b"" after parse_example): bin 0 with mask_value="", else hash of b""
-            auto pad_row = [&](int k) -> int64_t {
-                if (mask_empty) return k ? rb1 : rb0;
-                const uint64_t h = siphash24_dev(sd->salt[k], sd->salt[k], tok_bytes, 0);
-                return (k ? rb1 : rb0) + (int64_t)(h % (uint64_t)nbins);
-            };
-
-            if (comb == RF_COMB_NULL) {
-                const int Lo = lm;  // output positions are fixed by the batch max
-                for (int l = 0; l < Lo; ++l) {
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const bool real = l < len;
-                        const int64_t r = real ? row_of(k, l) : pad_row(k);
-#pragma unroll
-                        for (int cc = 0; cc < CPL; ++cc) {
-                            const int c = tl + cc * LPR;
-                            if (c >= nchunks) continue;
-                            float f[EPV];
-                            if (!real && mask_pad) {
-#pragma unroll
-                                for (int e = 0; e < EPV; ++e) f[e] = 0.0f;
-                            } else {
-                                unpack16<TT>(load_chunk(table, r, trows, dim, c), f);
-                            }
-                            store_chunk<OT, EPV>(orow + ((int64_t)k * Lo + l) * dim + c * EPV, f);
-                        }
-                    }
-                }
-                continue;
-            }
-
-            float acc[2][CPL][EPV];
-            if (comb == RF_COMB_FIRST || comb == RF_COMB_LAST) {
-                const int p = comb == RF_COMB_FIRST ? 0 : L - 1;
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int64_t r = L == 0 ? -1 : (p < len ? row_of(k, p) : pad_row(k));
-#pragma unroll
-                    for (int cc = 0; cc < CPL; ++cc) {
-                        const int c = tl + cc * LPR;
-                        if (L == 0 || c >= nchunks) {
-#pragma unroll
-                            for (int e = 0; e < EPV; ++e) acc[k][cc][e] = 0.0f;
-                        } else {
-                            unpack16<TT>(load_chunk(table, r, trows, dim, c), acc[k][cc]);
-                        }
-                    }
-                }
-            } else {
-                const float init = comb_init(comb);
-#pragma unroll
-                for (int k = 0; k < 2; ++k)
-#pragma unroll
-                    for (int cc = 0; cc < CPL; ++cc)
-#pragma unroll
-                        for (int e = 0; e < EPV; ++e) acc[k][cc][e] = init;
-                // real positions, 4 in flight per table
-                for (int l = 0; l < len; l += 4) {
-                    uint4 v[4][2][CPL];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (l + q < len) {
-#pragma unroll
-                            for (int k = 0; k < 2; ++k) {
-                                const int64_t r = row_of(k, l + q);
-#pragma unroll
-                                for (int cc = 0; cc < CPL; ++cc) {
-                                    const int c = tl + cc * LPR;
-                                    v[q][k][cc] = c < nchunks ? load_chunk(table, r, trows, dim, c) : make_uint4(0, 0, 0, 0);
-                                }
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (l + q < len) {
-#pragma unroll
-                            for (int k = 0; k < 2; ++k)
-#pragma unroll
-                                for (int cc = 0; cc < CPL; ++cc) {
-                                    float f[EPV];
-                                    unpack16<TT>(v[q][k][cc], f);
-#pragma unroll
-                                    for (int e = 0; e < EPV; ++e) acc[k][cc][e] = comb_step(comb, acc[k][cc][e], f[e]);
-                                }
-                        }
-                    }
-                }
-                // padding positions len..L-1 (reference parity): row pad, added one position at a time
-                const int npad = L - len;
-                if (npad > 0) {
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const int64_t r = pad_row(k);
-#pragma unroll
-                        for (int cc = 0; cc < CPL; ++cc) {
-                            const int c = tl + cc * LPR;
-                            if (c >= nchunks) continue;
-                            float f[EPV];
-                            unpack16<TT>(load_chunk(table, r, trows, dim, c), f);
-                            if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) {
-#pragma unroll
-                                for (int e = 0; e < EPV; ++e) acc[k][cc][e] = comb_step(comb, acc[k][cc][e], f[e]);
-                            } else {
-                                for (int p = 0; p < npad; ++p)
-#pragma unroll
-                                    for (int e = 0; e < EPV; ++e) acc[k][cc][e] = __fadd_rn(acc[k][cc][e], f[e]);
-                            }
-                        }
-                    }
-                }
-                if (comb == RF_COMB_AVG) {
-                    const float fl = (float)L;
-#pragma unroll
-                    for (int k = 0; k < 2; ++k)
-#pragma unroll
-                        for (int cc = 0; cc < CPL; ++cc)
-#pragma unroll
-                            for (int e = 0; e < EPV; ++e) acc[k][cc][e] = __fdiv_rn(acc[k][cc][e], fl);
-                }
-                if (mask_pad && L == 0) {  // masked empty bag -> zeros
-#pragma unroll
-                    for (int k = 0; k < 2; ++k)
-#pragma unroll
-                        for (int cc = 0; cc < CPL; ++cc)
-#pragma unroll
-                            for (int e = 0; e < EPV; ++e) acc[k][cc][e] = 0.0f;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 2; ++k)
-#pragma unroll
-                for (int cc = 0; cc < CPL; ++cc) {
-                    const int c = tl + cc * LPR;
-                    if (c < nchunks) store_chunk<OT, EPV>(orow + (int64_t)k * dim + c * EPV, acc[k][cc]);
-                }
-        }
-        wave_lds_sync();  // s_bag / s_bin are rewritten by the next item
-    }
-}
-
+using namespace rf;
 // ---------------------------------------------------------------------------------------------
 // EmbeddingBag over dense ids [batch][len]
 // ---------------------------------------------------------------------------------------------
@@ -496,36 +198,21 @@ extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_sl
     RF_REQUIRE(dim > 0 && dim % epv == 0, "rf_fused_hash_embed_fwd: dim (%d) must be a positive multiple of %d (16-byte rows chunks)", dim, epv);
     RF_REQUIRE(out_stride % epv == 0, "rf_fused_hash_embed_fwd: out_stride must be a multiple of %d", epv);
     RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)out & 15) == 0, "rf_fused_hash_embed_fwd: table/out must be 16-byte aligned");
-    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX)) == 0, "rf_fused_hash_embed_fwd: unknown flags");
+    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | 0x7f00)) == 0, "rf_fused_hash_embed_fwd: unknown flags");  // 0x7f00: reserved tuning/diagnostic bits
+    RF_REQUIRE(table_rows >= 1 && table_rows <= (int64_t)0xffffffff, "rf_fused_hash_embed_fwd: table_rows must be in [1, 2^32) (32-bit row ids in LDS)");
     const int64_t n_units = (int64_t)batch * n_slots;
     if (n_units == 0) return RF_OK;
     RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && lmax && table && out, "rf_fused_hash_embed_fwd: null pointer");
-    const int64_t items = (n_units + kUnits - 1) / kUnits;
-    const int grid = grid_for(items, kWaves, 256 * 8 * 2);
+    const int64_t items = (int64_t)n_slots * ((batch + kUnits - 1) / kUnits);  // slot-major items
+    const int grid = grid_for(items, kWaves, 256 * 32 * 2);
+    const int tune = (flags >> 8) & 0xf;  // reserved tuning bits: log2 of the max lanes per row (0 = default)
+    const int max_lpr = tune ? (1 << (tune - 1)) : kDefaultMaxLpr;
     hipStream_t st = rf_stream(stream);
-    return dispatch_lpr(dim / epv, [&](auto lpr, auto cpl) -> int {
-        constexpr int LPR = decltype(lpr)::value, CPL = decltype(cpl)::value;
-        if (table_dtype == RF_DTYPE_F32) {
-            if (out_dtype == RF_DTYPE_F32)
-                hipLaunchKernelGGL((fused_hash_embed_kernel<LPR, CPL, float, float>), dim3(grid), dim3(kWaves * 64), 0, st,
-                                   d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, (const float*)table,
-                                   table_rows, dim, (float*)out, out_stride, flags, idx_out);
-            else
-                hipLaunchKernelGGL((fused_hash_embed_kernel<LPR, CPL, float, uint16_t>), dim3(grid), dim3(kWaves * 64), 0, st,
-                                   d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, (const float*)table,
-                                   table_rows, dim, (uint16_t*)out, out_stride, flags, idx_out);
-        } else {
-            if (out_dtype == RF_DTYPE_F32)
-                hipLaunchKernelGGL((fused_hash_embed_kernel<LPR, CPL, uint16_t, float>), dim3(grid), dim3(kWaves * 64), 0, st,
-                                   d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, (const uint16_t*)table,
-                                   table_rows, dim, (float*)out, out_stride, flags, idx_out);
-            else
-                hipLaunchKernelGGL((fused_hash_embed_kernel<LPR, CPL, uint16_t, uint16_t>), dim3(grid), dim3(kWaves * 64), 0, st,
-                                   d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, (const uint16_t*)table,
-                                   table_rows, dim, (uint16_t*)out, out_stride, flags, idx_out);
-        }
-        return rf_check_launch("fused_hash_embed_kernel");
-    });
+    if (table_dtype == RF_DTYPE_F32)
+        return launch_fused_f32(d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table, table_rows, dim, out,
+                                out_dtype, out_stride, flags, idx_out, max_lpr, grid, st);
+    return launch_fused_bf16(d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table, table_rows, dim, out,
+                             out_dtype, out_stride, flags, idx_out, max_lpr, grid, st);
 }
 
 extern "C" int rf_embedding_bag_fwd(const int64_t* ids, int32_t batch, int32_t len, int64_t row_base, const void* table,

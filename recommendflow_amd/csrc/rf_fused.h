@@ -1,0 +1,455 @@
+// rf_fused.h — the fused multi-slot hash -> gather -> pool kernel (rf_fused_hash_embed_fwd), shared by the
+// per-table-dtype instantiation units rf_fused_f32.hip / rf_fused_bf16.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <type_traits>
+
+#include "rf_common.h"
+
+namespace rf {
+
+
+#ifndef RF_FUSED_WAVES
+#define RF_FUSED_WAVES 1
+#endif
+// waves per workgroup: items are wave-independent, and one-wave workgroups release their slots as soon
+// as their own item is done (a 4-wave workgroup holds its slots until the slowest of 4 items ends)
+constexpr int kWaves = RF_FUSED_WAVES;
+constexpr int kCap = 768;    // tokens per wave item kept in the LDS row bucket (more: hashed inline)
+constexpr int kUnits = 64;   // examples per wave item (one slot per item)
+constexpr int kDefaultMaxLpr = 16;  // lanes per row cap (tuned on MI355X)
+
+template <typename T>
+struct Elem {
+    static constexpr int EPV = 16 / (int)sizeof(T);  // elements per 16-byte chunk
+};
+
+template <typename TT>
+__device__ __forceinline__ void unpack16(const uint4& v, float* f) {
+    if constexpr (sizeof(TT) == 4) {
+        f[0] = __uint_as_float(v.x);
+        f[1] = __uint_as_float(v.y);
+        f[2] = __uint_as_float(v.z);
+        f[3] = __uint_as_float(v.w);
+    } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f[2 * i] = bf16_bits_to_f32(w[i] & 0xffffu);
+            f[2 * i + 1] = bf16_bits_to_f32(w[i] >> 16);
+        }
+    }
+}
+
+template <typename OT, int EPV>
+__device__ __forceinline__ void store_chunk(OT* dst, const float* f) {
+    if constexpr (sizeof(OT) == 4) {
+#pragma unroll
+        for (int i = 0; i < EPV; i += 4)
+            *reinterpret_cast<float4*>(dst + i) = make_float4(f[i], f[i + 1], f[i + 2], f[i + 3]);
+    } else {
+        uint32_t w[EPV / 2];
+#pragma unroll
+        for (int i = 0; i < EPV / 2; ++i) w[i] = f32_to_bf16_bits(f[2 * i]) | (f32_to_bf16_bits(f[2 * i + 1]) << 16);
+        if constexpr (EPV == 4)
+            *reinterpret_cast<uint2*>(dst) = make_uint2(w[0], w[1]);
+        else
+            *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+__device__ __forceinline__ uint4 nan_chunk() {
+    const uint32_t q = 0x7fc07fc0u;  // NaN as f32 and as a bf16 pair
+    return make_uint4(q, q, q, q);
+}
+
+template <typename TT>
+__device__ __forceinline__ uint4 load_chunk(const TT* __restrict__ table, int64_t row, int64_t table_rows, int dim,
+                                            int c) {
+    constexpr int EPV = Elem<TT>::EPV;
+    if (row < 0 || row >= table_rows) return nan_chunk();
+    return *reinterpret_cast<const uint4*>(table + row * (int64_t)dim + (int64_t)c * EPV);
+}
+
+__device__ __forceinline__ float comb_init(int comb) {
+    return comb == RF_COMB_MAX ? -INFINITY : comb == RF_COMB_MIN ? INFINITY : 0.0f;
+}
+
+__device__ __forceinline__ float comb_step(int comb, float a, float v) {
+    // sum/avg: one fp32 add per position in order (no fma, no reassociation)
+    return comb == RF_COMB_MAX ? (v > a ? v : a) : comb == RF_COMB_MIN ? (v < a ? v : a) : __fadd_rn(a, v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fused multi-slot hash -> gather -> pool
+// ---------------------------------------------------------------------------------------------
+// row r (already clamped into the table), 16-byte chunk c: no bounds branch on the hot path
+template <typename TT>
+__device__ __forceinline__ uint4 row_chunk(const TT* __restrict__ table, uint32_t r, int dim, int c) {
+    return *reinterpret_cast<const uint4*>(table + (int64_t)r * dim + (int64_t)c * Elem<TT>::EPV);
+}
+
+// Slot-major items: item = (slot s, examples b0 .. b0+kUnits-1). Every unit of an item shares the slot's
+// combiner, Lmax, salts, table segments and pad rows — all wave-uniform (scalar loads, one pad-row
+// prefetch per item) — and unit lengths follow one distribution, so the teams stay balanced.
+//  1a. lane j < nu reads unit j's token range; a wave prefix-scan lays the item's tokens out
+//      contiguously (item-local index i) in LDS;
+//  1b. lane-per-token: both SipHash-2-4 states over one read of the token, fused-table rows of both
+//      tables into the LDS bucket (indices never touch HBM);
+//  2.  the wave splits into TEAMS of LPR lanes (one 16-byte chunk per lane per row, CPL chunks);
+//      team t takes the units whose first token falls in the t-th share of the item's tokens and
+//      streams them through a two-stage software pipeline, accumulating in position order
+//      l = 0 .. L-1 with one fp32 add per position (bit-exact with the oracle); padded positions
+//      reuse the item's prefetched pad rows. Loads carry no branches: rows are clamped into the
+//      table in phase 1, and a slot whose descriptor does not fit the table is written as NaN.
+#ifndef RF_FUSED_MIN_WAVES
+#define RF_FUSED_MIN_WAVES 1
+#endif
+template <int LPR, int CPL, bool FULL, typename TT, typename OT>
+__global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_embed_kernel(
+    const rf_slot_desc* __restrict__ slots, int n_slots, const uint8_t* __restrict__ tok_bytes,
+    const int32_t* __restrict__ tok_off, const int32_t* __restrict__ bag_off, const int32_t* __restrict__ lmax,
+    int64_t n_units, const TT* __restrict__ table, int64_t table_rows, int dim, OT* __restrict__ out,
+    int64_t out_stride, int flags, int64_t* __restrict__ idx_out) {
+    constexpr int EPV = Elem<TT>::EPV;
+    constexpr int TEAMS = 64 / LPR;
+#ifdef RF_TOKENS_IN_FLIGHT
+    constexpr int C = RF_TOKENS_IN_FLIGHT;
+#else
+    constexpr int C = CPL >= 2 ? 1 : 2;  // tokens per pipeline stage per team (2 stages in flight)
+#endif
+    __shared__ uint32_t s_row[kWaves][2][kCap];
+    __shared__ int32_t s_loc[kWaves][kUnits + 1];
+    __shared__ int32_t s_gbeg[kWaves][kUnits];
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int team = lane / LPR, tl = lane % LPR;
+    const int nchunks = dim / EPV;
+    const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
+    const bool emit = (flags & RF_FLAG_EMIT_IDX) != 0 && idx_out != nullptr;
+    const bool abl_nohash = (flags & (1 << 12)) != 0, abl_nopool = (flags & (1 << 13)) != 0,
+               abl_nopad = (flags & (1 << 14)) != 0;  // diagnostic ablations (tools/kbench.py)
+    const int batch = (int)(n_units / n_slots);
+    const int nbb = (batch + kUnits - 1) / kUnits;
+    const int64_t n_items = (int64_t)n_slots * nbb;
+    int cidx[CPL];
+    bool cown[CPL];
+#pragma unroll
+    for (int cc = 0; cc < CPL; ++cc) {
+        const int c = tl + cc * LPR;
+        cown[cc] = FULL || c < nchunks;
+        cidx[cc] = FULL ? c : min(c, nchunks - 1);  // a lane past the row re-reads the last chunk, stores nothing
+    }
+
+    for (int64_t item = (int64_t)blockIdx.x * kWaves + wave; item < n_items; item += (int64_t)gridDim.x * kWaves) {
+        // ---- slot descriptor: wave-uniform ----
+        const int s = (int)(item / nbb);
+        const int b0 = (int)(item - (int64_t)s * nbb) * kUnits;
+        const int nu = min(kUnits, batch - b0);
+        const rf_slot_desc* sd = slots + s;
+        const int comb = sd->combiner;
+        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
+        const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
+        const int mask_empty = sd->mask_empty;
+        const int64_t out_off = sd->out_off;
+        const int lm = lmax[s];
+        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
+        // padded position = b"": bin 0 with mask_value "", else the bin of b""
+        int64_t pb0 = 0, pb1 = 0;
+        if (!mask_empty) {
+            pb0 = (int64_t)(siphash24_dev(salt0, salt0, tok_bytes, 0) % (uint64_t)nbins);
+            pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
+        }
+        const uint32_t pad0 = ok ? (uint32_t)(rb0 + pb0) : 0u, pad1 = ok ? (uint32_t)(rb1 + pb1) : 0u;
+
+        // ---- phase 1a: unit token ranges, wave prefix scan -> item-local token layout ----
+        int g0 = 0, len = 0;
+        if (lane < nu) {
+            const int64_t u = (int64_t)(b0 + lane) * n_slots + s;
+            g0 = bag_off[u];
+            len = bag_off[u + 1] - g0;
+        }
+        int incl = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane < nu) {
+            s_loc[wave][lane + 1] = incl;
+            s_gbeg[wave][lane] = g0;
+        }
+        if (lane == 0) s_loc[wave][0] = 0;
+        const int ntok = __shfl(incl, 63, 64);
+        wave_lds_sync();
+
+        // ---- phase 1b: lane-per-token double hashing into the LDS bucket ----
+        // (with RF_FLAG_EMIT_IDX every token of the item is hashed here, so ids past the bucket are
+        //  emitted even when the pooling never visits them — first/last/null)
+        const int nh = min(ntok, kCap);
+        if (abl_nohash) {
+            for (int i = lane; i < nh; i += 64) {
+                s_row[wave][0][i] = (uint32_t)(((uint64_t)i * 2654435761u + item) % (uint64_t)table_rows);
+                s_row[wave][1][i] = (uint32_t)(((uint64_t)i * 40503u + 7u + item) % (uint64_t)table_rows);
+            }
+        }
+        const int nhash = abl_nohash ? 0 : (emit ? ntok : nh);
+        for (int i = lane; i < nhash; i += 64) {
+            int lo = 0, hi = nu - 1;  // unit of item-local token i: last j with s_loc[j] <= i
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_loc[wave][mid] <= i) lo = mid; else hi = mid - 1;
+            }
+            const int t = s_gbeg[wave][lo] + (i - s_loc[wave][lo]);
+            const int tb = tok_off[t], n = tok_off[t + 1] - tb;
+            uint64_t h0, h1;
+            siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
+            const int64_t i0 = bucket_from_hash(h0, n, nbins, mask_empty);
+            const int64_t i1 = bucket_from_hash(h1, n, nbins, mask_empty);
+            if (i < kCap) {
+                s_row[wave][0][i] = ok ? (uint32_t)(rb0 + i0) : 0u;
+                s_row[wave][1][i] = ok ? (uint32_t)(rb1 + i1) : 0u;
+            }
+            if (emit) {
+                idx_out[2 * (int64_t)t] = i0;
+                idx_out[2 * (int64_t)t + 1] = i1;
+            }
+        }
+        wave_lds_sync();
+        if (abl_nopool) continue;
+
+        // ---- phase 2: token-balanced teams, pipelined gather + pool ----
+        auto bound = [&](int tm) -> int {  // first unit j whose first token lies in team tm's share
+            if (tm <= 0) return 0;
+            if (tm >= TEAMS) return nu;
+            int lo = 0, hi = nu;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int64_t)s_loc[wave][mid] * TEAMS >= (int64_t)tm * ntok) hi = mid; else lo = mid + 1;
+            }
+            return lo;
+        };
+        const int ja = bound(team), jb = bound(team + 1);
+
+        // the slot's pad rows, once per item
+        uint4 padv[2][CPL];
+#pragma unroll
+        for (int cc = 0; cc < CPL; ++cc) {
+            padv[0][cc] = row_chunk(table, pad0, dim, cidx[cc]);
+            padv[1][cc] = row_chunk(table, pad1, dim, cidx[cc]);
+        }
+        const float init = comb_init(comb);
+        int j = ja, ubeg = 0, uend = 0, Lu = 0;
+        int64_t obase = 0;
+        float acc[2][CPL][EPV];
+        auto start_unit = [&]() {
+            ubeg = s_loc[wave][j];
+            uend = s_loc[wave][j + 1];
+            const int ul = uend - ubeg;
+            Lu = comb == RF_COMB_NULL ? lm : ((mask_pad || abl_nopad) ? ul : max(lm, ul));
+            obase = (int64_t)(b0 + j) * out_stride + out_off;
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int cc = 0; cc < CPL; ++cc)
+#pragma unroll
+                    for (int e = 0; e < EPV; ++e) acc[k][cc][e] = init;
+        };
+        auto put = [&](int64_t off, const float* f) {  // one chunk; NaN if the slot does not fit the table
+            float g[EPV];
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) g[e] = ok ? f[e] : __builtin_nanf("");
+            store_chunk<OT, EPV>(out + off, g);
+        };
+        auto finish_unit = [&]() {
+            const int ul = uend - ubeg;
+            const int npad = Lu - ul;
+            if (comb == RF_COMB_NULL) {
+                for (int p = ul; p < Lu; ++p)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+#pragma unroll
+                        for (int cc = 0; cc < CPL; ++cc) {
+                            if (!cown[cc]) continue;
+                            float f[EPV];
+                            unpack16<TT>(padv[k][cc], f);
+                            if (mask_pad) {
+#pragma unroll
+                                for (int e = 0; e < EPV; ++e) f[e] = 0.0f;
+                            }
+                            put(obase + ((int64_t)k * Lu + p) * dim + cidx[cc] * EPV, f);
+                        }
+                return;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int cc = 0; cc < CPL; ++cc) {
+                    float* a = acc[k][cc];
+                    if (npad > 0) {
+                        float f[EPV];
+                        unpack16<TT>(padv[k][cc], f);
+                        if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) {
+                            for (int p = 0; p < npad; ++p)  // one add per padded position, in order
+#pragma unroll
+                                for (int e = 0; e < EPV; ++e) a[e] = __fadd_rn(a[e], f[e]);
+                        } else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) {
+#pragma unroll
+                            for (int e = 0; e < EPV; ++e) a[e] = comb_step(comb, a[e], f[e]);
+                        } else if (comb == RF_COMB_LAST || (comb == RF_COMB_FIRST && ul == 0)) {
+#pragma unroll
+                            for (int e = 0; e < EPV; ++e) a[e] = f[e];
+                        }
+                    }
+                    if (comb == RF_COMB_AVG) {
+                        const float fl = (float)Lu;
+#pragma unroll
+                        for (int e = 0; e < EPV; ++e) a[e] = __fdiv_rn(a[e], fl);
+                    }
+                    if (Lu == 0 && (mask_pad || comb == RF_COMB_FIRST || comb == RF_COMB_LAST)) {
+#pragma unroll
+                        for (int e = 0; e < EPV; ++e) a[e] = 0.0f;  // empty (masked) bag / no position -> zeros
+                    }
+                    if (cown[cc]) put(obase + (int64_t)k * dim + cidx[cc] * EPV, a);
+                }
+        };
+        auto consume = [&](const uint4 (&v)[2][CPL], int pos) {
+            if (comb == RF_COMB_NULL) {
+                if (pos < Lu)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+#pragma unroll
+                        for (int cc = 0; cc < CPL; ++cc) {
+                            if (!cown[cc]) continue;
+                            float f[EPV];
+                            unpack16<TT>(v[k][cc], f);
+                            put(obase + ((int64_t)k * Lu + pos) * dim + cidx[cc] * EPV, f);
+                        }
+                return;
+            }
+            if (comb == RF_COMB_FIRST && pos != 0) return;
+            if (comb == RF_COMB_LAST && pos != Lu - 1) return;
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int cc = 0; cc < CPL; ++cc) {
+                    float f[EPV];
+                    unpack16<TT>(v[k][cc], f);
+                    if (comb == RF_COMB_FIRST || comb == RF_COMB_LAST) {
+#pragma unroll
+                        for (int e = 0; e < EPV; ++e) acc[k][cc][e] = f[e];
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < EPV; ++e) acc[k][cc][e] = comb_step(comb, acc[k][cc][e], f[e]);
+                    }
+                }
+        };
+
+        if (ja < jb) {
+            start_unit();
+            const int tb0 = s_loc[wave][ja], tb1 = s_loc[wave][jb];
+            const int th = min(tb1, kCap);  // hot range: rows staged in LDS
+            auto issue = [&](uint4 (&v)[C][2][CPL], int c0) {
+#pragma unroll
+                for (int q = 0; q < C; ++q) {
+                    const int i = min(c0 + q, th - 1);  // past the range: re-read a valid row, ignored
+                    const uint32_t r0 = s_row[wave][0][i], r1 = s_row[wave][1][i];
+#pragma unroll
+                    for (int cc = 0; cc < CPL; ++cc) {
+                        v[q][0][cc] = row_chunk(table, r0, dim, cidx[cc]);
+                        v[q][1][cc] = row_chunk(table, r1, dim, cidx[cc]);
+                    }
+                }
+            };
+            auto drain = [&](const uint4 (&v)[C][2][CPL], int c0) {
+#pragma unroll
+                for (int q = 0; q < C; ++q) {
+                    const int i = c0 + q;
+                    if (i < th) {
+                        while (i >= uend) {  // close the current unit (and any empty ones after it)
+                            finish_unit();
+                            ++j;
+                            start_unit();
+                        }
+                        consume(v[q], i - ubeg);
+                    }
+                }
+            };
+            uint4 va[C][2][CPL], vb[C][2][CPL];
+            int c0 = tb0;
+            if (c0 < th) issue(va, c0);
+            while (c0 < th) {
+                if (c0 + C < th) issue(vb, c0 + C);
+                drain(va, c0);
+                c0 += C;
+                if (c0 >= th) break;
+                if (c0 + C < th) issue(va, c0 + C);
+                drain(vb, c0);
+                c0 += C;
+            }
+            // cold range (item holds more than kCap tokens): hash inline, one token at a time
+            for (int i = max(tb0, kCap); i < tb1; ++i) {
+                while (i >= uend) {
+                    finish_unit();
+                    ++j;
+                    start_unit();
+                }
+                const int t = s_gbeg[wave][j] + (i - ubeg);
+                const int tb = tok_off[t], n = tok_off[t + 1] - tb;
+                uint64_t h0, h1;
+                siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
+                const uint32_t r0 = ok ? (uint32_t)(rb0 + bucket_from_hash(h0, n, nbins, mask_empty)) : 0u;
+                const uint32_t r1 = ok ? (uint32_t)(rb1 + bucket_from_hash(h1, n, nbins, mask_empty)) : 0u;
+                uint4 v[2][CPL];
+#pragma unroll
+                for (int cc = 0; cc < CPL; ++cc) {
+                    v[0][cc] = row_chunk(table, r0, dim, cidx[cc]);
+                    v[1][cc] = row_chunk(table, r1, dim, cidx[cc]);
+                }
+                consume(v, i - ubeg);
+            }
+            while (true) {
+                finish_unit();
+                if (++j >= jb) break;
+                start_unit();
+            }
+        }
+        wave_lds_sync();  // the LDS bucket is rewritten by the next item
+    }
+}
+
+// lanes per row / 16-byte chunks per lane for `nchunks` chunks per row; max_lpr caps the team width so a
+// wave holds more teams (more rows in flight).
+template <typename F>
+int dispatch_fused(int nchunks, int max_lpr, F&& f) {
+    using std::integral_constant;
+    int lpr = 1;
+    while (lpr < nchunks && lpr < 64) lpr <<= 1;
+    lpr = std::min(lpr, max_lpr);
+    while ((nchunks + lpr - 1) / lpr > 4 && lpr < 64) lpr <<= 1;
+    const int cpl = (nchunks + lpr - 1) / lpr;
+    const int c = cpl <= 1 ? 1 : cpl <= 2 ? 2 : cpl <= 4 ? 4 : 0;
+    if (c == 0) return rf_set_error(RF_EINVAL, "embedding dim too large (> 256 16-byte chunks per row)");
+#define RF_CASE(L, CP) \
+    if (lpr == L && c == CP) return f(integral_constant<int, L>{}, integral_constant<int, CP>{});
+    RF_CASE(1, 1) RF_CASE(2, 1) RF_CASE(2, 2) RF_CASE(4, 1) RF_CASE(4, 2) RF_CASE(4, 4) RF_CASE(8, 1) RF_CASE(8, 2)
+    RF_CASE(8, 4) RF_CASE(16, 1) RF_CASE(16, 2) RF_CASE(16, 4) RF_CASE(32, 1) RF_CASE(32, 2) RF_CASE(32, 4)
+    RF_CASE(64, 1) RF_CASE(64, 2) RF_CASE(64, 4)
+#undef RF_CASE
+    return rf_set_error(RF_EINVAL, "no kernel for %d lanes x %d chunks", lpr, c);
+}
+
+// launch for one table dtype TT (defined in rf_fused_f32.hip / rf_fused_bf16.hip)
+int launch_fused_f32(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                     const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table, int64_t table_rows,
+                     int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, int64_t* idx_out,
+                     int max_lpr, int grid, hipStream_t st);
+int launch_fused_bf16(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                      const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table, int64_t table_rows,
+                      int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, int64_t* idx_out,
+                      int max_lpr, int grid, hipStream_t st);
+
+}  // namespace rf

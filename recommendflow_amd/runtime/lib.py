@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "librf.so"))
+LIB_PATH = os.environ.get("RF_LIB") or os.path.normpath(os.path.join(_HERE, "..", "lib", "librf.so"))  # RF_LIB: diagnostics only
 
 RF_OK, RF_EINVAL, RF_EHIP, RF_EOOB = 0, -1, -2, -3
 DT_F32, DT_BF16, DT_F16 = 0, 1, 2
