@@ -40,6 +40,7 @@ def parse():
     p.add_argument("--dim", type=int, default=64)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     p.add_argument("--uniform", action="store_true", help="uniform ids instead of Zipf(1.1)")
+    p.add_argument("--no-extras", action="store_true", help="skip the cfg3 ESIM / cfg2 DSSM full-forward lines")
     return p.parse_args()
 
 
@@ -118,6 +119,12 @@ def main():
     if world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(enc, host[0], args.cpu_seconds)
 
+    extras = None
+    if world == 1 and not args.no_extras:
+        del dev, out
+        torch.cuda.empty_cache()
+        extras = {"cfg3_esim_forward": bench_esim(args), "cfg2_dssm_forward": bench_dssm(args, enc, host)}
+
     value = args.batch * world * args.steps / elapsed
     line = {
         "metric": METRIC,
@@ -154,10 +161,131 @@ def main():
             "kernel_ms": round(avg_kern_s * 1e3, 4),
         },
         "cpu_baseline": cpu,
+        "extras": extras,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _time_stages(stages, steps, warmup):
+    """stages: list of (name, fn). HIP events around every stage on the current stream; returns
+    (ms per step, {stage: ms})."""
+    import torch
+
+    for _ in range(warmup):
+        for _, fn in stages:
+            fn()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record()
+        for k, (_, fn) in enumerate(stages):
+            fn()
+            ev[i][k + 1].record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps * 1e3
+    per = {name: sum(ev[i][k].elapsed_time(ev[i][k + 1]) for i in range(steps)) / steps for k, (name, _) in enumerate(stages)}
+    return wall, per
+
+
+def bench_esim(args):
+    """cfg3: ESIM ranking, 200 slots (100 user = q, 100 ad = a) x 1M bins per hash table, D = 64 bf16
+    (token dim 128; fused tables 2 x 200M x 64 bf16 = 51.2 GB), 16 dense features, B = 4096."""
+    import torch
+
+    from recommendflow_amd.backend.encoder.sparse_encoder import SlotSpec
+    from recommendflow_amd.models.ranking.esim import Esim
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    B, Ls = args.batch, 100
+    user = [SlotSpec(f"u{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)]
+    ad = [SlotSpec(f"a{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)]
+    model = Esim(user, ad, n_dense=16, dim=64, table_dtype=torch.bfloat16, seed=3)
+    hu = [synthetic_batch(B, [False] * Ls, seed=77 + i, slot_ids=range(Ls)).to("cuda") for i in range(2)]
+    ha = [synthetic_batch(B, [False] * Ls, seed=99 + i, slot_ids=range(Ls, 2 * Ls)).to("cuda") for i in range(2)]
+    dense = torch.randn(B, 16, device="cuda")
+    st = {"i": 0}
+    q = torch.empty((B, Ls * 128), dtype=torch.bfloat16, device="cuda")
+    a = torch.empty_like(q)
+    pooled = torch.empty((B, model.pooled_width), device="cuda")
+    from recommendflow_amd.backend.layers.attention_layers import esim_soft_attention_pool
+
+    def enc():
+        i = st["i"] = st["i"] + 1
+        model.enc_q(hu[i % 2], out=q)
+        model.enc_a(ha[i % 2], out=a)
+
+    def att():
+        esim_soft_attention_pool(q.view(B, Ls, 128), a.view(B, Ls, 128), out=pooled, out_col=model.d_emb)
+
+    def mlp():
+        x = dense
+        for k, (norm, dl) in enumerate(zip(model.input_mlp.norms, model.input_mlp.denses)):
+            x = dl(norm(x, out_dtype=torch.bfloat16), out=pooled[:, : model.d_emb] if k == len(model.input_mlp.denses) - 1 else None)
+        model.dense_output(model.output_mlp(pooled))
+
+    steps = max(10, args.steps // 2)
+    wall, per = _time_stages([("sparse_encoders", enc), ("esim_attention", att), ("mlp_scorer", mlp)], steps, 3)
+    att_flops = 2 * Ls * Ls * 128 * 3 * B
+    mlp_flops = (model.flops_per_example() - 2 * Ls * Ls * 128 * 3) * B
+    tok_bytes = sum(int(h.tok_bytes.numel()) + 4 * h.n_tokens for h in (hu[0], ha[0]))
+    enc_bytes = 2 * (2 * B * Ls * 128 + B * Ls * 2 * 64 * 2) + tok_bytes
+    return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4),
+            "stage_ms": {k: round(v, 4) for k, v in per.items()},
+            "encoder_GBs": round(enc_bytes / per["sparse_encoders"] / 1e6, 1),
+            "esim_TFLOPs": round(att_flops / per["esim_attention"] / 1e9, 1),
+            "esim_mfma_frac_of_2500TF": round(att_flops / per["esim_attention"] / 1e9 / 2500, 4),
+            "mlp_TFLOPs": round(mlp_flops / per["mlp_scorer"] / 1e9, 1),
+            "config": "200 slots (100 q + 100 a) x 1M bins/hash, D=64 bf16 (tables 51.2 GB), L=100, d=128, "
+                      "input_mlp 16->256->512, output_mlp 1280->1024->512, Dense(2, softmax), bf16 MFMA"}
+
+
+def bench_dssm(args, enc, host):
+    """cfg2 full forward: the same 229-slot fused table split into user (69) / ad (160) encoders + fp32
+    towers [1024, 512, 256] selu/BatchNorm (exact-fp32 MFMA) + l2norm + dot."""
+    import numpy as np
+    import torch
+
+    from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder
+    from recommendflow_amd.config_parser.configuration import Configuration
+    from recommendflow_amd.models.matching.dssm import Dssm
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "base_recall_sdpa.yaml"))
+    B = args.batch
+    specs = enc.slots
+    users = [i for i, f in enumerate(conf.features.hashing_features) if f.tower.value == "user"]
+    ads = [i for i, f in enumerate(conf.features.hashing_features) if f.tower.value == "ad"]
+    eu = FusedSparseEncoder([specs[i] for i in users], enc.dim, table=enc.table, row_base0=0)
+    ea = FusedSparseEncoder([specs[i] for i in ads], enc.dim, table=enc.table,
+                            row_base0=int(enc.host_desc[ads[0]]["row_base"][0]))
+    model = Dssm(eu, ea, seed=5)
+    mv = [bool(f.multivalued) for f in conf.features.hashing_features]
+    hu = synthetic_batch(B, [mv[i] for i in users], seed=11, slot_ids=users).to("cuda")
+    ha = synthetic_batch(B, [mv[i] for i in ads], seed=12, slot_ids=ads).to("cuda")
+    xu = torch.empty((B, eu.out_width), device="cuda")
+    xa = torch.empty((B, ea.out_width), device="cuda")
+
+    def sparse():
+        eu(hu, out=xu)
+        ea(ha, out=xa)
+
+    def towers():
+        u = torch.nn.functional.normalize(model.user_dense(xu), dim=-1, eps=1e-6)
+        v = torch.nn.functional.normalize(model.ad_dense(xa), dim=-1, eps=1e-6)
+        (u * v).sum(-1)
+
+    steps = max(5, args.steps // 5)
+    wall, per = _time_stages([("sparse_encoders", sparse), ("fp32_towers", towers)], steps, 2)
+    flops = model.flops_per_example() * B
+    return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4),
+            "stage_ms": {k: round(v, 4) for k, v in per.items()},
+            "towers_TFLOPs_fp32": round(flops / per["fp32_towers"] / 1e9, 1),
+            "towers_frac_of_157TF_fp32": round(flops / per["fp32_towers"] / 1e9 / 157.3, 4),
+            "config": "base_recall_sdpa.yaml: 69 user + 160 ad slots, 10M x 64 fp32 table, towers [1024,512,256] "
+                      "selu + BatchNorm fp32"}
 
 
 def cpu_baseline(enc, hb, budget_s):

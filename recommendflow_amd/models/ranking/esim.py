@@ -1,0 +1,69 @@
+"""ESIM ranker on the MI355X hot path (reference: models/ranking/esim.py:13-93).
+
+Forward (reference lines in brackets):
+  d_emb  = input_mlp(dense)                                   [esim.py:70-75; create_mlp gelu + LayerNorm]
+  q, a   = user / ad sparse-slot token sequences [B, L, 2D]   (deviation D-esim-inputs: the reference takes
+           BERT token sequences; here each slot is one token = its DoubleHashingEmbedding output, so the
+           sequence comes straight out of one fused encoder launch per tower)
+  pooled = [d_emb, avg_q, max_q, avg_a, max_a, avg_q-avg_a, max_q-max_a]   [esim.py:78-84; one fused kernel]
+  p      = softmax(output_mlp(pooled) W + b)                  [esim.py:85-88; Dropout = identity]
+Buffers: the ESIM kernel and the input MLP write straight into column ranges of one [B, 512 + 6d] tensor.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from ...backend.blocks.mlp import create_mlp
+from ...backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
+from ...backend.layers.attention_layers import esim_soft_attention_pool
+from ...backend.layers.core import Dense, LayerNormalization
+from ...runtime.batch import SparseBatch
+
+
+class Esim(torch.nn.Module):
+    def __init__(self, user_slots: Sequence[SlotSpec], ad_slots: Sequence[SlotSpec], n_dense: int, dim: int = 64,
+                 table_dtype=torch.bfloat16, mlp_dtype=torch.bfloat16, input_units=(256, 512), output_units=(1024, 512),
+                 seed: int = 0, device="cuda", encoders: Optional[tuple] = None):
+        super().__init__()
+        if len(user_slots) != len(ad_slots):
+            raise ValueError("SoftAttention needs equal q / a lengths (attention_layers.py:74)")
+        self.L = len(user_slots)
+        self.d = 2 * dim
+        if encoders is None:
+            encoders = (FusedSparseEncoder(user_slots, dim, table_dtype=table_dtype, seed=seed + 1, device=device),
+                        FusedSparseEncoder(ad_slots, dim, table_dtype=table_dtype, seed=seed + 2, device=device))
+        self.enc_q, self.enc_a = encoders
+        ln = LayerNormalization(epsilon=1e-6)
+        self.input_mlp = create_mlp(list(input_units), 0.3, "gelu", ln, in_features=n_dense, dtype=mlp_dtype,
+                                    seed=seed + 10, device=device)
+        self.d_emb = self.input_mlp.out_features
+        self.pooled_width = self.d_emb + 6 * self.d
+        self.output_mlp = create_mlp(list(output_units), 0.3, "gelu", ln, in_features=self.pooled_width,
+                                     dtype=mlp_dtype, seed=seed + 20, device=device)
+        self.dense_output = Dense(self.output_mlp.out_features, 2, activation="softmax", dtype=mlp_dtype,
+                                  seed=seed + 30, device=device)
+
+    def forward(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor) -> torch.Tensor:
+        B = user.batch
+        q = self.enc_q(user).view(B, self.L, self.d)
+        a = self.enc_a(ad).view(B, self.L, self.d)
+        pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=q.device)
+        x = dense
+        for i, (norm, dense_l) in enumerate(zip(self.input_mlp.norms, self.input_mlp.denses)):
+            h = norm(x, out_dtype=self.input_mlp.dtype)
+            last = i == len(self.input_mlp.denses) - 1
+            x = dense_l(h, out=pooled[:, : self.d_emb] if last else None)
+        esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
+        return self.dense_output(self.output_mlp(pooled))
+
+    def flops_per_example(self) -> float:
+        """Dense FLOPs per example: ESIM products (2 L^2 d for E + 2 * 2 L^2 d for the alignments) + MLP GEMMs."""
+        att = 2 * self.L * self.L * self.d * 3
+        mlp = 0
+        for m in (self.input_mlp, self.output_mlp):
+            for dn in m.denses:
+                mlp += 2 * dn.in_features * dn.units
+        mlp += 2 * self.dense_output.in_features * 2
+        return float(att + mlp)
