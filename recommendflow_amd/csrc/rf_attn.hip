@@ -2,7 +2,8 @@
 //   rf_esim_soft_attention_fwd  SoftAttention + ESIM combine/pool  (attention_layers.py:15-74, esim.py:78-84)
 //   rf_sdpa_fwd                 masked multi-head SDPA             (layer_utils.py:4-38, attention_layers.py:153-168)
 //
-// Both kernels keep one example (or one (example, head)) per workgroup of 4 waves:
+// ESIM runs persistent 8-wave workgroups (one per CU, next example prefetched into registers); SDPA one
+// (example, head) per 4-wave workgroup. Shared structure:
 //   * the [L, d] operand images sit in LDS with a 16-byte row pad (conflict-free ds_read_b128 for the
 //     16x16x32 A/B fragments, 8-byte aligned rows for ds_read_b64_tr_b16);
 //   * each wave owns 16-row stripes of the score matrix; scores stay in registers (never HBM), the
@@ -13,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "rf_common.h"
@@ -80,168 +82,219 @@ __device__ __forceinline__ float group16_sum(float v) {
     return v;
 }
 
+// Reductions across the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48) in VALU, no LDS:
+// v_permlane16_swap(x, x) -> {row0,row0,row2,row2} / {row1,row1,row3,row3};
+// v_permlane32_swap(x, x) -> {lo,lo} / {hi,hi} (semantics probed on MI355X, tools/probes/permlane.hip).
+__device__ __forceinline__ float rows4_sum(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float rows4_max(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float s = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// B fragment with the k order of an accumulator-sourced A operand: element j of lane (lr, g) holds
+// k = k0 + (j < 4 ? 4g + j : 16 + 4g + j - 4) — rows 4g..4g+3 and 16+4g..16+4g+3 of the 32-row step.
+template <typename frag>
+__device__ __forceinline__ frag v_frag_tr_acc(const uint16_t* V, int rs, int k0, int n0, int lane) {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+    const uint16_t* base = V + (k0 + 4 * g + qq) * rs + n0 + 4 * p;
+    const s4v lo = tr_read(base);
+    const s4v hi = tr_read(base + 16 * rs);
+    const s8v x = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(frag, x);
+}
+
 // ---------------------------------------------------------------------------------------------
-// ESIM: one workgroup per example
+// ESIM: persistent workgroups of 8 waves (2 per SIMD), one per CU; each loops over examples
+//   stage   q, a of example e (prefetched into registers during example e - G) -> LDS images
+//   prefetch the next example's q, a into registers (in flight during this example's compute)
+//   wave w  owns score stripe w (16 rows of a): E = a_stripe q^T (MFMA), row softmax in fp32, P -> LDS,
+//           att = P [q | a] (MFMA, transposed V reads), ESIM combine statistics -> per-wave LDS slots
+//   reduce  threads n < D combine the 8 waves' statistics with the column sums of q / a
 // ---------------------------------------------------------------------------------------------
+constexpr int kEsimWaves = 8;
+
 template <bool F16, int D>
-__global__ __launch_bounds__(256) void esim_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ a, int L,
-                                                   int64_t ex_stride, int64_t ld, float* __restrict__ out,
-                                                   int64_t out_stride, int64_t out_off, float* __restrict__ att_out) {
+__global__ __launch_bounds__(kEsimWaves * 64) void esim_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ a,
+                                                           int batch, int L, int64_t ex_stride, int64_t ld,
+                                                           float* __restrict__ out, int64_t out_stride, int64_t out_off,
+                                                           float* __restrict__ att_out) {
     using M = Mfma<F16>;
     using frag = typename M::frag;
+    constexpr int NTH = kEsimWaves * 64;
     constexpr int RS = D + 8;       // LDS row stride (elements) of the q / a images
     constexpr int DK = D / 32;      // k-steps of the score product
     constexpr int NT = D / 16;      // n-tiles of the P @ V product (per side)
+    constexpr int CPR = D / 8;      // 16-byte chunks per row
+    constexpr int NCH = 2 * 128 * CPR / NTH;  // chunks per thread at L <= 128
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int64_t b = blockIdx.x;
     const int Lk = (L + 31) & ~31;  // k extent of P @ V (zero rows past L)
-    const int nt = (L + 15) >> 4;   // 16-wide tiles over positions
-    const int SS = Lk + 8;          // row stride of a wave's P stripe
+    const int nt = (L + 15) >> 4;   // 16-wide tiles over positions (<= 8 = waves)
     uint16_t* qs = reinterpret_cast<uint16_t*>(smem);
     uint16_t* as = qs + Lk * RS;
-    uint16_t* pbuf = as + Lk * RS;
-    float* st = reinterpret_cast<float*>(pbuf + 4 * 16 * SS);  // [wave][stat 6][side*D + n]
+    float* st = reinterpret_cast<float*>(as + Lk * RS);  // [wave][stat 3][side*D + n]
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
 
-    // stage q and a (rows >= L zero), 16-byte chunks
-    constexpr int CPR = D / 8;
-    for (int c = tid; c < 2 * Lk * CPR; c += 256) {
-        const int m = c / (Lk * CPR), rem = c - m * Lk * CPR, r = rem / CPR, ch = rem - r * CPR;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (r < L) v = *reinterpret_cast<const uint4*>((m ? a : q) + b * ex_stride + (int64_t)r * ld + ch * 8);
-        *reinterpret_cast<uint4*>((m ? as : qs) + r * RS + ch * 8) = v;
-    }
-    for (int i = tid; i < 4 * 6 * 2 * D; i += 256) st[i] = ((i / (2 * D)) % 6) < 3 ? 0.0f : -INFINITY;
-    __syncthreads();
-
-    float* wst = st + wave * 6 * 2 * D;
-    uint16_t* pw = pbuf + wave * 16 * SS;
-    for (int sp = wave; sp < nt; sp += 4) {
-        // E[i, j] = sum_k a[i, k] q[j, k] for the stripe's 16 rows i (attention_layers.py:44-47)
-        frag af[DK];
+    // chunk i of this thread: matrix m = i / (NCH/2) (q first), row r, 16-byte column ch; every index is a
+    // compile-time power-of-two split (no runtime divisions on the staging path)
+    constexpr int HALF = NCH / 2;
+    constexpr int LOG_CPR = D == 128 ? 4 : 3;
+    uint4 pre[NCH];
+    auto prefetch = [&](int64_t e) {
 #pragma unroll
-        for (int kk = 0; kk < DK; ++kk) af[kk] = lds_frag<frag>(as + (sp * 16 + lr) * RS + kk * 32 + lg * 8);
-        f4 e[8];
-#pragma unroll
-        for (int jt = 0; jt < 8; ++jt) {
-            e[jt] = f4{0.f, 0.f, 0.f, 0.f};
-            if (jt < nt) {
-#pragma unroll
-                for (int kk = 0; kk < DK; ++kk)
-                    e[jt] = M::mma(af[kk], lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8), e[jt]);
-            }
+        for (int i = 0; i < NCH; ++i) {
+            const int cm = tid + (i % HALF) * NTH;
+            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
+            pre[i] = make_uint4(0, 0, 0, 0);
+            if (r < L) pre[i] = *reinterpret_cast<const uint4*>((i < HALF ? q : a) + e * ex_stride + (int64_t)r * ld + ch * 8);
         }
-        // row softmax over j < L (max-subtracted, attention_layers.py:69-72), fp32
-        float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    };
+    int64_t e = blockIdx.x;
+    if (e < batch) prefetch(e);
+    for (; e < batch; e += gridDim.x) {
+        __syncthreads();  // the previous example's LDS images are no longer read
 #pragma unroll
-        for (int jt = 0; jt < 8; ++jt)
-            if (jt < nt) {
-                const bool valid = jt * 16 + lr < L;
+        for (int i = 0; i < NCH; ++i) {
+            const int cm = tid + (i % HALF) * NTH;
+            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
+            if (r < Lk) *reinterpret_cast<uint4*>((i < HALF ? qs : as) + r * RS + ch * 8) = pre[i];
+        }
+        __syncthreads();
+        if (e + gridDim.x < batch) prefetch(e + gridDim.x);  // in flight while this example computes
+
+        const int sp = wave;
+        if (sp < nt) {
+            float* wst = st + wave * 3 * 2 * D;
+            // E^T[j, i] = sum_k q[j, k] a[i, k] for the stripe's 16 columns i (attention_layers.py:44-47):
+            // A = q rows j, B = a rows i; the C layout puts j on (lane >> 4, register) and i on lane & 15
+            frag bf[DK];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if (!valid) e[jt][r] = -INFINITY;
-                    mx[r] = fmaxf(mx[r], e[jt][r]);
+            for (int kk = 0; kk < DK; ++kk) bf[kk] = lds_frag<frag>(as + (sp * 16 + lr) * RS + kk * 32 + lg * 8);
+            f4 ev[8];
+#pragma unroll
+            for (int jt = 0; jt < 8; ++jt) {
+                ev[jt] = f4{0.f, 0.f, 0.f, 0.f};
+                if (jt < nt) {
+#pragma unroll
+                    for (int kk = 0; kk < DK; ++kk)
+                        ev[jt] = M::mma(lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8), bf[kk], ev[jt]);
                 }
             }
-        float sm[4];
+            // softmax over j < L for column i (attention_layers.py:69-72), fp32: in-lane over (tile, register),
+            // then across the four 16-lane rows
+            float mx = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            mx[r] = group16_max(mx[r]);
-            sm[r] = 0.f;
-        }
+            for (int jt = 0; jt < 8; ++jt)
+                if (jt < nt)
 #pragma unroll
-        for (int jt = 0; jt < 8; ++jt)
-            if (jt < nt)
+                    for (int r = 0; r < 4; ++r) {
+                        if (jt * 16 + lg * 4 + r >= L) ev[jt][r] = -INFINITY;
+                        mx = fmaxf(mx, ev[jt][r]);
+                    }
+            mx = rows4_max(mx);
+            float sm = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < 8; ++jt)
+                if (jt < nt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        ev[jt][r] = expf(ev[jt][r] - mx);
+                        sm += ev[jt][r];
+                    }
+            const float inv = 1.0f / rows4_sum(sm);
+            // P as the A operand of P @ V, straight from the accumulators: step kt takes tiles 2kt, 2kt+1
+            frag pa[4];
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                uint16_t h[8];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    e[jt][r] = expf(e[jt][r] - mx[r]);
-                    sm[r] += e[jt][r];
+                    h[r] = 2 * kt < nt ? M::from_f(ev[2 * kt][r] * inv) : (uint16_t)0;
+                    h[4 + r] = 2 * kt + 1 < nt ? M::from_f(ev[2 * kt + 1][r] * inv) : (uint16_t)0;
                 }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sm[r] = 1.0f / group16_sum(sm[r]);
-        // P stripe -> LDS (MFMA dtype), zero past the valid tiles up to Lk
-#pragma unroll
-        for (int jt = 0; jt < 8; ++jt)
-            if (jt * 16 < Lk)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    pw[(lg * 4 + r) * SS + jt * 16 + lr] = jt < nt ? M::from_f(e[jt][r] * sm[r]) : (uint16_t)0;
-        wave_lds_sync();
-
-        // att_side = P @ side (attention_layers.py:74), then the ESIM combine statistics (esim.py:79-82)
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            const uint16_t* V = side ? as : qs;
-            f4 acc[NT];
-#pragma unroll
-            for (int nn = 0; nn < NT; ++nn) acc[nn] = f4{0.f, 0.f, 0.f, 0.f};
-            for (int kt = 0; kt < Lk; kt += 32) {
-                const frag pa = lds_frag<frag>(pw + lr * SS + kt + lg * 8);
-#pragma unroll
-                for (int nn = 0; nn < NT; ++nn) acc[nn] = M::mma(pa, v_frag_tr<frag>(V, RS, kt, nn * 16, lane), acc[nn]);
+                const s8v x = {(short)h[0], (short)h[1], (short)h[2], (short)h[3], (short)h[4], (short)h[5], (short)h[6], (short)h[7]};
+                pa[kt] = __builtin_bit_cast(frag, x);
             }
+
+            // att_side = P @ side (attention_layers.py:74), then the ESIM combine statistics (esim.py:79-82)
 #pragma unroll
-            for (int nn = 0; nn < NT; ++nn) {
-                const int n = nn * 16 + lr;
-                float s_att = 0.f, s_dif = 0.f, s_mul = 0.f, m_att = -INFINITY, m_dif = -INFINITY, m_mul = -INFINITY;
+            for (int side = 0; side < 2; ++side) {
+                const uint16_t* V = side ? as : qs;
+                f4 acc[NT];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = sp * 16 + lg * 4 + r;
-                    if (row < L) {
-                        const float x = M::to_f(V[row * RS + n]);
-                        const float at = acc[nn][r];
-                        const float df = x - at, ml = x * at;
-                        s_att += at; s_dif += df; s_mul += ml;
-                        m_att = fmaxf(m_att, at); m_dif = fmaxf(m_dif, df); m_mul = fmaxf(m_mul, ml);
-                        if (att_out) att_out[((b * 2 + side) * L + row) * D + n] = at;
+                for (int nn = 0; nn < NT; ++nn) acc[nn] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt) {
+                    if (kt * 32 < Lk) {
+#pragma unroll
+                        for (int nn = 0; nn < NT; ++nn)
+                            acc[nn] = M::mma(pa[kt], v_frag_tr_acc<frag>(V, RS, kt * 32, nn * 16, lane), acc[nn]);
                     }
                 }
 #pragma unroll
-                for (int o = 16; o < 64; o <<= 1) {
-                    s_att += __shfl_xor(s_att, o, 64); s_dif += __shfl_xor(s_dif, o, 64); s_mul += __shfl_xor(s_mul, o, 64);
-                    m_att = fmaxf(m_att, __shfl_xor(m_att, o, 64)); m_dif = fmaxf(m_dif, __shfl_xor(m_dif, o, 64));
-                    m_mul = fmaxf(m_mul, __shfl_xor(m_mul, o, 64));
-                }
-                if (lg == 0) {
-                    float* w = wst + side * D + n;
-                    w[0 * 2 * D] += s_att; w[1 * 2 * D] += s_dif; w[2 * 2 * D] += s_mul;
-                    w[3 * 2 * D] = fmaxf(w[3 * 2 * D], m_att); w[4 * 2 * D] = fmaxf(w[4 * 2 * D], m_dif);
-                    w[5 * 2 * D] = fmaxf(w[5 * 2 * D], m_mul);
-                }
-            }
-        }
-        wave_lds_sync();
-    }
-    __syncthreads();
-
-    // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84)
-    for (int n = tid; n < D; n += 256) {
-        float avg[2], mxv[2];
+                for (int nn = 0; nn < NT; ++nn) {
+                    // mean over the 4L rows of [x; att; x - att; x * att] = (2 sum x + sum x*att) / 4L exactly
+                    // (sum att + sum (x - att) = sum x); the four maxima fold into one (max is exact).
+                    // x[i][n] for this lane's 4 rows i: one transposed read of the row-major image
+                    const s4v xv = tr_read(V + (sp * 16 + lg * 4 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3));
+                    const int n = nn * 16 + lr;
+                    float s_x = 0.f, s_mul = 0.f, m_all = -INFINITY;
 #pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            const uint16_t* V = side ? as : qs;
-            float sx = 0.f, mxx = -INFINITY;
-            for (int i = 0; i < L; ++i) {
-                const float x = M::to_f(V[i * RS + n]);
-                sx += x;
-                mxx = fmaxf(mxx, x);
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = sp * 16 + lg * 4 + r;
+                        if (row < L) {
+                            const float x = M::to_f((uint16_t)xv[r]);
+                            const float at = acc[nn][r];
+                            const float ml = x * at;
+                            s_x += x;
+                            s_mul += ml;
+                            m_all = fmaxf(m_all, fmaxf(fmaxf(x, at), fmaxf(x - at, ml)));
+                            if (att_out) att_out[((e * 2 + side) * L + row) * D + n] = at;
+                        }
+                    }
+                    s_x = rows4_sum(s_x);
+                    s_mul = rows4_sum(s_mul);
+                    m_all = rows4_max(m_all);
+                    if (lg == 0) {
+                        float* w = wst + side * D + n;
+                        w[0] = s_x;
+                        w[2 * D] = s_mul;
+                        w[4 * D] = m_all;
+                    }
+                }
             }
-            float s3 = 0.f, m3 = mxx;
-            for (int w = 0; w < 4; ++w) {
-                const float* ws = st + w * 6 * 2 * D + side * D + n;
-                s3 += ws[0] + ws[2 * D] + ws[4 * D];
-                m3 = fmaxf(m3, fmaxf(ws[6 * D], fmaxf(ws[8 * D], ws[10 * D])));
-            }
-            avg[side] = (sx + s3) / (float)(4 * L);
-            mxv[side] = m3;
         }
-        float* o = out + b * out_stride + out_off + n;
-        o[0] = avg[0];
-        o[D] = mxv[0];
-        o[2 * D] = avg[1];
-        o[3 * D] = mxv[1];
-        o[4 * D] = avg[0] - avg[1];
-        o[5 * D] = mxv[0] - mxv[1];
+        __syncthreads();
+
+        // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84)
+        for (int n = tid; n < D; n += NTH) {
+            float avg[2], mxv[2];
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                float sx = 0.f, smul = 0.f, m3 = -INFINITY;  // waves in order: deterministic
+                for (int w = 0; w < nt; ++w) {
+                    const float* ws = st + w * 3 * 2 * D + side * D + n;
+                    sx += ws[0];
+                    smul += ws[2 * D];
+                    m3 = fmaxf(m3, ws[4 * D]);
+                }
+                avg[side] = (2.0f * sx + smul) / (float)(4 * L);
+                mxv[side] = m3;
+            }
+            float* o = out + e * out_stride + out_off + n;
+            o[0] = avg[0];
+            o[D] = mxv[0];
+            o[2 * D] = avg[1];
+            o[3 * D] = mxv[1];
+            o[4 * D] = avg[0] - avg[1];
+            o[5 * D] = mxv[0] - mxv[1];
+        }
     }
 }
 
@@ -386,15 +439,18 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     if (batch == 0) return RF_OK;
     RF_REQUIRE(q && a && out, "rf_esim_soft_attention_fwd: null pointer");
     const int Lk = (L + 31) & ~31;
-    const size_t lds = (size_t)2 * Lk * (d + 8) * 2 + (size_t)4 * 16 * (Lk + 8) * 2 + (size_t)4 * 6 * 2 * d * 4;
+    const size_t lds = (size_t)2 * Lk * (d + 8) * 2 + (size_t)kEsimWaves * 3 * 2 * d * 4;
     hipStream_t st = rf_stream(stream);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = (int)std::min<int64_t>(batch, cus);  // persistent: one 8-wave workgroup per CU
 #define RF_ESIM_LAUNCH(F16, D)                                                                                     \
     {                                                                                                              \
         auto kern = esim_kernel<F16, D>;                                                                           \
-        int rc = launch_big_lds(kern, batch, lds, st, "esim_kernel");                                              \
+        int rc = launch_big_lds(kern, grid, lds, st, "esim_kernel");                                               \
         if (rc) return rc;                                                                                         \
-        hipLaunchKernelGGL(kern, dim3(batch), dim3(256), lds, st, (const uint16_t*)q, (const uint16_t*)a, L,       \
-                           ex_stride, ld, out, out_stride, out_off, att_out);                                      \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsimWaves * 64), lds, st, (const uint16_t*)q, (const uint16_t*)a, \
+                           batch, L, ex_stride, ld, out, out_stride, out_off, att_out);                            \
     }
     if (dtype == RF_DTYPE_BF16) {
         if (d == 64) RF_ESIM_LAUNCH(false, 64) else RF_ESIM_LAUNCH(false, 128)
