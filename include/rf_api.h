@@ -202,6 +202,23 @@ size_t rf_bucketize_ws_bytes(int64_t n, int32_t nranks);
 int rf_bucketize_owner(const int64_t* rows, int64_t n, int32_t nranks, int32_t* counts, int32_t* perm,
                        int64_t* local_rows, void* ws, size_t ws_bytes, void* stream);
 
+/*
+ * Global fused-table rows of every token, both tables: rows_out[2*t + k] = row_base[k] + bucket_k(token t)
+ * (the index half of rf_fused_hash_embed_fwd; the requester side of the sharded lookup).
+ */
+int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                 const int32_t* bag_off, int32_t batch, int64_t* rows_out, void* stream);
+
+/*
+ * Pool pre-gathered rows with exactly the semantics and accumulation order of rf_fused_hash_embed_fwd
+ * (so a sharded lookup is bit-identical to the single-GPU one). `gathered` holds [2*n_tok + 2*n_slots][dim]:
+ * row 2*t + k = the table-k row of token t, row 2*n_tok + 2*s + k = the padding row of slot s, table k
+ * (bin 0 of the segment, or the bin of b"" when mask_empty == 0). Descriptors supply combiner, out_off, dim.
+ */
+int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
+                     int32_t batch, int64_t n_tok, const void* gathered, int32_t dtype, int32_t dim, void* out,
+                     int32_t out_dtype, int64_t out_stride, int32_t flags, void* stream);
+
 /* Gather whole rows: out[i] = table[rows[i]] (owner side of the sharded lookup). */
 int rf_gather_rows(const int64_t* rows, int64_t n, const void* table, int32_t dtype, int64_t table_rows,
                    int32_t dim, void* out, void* stream);

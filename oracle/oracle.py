@@ -75,6 +75,10 @@ def lib():
         L.orf_fused_hash_embed_fwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i32, i64, i32, vp, i32, i64, i32, vp, i32]
         L.orf_embedding_bag_fwd.restype = ctypes.c_int
         L.orf_embedding_bag_fwd.argtypes = [vp, i32, i32, i64, vp, i32, i64, i32, i32, vp, i32, i64, i64]
+        L.orf_hash_rows.restype = None
+        L.orf_hash_rows.argtypes = [vp, i32, vp, vp, vp, i32, vp]
+        L.orf_pool_rows_fwd.restype = ctypes.c_int
+        L.orf_pool_rows_fwd.argtypes = [vp, i32, vp, vp, i32, i64, vp, i32, i32, vp, i32, i64, i32]
         L.orf_bucketize_owner.restype = None
         L.orf_bucketize_owner.argtypes = [vp, i64, i32, vp, vp, vp]
         _lib = L
@@ -151,6 +155,32 @@ def embedding_bag(ids: np.ndarray, table: np.ndarray, combiner: str, row_base: i
                                      _p(out), out_dtype, width, 0)
     if rc != 0:
         raise RuntimeError(f"oracle embedding_bag failed rc={rc}")
+    return out
+
+
+def hash_rows(slots, tok_bytes, tok_off, bag_off, batch) -> np.ndarray:
+    """rf_hash_rows restated: int64 [2 * n_tok] global fused-table rows."""
+    slots = np.ascontiguousarray(slots, dtype=SLOT_DTYPE)
+    tok_bytes = np.ascontiguousarray(tok_bytes, dtype=np.uint8)
+    if tok_bytes.size == 0:
+        tok_bytes = np.zeros(1, np.uint8)
+    tok_off = np.ascontiguousarray(tok_off, dtype=np.int32)
+    bag_off = np.ascontiguousarray(bag_off, dtype=np.int32)
+    out = np.zeros(2 * (len(tok_off) - 1), np.int64)
+    lib().orf_hash_rows(_p(slots), len(slots), _p(tok_bytes), _p(tok_off), _p(bag_off), batch, _p(out))
+    return out
+
+
+def pool_rows(slots, bag_off, lmax, batch, n_tok, gathered, dim, out_stride, flags=0):
+    """rf_pool_rows_fwd restated (fp32 gathered rows -> fp32 out)."""
+    slots = np.ascontiguousarray(slots, dtype=SLOT_DTYPE)
+    gathered = np.ascontiguousarray(gathered, dtype=np.float32)
+    out = np.zeros((batch, out_stride), np.float32)
+    rc = lib().orf_pool_rows_fwd(_p(slots), len(slots), _p(np.ascontiguousarray(bag_off, np.int32)),
+                                 _p(np.ascontiguousarray(lmax, np.int32)), batch, n_tok, _p(gathered), DT_F32, dim,
+                                 _p(out), DT_F32, out_stride, flags)
+    if rc:
+        raise RuntimeError(f"oracle pool_rows failed rc={rc}")
     return out
 
 

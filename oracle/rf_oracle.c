@@ -303,3 +303,60 @@ void orf_bucketize_owner(const int64_t* rows, int64_t n, int32_t nranks, int32_t
     }
     free(start);
 }
+
+/* rf_hash_rows restated: rows_out[2t + k] = row_base[k] + bucket_k(token t). */
+void orf_hash_rows(const rf_slot_desc* slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                   const int32_t* bag_off, int32_t batch, int64_t* rows_out) {
+    for (int64_t u = 0; u < (int64_t)batch * n_slots; ++u) {
+        const rf_slot_desc* sd = &slots[u % n_slots];
+        for (int32_t t = bag_off[u]; t < bag_off[u + 1]; ++t)
+            for (int k = 0; k < 2; ++k)
+                rows_out[2 * (int64_t)t + k] = sd->row_base[k] + orf_hash_bucket(sd->salt[k], sd->salt[k], tok_bytes + tok_off[t],
+                                                                                tok_off[t + 1] - tok_off[t], sd->num_bins,
+                                                                                sd->mask_empty);
+    }
+}
+
+/* rf_pool_rows_fwd restated: the pooling of orf_fused_hash_embed_fwd over pre-gathered rows (token t,
+   table k -> row 2t + k; pad row of slot s, table k -> row 2*n_tok + 2s + k). */
+int orf_pool_rows_fwd(const rf_slot_desc* slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
+                      int32_t batch, int64_t n_tok, const void* gathered, int32_t dtype, int32_t dim, void* out,
+                      int32_t out_dtype, int64_t out_stride, int32_t flags) {
+    int32_t maxL = 1;
+    for (int32_t s = 0; s < n_slots; ++s) if (lmax[s] > maxL) maxL = lmax[s];
+    for (int64_t u = 0; u < (int64_t)batch * n_slots; ++u)
+        if (bag_off[u + 1] - bag_off[u] > maxL) maxL = bag_off[u + 1] - bag_off[u];
+    int64_t* rows = (int64_t*)malloc(sizeof(int64_t) * (size_t)maxL);
+    float* acc = (float*)malloc(sizeof(float) * (size_t)dim);
+    const int64_t nrows = 2 * n_tok + 2 * (int64_t)n_slots;
+    int status = 0;
+    for (int32_t b = 0; b < batch && !status; ++b)
+        for (int32_t s = 0; s < n_slots && !status; ++s) {
+            const rf_slot_desc* sd = &slots[s];
+            const int64_t u = (int64_t)b * n_slots + s;
+            const int32_t t0 = bag_off[u], len = bag_off[u + 1] - t0;
+            const int32_t L = (flags & RF_FLAG_MASK_PADDING) ? len : (lmax[s] > len ? lmax[s] : len);
+            for (int k = 0; k < 2; ++k) {
+                for (int32_t l = 0; l < len; ++l) rows[l] = 2 * (int64_t)(t0 + l) + k;
+                const int64_t pad = 2 * n_tok + 2 * (int64_t)s + k;
+                char* ob = (char*)out;
+                if (sd->combiner == RF_COMB_NULL) {
+                    for (int32_t l = 0; l < L; ++l)
+                        for (int32_t d = 0; d < dim; ++d)
+                            store_elem(ob, out_dtype, (int64_t)b * out_stride + sd->out_off + ((int64_t)k * L + l) * dim + d,
+                                       (l >= len && (flags & RF_FLAG_MASK_PADDING)) ? 0.0f
+                                                                                   : load_elem(gathered, dtype, (l < len ? rows[l] : pad) * dim + d));
+                    continue;
+                }
+                if (L == 0 && (flags & RF_FLAG_MASK_PADDING))
+                    memset(acc, 0, sizeof(float) * (size_t)dim);
+                else
+                    status = pool_bag(gathered, dtype, nrows, dim, rows, len, L, pad, sd->combiner, acc);
+                for (int32_t d = 0; d < dim; ++d)
+                    store_elem(ob, out_dtype, (int64_t)b * out_stride + sd->out_off + (int64_t)k * dim + d, acc[d]);
+            }
+        }
+    free(rows);
+    free(acc);
+    return status;
+}

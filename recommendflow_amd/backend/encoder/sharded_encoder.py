@@ -1,0 +1,233 @@
+"""Row-sharded fused sparse encoder: the fused table of one tower split over P ranks.
+
+The reference never shards a table: it runs MirroredStrategy (one full replica per device, gradients
+all-reduced; run/train.py) and its largest table is what fits one device. Here the fused
+table of `FusedSparseEncoder` is row-sharded over the P ranks of the job so a 1e9 x 128 table (512 GB
+fp32) spans 8 x 288 GB of HBM:
+
+* owner(g) = g mod P, local(g) = g div P (round-robin rows: hot low bins and hot slots spread evenly);
+* shard r holds rows g = r, r + P, ... and is initialised with the same counter-based generator as the
+  unsharded table (rf_table_init_uniform, row0 = r, row_stride = P), so for a given seed every P
+  produces the same logical table, and the pooled output is bit-identical to the single-GPU kernel.
+
+One forward per rank (requester) is four C-ABI launches and two all-to-alls:
+
+  route   : rf_hash_rows (2 global rows per token) + 2*S padding rows -> rf_bucketize_owner
+            (stable owner-major permutation, local row ids, per-owner counts)
+  exchange: all_to_all(counts); all_to_all_single(local ids)           -> owners
+  serve   : rf_gather_rows on the local shard                           (owner side)
+  exchange: all_to_all_single(row vectors)                              -> requesters
+  combine : un-permute (index_copy) + rf_pool_rows_fwd                  (same pooling code and order
+            as rf_fused_hash_embed_fwd, so the result is bit-identical)
+
+The communication object is pluggable: `TorchDistComm` (torch.distributed; RCCL on the GPU box, gloo in
+the CPU tests) and `simulate_sharded_forward` (P shards in one process, for single-GPU parity tests).
+The kernel ops are pluggable the same way (`GpuShardOps` = librf; the CPU tests pass oracle-backed ops
+from tests/, never the product).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ...runtime import lib as L
+from ...runtime.batch import SparseBatch, from_lists
+from .sparse_encoder import POOLED, SLOT_DTYPE, SlotSpec
+
+
+def shard_rows(total_rows: int, rank: int, nranks: int) -> int:
+    """Rows of the global table owned by `rank` (g = rank, rank + P, ...)."""
+    return max(0, (total_rows - rank + nranks - 1) // nranks)
+
+
+def build_slot_desc(slots: Sequence[SlotSpec], dim: int, row_base0: int = 0):
+    """Descriptors of the fused layout (identical to FusedSparseEncoder's)."""
+    desc = np.zeros(len(slots), SLOT_DTYPE)
+    base = int(row_base0)
+    for i, sp in enumerate(slots):
+        if sp.num_bins is None or sp.num_bins <= 0:
+            raise ValueError("`num_bins` cannot be `None` or non-positive values.")
+        if sp.combiner not in POOLED:
+            raise ValueError(f"Do not support combiner = '{sp.combiner}' in a sharded encoder")
+        desc[i]["row_base"] = (base, base + sp.num_bins)
+        desc[i]["num_bins"] = sp.num_bins
+        desc[i]["salt"] = (sp.seeds[0] & (2 ** 64 - 1), sp.seeds[1] & (2 ** 64 - 1))
+        desc[i]["out_off"] = i * 2 * dim
+        desc[i]["dim"] = dim
+        desc[i]["combiner"] = L.COMB[sp.combiner]
+        desc[i]["mask_empty"] = int(sp.mask_empty)
+        base += 2 * sp.num_bins
+    return desc, base
+
+
+class GpuShardOps:
+    """The four device stages of the sharded lookup, through librf (include/rf_api.h)."""
+
+    def __init__(self, device="cuda"):
+        L.load()
+        L.require_gpu()
+        self.device = torch.device(device)
+
+    def prepare_batch(self, batch: SparseBatch) -> SparseBatch:
+        return batch if batch.is_device() else batch.to(self.device)
+
+    def upload_desc(self, desc: np.ndarray):
+        return torch.from_numpy(desc.view(np.uint8).copy()).to(self.device)
+
+    def init_shard(self, rows: int, dim: int, dtype, rank: int, nranks: int, seed: int, lo: float, hi: float):
+        t = torch.empty((max(rows, 1), dim), dtype=dtype, device=self.device)
+        if rows:
+            L.call("rf_table_init_uniform", L.ptr(t), L.torch_dtype_code(dtype), rows, dim, rank, nranks, seed, lo, hi,
+                   L.stream_ptr(None))
+        return t[:rows]
+
+    def hash_rows(self, desc, n_slots: int, batch: SparseBatch) -> torch.Tensor:
+        out = torch.empty(max(2 * batch.n_tokens, 1), dtype=torch.int64, device=self.device)
+        L.call("rf_hash_rows", L.ptr(desc), n_slots, L.ptr(batch.tok_bytes), L.ptr(batch.tok_off), L.ptr(batch.bag_off),
+               batch.batch, L.ptr(out), L.stream_ptr(None))
+        return out[: 2 * batch.n_tokens]
+
+    def bucketize(self, rows: torch.Tensor, nranks: int):
+        n = rows.numel()
+        counts = torch.empty(nranks, dtype=torch.int32, device=self.device)
+        perm = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        local = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        ws_bytes = L.load().rf_bucketize_ws_bytes(n, nranks)
+        ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=self.device)
+        L.call("rf_bucketize_owner", L.ptr(rows), n, nranks, L.ptr(counts), L.ptr(perm), L.ptr(local), L.ptr(ws),
+               ws_bytes, L.stream_ptr(None))
+        return counts, perm[:n], local[:n]
+
+    def gather(self, shard: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
+        n = local.numel()
+        out = torch.empty((max(n, 1), shard.shape[1]), dtype=shard.dtype, device=self.device)
+        if n:
+            L.call("rf_gather_rows", L.ptr(local), n, L.ptr(shard), L.torch_dtype_code(shard.dtype), shard.shape[0],
+                   shard.shape[1], L.ptr(out), L.stream_ptr(None))
+        return out[:n]
+
+    def pool(self, desc, n_slots: int, batch: SparseBatch, gathered: torch.Tensor, out: torch.Tensor, flags: int):
+        L.call("rf_pool_rows_fwd", L.ptr(desc), n_slots, L.ptr(batch.bag_off), L.ptr(batch.lmax), batch.batch,
+               batch.n_tokens, L.ptr(gathered), L.torch_dtype_code(gathered.dtype), gathered.shape[1], L.ptr(out),
+               L.torch_dtype_code(out.dtype), out.stride(0), flags, L.stream_ptr(None))
+        return out
+
+
+class TorchDistComm:
+    """Exchange over torch.distributed: RCCL on MI355X (xGMI point-to-point), gloo in the CPU tests."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def exchange_counts(self, counts: torch.Tensor) -> torch.Tensor:
+        recv = torch.empty_like(counts)
+        self.dist.all_to_all_single(recv, counts, group=self.group)
+        return recv
+
+    def exchange(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]) -> torch.Tensor:
+        out = torch.empty((sum(recv_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        self.dist.all_to_all_single(out, x.contiguous(), output_split_sizes=recv_splits, input_split_sizes=send_splits,
+                                    group=self.group)
+        return out
+
+
+@dataclass
+class RouteState:
+    counts: List[int]          # rows this rank requests from each owner
+    perm: torch.Tensor         # int32 [n]: request i (owner-major) came from position perm[i]
+    local: torch.Tensor        # int64 [n]: local row id at its owner, owner-major
+    n_requests: int
+
+
+class ShardedFusedEncoder(torch.nn.Module):
+    """One rank's view of a row-sharded fused table (same slots / output as FusedSparseEncoder)."""
+
+    def __init__(self, slots: Sequence[SlotSpec], dim: int, rank: int, nranks: int, comm=None, ops=None,
+                 table_dtype=torch.float32, out_dtype=None, seed: int = 0, mask_padding: bool = False,
+                 init_range=(-0.05, 0.05), device="cuda"):
+        super().__init__()
+        if not slots:
+            raise ValueError("ShardedFusedEncoder needs at least one slot")
+        if not (0 <= rank < nranks):
+            raise ValueError(f"rank {rank} outside [0, {nranks})")
+        self.slots = list(slots)
+        self.dim = int(dim)
+        self.rank, self.nranks = int(rank), int(nranks)
+        self.comm = comm
+        self.ops = ops if ops is not None else GpuShardOps(device)
+        self.table_dtype = table_dtype
+        self.out_dtype = out_dtype or table_dtype
+        self.mask_padding = bool(mask_padding)
+        self.host_desc, self.table_rows = build_slot_desc(self.slots, self.dim)
+        self.out_width = 2 * self.dim * len(self.slots)
+        self.desc = self.ops.upload_desc(self.host_desc)
+        self.local_rows = shard_rows(self.table_rows, self.rank, self.nranks)
+        self.shard = self.ops.init_shard(self.local_rows, self.dim, table_dtype, self.rank, self.nranks, int(seed),
+                                         *init_range)
+        # padding rows of every slot and table: the rows the empty string hashes to (pad positions gather
+        # the bin of b"": bin 0 with mask_value="", the SipHash bin otherwise), computed by rf_hash_rows
+        # on a one-example batch of empty tokens so the rule lives in one place.
+        S = len(self.slots)
+        empty = self.ops.prepare_batch(from_lists([[[b""] for _ in range(S)]]))
+        self.pad_rows = self.ops.hash_rows(self.desc, S, empty)
+
+    # -- the three local stages -------------------------------------------------------------------
+    def route(self, batch: SparseBatch) -> RouteState:
+        rows = self.ops.hash_rows(self.desc, len(self.slots), batch)
+        req = torch.cat([rows, self.pad_rows])
+        counts, perm, local = self.ops.bucketize(req, self.nranks)
+        return RouteState([int(c) for c in counts.cpu().tolist()], perm, local, req.numel())
+
+    def serve(self, local_rows: torch.Tensor) -> torch.Tensor:
+        if local_rows.numel() and int(local_rows.max()) >= self.local_rows:
+            raise IndexError("row request beyond this rank's shard")
+        return self.ops.gather(self.shard, local_rows)
+
+    def combine(self, batch: SparseBatch, st: RouteState, back: torch.Tensor, out: Optional[torch.Tensor] = None):
+        gathered = torch.empty_like(back)
+        gathered.index_copy_(0, st.perm.long(), back)
+        if out is None:
+            out = torch.empty((batch.batch, self.out_width), dtype=self.out_dtype, device=back.device)
+        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        return self.ops.pool(self.desc, len(self.slots), batch, gathered, out, flags)
+
+    def forward(self, batch: SparseBatch, out: Optional[torch.Tensor] = None):
+        if self.comm is None:
+            raise RuntimeError("ShardedFusedEncoder.forward needs a comm (TorchDistComm); "
+                               "use simulate_sharded_forward for in-process shards")
+        if batch.n_slots != len(self.slots):
+            raise ValueError(f"batch has {batch.n_slots} slots, encoder {len(self.slots)}")
+        batch = self.ops.prepare_batch(batch)
+        st = self.route(batch)
+        counts_t = torch.tensor(st.counts, dtype=torch.int64, device=st.local.device)
+        recv_counts = [int(c) for c in self.comm.exchange_counts(counts_t).cpu().tolist()]
+        wanted = self.comm.exchange(st.local, st.counts, recv_counts)        # ids other ranks want from me
+        vec = self.serve(wanted)
+        back = self.comm.exchange(vec, recv_counts, st.counts)               # my rows, owner-major
+        return self.combine(batch, st, back, out)
+
+
+def simulate_sharded_forward(encoders: Sequence[ShardedFusedEncoder], batches: Sequence[SparseBatch]):
+    """All P ranks in one process (no collective): the exchange done by slicing, for parity tests."""
+    P = len(encoders)
+    batches = [enc.ops.prepare_batch(b) for enc, b in zip(encoders, batches)]
+    states = [enc.route(b) for enc, b in zip(encoders, batches)]
+    offs = [np.concatenate([[0], np.cumsum(st.counts)]) for st in states]
+    vec = []
+    for o in range(P):
+        wanted = torch.cat([states[r].local[offs[r][o]: offs[r][o + 1]] for r in range(P)])
+        vec.append(encoders[o].serve(wanted))
+    outs = []
+    for r in range(P):
+        pos = [int(sum(states[q].counts[o] for q in range(r))) for o in range(P)]
+        back = torch.cat([vec[o][pos[o]: pos[o] + states[r].counts[o]] for o in range(P)])
+        outs.append(encoders[r].combine(batches[r], states[r], back))
+    return outs

@@ -150,6 +150,25 @@ __global__ __launch_bounds__(256) void table_init_kernel(TT* __restrict__ table,
     }
 }
 
+// rf_hash_rows: thread per (example, slot) unit, both salts over one read of each token
+__global__ __launch_bounds__(256) void hash_rows_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
+                                                        const uint8_t* __restrict__ tok_bytes,
+                                                        const int32_t* __restrict__ tok_off,
+                                                        const int32_t* __restrict__ bag_off, int64_t n_units,
+                                                        int64_t* __restrict__ rows_out) {
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += (int64_t)gridDim.x * blockDim.x) {
+        const rf_slot_desc* sd = slots + (int)(u % n_slots);
+        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
+        for (int t = bag_off[u]; t < bag_off[u + 1]; ++t) {
+            const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
+            uint64_t h0, h1;
+            siphash24x2_dev(sd->salt[0], sd->salt[1], tok_bytes + b0, n, h0, h1);
+            rows_out[2 * (int64_t)t] = rb0 + bucket_from_hash(h0, n, nbins, sd->mask_empty);
+            rows_out[2 * (int64_t)t + 1] = rb1 + bucket_from_hash(h1, n, nbins, sd->mask_empty);
+        }
+    }
+}
+
 int grid_for(int64_t work_items, int per_block, int cap = 256 * 16) {
     int64_t g = (work_items + per_block - 1) / per_block;
     return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
@@ -213,6 +232,45 @@ extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_sl
                                 out_dtype, out_stride, flags, idx_out, max_lpr, grid, st);
     return launch_fused_bf16(d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table, table_rows, dim, out,
                              out_dtype, out_stride, flags, idx_out, max_lpr, grid, st);
+}
+
+extern "C" int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                            const int32_t* tok_off, const int32_t* bag_off, int32_t batch, int64_t* rows_out,
+                            void* stream) {
+    RF_REQUIRE(n_slots >= 1 && batch >= 0, "rf_hash_rows: need n_slots >= 1, batch >= 0");
+    const int64_t n_units = (int64_t)batch * n_slots;
+    if (n_units == 0) return RF_OK;
+    RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && rows_out, "rf_hash_rows: null pointer");
+    hipLaunchKernelGGL(hash_rows_kernel, dim3(grid_for(n_units, 256)), dim3(256), 0, rf_stream(stream), d_slots,
+                       n_slots, tok_bytes, tok_off, bag_off, n_units, rows_out);
+    return rf_check_launch("hash_rows_kernel");
+}
+
+extern "C" int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off,
+                                const int32_t* lmax, int32_t batch, int64_t n_tok, const void* gathered, int32_t dtype,
+                                int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
+                                void* stream) {
+    RF_REQUIRE(n_slots >= 1 && batch >= 0 && n_tok >= 0, "rf_pool_rows_fwd: need n_slots >= 1, batch, n_tok >= 0");
+    RF_REQUIRE(dtype == RF_DTYPE_F32 || dtype == RF_DTYPE_BF16, "rf_pool_rows_fwd: dtype must be F32 or BF16");
+    RF_REQUIRE(out_dtype == RF_DTYPE_F32 || out_dtype == RF_DTYPE_BF16, "rf_pool_rows_fwd: out dtype must be F32 or BF16");
+    const int epv = dtype == RF_DTYPE_F32 ? 4 : 8;
+    RF_REQUIRE(dim > 0 && dim % epv == 0 && out_stride % epv == 0, "rf_pool_rows_fwd: dim/out_stride must be multiples of %d", epv);
+    RF_REQUIRE((flags & ~RF_FLAG_MASK_PADDING) == 0, "rf_pool_rows_fwd: only RF_FLAG_MASK_PADDING is accepted");
+    const int64_t rows = 2 * n_tok + 2 * (int64_t)n_slots;
+    RF_REQUIRE(rows <= (int64_t)0xffffffff, "rf_pool_rows_fwd: too many rows");
+    RF_REQUIRE(((uintptr_t)gathered & 15) == 0 && ((uintptr_t)out & 15) == 0, "rf_pool_rows_fwd: buffers must be 16-byte aligned");
+    const int64_t n_units = (int64_t)batch * n_slots;
+    if (n_units == 0) return RF_OK;
+    RF_REQUIRE(d_slots && bag_off && lmax && gathered && out, "rf_pool_rows_fwd: null pointer");
+    const int64_t items = (int64_t)n_slots * ((batch + kUnits - 1) / kUnits);
+    const int grid = grid_for(items, kWaves, 256 * 32 * 2);
+    hipStream_t st = rf_stream(stream);
+    const int fl = flags | kFlagPregathered;
+    if (dtype == RF_DTYPE_F32)
+        return launch_fused_f32(d_slots, n_slots, nullptr, nullptr, bag_off, lmax, n_units, gathered, rows, dim, out,
+                                out_dtype, out_stride, fl, nullptr, kDefaultMaxLpr, grid, st);
+    return launch_fused_bf16(d_slots, n_slots, nullptr, nullptr, bag_off, lmax, n_units, gathered, rows, dim, out,
+                             out_dtype, out_stride, fl, nullptr, kDefaultMaxLpr, grid, st);
 }
 
 extern "C" int rf_embedding_bag_fwd(const int64_t* ids, int32_t batch, int32_t len, int64_t row_base, const void* table,

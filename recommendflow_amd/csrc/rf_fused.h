@@ -21,6 +21,7 @@ constexpr int kWaves = RF_FUSED_WAVES;
 constexpr int kCap = 768;    // tokens per wave item kept in the LDS row bucket (more: hashed inline)
 constexpr int kUnits = 64;   // examples per wave item (one slot per item)
 constexpr int kDefaultMaxLpr = 16;  // lanes per row cap (tuned on MI355X)
+constexpr int kFlagPregathered = 1 << 15;  // internal: rf_pool_rows_fwd
 
 template <typename T>
 struct Elem {
@@ -132,6 +133,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
     const bool emit = (flags & RF_FLAG_EMIT_IDX) != 0 && idx_out != nullptr;
     const bool abl_nohash = (flags & (1 << 12)) != 0, abl_nopool = (flags & (1 << 13)) != 0,
                abl_nopad = (flags & (1 << 14)) != 0;  // diagnostic ablations (tools/kbench.py)
+    // rf_pool_rows_fwd: `table` holds pre-gathered rows (token t, table k -> row 2t + k; pad rows after)
+    const bool pregathered = (flags & kFlagPregathered) != 0;
     const int batch = (int)(n_units / n_slots);
     const int nbb = (batch + kUnits - 1) / kUnits;
     const int64_t n_items = (int64_t)n_slots * nbb;
@@ -156,14 +159,18 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         const int mask_empty = sd->mask_empty;
         const int64_t out_off = sd->out_off;
         const int lm = lmax[s];
-        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
+        const bool ok = pregathered || (rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows);
         // padded position = b"": bin 0 with mask_value "", else the bin of b""
         int64_t pb0 = 0, pb1 = 0;
-        if (!mask_empty) {
+        if (!mask_empty && !pregathered) {
             pb0 = (int64_t)(siphash24_dev(salt0, salt0, tok_bytes, 0) % (uint64_t)nbins);
             pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
         }
-        const uint32_t pad0 = ok ? (uint32_t)(rb0 + pb0) : 0u, pad1 = ok ? (uint32_t)(rb1 + pb1) : 0u;
+        uint32_t pad0 = ok ? (uint32_t)(rb0 + pb0) : 0u, pad1 = ok ? (uint32_t)(rb1 + pb1) : 0u;
+        if (pregathered) {  // pad rows follow the 2 * n_tok token rows
+            pad0 = (uint32_t)(table_rows - 2 * (int64_t)n_slots + 2 * s);
+            pad1 = pad0 + 1;
+        }
 
         // ---- phase 1a: unit token ranges, wave prefix scan -> item-local token layout ----
         int g0 = 0, len = 0;
@@ -190,13 +197,25 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         // (with RF_FLAG_EMIT_IDX every token of the item is hashed here, so ids past the bucket are
         //  emitted even when the pooling never visits them — first/last/null)
         const int nh = min(ntok, kCap);
+        if (pregathered) {
+            for (int i = lane; i < nh; i += 64) {
+                int lo = 0, hi = nu - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_loc[wave][mid] <= i) lo = mid; else hi = mid - 1;
+                }
+                const uint32_t t = (uint32_t)(s_gbeg[wave][lo] + (i - s_loc[wave][lo]));
+                s_row[wave][0][i] = 2 * t;
+                s_row[wave][1][i] = 2 * t + 1;
+            }
+        }
         if (abl_nohash) {
             for (int i = lane; i < nh; i += 64) {
                 s_row[wave][0][i] = (uint32_t)(((uint64_t)i * 2654435761u + item) % (uint64_t)table_rows);
                 s_row[wave][1][i] = (uint32_t)(((uint64_t)i * 40503u + 7u + item) % (uint64_t)table_rows);
             }
         }
-        const int nhash = abl_nohash ? 0 : (emit ? ntok : nh);
+        const int nhash = (abl_nohash || pregathered) ? 0 : (emit ? ntok : nh);
         for (int i = lane; i < nhash; i += 64) {
             int lo = 0, hi = nu - 1;  // unit of item-local token i: last j with s_loc[j] <= i
             while (lo < hi) {
@@ -398,11 +417,17 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     start_unit();
                 }
                 const int t = s_gbeg[wave][j] + (i - ubeg);
-                const int tb = tok_off[t], n = tok_off[t + 1] - tb;
-                uint64_t h0, h1;
-                siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
-                const uint32_t r0 = ok ? (uint32_t)(rb0 + bucket_from_hash(h0, n, nbins, mask_empty)) : 0u;
-                const uint32_t r1 = ok ? (uint32_t)(rb1 + bucket_from_hash(h1, n, nbins, mask_empty)) : 0u;
+                uint32_t r0, r1;
+                if (pregathered) {
+                    r0 = 2u * (uint32_t)t;
+                    r1 = r0 + 1;
+                } else {
+                    const int tb = tok_off[t], n = tok_off[t + 1] - tb;
+                    uint64_t h0, h1;
+                    siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
+                    r0 = ok ? (uint32_t)(rb0 + bucket_from_hash(h0, n, nbins, mask_empty)) : 0u;
+                    r1 = ok ? (uint32_t)(rb1 + bucket_from_hash(h1, n, nbins, mask_empty)) : 0u;
+                }
                 uint4 v[2][CPL];
 #pragma unroll
                 for (int cc = 0; cc < CPL; ++cc) {

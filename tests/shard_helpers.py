@@ -1,0 +1,70 @@
+"""Oracle-backed stage ops for the sharded-lookup tests (test infrastructure; the product uses GpuShardOps).
+
+Each method restates the librf stage it stands in for (oracle/rf_oracle.c: orf_hash_rows,
+orf_bucketize_owner, orf_pool_rows_fwd, orf_table_init_uniform), so ShardedFusedEncoder's routing,
+exchange and un-permute logic can run on CPU ranks over gloo.
+"""
+import os
+
+import numpy as np
+import torch
+
+from oracle import oracle as O
+from recommendflow_amd.backend.encoder.sparse_encoder import SlotSpec
+from recommendflow_amd.runtime.batch import synthetic_batch
+
+
+class OracleShardOps:
+    device = torch.device("cpu")
+
+    def prepare_batch(self, batch):
+        return batch.numpy()
+
+    def upload_desc(self, desc):
+        return np.ascontiguousarray(desc)
+
+    def init_shard(self, rows, dim, dtype, rank, nranks, seed, lo, hi):
+        assert dtype == torch.float32
+        return torch.from_numpy(O.table_init_uniform(rows, dim, seed=seed, row0=rank, row_stride=nranks, lo=lo, hi=hi))
+
+    def hash_rows(self, desc, n_slots, batch):
+        return torch.from_numpy(O.hash_rows(desc, batch.tok_bytes, batch.tok_off, batch.bag_off, batch.batch))
+
+    def bucketize(self, rows, nranks):
+        c, p, l = O.bucketize_owner(rows.numpy(), nranks)
+        return torch.from_numpy(c), torch.from_numpy(p), torch.from_numpy(l)
+
+    def gather(self, shard, local):
+        return shard[local]
+
+    def pool(self, desc, n_slots, batch, gathered, out, flags):
+        res = O.pool_rows(desc, batch.bag_off, batch.lmax, batch.batch, batch.n_tokens, gathered.numpy(),
+                          gathered.shape[1], out.shape[1], flags)
+        out.copy_(torch.from_numpy(res))
+        return out
+
+
+def small_slots(n=12, seed=0):
+    rng = np.random.default_rng(seed)
+    comb = ["sum", "avg", "max", "min", "first", "last"]
+    return [SlotSpec(f"s{i}", int(rng.integers(50, 3000)), (2022 + i, 2029 + i), comb[i % 6], mask_empty=(i % 5 != 3))
+            for i in range(n)]
+
+
+def rank_batch(rank, B=24, n=12):
+    return synthetic_batch(B, [i % 3 == 0 for i in range(n)], seed=100 + rank, id_max=5000, max_len=9)
+
+
+def dist_worker(rank, world, port, dim, seed, result_dir):
+    import torch.distributed as dist
+
+    from recommendflow_amd.backend.encoder.sharded_encoder import ShardedFusedEncoder, TorchDistComm
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        enc = ShardedFusedEncoder(small_slots(), dim, rank, world, comm=TorchDistComm(), ops=OracleShardOps(),
+                                  seed=seed, device="cpu")
+        out = enc(rank_batch(rank))
+        np.save(os.path.join(result_dir, f"out{rank}.npy"), out.numpy())
+    finally:
+        dist.destroy_process_group()
