@@ -41,6 +41,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     p.add_argument("--uniform", action="store_true", help="uniform ids instead of Zipf(1.1)")
     p.add_argument("--no-extras", action="store_true", help="skip the cfg3 ESIM / cfg2 DSSM full-forward lines")
+    p.add_argument("--no-sharded", action="store_true", help="skip the cfg4 row-sharded extra")
+    p.add_argument("--shard-rows", type=int, default=125_000_000, help="cfg4 weak scaling: fused-table rows per GPU")
+    p.add_argument("--shard-dim", type=int, default=128)
+    p.add_argument("--shard-batch", type=int, default=8192, help="cfg4: examples per GPU (65536 at P=8)")
     return p.parse_args()
 
 
@@ -104,6 +108,12 @@ def main():
     achieved = bytes_per_launch / avg_kern_s / 1e9
     n_tok = sum(h.n_tokens for h in host) / len(host)
 
+    sharded = None
+    if not args.no_sharded:
+        del dev, out
+        torch.cuda.empty_cache()
+        sharded = bench_sharded(args, specs, multi, rank, world)
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -121,7 +131,8 @@ def main():
 
     extras = None
     if world == 1 and not args.no_extras:
-        del dev, out
+        if args.no_sharded:
+            del dev, out
         torch.cuda.empty_cache()
         extras = {"cfg3_esim_forward": bench_esim(args), "cfg2_dssm_forward": bench_dssm(args, enc, host)}
 
@@ -162,6 +173,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "extras": extras,
+        "cfg4_sharded": sharded,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
@@ -286,6 +298,79 @@ def bench_dssm(args, enc, host):
             "towers_frac_of_157TF_fp32": round(flops / per["fp32_towers"] / 1e9 / 157.3, 4),
             "config": "base_recall_sdpa.yaml: 69 user + 160 ad slots, 10M x 64 fp32 table, towers [1024,512,256] "
                       "selu + BatchNorm fp32"}
+
+
+def bench_sharded(args, specs, multi, rank, world):
+    """cfg4, weak scaling: the cfg2 slot layout over a row-sharded fused fp32 table of
+    shard_rows x P rows x shard_dim (owner = row mod P), shard_batch examples per GPU. One step =
+    route (hash rows + owner bucketize) -> all-to-all ids -> gather local rows -> all-to-all vectors ->
+    un-permute + pool. Bit-identical to the unsharded kernel (tests/test_sharded_gpu.py). All ranks run;
+    value = examples of all ranks / max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+
+    from recommendflow_amd.backend.encoder.sharded_encoder import LocalComm, ShardedFusedEncoder, TorchDistComm
+    from recommendflow_amd.backend.encoder.sparse_encoder import SlotSpec
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    P, B, D = world, args.shard_batch, args.shard_dim
+    S = len(specs)
+    n_bins = args.shard_rows * P // (2 * S)
+    sp = [SlotSpec(s.name, n_bins, s.seeds, s.combiner, s.mask_empty) for s in specs]
+    comm = TorchDistComm() if world > 1 else LocalComm()
+    enc = ShardedFusedEncoder(sp, D, rank, P, comm=comm, seed=2024)
+    batches = [synthetic_batch(B, multi, seed=4321 + 1000 * rank + i).to("cuda") for i in range(2)]
+    out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
+    ev_names = ["route", "a2a_ids", "gather", "a2a_rows", "pool"]
+    st = {}
+
+    def step(i, ev=None):
+        b = batches[i % 2]
+        r = enc.route(b)
+        if ev: ev[1].record()
+        counts_t = torch.tensor(r.counts, dtype=torch.int64, device="cuda")
+        recv = [int(c) for c in comm.exchange_counts(counts_t).cpu().tolist()]
+        wanted = comm.exchange(r.local, r.counts, recv)
+        if ev: ev[2].record()
+        vec = enc.serve(wanted)
+        if ev: ev[3].record()
+        back = comm.exchange(vec, recv, r.counts)
+        if ev: ev[4].record()
+        enc.combine(b, r, back, out)
+        if ev: ev[5].record()
+        st["req"], st["served"] = r.n_requests, int(wanted.shape[0])
+
+    steps = max(5, args.steps // 5)
+    for i in range(3):
+        step(i)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record()
+        step(i, evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    stage = {n: round(sum(e[k].elapsed_time(e[k + 1]) for e in evs) / steps, 4) for k, n in enumerate(ev_names)}
+    row_b = D * 4
+    xgmi = (st["req"] * (8 + row_b)) * (P - 1) / P if P > 1 else 0
+    res = {"examples_per_s": round(B * P * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+           "stage_ms_rank0": stage, "gather_GBs": round(st["served"] * (2 * row_b + 8) / stage["gather"] / 1e6, 1),
+           "a2a_bytes_per_rank_each_way": int(xgmi),
+           "config": f"cfg2 slots ({S}) over a {enc.table_rows}x{D} fp32 fused table row-sharded over {P} GPU(s) "
+                     f"({enc.local_rows} rows/GPU), {B} examples/GPU (global {B * P}), owner = row mod P, "
+                     f"RCCL all_to_all_single for ids and rows, no dedup"}
+    del enc, batches, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def cpu_baseline(enc, hb, budget_s):

@@ -195,12 +195,13 @@ int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int3
 /*
  * Row-sharded tables: route fused-table rows to their owner rank (owner = g mod P, local = g div P).
  * Stage 1 of the sharded lookup: for n global rows, write counts[P] (int32) and a
- * stable owner-major permutation perm[n] (int32) with local_rows[n] (int64) in permuted order.
+ * stable owner-major permutation perm[n] (int32; perm[pos] = source index) with local_rows[n] (int64)
+ * in permuted order, and (if inv_perm != NULL) its inverse inv_perm[i] = pos.
  * ws must hold rf_bucketize_ws_bytes(n, P) bytes.
  */
 size_t rf_bucketize_ws_bytes(int64_t n, int32_t nranks);
 int rf_bucketize_owner(const int64_t* rows, int64_t n, int32_t nranks, int32_t* counts, int32_t* perm,
-                       int64_t* local_rows, void* ws, size_t ws_bytes, void* stream);
+                       int32_t* inv_perm, int64_t* local_rows, void* ws, size_t ws_bytes, void* stream);
 
 /*
  * Global fused-table rows of every token, both tables: rows_out[2*t + k] = row_base[k] + bucket_k(token t)
@@ -214,10 +215,12 @@ int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* to
  * (so a sharded lookup is bit-identical to the single-GPU one). `gathered` holds [2*n_tok + 2*n_slots][dim]:
  * row 2*t + k = the table-k row of token t, row 2*n_tok + 2*s + k = the padding row of slot s, table k
  * (bin 0 of the segment, or the bin of b"" when mask_empty == 0). Descriptors supply combiner, out_off, dim.
+ * row_map (int32 [2*n_tok + 2*n_slots], may be NULL = identity): logical row j is read from gathered row
+ * row_map[j] — pass rf_bucketize_owner's inv_perm to pool straight from the all-to-all receive buffer.
  */
 int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
-                     int32_t batch, int64_t n_tok, const void* gathered, int32_t dtype, int32_t dim, void* out,
-                     int32_t out_dtype, int64_t out_stride, int32_t flags, void* stream);
+                     int32_t batch, int64_t n_tok, const void* gathered, const int32_t* row_map, int32_t dtype,
+                     int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, void* stream);
 
 /* Gather whole rows: out[i] = table[rows[i]] (owner side of the sharded lookup). */
 int rf_gather_rows(const int64_t* rows, int64_t n, const void* table, int32_t dtype, int64_t table_rows,

@@ -78,9 +78,9 @@ def lib():
         L.orf_hash_rows.restype = None
         L.orf_hash_rows.argtypes = [vp, i32, vp, vp, vp, i32, vp]
         L.orf_pool_rows_fwd.restype = ctypes.c_int
-        L.orf_pool_rows_fwd.argtypes = [vp, i32, vp, vp, i32, i64, vp, i32, i32, vp, i32, i64, i32]
+        L.orf_pool_rows_fwd.argtypes = [vp, i32, vp, vp, i32, i64, vp, vp, i32, i32, vp, i32, i64, i32]
         L.orf_bucketize_owner.restype = None
-        L.orf_bucketize_owner.argtypes = [vp, i64, i32, vp, vp, vp]
+        L.orf_bucketize_owner.argtypes = [vp, i64, i32, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -171,13 +171,15 @@ def hash_rows(slots, tok_bytes, tok_off, bag_off, batch) -> np.ndarray:
     return out
 
 
-def pool_rows(slots, bag_off, lmax, batch, n_tok, gathered, dim, out_stride, flags=0):
-    """rf_pool_rows_fwd restated (fp32 gathered rows -> fp32 out)."""
+def pool_rows(slots, bag_off, lmax, batch, n_tok, gathered, dim, out_stride, flags=0, row_map=None):
+    """rf_pool_rows_fwd restated (fp32 gathered rows -> fp32 out; row_map: int32 logical -> gathered row)."""
+    rm = None if row_map is None else np.ascontiguousarray(row_map, np.int32)
     slots = np.ascontiguousarray(slots, dtype=SLOT_DTYPE)
     gathered = np.ascontiguousarray(gathered, dtype=np.float32)
     out = np.zeros((batch, out_stride), np.float32)
     rc = lib().orf_pool_rows_fwd(_p(slots), len(slots), _p(np.ascontiguousarray(bag_off, np.int32)),
-                                 _p(np.ascontiguousarray(lmax, np.int32)), batch, n_tok, _p(gathered), DT_F32, dim,
+                                 _p(np.ascontiguousarray(lmax, np.int32)), batch, n_tok, _p(gathered),
+                                 None if rm is None else _p(rm), DT_F32, dim,
                                  _p(out), DT_F32, out_stride, flags)
     if rc:
         raise RuntimeError(f"oracle pool_rows failed rc={rc}")
@@ -189,8 +191,9 @@ def bucketize_owner(rows: np.ndarray, nranks: int):
     counts = np.zeros(nranks, np.int32)
     perm = np.zeros(len(rows), np.int32)
     local = np.zeros(len(rows), np.int64)
-    lib().orf_bucketize_owner(_p(rows), len(rows), nranks, _p(counts), _p(perm), _p(local))
-    return counts, perm, local
+    inv = np.zeros(len(rows), np.int32)
+    lib().orf_bucketize_owner(_p(rows), len(rows), nranks, _p(counts), _p(perm), _p(inv), _p(local))
+    return counts, perm, local, inv
 
 
 def bf16_to_f32(u16: np.ndarray) -> np.ndarray:

@@ -290,7 +290,7 @@ int orf_embedding_bag_fwd(const int64_t* ids, int32_t batch, int32_t len, int64_
 
 /* Owner routing of the row-sharded table: owner = g mod P, local = g div P, stable. */
 void orf_bucketize_owner(const int64_t* rows, int64_t n, int32_t nranks, int32_t* counts, int32_t* perm,
-                         int64_t* local_rows) {
+                         int32_t* inv_perm, int64_t* local_rows) {
     int64_t* start = (int64_t*)calloc((size_t)nranks + 1, sizeof(int64_t));
     for (int32_t p = 0; p < nranks; ++p) counts[p] = 0;
     for (int64_t i = 0; i < n; ++i) counts[rows[i] % nranks]++;
@@ -299,6 +299,7 @@ void orf_bucketize_owner(const int64_t* rows, int64_t n, int32_t nranks, int32_t
         int32_t p = (int32_t)(rows[i] % nranks);
         int64_t pos = start[p]++;
         perm[pos] = (int32_t)i;
+        if (inv_perm) inv_perm[i] = (int32_t)pos;
         local_rows[pos] = rows[i] / nranks;
     }
     free(start);
@@ -320,8 +321,8 @@ void orf_hash_rows(const rf_slot_desc* slots, int32_t n_slots, const uint8_t* to
 /* rf_pool_rows_fwd restated: the pooling of orf_fused_hash_embed_fwd over pre-gathered rows (token t,
    table k -> row 2t + k; pad row of slot s, table k -> row 2*n_tok + 2s + k). */
 int orf_pool_rows_fwd(const rf_slot_desc* slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
-                      int32_t batch, int64_t n_tok, const void* gathered, int32_t dtype, int32_t dim, void* out,
-                      int32_t out_dtype, int64_t out_stride, int32_t flags) {
+                      int32_t batch, int64_t n_tok, const void* gathered, const int32_t* row_map, int32_t dtype,
+                      int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags) {
     int32_t maxL = 1;
     for (int32_t s = 0; s < n_slots; ++s) if (lmax[s] > maxL) maxL = lmax[s];
     for (int64_t u = 0; u < (int64_t)batch * n_slots; ++u)
@@ -337,8 +338,12 @@ int orf_pool_rows_fwd(const rf_slot_desc* slots, int32_t n_slots, const int32_t*
             const int32_t t0 = bag_off[u], len = bag_off[u + 1] - t0;
             const int32_t L = (flags & RF_FLAG_MASK_PADDING) ? len : (lmax[s] > len ? lmax[s] : len);
             for (int k = 0; k < 2; ++k) {
-                for (int32_t l = 0; l < len; ++l) rows[l] = 2 * (int64_t)(t0 + l) + k;
-                const int64_t pad = 2 * n_tok + 2 * (int64_t)s + k;
+                for (int32_t l = 0; l < len; ++l) {
+                    rows[l] = 2 * (int64_t)(t0 + l) + k;
+                    if (row_map) rows[l] = row_map[rows[l]];
+                }
+                int64_t pad = 2 * n_tok + 2 * (int64_t)s + k;
+                if (row_map) pad = row_map[pad];
                 char* ob = (char*)out;
                 if (sd->combiner == RF_COMB_NULL) {
                     for (int32_t l = 0; l < L; ++l)

@@ -17,8 +17,9 @@ One forward per rank (requester) is four C-ABI launches and two all-to-alls:
   exchange: all_to_all(counts); all_to_all_single(local ids)           -> owners
   serve   : rf_gather_rows on the local shard                           (owner side)
   exchange: all_to_all_single(row vectors)                              -> requesters
-  combine : un-permute (index_copy) + rf_pool_rows_fwd                  (same pooling code and order
-            as rf_fused_hash_embed_fwd, so the result is bit-identical)
+  combine : rf_pool_rows_fwd straight from the receive buffer, reading logical row j at inv_perm[j]
+            (the un-permute is fused into the pooling loads; same pooling code and accumulation order as
+            rf_fused_hash_embed_fwd, so the result is bit-identical)
 
 The communication object is pluggable: `TorchDistComm` (torch.distributed; RCCL on the GPU box, gloo in
 the CPU tests) and `simulate_sharded_forward` (P shards in one process, for single-GPU parity tests).
@@ -94,12 +95,13 @@ class GpuShardOps:
         n = rows.numel()
         counts = torch.empty(nranks, dtype=torch.int32, device=self.device)
         perm = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        inv = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         local = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
         ws_bytes = L.load().rf_bucketize_ws_bytes(n, nranks)
         ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=self.device)
-        L.call("rf_bucketize_owner", L.ptr(rows), n, nranks, L.ptr(counts), L.ptr(perm), L.ptr(local), L.ptr(ws),
+        L.call("rf_bucketize_owner", L.ptr(rows), n, nranks, L.ptr(counts), L.ptr(perm), L.ptr(inv), L.ptr(local), L.ptr(ws),
                ws_bytes, L.stream_ptr(None))
-        return counts, perm[:n], local[:n]
+        return counts, perm[:n], local[:n], inv[:n]
 
     def gather(self, shard: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
         n = local.numel()
@@ -109,9 +111,10 @@ class GpuShardOps:
                    shard.shape[1], L.ptr(out), L.stream_ptr(None))
         return out[:n]
 
-    def pool(self, desc, n_slots: int, batch: SparseBatch, gathered: torch.Tensor, out: torch.Tensor, flags: int):
+    def pool(self, desc, n_slots: int, batch: SparseBatch, gathered: torch.Tensor, out: torch.Tensor, flags: int,
+             row_map: Optional[torch.Tensor] = None):
         L.call("rf_pool_rows_fwd", L.ptr(desc), n_slots, L.ptr(batch.bag_off), L.ptr(batch.lmax), batch.batch,
-               batch.n_tokens, L.ptr(gathered), L.torch_dtype_code(gathered.dtype), gathered.shape[1], L.ptr(out),
+               batch.n_tokens, L.ptr(gathered), L.ptr(row_map), L.torch_dtype_code(gathered.dtype), gathered.shape[1], L.ptr(out),
                L.torch_dtype_code(out.dtype), out.stride(0), flags, L.stream_ptr(None))
         return out
 
@@ -139,11 +142,24 @@ class TorchDistComm:
         return out
 
 
+class LocalComm:
+    """P = 1: the exchange is the identity (the sharded pipeline on one GPU, for weak-scaling baselines)."""
+
+    rank, world = 0, 1
+
+    def exchange_counts(self, counts: torch.Tensor) -> torch.Tensor:
+        return counts
+
+    def exchange(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]) -> torch.Tensor:
+        return x
+
+
 @dataclass
 class RouteState:
     counts: List[int]          # rows this rank requests from each owner
     perm: torch.Tensor         # int32 [n]: request i (owner-major) came from position perm[i]
     local: torch.Tensor        # int64 [n]: local row id at its owner, owner-major
+    inv: torch.Tensor          # int32 [n]: position j sits at owner-major slot inv[j]
     n_requests: int
 
 
@@ -183,21 +199,18 @@ class ShardedFusedEncoder(torch.nn.Module):
     def route(self, batch: SparseBatch) -> RouteState:
         rows = self.ops.hash_rows(self.desc, len(self.slots), batch)
         req = torch.cat([rows, self.pad_rows])
-        counts, perm, local = self.ops.bucketize(req, self.nranks)
-        return RouteState([int(c) for c in counts.cpu().tolist()], perm, local, req.numel())
+        counts, perm, local, inv = self.ops.bucketize(req, self.nranks)
+        return RouteState([int(c) for c in counts.cpu().tolist()], perm, local, inv, req.numel())
 
     def serve(self, local_rows: torch.Tensor) -> torch.Tensor:
-        if local_rows.numel() and int(local_rows.max()) >= self.local_rows:
-            raise IndexError("row request beyond this rank's shard")
+        # rows beyond the shard come back NaN (rf_gather_rows), poisoning the pooled output loudly
         return self.ops.gather(self.shard, local_rows)
 
     def combine(self, batch: SparseBatch, st: RouteState, back: torch.Tensor, out: Optional[torch.Tensor] = None):
-        gathered = torch.empty_like(back)
-        gathered.index_copy_(0, st.perm.long(), back)
         if out is None:
             out = torch.empty((batch.batch, self.out_width), dtype=self.out_dtype, device=back.device)
         flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
-        return self.ops.pool(self.desc, len(self.slots), batch, gathered, out, flags)
+        return self.ops.pool(self.desc, len(self.slots), batch, back, out, flags, row_map=st.inv)
 
     def forward(self, batch: SparseBatch, out: Optional[torch.Tensor] = None):
         if self.comm is None:

@@ -442,7 +442,7 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     const size_t lds = (size_t)2 * Lk * (d + 8) * 2 + (size_t)kEsimWaves * 3 * 2 * d * 4;
     hipStream_t st = rf_stream(stream);
     int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int grid = (int)std::min<int64_t>(batch, cus);  // persistent: one 8-wave workgroup per CU
 #define RF_ESIM_LAUNCH(F16, D)                                                                                     \
     {                                                                                                              \

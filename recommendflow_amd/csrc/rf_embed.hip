@@ -247,8 +247,8 @@ extern "C" int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const 
 }
 
 extern "C" int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off,
-                                const int32_t* lmax, int32_t batch, int64_t n_tok, const void* gathered, int32_t dtype,
-                                int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
+                                const int32_t* lmax, int32_t batch, int64_t n_tok, const void* gathered,
+                                const int32_t* row_map, int32_t dtype, int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
                                 void* stream) {
     RF_REQUIRE(n_slots >= 1 && batch >= 0 && n_tok >= 0, "rf_pool_rows_fwd: need n_slots >= 1, batch, n_tok >= 0");
     RF_REQUIRE(dtype == RF_DTYPE_F32 || dtype == RF_DTYPE_BF16, "rf_pool_rows_fwd: dtype must be F32 or BF16");
@@ -265,11 +265,11 @@ extern "C" int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, co
     const int64_t items = (int64_t)n_slots * ((batch + kUnits - 1) / kUnits);
     const int grid = grid_for(items, kWaves, 256 * 32 * 2);
     hipStream_t st = rf_stream(stream);
-    const int fl = flags | kFlagPregathered;
+    const int fl = flags;
     if (dtype == RF_DTYPE_F32)
-        return launch_fused_f32(d_slots, n_slots, nullptr, nullptr, bag_off, lmax, n_units, gathered, rows, dim, out,
+        return launch_pool_f32(d_slots, n_slots, nullptr, row_map, bag_off, lmax, n_units, gathered, rows, dim, out,
                                 out_dtype, out_stride, fl, nullptr, kDefaultMaxLpr, grid, st);
-    return launch_fused_bf16(d_slots, n_slots, nullptr, nullptr, bag_off, lmax, n_units, gathered, rows, dim, out,
+    return launch_pool_bf16(d_slots, n_slots, nullptr, row_map, bag_off, lmax, n_units, gathered, rows, dim, out,
                              out_dtype, out_stride, fl, nullptr, kDefaultMaxLpr, grid, st);
 }
 

@@ -21,7 +21,6 @@ constexpr int kWaves = RF_FUSED_WAVES;
 constexpr int kCap = 768;    // tokens per wave item kept in the LDS row bucket (more: hashed inline)
 constexpr int kUnits = 64;   // examples per wave item (one slot per item)
 constexpr int kDefaultMaxLpr = 16;  // lanes per row cap (tuned on MI355X)
-constexpr int kFlagPregathered = 1 << 15;  // internal: rf_pool_rows_fwd
 
 template <typename T>
 struct Elem {
@@ -109,7 +108,7 @@ __device__ __forceinline__ uint4 row_chunk(const TT* __restrict__ table, uint32_
 #ifndef RF_FUSED_MIN_WAVES
 #define RF_FUSED_MIN_WAVES 1
 #endif
-template <int LPR, int CPL, bool FULL, typename TT, typename OT>
+template <int LPR, int CPL, bool FULL, typename TT, typename OT, bool PRE>
 __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_embed_kernel(
     const rf_slot_desc* __restrict__ slots, int n_slots, const uint8_t* __restrict__ tok_bytes,
     const int32_t* __restrict__ tok_off, const int32_t* __restrict__ bag_off, const int32_t* __restrict__ lmax,
@@ -134,7 +133,10 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
     const bool abl_nohash = (flags & (1 << 12)) != 0, abl_nopool = (flags & (1 << 13)) != 0,
                abl_nopad = (flags & (1 << 14)) != 0;  // diagnostic ablations (tools/kbench.py)
     // rf_pool_rows_fwd: `table` holds pre-gathered rows (token t, table k -> row 2t + k; pad rows after)
-    const bool pregathered = (flags & kFlagPregathered) != 0;
+    constexpr bool pregathered = PRE;
+    // PRE: tok_bytes is unused and tok_off carries the optional row map (logical row j of the pre-gathered
+    // buffer lives at row_map[j]; nullptr = identity) — rf_pool_rows_fwd's un-permute, fused into the loads
+    const int32_t* row_map = PRE ? tok_off : nullptr;
     const int batch = (int)(n_units / n_slots);
     const int nbb = (batch + kUnits - 1) / kUnits;
     const int64_t n_items = (int64_t)n_slots * nbb;
@@ -167,9 +169,13 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
             pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
         }
         uint32_t pad0 = ok ? (uint32_t)(rb0 + pb0) : 0u, pad1 = ok ? (uint32_t)(rb1 + pb1) : 0u;
-        if (pregathered) {  // pad rows follow the 2 * n_tok token rows
+        if (pregathered) {  // pad rows follow the 2 * n_tok token rows (through the row map when given)
             pad0 = (uint32_t)(table_rows - 2 * (int64_t)n_slots + 2 * s);
             pad1 = pad0 + 1;
+            if (row_map) {
+                pad0 = (uint32_t)row_map[pad0];
+                pad1 = (uint32_t)row_map[pad1];
+            }
         }
 
         // ---- phase 1a: unit token ranges, wave prefix scan -> item-local token layout ----
@@ -205,8 +211,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     if (s_loc[wave][mid] <= i) lo = mid; else hi = mid - 1;
                 }
                 const uint32_t t = (uint32_t)(s_gbeg[wave][lo] + (i - s_loc[wave][lo]));
-                s_row[wave][0][i] = 2 * t;
-                s_row[wave][1][i] = 2 * t + 1;
+                s_row[wave][0][i] = row_map ? (uint32_t)row_map[2 * t] : 2 * t;
+                s_row[wave][1][i] = row_map ? (uint32_t)row_map[2 * t + 1] : 2 * t + 1;
             }
         }
         if (abl_nohash) {
@@ -421,6 +427,10 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                 if (pregathered) {
                     r0 = 2u * (uint32_t)t;
                     r1 = r0 + 1;
+                    if (row_map) {
+                        r0 = (uint32_t)row_map[r0];
+                        r1 = (uint32_t)row_map[r1];
+                    }
                 } else {
                     const int tb = tok_off[t], n = tok_off[t + 1] - tb;
                     uint64_t h0, h1;
@@ -467,14 +477,41 @@ int dispatch_fused(int nchunks, int max_lpr, F&& f) {
     return rf_set_error(RF_EINVAL, "no kernel for %d lanes x %d chunks", lpr, c);
 }
 
-// launch for one table dtype TT (defined in rf_fused_f32.hip / rf_fused_bf16.hip)
-int launch_fused_f32(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
-                     const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table, int64_t table_rows,
-                     int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, int64_t* idx_out,
-                     int max_lpr, int grid, hipStream_t st);
-int launch_fused_bf16(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
-                      const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table, int64_t table_rows,
-                      int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, int64_t* idx_out,
-                      int max_lpr, int grid, hipStream_t st);
+// One launcher per (table dtype, mode); PRE = pooling of pre-gathered rows (rf_pool_rows_fwd), a separate
+// instantiation so the hashing kernel's register allocation is not affected by the extra mode.
+template <typename TT, bool PRE>
+int launch_fused_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                      const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table,
+                      int64_t table_rows, int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
+                      int64_t* idx_out, int max_lpr, int grid, hipStream_t st) {
+    constexpr int epv = Elem<TT>::EPV;
+    return dispatch_fused(dim / epv, max_lpr, [&](auto lpr, auto cpl) -> int {
+        constexpr int LPR = decltype(lpr)::value, CPL = decltype(cpl)::value;
+        const bool full = dim / epv == LPR * CPL;
+#define RF_FUSED_LAUNCH(FULL, OT)                                                                                    \
+    hipLaunchKernelGGL((fused_hash_embed_kernel<LPR, CPL, FULL, TT, OT, PRE>), dim3(grid), dim3(kWaves * 64), 0, st, \
+                       d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, (const TT*)table, table_rows,     \
+                       dim, (OT*)out, out_stride, flags, idx_out)
+        if (out_dtype == RF_DTYPE_F32) {
+            if (full) RF_FUSED_LAUNCH(true, float); else RF_FUSED_LAUNCH(false, float);
+        } else {
+            if (full) RF_FUSED_LAUNCH(true, uint16_t); else RF_FUSED_LAUNCH(false, uint16_t);
+        }
+#undef RF_FUSED_LAUNCH
+        return rf_check_launch(PRE ? "fused_pool_rows_kernel" : "fused_hash_embed_kernel");
+    });
+}
+
+#define RF_FUSED_LAUNCH_DECL(NAME)                                                                                     \
+    int NAME(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,          \
+             const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table, int64_t table_rows,      \
+             int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, int64_t* idx_out,          \
+             int max_lpr, int grid, hipStream_t st)
+// defined in rf_fused_{f32,bf16}.hip (hashing) and rf_pool_{f32,bf16}.hip (pre-gathered)
+RF_FUSED_LAUNCH_DECL(launch_fused_f32);
+RF_FUSED_LAUNCH_DECL(launch_fused_bf16);
+RF_FUSED_LAUNCH_DECL(launch_pool_f32);
+RF_FUSED_LAUNCH_DECL(launch_pool_bf16);
+
 
 }  // namespace rf

@@ -31,15 +31,15 @@ class OracleShardOps:
         return torch.from_numpy(O.hash_rows(desc, batch.tok_bytes, batch.tok_off, batch.bag_off, batch.batch))
 
     def bucketize(self, rows, nranks):
-        c, p, l = O.bucketize_owner(rows.numpy(), nranks)
-        return torch.from_numpy(c), torch.from_numpy(p), torch.from_numpy(l)
+        c, p, l, inv = O.bucketize_owner(rows.numpy(), nranks)
+        return torch.from_numpy(c), torch.from_numpy(p), torch.from_numpy(l), torch.from_numpy(inv)
 
     def gather(self, shard, local):
         return shard[local]
 
-    def pool(self, desc, n_slots, batch, gathered, out, flags):
+    def pool(self, desc, n_slots, batch, gathered, out, flags, row_map=None):
         res = O.pool_rows(desc, batch.bag_off, batch.lmax, batch.batch, batch.n_tokens, gathered.numpy(),
-                          gathered.shape[1], out.shape[1], flags)
+                          gathered.shape[1], out.shape[1], flags, None if row_map is None else row_map.numpy())
         out.copy_(torch.from_numpy(res))
         return out
 

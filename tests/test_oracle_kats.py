@@ -123,7 +123,8 @@ def test_table_init_is_shard_invariant(O):
 
 def test_bucketize_owner(O):
     rows = np.array([5, 2, 7, 4, 9, 0, 3, 6], np.int64)
-    counts, perm, local = O.bucketize_owner(rows, 3)
+    counts, perm, local, inv = O.bucketize_owner(rows, 3)
+    np.testing.assert_array_equal(inv[perm], np.arange(len(rows)))
     assert counts.tolist() == [4, 2, 2]  # owners 2 2 1 1 0 0 0 0
     assert perm.tolist() == [4, 5, 6, 7, 2, 3, 0, 1]  # owner-major, stable
     np.testing.assert_array_equal(local, rows[perm] // 3)

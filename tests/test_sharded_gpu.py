@@ -37,6 +37,20 @@ def test_hash_rows_matches_oracle(O, cuda):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("P", [1, 2, 3, 8, 64, 1000])
+@pytest.mark.parametrize("n", [0, 1, 63, 2047, 2048, 2049, 300001])
+def test_bucketize_matches_oracle(O, cuda, P, n):
+    rng = np.random.default_rng(n * 7 + P)
+    rows = rng.integers(0, 10 ** 9, n).astype(np.int64)
+    rows[: n // 3] = rng.integers(0, 50, n // 3)  # hot rows: many equal owners in a round
+    c, p, l, inv = GpuShardOps().bucketize(torch.from_numpy(rows).cuda(), P)
+    wc, wp, wl, winv = O.bucketize_owner(rows, P)
+    np.testing.assert_array_equal(c.cpu().numpy(), wc)
+    np.testing.assert_array_equal(p.cpu().numpy(), wp)
+    np.testing.assert_array_equal(l.cpu().numpy(), wl)
+    np.testing.assert_array_equal(inv.cpu().numpy(), winv)
+
+
 @pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("mask_padding", [False, True])
 @pytest.mark.parametrize("dim", [16, 64, 128])
@@ -53,6 +67,13 @@ def test_pool_rows_equals_fused(O, cuda, tdt, mask_padding, dim):
     req = torch.cat([ops.hash_rows(enc.desc, len(sp), db), sh.pad_rows])
     gathered = ops.gather(enc.table, req)
     got = ops.pool(enc.desc, len(sp), db, gathered, torch.empty_like(want), 1 if mask_padding else 0)
+    np.testing.assert_array_equal(bits(got), bits(want))
+    # through a row map: gathered rows stored permuted, read back at row_map[j]
+    perm = torch.randperm(req.numel(), generator=torch.Generator().manual_seed(dim)).cuda()
+    shuffled = torch.empty_like(gathered)
+    shuffled[perm] = gathered
+    got = ops.pool(enc.desc, len(sp), db, shuffled, torch.empty_like(want), 1 if mask_padding else 0,
+                   row_map=perm.to(torch.int32))
     np.testing.assert_array_equal(bits(got), bits(want))
 
 
