@@ -338,7 +338,7 @@ def bench_sharded(args, specs, multi, rank, world):
         if ev: ev[4].record()
         enc.combine(b, r, back, out)
         if ev: ev[5].record()
-        st["req"], st["served"] = r.n_requests, int(wanted.shape[0])
+        st["req"], st["served"], st["logical"] = r.n_requests, int(wanted.shape[0]), r.n_logical
 
     steps = max(5, args.steps // 5)
     for i in range(3):
@@ -365,9 +365,11 @@ def bench_sharded(args, specs, multi, rank, world):
     res = {"examples_per_s": round(B * P * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
            "stage_ms_rank0": stage, "gather_GBs": round(st["served"] * (2 * row_b + 8) / stage["gather"] / 1e6, 1),
            "a2a_bytes_per_rank_each_way": int(xgmi),
+           "rows_read_by_pool": st["logical"], "rows_requested_after_dedup": st["req"],
+           "dedup_factor": round(st["logical"] / max(st["req"], 1), 3),
            "config": f"cfg2 slots ({S}) over a {enc.table_rows}x{D} fp32 fused table row-sharded over {P} GPU(s) "
                      f"({enc.local_rows} rows/GPU), {B} examples/GPU (global {B * P}), owner = row mod P, "
-                     f"RCCL all_to_all_single for ids and rows, no dedup"}
+                     f"per-step row dedup, RCCL all_to_all_single for ids and rows"}
     del enc, batches, out
     torch.cuda.empty_cache()
     return res

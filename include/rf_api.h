@@ -222,6 +222,19 @@ int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t
                      int32_t batch, int64_t n_tok, const void* gathered, const int32_t* row_map, int32_t dtype,
                      int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, void* stream);
 
+/*
+ * Route one step's row requests WITH dedup (the default requester stage of the sharded lookup; SURVEY
+ * §8e "per-owner dedup"). For n global rows g < table_rows and P ranks (owner = g mod P, local = g div P):
+ *   every distinct row once, sorted by (owner, local): local_out[0 .. n_uniq) (int64; -1 for a row outside
+ *   [0, table_rows), which rf_gather_rows returns as NaN), counts[P] = distinct rows per owner (int32),
+ *   row_map[j] = position of request j's row in that order (int32) — i.e. in the all-to-all receive
+ *   buffer, so rf_pool_rows_fwd can take it as its row_map. n_uniq: DEVICE int32 (may be NULL).
+ * Deterministic (radix sort, no atomics). ws: rf_route_ws_bytes(n, P, table_rows) bytes, 256-B aligned.
+ */
+size_t rf_route_ws_bytes(int64_t n, int32_t nranks, int64_t table_rows);
+int rf_route_rows(const int64_t* rows, int64_t n, int32_t nranks, int64_t table_rows, int32_t* counts,
+                  int64_t* local_out, int32_t* row_map, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
+
 /* Gather whole rows: out[i] = table[rows[i]] (owner side of the sharded lookup). */
 int rf_gather_rows(const int64_t* rows, int64_t n, const void* table, int32_t dtype, int64_t table_rows,
                    int32_t dim, void* out, void* stream);

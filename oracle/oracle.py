@@ -196,6 +196,20 @@ def bucketize_owner(rows: np.ndarray, nranks: int):
     return counts, perm, local, inv
 
 
+def route_rows(rows: np.ndarray, nranks: int, table_rows: int):
+    """rf_route_rows restated: distinct rows sorted by (owner = g mod P, local = g div P).
+    Returns (counts int32 [P], local int64 [U], row_map int32 [n])."""
+    rows = np.asarray(rows, np.int64)
+    lp = -(-table_rows // nranks)
+    ok = (rows >= 0) & (rows < table_rows)
+    keys = np.where(ok, (rows % nranks) * lp + rows // nranks, nranks * lp)
+    uniq, row_map = np.unique(keys, return_inverse=True)
+    local = np.where(uniq < nranks * lp, uniq % lp, -1).astype(np.int64)
+    owner = np.minimum(uniq // lp, nranks - 1)
+    counts = np.bincount(owner, minlength=nranks).astype(np.int32)
+    return counts, local, row_map.astype(np.int32).reshape(-1)
+
+
 def bf16_to_f32(u16: np.ndarray) -> np.ndarray:
     return (np.asarray(u16, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
 

@@ -12,12 +12,13 @@ fp32) spans 8 x 288 GB of HBM:
 
 One forward per rank (requester) is four C-ABI launches and two all-to-alls:
 
-  route   : rf_hash_rows (2 global rows per token) + 2*S padding rows -> rf_bucketize_owner
-            (stable owner-major permutation, local row ids, per-owner counts)
+  route   : rf_hash_rows (2 global rows per token) + 2*S padding rows -> rf_route_rows (each distinct
+            row once, sorted owner-major: local ids, per-owner counts, and the row map from each
+            logical row to its slot in the receive buffer); dedup=False uses rf_bucketize_owner instead
   exchange: all_to_all(counts); all_to_all_single(local ids)           -> owners
   serve   : rf_gather_rows on the local shard                           (owner side)
   exchange: all_to_all_single(row vectors)                              -> requesters
-  combine : rf_pool_rows_fwd straight from the receive buffer, reading logical row j at inv_perm[j]
+  combine : rf_pool_rows_fwd straight from the receive buffer, reading logical row j at row_map[j]
             (the un-permute is fused into the pooling loads; same pooling code and accumulation order as
             rf_fused_hash_embed_fwd, so the result is bit-identical)
 
@@ -103,6 +104,18 @@ class GpuShardOps:
                ws_bytes, L.stream_ptr(None))
         return counts, perm[:n], local[:n], inv[:n]
 
+    def route(self, rows: torch.Tensor, nranks: int, table_rows: int):
+        """Dedup + owner-major routing (rf_route_rows) -> (counts int32 [P], local int64 [U], row_map int32 [n])."""
+        n = rows.numel()
+        counts = torch.empty(nranks, dtype=torch.int32, device=self.device)
+        local = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        row_map = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        ws_bytes = L.load().rf_route_ws_bytes(n, nranks, table_rows)
+        ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=self.device)
+        L.call("rf_route_rows", L.ptr(rows), n, nranks, table_rows, L.ptr(counts), L.ptr(local), L.ptr(row_map), None,
+               L.ptr(ws), ws_bytes, L.stream_ptr(None))
+        return counts, local, row_map[:n]
+
     def gather(self, shard: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
         n = local.numel()
         out = torch.empty((max(n, 1), shard.shape[1]), dtype=shard.dtype, device=self.device)
@@ -157,10 +170,10 @@ class LocalComm:
 @dataclass
 class RouteState:
     counts: List[int]          # rows this rank requests from each owner
-    perm: torch.Tensor         # int32 [n]: request i (owner-major) came from position perm[i]
-    local: torch.Tensor        # int64 [n]: local row id at its owner, owner-major
-    inv: torch.Tensor          # int32 [n]: position j sits at owner-major slot inv[j]
-    n_requests: int
+    local: torch.Tensor        # int64: local row id at its owner, owner-major (the id send buffer)
+    row_map: torch.Tensor      # int32 [2*n_tok + 2*S]: logical row j arrives at row row_map[j]
+    n_requests: int            # rows requested (after dedup)
+    n_logical: int             # rows the pooling reads (2*n_tok + 2*S)
 
 
 class ShardedFusedEncoder(torch.nn.Module):
@@ -168,7 +181,7 @@ class ShardedFusedEncoder(torch.nn.Module):
 
     def __init__(self, slots: Sequence[SlotSpec], dim: int, rank: int, nranks: int, comm=None, ops=None,
                  table_dtype=torch.float32, out_dtype=None, seed: int = 0, mask_padding: bool = False,
-                 init_range=(-0.05, 0.05), device="cuda"):
+                 init_range=(-0.05, 0.05), device="cuda", dedup: bool = True):
         super().__init__()
         if not slots:
             raise ValueError("ShardedFusedEncoder needs at least one slot")
@@ -182,6 +195,7 @@ class ShardedFusedEncoder(torch.nn.Module):
         self.table_dtype = table_dtype
         self.out_dtype = out_dtype or table_dtype
         self.mask_padding = bool(mask_padding)
+        self.dedup = bool(dedup)  # send each distinct row once per step (rf_route_rows)
         self.host_desc, self.table_rows = build_slot_desc(self.slots, self.dim)
         self.out_width = 2 * self.dim * len(self.slots)
         self.desc = self.ops.upload_desc(self.host_desc)
@@ -199,8 +213,14 @@ class ShardedFusedEncoder(torch.nn.Module):
     def route(self, batch: SparseBatch) -> RouteState:
         rows = self.ops.hash_rows(self.desc, len(self.slots), batch)
         req = torch.cat([rows, self.pad_rows])
-        counts, perm, local, inv = self.ops.bucketize(req, self.nranks)
-        return RouteState([int(c) for c in counts.cpu().tolist()], perm, local, inv, req.numel())
+        if self.dedup:
+            counts, local, row_map = self.ops.route(req, self.nranks, self.table_rows)
+            counts = [int(c) for c in counts.cpu().tolist()]
+            local = local[: sum(counts)]
+        else:
+            counts, _, local, row_map = self.ops.bucketize(req, self.nranks)
+            counts = [int(c) for c in counts.cpu().tolist()]
+        return RouteState(counts, local, row_map, int(local.numel()), req.numel())
 
     def serve(self, local_rows: torch.Tensor) -> torch.Tensor:
         # rows beyond the shard come back NaN (rf_gather_rows), poisoning the pooled output loudly
@@ -210,7 +230,7 @@ class ShardedFusedEncoder(torch.nn.Module):
         if out is None:
             out = torch.empty((batch.batch, self.out_width), dtype=self.out_dtype, device=back.device)
         flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
-        return self.ops.pool(self.desc, len(self.slots), batch, back, out, flags, row_map=st.inv)
+        return self.ops.pool(self.desc, len(self.slots), batch, back, out, flags, row_map=st.row_map)
 
     def forward(self, batch: SparseBatch, out: Optional[torch.Tensor] = None):
         if self.comm is None:

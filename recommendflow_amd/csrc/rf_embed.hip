@@ -150,21 +150,37 @@ __global__ __launch_bounds__(256) void table_init_kernel(TT* __restrict__ table,
     }
 }
 
-// rf_hash_rows: thread per (example, slot) unit, both salts over one read of each token
-__global__ __launch_bounds__(256) void hash_rows_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
-                                                        const uint8_t* __restrict__ tok_bytes,
-                                                        const int32_t* __restrict__ tok_off,
-                                                        const int32_t* __restrict__ bag_off, int64_t n_units,
-                                                        int64_t* __restrict__ rows_out) {
-    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += (int64_t)gridDim.x * blockDim.x) {
-        const rf_slot_desc* sd = slots + (int)(u % n_slots);
-        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
-        for (int t = bag_off[u]; t < bag_off[u + 1]; ++t) {
+// rf_hash_rows: a block takes 256 consecutive (example, slot) units = one contiguous token range; a
+// thread per TOKEN (its unit found by binary search over the block's 257 bag offsets in LDS), so the
+// multi-valued slots do not serialise a thread; both salts over one read of each token, 16-byte stores.
+constexpr int kHashUnits = 256;
+__global__ __launch_bounds__(kHashUnits) void hash_rows_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
+                                                               const uint8_t* __restrict__ tok_bytes,
+                                                               const int32_t* __restrict__ tok_off,
+                                                               const int32_t* __restrict__ bag_off, int64_t n_units,
+                                                               int64_t* __restrict__ rows_out) {
+    __shared__ int32_t s_off[kHashUnits + 1];
+    for (int64_t u0 = (int64_t)blockIdx.x * kHashUnits; u0 < n_units; u0 += (int64_t)gridDim.x * kHashUnits) {
+        const int nu = (int)min<int64_t>(kHashUnits, n_units - u0);
+        __syncthreads();
+        for (int j = threadIdx.x; j <= nu; j += kHashUnits) s_off[j] = bag_off[u0 + j];
+        __syncthreads();
+        const int t0 = s_off[0], t1 = s_off[nu];
+        for (int t = t0 + (int)threadIdx.x; t < t1; t += kHashUnits) {
+            int lo = 0, hi = nu - 1;  // last unit j with s_off[j] <= t
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] <= t) lo = mid; else hi = mid - 1;
+            }
+            const rf_slot_desc* sd = slots + (int)((u0 + lo) % n_slots);
             const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
             uint64_t h0, h1;
             siphash24x2_dev(sd->salt[0], sd->salt[1], tok_bytes + b0, n, h0, h1);
-            rows_out[2 * (int64_t)t] = rb0 + bucket_from_hash(h0, n, nbins, sd->mask_empty);
-            rows_out[2 * (int64_t)t + 1] = rb1 + bucket_from_hash(h1, n, nbins, sd->mask_empty);
+            const int64_t nbins = sd->num_bins;
+            longlong2 r;
+            r.x = sd->row_base[0] + bucket_from_hash(h0, n, nbins, sd->mask_empty);
+            r.y = sd->row_base[1] + bucket_from_hash(h1, n, nbins, sd->mask_empty);
+            reinterpret_cast<longlong2*>(rows_out)[t] = r;
         }
     }
 }
@@ -241,7 +257,8 @@ extern "C" int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const 
     const int64_t n_units = (int64_t)batch * n_slots;
     if (n_units == 0) return RF_OK;
     RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && rows_out, "rf_hash_rows: null pointer");
-    hipLaunchKernelGGL(hash_rows_kernel, dim3(grid_for(n_units, 256)), dim3(256), 0, rf_stream(stream), d_slots,
+    RF_REQUIRE(((uintptr_t)rows_out & 15) == 0, "rf_hash_rows: rows_out must be 16-byte aligned");
+    hipLaunchKernelGGL(hash_rows_kernel, dim3(grid_for(n_units, kHashUnits, 256 * 64)), dim3(kHashUnits), 0, rf_stream(stream), d_slots,
                        n_slots, tok_bytes, tok_off, bag_off, n_units, rows_out);
     return rf_check_launch("hash_rows_kernel");
 }

@@ -2,6 +2,7 @@
 // whole tables per GPU under MirroredStrategy, backend/utils/gpu_utils.py:13-14).
 //   rf_bucketize_owner  owner = g mod P, local = g div P; counts + STABLE owner-major permutation
 //   rf_gather_rows      owner-side gather of whole rows for the vector return
+//   (rf_route_rows, the dedup'ing alternative to rf_bucketize_owner, is in rf_route.hip)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -171,3 +172,4 @@ extern "C" int rf_gather_rows(const int64_t* rows, int64_t n, const void* table,
                        (const uint4*)table, table_rows, chunks, (uint4*)out);
     return rf_check_launch("gather_rows_kernel");
 }
+

@@ -38,6 +38,8 @@ _SIGS = {
     "rf_bucketize_owner": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_gather_rows": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i64, _i32, _vp, _vp]),
     "rf_hash_rows": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "rf_route_ws_bytes": (ctypes.c_size_t, [_i64, _i32, _i64]),
+    "rf_route_rows": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_pool_rows_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _i32, _i64, _i32, _vp]),
 }
 EXPORTED = tuple(_SIGS)

@@ -34,6 +34,10 @@ class OracleShardOps:
         c, p, l, inv = O.bucketize_owner(rows.numpy(), nranks)
         return torch.from_numpy(c), torch.from_numpy(p), torch.from_numpy(l), torch.from_numpy(inv)
 
+    def route(self, rows, nranks, table_rows):
+        c, l, m = O.route_rows(rows.numpy(), nranks, table_rows)
+        return torch.from_numpy(c), torch.from_numpy(l), torch.from_numpy(m)
+
     def gather(self, shard, local):
         return shard[local]
 

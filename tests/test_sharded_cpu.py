@@ -47,8 +47,10 @@ def test_pool_rows_equals_fused(O):
 
 
 @pytest.mark.parametrize("P", [1, 2, 3, 8])
-def test_simulated_shards_bit_exact(O, P):
-    encs = [ShardedFusedEncoder(small_slots(), DIM, r, P, ops=OracleShardOps(), seed=SEED, device="cpu") for r in range(P)]
+@pytest.mark.parametrize("dedup", [False, True])
+def test_simulated_shards_bit_exact(O, P, dedup):
+    encs = [ShardedFusedEncoder(small_slots(), DIM, r, P, ops=OracleShardOps(), seed=SEED, device="cpu", dedup=dedup)
+            for r in range(P)]
     assert sum(e.local_rows for e in encs) == encs[0].table_rows
     outs = simulate_sharded_forward(encs, [rank_batch(r) for r in range(P)])
     for r in range(P):

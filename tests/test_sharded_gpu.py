@@ -77,12 +77,29 @@ def test_pool_rows_equals_fused(O, cuda, tdt, mask_padding, dim):
     np.testing.assert_array_equal(bits(got), bits(want))
 
 
+@pytest.mark.parametrize("P", [1, 2, 8, 1000])
+@pytest.mark.parametrize("n", [0, 1, 1000, 300001])
+def test_route_rows_matches_oracle(O, cuda, P, n):
+    rng = np.random.default_rng(n + P)
+    R = 50_000_000
+    rows = (rng.zipf(1.2, n) * 7919 % R).astype(np.int64)
+    if n > 10:
+        rows[3] = -5          # invalid rows: local -1 (gathered as NaN)
+        rows[7] = R + 11
+    c, l, m = GpuShardOps().route(torch.from_numpy(rows).cuda(), P, R)
+    wc, wl, wm = O.route_rows(rows, P, R)
+    np.testing.assert_array_equal(c.cpu().numpy(), wc)
+    np.testing.assert_array_equal(l.cpu().numpy()[: int(wc.sum())], wl)
+    np.testing.assert_array_equal(m.cpu().numpy(), wm)
+
+
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
-def test_simulated_shards_bit_exact(cuda, P, tdt):
+@pytest.mark.parametrize("dedup", [False, True])
+def test_simulated_shards_bit_exact(cuda, P, tdt, dedup):
     sp = slots(48, seed=P)
     full = FusedSparseEncoder(sp, 64, table_dtype=tdt, seed=21)
-    encs = [ShardedFusedEncoder(sp, 64, r, P, table_dtype=tdt, seed=21) for r in range(P)]
+    encs = [ShardedFusedEncoder(sp, 64, r, P, table_dtype=tdt, seed=21, dedup=dedup) for r in range(P)]
     batches = [synthetic_batch(200 + 17 * r, [i % 3 == 0 for i in range(len(sp))], seed=40 + r) for r in range(P)]
     outs = simulate_sharded_forward(encs, batches)
     for r in range(P):
