@@ -233,21 +233,16 @@ extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_sl
     RF_REQUIRE(dim > 0 && dim % epv == 0, "rf_fused_hash_embed_fwd: dim (%d) must be a positive multiple of %d (16-byte rows chunks)", dim, epv);
     RF_REQUIRE(out_stride % epv == 0, "rf_fused_hash_embed_fwd: out_stride must be a multiple of %d", epv);
     RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)out & 15) == 0, "rf_fused_hash_embed_fwd: table/out must be 16-byte aligned");
-    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | 0x7f00)) == 0, "rf_fused_hash_embed_fwd: unknown flags");  // 0x7f00: reserved tuning/diagnostic bits
+    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | 0x7000)) == 0, "rf_fused_hash_embed_fwd: unknown flags");  // 0x7000: reserved diagnostic bits
     RF_REQUIRE(table_rows >= 1 && table_rows <= (int64_t)0xffffffff, "rf_fused_hash_embed_fwd: table_rows must be in [1, 2^32) (32-bit row ids in LDS)");
     const int64_t n_units = (int64_t)batch * n_slots;
     if (n_units == 0) return RF_OK;
     RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && lmax && table && out, "rf_fused_hash_embed_fwd: null pointer");
     const int64_t items = (int64_t)n_slots * ((batch + kUnits - 1) / kUnits);  // slot-major items
     const int grid = grid_for(items, kWaves, 256 * 32 * 2);
-    const int tune = (flags >> 8) & 0xf;  // reserved tuning bits: log2 of the max lanes per row (0 = default)
-    const int max_lpr = tune ? (1 << (tune - 1)) : kDefaultMaxLpr;
     hipStream_t st = rf_stream(stream);
-    if (table_dtype == RF_DTYPE_F32)
-        return launch_fused_f32(d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table, table_rows, dim, out,
-                                out_dtype, out_stride, flags, idx_out, max_lpr, grid, st);
-    return launch_fused_bf16(d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table, table_rows, dim, out,
-                             out_dtype, out_stride, flags, idx_out, max_lpr, grid, st);
+    return launch_fused_any(false, table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,
+                            table, table_rows, dim, out, out_stride, flags, idx_out, grid, st);
 }
 
 extern "C" int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
@@ -283,11 +278,8 @@ extern "C" int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, co
     const int grid = grid_for(items, kWaves, 256 * 32 * 2);
     hipStream_t st = rf_stream(stream);
     const int fl = flags;
-    if (dtype == RF_DTYPE_F32)
-        return launch_pool_f32(d_slots, n_slots, nullptr, row_map, bag_off, lmax, n_units, gathered, rows, dim, out,
-                                out_dtype, out_stride, fl, nullptr, kDefaultMaxLpr, grid, st);
-    return launch_pool_bf16(d_slots, n_slots, nullptr, row_map, bag_off, lmax, n_units, gathered, rows, dim, out,
-                             out_dtype, out_stride, fl, nullptr, kDefaultMaxLpr, grid, st);
+    return launch_fused_any(true, dtype, out_dtype, d_slots, n_slots, nullptr, row_map, bag_off, lmax, n_units,
+                            gathered, rows, dim, out, out_stride, fl, nullptr, grid, st);
 }
 
 extern "C" int rf_embedding_bag_fwd(const int64_t* ids, int32_t batch, int32_t len, int64_t row_base, const void* table,

@@ -83,6 +83,21 @@ __device__ __forceinline__ float comb_step(int comb, float a, float v) {
     return comb == RF_COMB_MAX ? (v > a ? v : a) : comb == RF_COMB_MIN ? (v < a ? v : a) : __fadd_rn(a, v);
 }
 
+// a[e] += f[e] for e < N (N even), two lanes of fp32 per v_pk_add_f32: the same RN add per element,
+// half the VALU issue of scalar adds (sum/avg pooling and the padded-position adds are VALU-heavy)
+template <int N>
+__device__ __forceinline__ void add_pk(float* a, const float* f) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int e = 0; e < N; e += 2) {
+        f2 x = {a[e], a[e + 1]};
+        const f2 y = {f[e], f[e + 1]};
+        x = x + y;
+        a[e] = x.x;
+        a[e + 1] = x.y;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // fused multi-slot hash -> gather -> pool
 // ---------------------------------------------------------------------------------------------
@@ -309,6 +324,29 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                         }
                 return;
             }
+            if (npad > 0 && (comb == RF_COMB_SUM || comb == RF_COMB_AVG)) {
+                // one add per padded position, in order; both tables' chains in one loop, unrolled by 2
+                float pf[2][CPL][EPV];
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+#pragma unroll
+                    for (int cc = 0; cc < CPL; ++cc) unpack16<TT>(padv[k][cc], pf[k][cc]);
+                int p = 0;
+                for (; p + 2 <= npad; p += 2) {
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+#pragma unroll
+                        for (int k = 0; k < 2; ++k)
+#pragma unroll
+                            for (int cc = 0; cc < CPL; ++cc) add_pk<EPV>(acc[k][cc], pf[k][cc]);
+                }
+                if (p < npad) {
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+#pragma unroll
+                        for (int cc = 0; cc < CPL; ++cc) add_pk<EPV>(acc[k][cc], pf[k][cc]);
+                }
+            }
 #pragma unroll
             for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -317,11 +355,7 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     if (npad > 0) {
                         float f[EPV];
                         unpack16<TT>(padv[k][cc], f);
-                        if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) {
-                            for (int p = 0; p < npad; ++p)  // one add per padded position, in order
-#pragma unroll
-                                for (int e = 0; e < EPV; ++e) a[e] = __fadd_rn(a[e], f[e]);
-                        } else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) {
+                        if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) {
 #pragma unroll
                             for (int e = 0; e < EPV; ++e) a[e] = comb_step(comb, a[e], f[e]);
                         } else if (comb == RF_COMB_LAST || (comb == RF_COMB_FIRST && ul == 0)) {
@@ -366,6 +400,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     if (comb == RF_COMB_FIRST || comb == RF_COMB_LAST) {
 #pragma unroll
                         for (int e = 0; e < EPV; ++e) acc[k][cc][e] = f[e];
+                    } else if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) {
+                        add_pk<EPV>(acc[k][cc], f);
                     } else {
 #pragma unroll
                         for (int e = 0; e < EPV; ++e) acc[k][cc][e] = comb_step(comb, acc[k][cc][e], f[e]);
@@ -456,47 +492,42 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
     }
 }
 
-// lanes per row / 16-byte chunks per lane for `nchunks` chunks per row; max_lpr caps the team width so a
-// wave holds more teams (more rows in flight).
+// lanes per row / 16-byte chunks per lane for `nchunks` 16-byte chunks per row: teams of up to
+// kDefaultMaxLpr = 16 lanes (tuned on MI355X: 16 > 8 >> 4, 2), at most 4 chunks per lane.
 template <typename F>
-int dispatch_fused(int nchunks, int max_lpr, F&& f) {
+int dispatch_fused(int nchunks, F&& f) {
     using std::integral_constant;
     int lpr = 1;
-    while (lpr < nchunks && lpr < 64) lpr <<= 1;
-    lpr = std::min(lpr, max_lpr);
+    while (lpr < nchunks && lpr < kDefaultMaxLpr) lpr <<= 1;
     while ((nchunks + lpr - 1) / lpr > 4 && lpr < 64) lpr <<= 1;
     const int cpl = (nchunks + lpr - 1) / lpr;
     const int c = cpl <= 1 ? 1 : cpl <= 2 ? 2 : cpl <= 4 ? 4 : 0;
     if (c == 0) return rf_set_error(RF_EINVAL, "embedding dim too large (> 256 16-byte chunks per row)");
 #define RF_CASE(L, CP) \
     if (lpr == L && c == CP) return f(integral_constant<int, L>{}, integral_constant<int, CP>{});
-    RF_CASE(1, 1) RF_CASE(2, 1) RF_CASE(2, 2) RF_CASE(4, 1) RF_CASE(4, 2) RF_CASE(4, 4) RF_CASE(8, 1) RF_CASE(8, 2)
-    RF_CASE(8, 4) RF_CASE(16, 1) RF_CASE(16, 2) RF_CASE(16, 4) RF_CASE(32, 1) RF_CASE(32, 2) RF_CASE(32, 4)
-    RF_CASE(64, 1) RF_CASE(64, 2) RF_CASE(64, 4)
+    RF_CASE(1, 1) RF_CASE(2, 1) RF_CASE(4, 1) RF_CASE(8, 1) RF_CASE(16, 1) RF_CASE(16, 2) RF_CASE(16, 4)
+    RF_CASE(32, 4) RF_CASE(64, 4)
 #undef RF_CASE
     return rf_set_error(RF_EINVAL, "no kernel for %d lanes x %d chunks", lpr, c);
 }
 
-// One launcher per (table dtype, mode); PRE = pooling of pre-gathered rows (rf_pool_rows_fwd), a separate
-// instantiation so the hashing kernel's register allocation is not affected by the extra mode.
-template <typename TT, bool PRE>
+// One launcher per (table dtype, mode, output dtype), each in its own translation unit (parallel build).
+// PRE = pooling of pre-gathered rows (rf_pool_rows_fwd): a separate instantiation so the hashing
+// kernel's register allocation is not affected by the extra mode.
+template <typename TT, bool PRE, typename OT>
 int launch_fused_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
                       const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table,
-                      int64_t table_rows, int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
-                      int64_t* idx_out, int max_lpr, int grid, hipStream_t st) {
+                      int64_t table_rows, int32_t dim, void* out, int64_t out_stride, int32_t flags,
+                      int64_t* idx_out, int grid, hipStream_t st) {
     constexpr int epv = Elem<TT>::EPV;
-    return dispatch_fused(dim / epv, max_lpr, [&](auto lpr, auto cpl) -> int {
+    return dispatch_fused(dim / epv, [&](auto lpr, auto cpl) -> int {
         constexpr int LPR = decltype(lpr)::value, CPL = decltype(cpl)::value;
         const bool full = dim / epv == LPR * CPL;
-#define RF_FUSED_LAUNCH(FULL, OT)                                                                                    \
+#define RF_FUSED_LAUNCH(FULL)                                                                                        \
     hipLaunchKernelGGL((fused_hash_embed_kernel<LPR, CPL, FULL, TT, OT, PRE>), dim3(grid), dim3(kWaves * 64), 0, st, \
                        d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, (const TT*)table, table_rows,     \
                        dim, (OT*)out, out_stride, flags, idx_out)
-        if (out_dtype == RF_DTYPE_F32) {
-            if (full) RF_FUSED_LAUNCH(true, float); else RF_FUSED_LAUNCH(false, float);
-        } else {
-            if (full) RF_FUSED_LAUNCH(true, uint16_t); else RF_FUSED_LAUNCH(false, uint16_t);
-        }
+        if (full) RF_FUSED_LAUNCH(true); else RF_FUSED_LAUNCH(false);
 #undef RF_FUSED_LAUNCH
         return rf_check_launch(PRE ? "fused_pool_rows_kernel" : "fused_hash_embed_kernel");
     });
@@ -505,13 +536,29 @@ int launch_fused_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_
 #define RF_FUSED_LAUNCH_DECL(NAME)                                                                                     \
     int NAME(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,          \
              const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table, int64_t table_rows,      \
-             int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, int64_t* idx_out,          \
-             int max_lpr, int grid, hipStream_t st)
-// defined in rf_fused_{f32,bf16}.hip (hashing) and rf_pool_{f32,bf16}.hip (pre-gathered)
-RF_FUSED_LAUNCH_DECL(launch_fused_f32);
-RF_FUSED_LAUNCH_DECL(launch_fused_bf16);
-RF_FUSED_LAUNCH_DECL(launch_pool_f32);
-RF_FUSED_LAUNCH_DECL(launch_pool_bf16);
+             int32_t dim, void* out, int64_t out_stride, int32_t flags, int64_t* idx_out, int grid, hipStream_t st)
+// rf_{fused,pool}_<table dtype>_o<out dtype>.hip
+RF_FUSED_LAUNCH_DECL(launch_fused_f32_of32);
+RF_FUSED_LAUNCH_DECL(launch_fused_f32_obf16);
+RF_FUSED_LAUNCH_DECL(launch_fused_bf16_of32);
+RF_FUSED_LAUNCH_DECL(launch_fused_bf16_obf16);
+RF_FUSED_LAUNCH_DECL(launch_pool_f32_of32);
+RF_FUSED_LAUNCH_DECL(launch_pool_f32_obf16);
+RF_FUSED_LAUNCH_DECL(launch_pool_bf16_of32);
+RF_FUSED_LAUNCH_DECL(launch_pool_bf16_obf16);
 
+// picks the launcher for (table dtype, output dtype)
+inline int launch_fused_any(bool pre, int32_t table_dtype, int32_t out_dtype, const rf_slot_desc* d_slots,
+                            int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off, const int32_t* bag_off,
+                            const int32_t* lmax, int64_t n_units, const void* table, int64_t table_rows, int32_t dim,
+                            void* out, int64_t out_stride, int32_t flags, int64_t* idx_out, int grid, hipStream_t st) {
+    const bool tf = table_dtype == RF_DTYPE_F32, of = out_dtype == RF_DTYPE_F32;
+    auto* fn = pre ? (tf ? (of ? launch_pool_f32_of32 : launch_pool_f32_obf16)
+                         : (of ? launch_pool_bf16_of32 : launch_pool_bf16_obf16))
+                   : (tf ? (of ? launch_fused_f32_of32 : launch_fused_f32_obf16)
+                         : (of ? launch_fused_bf16_of32 : launch_fused_bf16_obf16));
+    return fn(d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table, table_rows, dim, out, out_stride,
+              flags, idx_out, grid, st);
+}
 
 }  // namespace rf

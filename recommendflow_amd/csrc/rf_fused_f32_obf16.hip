@@ -1,0 +1,11 @@
+// rf_fused_f32_obf16.hip — hashing instantiations of the fused kernel (rf_fused.h): float table, uint16_t output.
+#include "rf_fused.h"
+
+namespace rf {
+
+RF_FUSED_LAUNCH_DECL(launch_fused_f32_obf16) {
+    return launch_fused_impl<float, false, uint16_t>(d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table,
+                                             table_rows, dim, out, out_stride, flags, idx_out, grid, st);
+}
+
+}  // namespace rf
