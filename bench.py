@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--shard-rows", type=int, default=125_000_000, help="cfg4 weak scaling: fused-table rows per GPU")
     p.add_argument("--shard-dim", type=int, default=128)
     p.add_argument("--shard-batch", type=int, default=8192, help="cfg4: examples per GPU (65536 at P=8)")
+    p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
+    p.add_argument("--pipe-examples", type=int, default=16384, help="feature pipe: examples written and read back")
+    p.add_argument("--pipe-threads", type=int, default=16, help="feature pipe: reader threads (the box's CPU share)")
     return p.parse_args()
 
 
@@ -135,6 +138,8 @@ def main():
             del dev, out
         torch.cuda.empty_cache()
         extras = {"cfg3_esim_forward": bench_esim(args), "cfg2_dssm_forward": bench_dssm(args, enc, host)}
+    if world == 1 and not args.no_pipe:
+        extras = dict(extras or {}, feature_pipe=bench_pipe(args, enc, specs, multi))
 
     value = args.batch * world * args.steps / elapsed
     line = {
@@ -373,6 +378,72 @@ def bench_sharded(args, specs, multi, rank, world):
     del enc, batches, out
     torch.cuda.empty_cache()
     return res
+
+
+def bench_pipe(args, enc, specs, multi):
+    """cfg2 examples as GZIP TFRecord files (the reference's on-disk format,
+    make_tfrecord.py:142) -> C++ decode (inflate + framing CRC + tf.train.Example parse) into pinned
+    buffers -> side-stream H2D -> the fused encoder. Reports the host decode rate alone and the
+    end-to-end rate with the encoder consuming every batch (the pipe overlaps decode, copy and
+    kernel). Files are written first with zlib level 1 (not timed)."""
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    import torch
+
+    from recommendflow_amd.runtime import tfrecord as T
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    n_files = 8
+    per = max(1, args.pipe_examples // n_files)
+    fspecs = [T.FeatureSpec(s.name, T.BYTES, T.SEQ, "") for s in specs] + [T.FeatureSpec("label", T.FLOAT, T.SCALAR, 0.0)]
+    tmp = tempfile.mkdtemp(prefix="rf_pipe_", dir="/tmp")
+    paths = [os.path.join(tmp, f"part-{f:02d}.tfrecord.gz") for f in range(n_files)]
+
+    def write(f):
+        hb = synthetic_batch(per, multi, seed=777 + f)
+        fb = T.FeatureBatch(per, hb, [s.name for s in specs], None, None, np.zeros((per, 0), np.int64), [],
+                            np.ones((per, 1), np.float32), ["label"])
+        data, off = T.encode_examples(fspecs, fb)
+        with T.TFRecordWriter(paths[f], "GZIP", level=1) as w:
+            w.write_many(data, off)
+        return int(off[-1])
+
+    try:
+        with ThreadPoolExecutor(n_files) as ex:
+            raw = sum(ex.map(write, range(n_files)))
+        gz = sum(os.path.getsize(p) for p in paths)
+        B, thr = args.batch, args.pipe_threads
+        rd = T.TFRecordReader(paths, fspecs, B, thread_num=thr, pinned=True)
+        cols, n = rd.new_columns(), 0
+        t0 = time.perf_counter()
+        while True:
+            r = rd.read_into(cols)
+            if r is None:
+                break
+            cols, c = r
+            n += c.batch
+        dec = time.perf_counter() - t0
+        rd.close()
+        out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
+        pipe = T.FeaturePipe(paths, fspecs, B, thread_num=thr, prefetch=3)
+        torch.cuda.synchronize()
+        t0, m = time.perf_counter(), 0
+        for fb in pipe:
+            enc(fb.sparse, out=out[: fb.batch])
+            m += fb.batch
+        torch.cuda.synchronize()
+        e2e = time.perf_counter() - t0
+        pipe.close()
+        return {"decode_examples_per_s": round(n / dec, 1), "decode_raw_GBs": round(raw / dec / 1e9, 3),
+                "pipe_to_encoder_examples_per_s": round(m / e2e, 1), "examples": n, "threads": thr,
+                "bytes_per_example_raw": round(raw / n, 1), "bytes_per_example_gzip": round(gz / n, 1),
+                "config": f"{n_files} GZIP TFRecord files x {per} cfg2 examples (229 bytes features + label), "
+                          f"batch {B}, {thr} reader threads, pinned ring of 3, side-stream H2D, fused encoder consumes"}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def cpu_baseline(enc, hb, budget_s):

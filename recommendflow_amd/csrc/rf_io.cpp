@@ -1,0 +1,1263 @@
+// rf_io.cpp — TFRecord(GZIP) <-> batched-CSR feature pipe (include/rf_io.h). Host code only.
+//
+// Reader: per-file decompression threads (zlib inflate + TFRecord framing with masked CRC-32C)
+// feed a deterministic block_length-1 interleave (tf.data TFRecordDataset(num_parallel_reads),
+// backend/core/dataloader.py:567-570); a fork-join parse pool turns a batch of serialized
+// tf.train.Example records into the columns parse_example would produce
+// (dataloader.py:23-44, 77-89), two passes per example range: (1) locate every schema key and
+// count its values, (2) after a prefix sum over ranges, write CSR offsets and values straight into
+// the caller's (pinned) buffers. The protobuf wire format is decoded by hand (no libprotobuf).
+//
+// Writer: tf.io.TFRecordWriter(path, "GZIP") (utils/make_tfrecord.py:142) and the
+// tf.train.Example serialisation of build_tfrecord (make_tfrecord.py:94-119).
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rf_io.h"
+
+#if defined(__x86_64__)
+#include <nmmintrin.h>
+#endif
+
+int rf_set_error(int code, const char* fmt, ...);  // rf_api.cpp
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// CRC-32C (Castagnoli). SSE4.2 crc32 instruction when the host has it, slicing-by-8 otherwise.
+// ------------------------------------------------------------------------------------------------
+struct Crc32cTables {
+    uint32_t t[8][256];
+    Crc32cTables() {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+            t[0][i] = c;
+        }
+        for (uint32_t i = 0; i < 256; ++i)
+            for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xff];
+    }
+};
+const Crc32cTables& crc_tables() {
+    static const Crc32cTables tabs;
+    return tabs;
+}
+
+uint32_t crc32c_sw(uint32_t c, const uint8_t* p, size_t n) {
+    const auto& T = crc_tables().t;
+    while (n && (reinterpret_cast<uintptr_t>(p) & 7)) { c = (c >> 8) ^ T[0][(c ^ *p++) & 0xff]; --n; }
+    while (n >= 8) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        w ^= c;
+        c = T[7][w & 0xff] ^ T[6][(w >> 8) & 0xff] ^ T[5][(w >> 16) & 0xff] ^ T[4][(w >> 24) & 0xff] ^
+            T[3][(w >> 32) & 0xff] ^ T[2][(w >> 40) & 0xff] ^ T[1][(w >> 48) & 0xff] ^ T[0][w >> 56];
+        p += 8;
+        n -= 8;
+    }
+    while (n--) c = (c >> 8) ^ T[0][(c ^ *p++) & 0xff];
+    return c;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(uint32_t c, const uint8_t* p, size_t n) {
+    uint64_t c64 = c;
+    while (n >= 8) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        c64 = _mm_crc32_u64(c64, w);
+        p += 8;
+        n -= 8;
+    }
+    c = static_cast<uint32_t>(c64);
+    while (n--) c = _mm_crc32_u8(c, *p++);
+    return c;
+}
+const bool g_have_sse42 = __builtin_cpu_supports("sse4.2");
+#endif
+
+uint32_t crc32c(uint32_t crc, const void* data, size_t n) {
+    const uint8_t* p = static_cast<const uint8_t*>(data);
+    uint32_t c = ~crc;
+#if defined(__x86_64__)
+    c = g_have_sse42 ? crc32c_hw(c, p, n) : crc32c_sw(c, p, n);
+#else
+    c = crc32c_sw(c, p, n);
+#endif
+    return ~c;
+}
+
+inline uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+inline uint32_t load_u32(const uint8_t* p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+inline uint64_t load_u64(const uint8_t* p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+
+struct Status {
+    int code = RF_OK;
+    std::string msg;
+    bool ok() const { return code == RF_OK; }
+};
+Status fail(int code, std::string msg) { return Status{code, std::move(msg)}; }
+
+// ------------------------------------------------------------------------------------------------
+// Byte stream over a file, plain or gzip (concatenated members allowed).
+// ------------------------------------------------------------------------------------------------
+class InStream {
+  public:
+    InStream(const std::string& path, bool gz) : path_(path), gz_(gz) {}
+    ~InStream() {
+        if (gz_ && z_init_) inflateEnd(&zs_);
+        if (f_) std::fclose(f_);
+    }
+    Status open() {
+        f_ = std::fopen(path_.c_str(), "rb");
+        if (!f_) return fail(RF_EIO, "cannot open " + path_ + ": " + std::strerror(errno));
+        out_.resize(1 << 20);
+        if (gz_) {
+            in_.resize(1 << 20);
+            std::memset(&zs_, 0, sizeof(zs_));
+            if (inflateInit2(&zs_, 16 + MAX_WBITS) != Z_OK) return fail(RF_EIO, "inflateInit2 failed");
+            z_init_ = true;
+        }
+        return {};
+    }
+    // Reads exactly n bytes unless the stream ends first; *got = bytes delivered.
+    Status read(uint8_t* dst, size_t n, size_t* got) {
+        *got = 0;
+        while (*got < n) {
+            if (pos_ == len_) {
+                bool eof = false;
+                Status s = refill(&eof);
+                if (!s.ok()) return s;
+                if (eof) return {};
+            }
+            const size_t k = std::min(n - *got, len_ - pos_);
+            std::memcpy(dst + *got, out_.data() + pos_, k);
+            pos_ += k;
+            *got += k;
+        }
+        return {};
+    }
+
+  private:
+    Status refill(bool* eof) {
+        pos_ = len_ = 0;
+        if (!gz_) {
+            len_ = std::fread(out_.data(), 1, out_.size(), f_);
+            if (len_ == 0) {
+                if (std::ferror(f_)) return fail(RF_EIO, "read error in " + path_);
+                *eof = true;
+            }
+            return {};
+        }
+        while (len_ == 0) {
+            if (zs_.avail_in == 0) {
+                const size_t k = std::fread(in_.data(), 1, in_.size(), f_);
+                if (k == 0) {
+                    if (std::ferror(f_)) return fail(RF_EIO, "read error in " + path_);
+                    if (!member_open_) { *eof = true; return {}; }
+                    return fail(RF_EDATA, "truncated gzip stream in " + path_);
+                }
+                zs_.next_in = in_.data();
+                zs_.avail_in = static_cast<uInt>(k);
+            }
+            if (!member_open_) {
+                // a new gzip member begins (the first, or one concatenated after a finished one)
+                member_open_ = true;
+            }
+            zs_.next_out = out_.data();
+            zs_.avail_out = static_cast<uInt>(out_.size());
+            const int rc = inflate(&zs_, Z_NO_FLUSH);
+            len_ = out_.size() - zs_.avail_out;
+            if (rc == Z_STREAM_END) {
+                member_open_ = false;
+                if (inflateReset(&zs_) != Z_OK) return fail(RF_EIO, "inflateReset failed");
+            } else if (rc != Z_OK && rc != Z_BUF_ERROR) {
+                return fail(RF_EDATA, std::string("corrupt gzip stream in ") + path_ + ": " +
+                                          (zs_.msg ? zs_.msg : "inflate error"));
+            }
+        }
+        return {};
+    }
+
+    std::string path_;
+    bool gz_;
+    FILE* f_ = nullptr;
+    z_stream zs_;
+    bool z_init_ = false, member_open_ = false;
+    std::vector<uint8_t> in_, out_;
+    size_t pos_ = 0, len_ = 0;
+};
+
+// Records of one file in decode order, packed into chunks.
+struct Chunk {
+    std::vector<uint8_t> data;
+    std::vector<uint64_t> off{0};  // record i = data[off[i], off[i+1])
+    size_t size() const { return off.size() - 1; }
+};
+
+// One open file: a thread decompresses and de-frames records into a bounded chunk queue.
+class FileProducer {
+  public:
+    FileProducer(std::string path, bool gz) : path_(std::move(path)), gz_(gz) {
+        th_ = std::thread([this] { run(); });
+    }
+    ~FileProducer() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // 1 = record, 0 = end of file, -1 = error (status()).
+    int next(const uint8_t** p, uint32_t* n, std::shared_ptr<Chunk>* hold) {
+        if (!cur_ || idx_ == cur_->size()) {
+            std::unique_lock<std::mutex> g(mu_);
+            cv_.wait(g, [this] { return !q_.empty() || done_; });
+            if (q_.empty()) return st_.ok() ? 0 : -1;
+            cur_ = std::move(q_.front());
+            q_.pop_front();
+            idx_ = 0;
+            g.unlock();
+            cv_.notify_all();
+        }
+        *p = cur_->data.data() + cur_->off[idx_];
+        *n = static_cast<uint32_t>(cur_->off[idx_ + 1] - cur_->off[idx_]);
+        *hold = cur_;
+        ++idx_;
+        return 1;
+    }
+    const Status& status() const { return st_; }
+
+  private:
+    static constexpr size_t kChunkRecords = 1024, kChunkBytes = 4u << 20, kQueueChunks = 6;
+
+    void run() {
+        Status s = produce();
+        std::lock_guard<std::mutex> g(mu_);
+        st_ = s;
+        done_ = true;
+        cv_.notify_all();
+    }
+    Status produce() {
+        InStream in(path_, gz_);
+        Status s = in.open();
+        if (!s.ok()) return s;
+        auto chunk = std::make_shared<Chunk>();
+        uint64_t rec_no = 0;
+        for (;;) {
+            uint8_t hdr[12];
+            size_t got = 0;
+            s = in.read(hdr, 12, &got);
+            if (!s.ok()) return s;
+            if (got == 0) break;
+            if (got < 12) return fail(RF_EDATA, "truncated record header at record " + std::to_string(rec_no) + " of " + path_);
+            const uint64_t len = load_u64(hdr);
+            if (mask_crc(crc32c(0, hdr, 8)) != load_u32(hdr + 8))
+                return fail(RF_EDATA, "corrupted record length crc at record " + std::to_string(rec_no) + " of " + path_);
+            if (len > (1ull << 31)) return fail(RF_EDATA, "record too large at record " + std::to_string(rec_no) + " of " + path_);
+            const size_t base = chunk->data.size();
+            chunk->data.resize(base + len + 4);
+            s = in.read(chunk->data.data() + base, len + 4, &got);
+            if (!s.ok()) return s;
+            if (got < len + 4) return fail(RF_EDATA, "truncated record at record " + std::to_string(rec_no) + " of " + path_);
+            const uint32_t want = load_u32(chunk->data.data() + base + len);
+            if (mask_crc(crc32c(0, chunk->data.data() + base, len)) != want)
+                return fail(RF_EDATA, "corrupted record data crc at record " + std::to_string(rec_no) + " of " + path_);
+            chunk->data.resize(base + len);
+            chunk->off.push_back(base + len);
+            ++rec_no;
+            if (chunk->size() >= kChunkRecords || chunk->data.size() >= kChunkBytes) {
+                if (!push(std::move(chunk))) return {};
+                chunk = std::make_shared<Chunk>();
+            }
+        }
+        if (chunk->size()) push(std::move(chunk));
+        return {};
+    }
+    bool push(std::shared_ptr<Chunk> c) {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [this] { return q_.size() < kQueueChunks || stop_; });
+        if (stop_) return false;
+        q_.push_back(std::move(c));
+        cv_.notify_all();
+        return true;
+    }
+
+    std::string path_;
+    bool gz_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Chunk>> q_;
+    bool done_ = false, stop_ = false;
+    Status st_;
+    std::shared_ptr<Chunk> cur_;
+    size_t idx_ = 0;
+    std::thread th_;
+};
+
+// Fork-join pool: run(n, f) calls f(0..n-1) on the workers plus the calling thread.
+class Pool {
+  public:
+    explicit Pool(int n_threads) {
+        for (int i = 1; i < n_threads; ++i) ws_.emplace_back([this] { work(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : ws_) t.join();
+    }
+    int size() const { return static_cast<int>(ws_.size()) + 1; }
+    void run(int n, const std::function<void(int)>& f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &f;
+            n_ = n;
+            next_.store(0);
+            pending_ = n;
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void drain() {
+        for (;;) {
+            const int i = next_.fetch_add(1);
+            if (i >= n_) return;
+            (*fn_)(i);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_cv_.notify_all();
+        }
+    }
+    void work() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            drain();
+        }
+    }
+    std::vector<std::thread> ws_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int n_ = 0, pending_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Protobuf wire decoding (tf.train.Example / Features / Feature / {Bytes,Float,Int64}List).
+// ------------------------------------------------------------------------------------------------
+inline bool get_varint(const uint8_t*& p, const uint8_t* e, uint64_t* v) {
+    uint64_t r = 0;
+    for (int s = 0; s < 64 && p < e; s += 7) {
+        const uint8_t b = *p++;
+        r |= static_cast<uint64_t>(b & 0x7f) << s;
+        if (!(b & 0x80)) { *v = r; return true; }
+    }
+    return false;
+}
+
+// Skips a field of the given wire type; false if malformed.
+inline bool skip_field(const uint8_t*& p, const uint8_t* e, uint32_t wt) {
+    uint64_t v;
+    switch (wt) {
+        case 0: return get_varint(p, e, &v);
+        case 1: if (e - p < 8) return false; p += 8; return true;
+        case 2: if (!get_varint(p, e, &v) || static_cast<uint64_t>(e - p) < v) return false; p += v; return true;
+        case 5: if (e - p < 4) return false; p += 4; return true;
+        default: return false;
+    }
+}
+
+// Reads a length-delimited payload span.
+inline bool get_span(const uint8_t*& p, const uint8_t* e, const uint8_t** s, uint32_t* n) {
+    uint64_t v;
+    if (!get_varint(p, e, &v) || static_cast<uint64_t>(e - p) < v) return false;
+    *s = p;
+    *n = static_cast<uint32_t>(v);
+    p += v;
+    return true;
+}
+
+struct Span {
+    const uint8_t* p = nullptr;
+    uint32_t n = 0;
+    int32_t kind = -1;  // RF_TFR_* of the list, -1 = key absent, -2 = Feature with no kind set
+};
+
+// Feature message -> (kind, list span). oneof: the last kind field wins.
+inline bool decode_feature(const uint8_t* p, uint32_t n, Span* out) {
+    const uint8_t* e = p + n;
+    out->kind = -2;
+    out->p = nullptr;
+    out->n = 0;
+    while (p < e) {
+        uint64_t tag;
+        if (!get_varint(p, e, &tag)) return false;
+        const uint32_t field = static_cast<uint32_t>(tag >> 3), wt = tag & 7;
+        if (wt == 2 && field >= 1 && field <= 3) {
+            if (!get_span(p, e, &out->p, &out->n)) return false;
+            out->kind = field == 1 ? RF_TFR_BYTES : field == 2 ? RF_TFR_FLOAT : RF_TFR_INT64;
+        } else if (!skip_field(p, e, wt)) {
+            return false;
+        }
+    }
+    return true;
+}
+
+// Counts the values of a list (and the payload bytes of a BytesList).
+inline bool count_list(const Span& s, int64_t* count, int64_t* nbytes) {
+    const uint8_t* p = s.p;
+    const uint8_t* e = p + s.n;
+    int64_t c = 0, b = 0;
+    while (p < e) {
+        uint64_t tag;
+        if (!get_varint(p, e, &tag)) return false;
+        const uint32_t field = static_cast<uint32_t>(tag >> 3), wt = tag & 7;
+        if (field != 1) {
+            if (!skip_field(p, e, wt)) return false;
+            continue;
+        }
+        if (s.kind == RF_TFR_BYTES) {
+            if (wt != 2) return false;
+            const uint8_t* v;
+            uint32_t n;
+            if (!get_span(p, e, &v, &n)) return false;
+            ++c;
+            b += n;
+        } else if (s.kind == RF_TFR_FLOAT) {
+            if (wt == 5) {
+                if (e - p < 4) return false;
+                p += 4;
+                ++c;
+            } else if (wt == 2) {
+                const uint8_t* v;
+                uint32_t n;
+                if (!get_span(p, e, &v, &n) || (n & 3)) return false;
+                c += n / 4;
+            } else {
+                return false;
+            }
+        } else {
+            if (wt == 0) {
+                uint64_t v;
+                if (!get_varint(p, e, &v)) return false;
+                ++c;
+            } else if (wt == 2) {
+                const uint8_t* v;
+                uint32_t n;
+                if (!get_span(p, e, &v, &n)) return false;
+                const uint8_t* q = v;
+                const uint8_t* qe = v + n;
+                while (q < qe) {
+                    uint64_t x;
+                    if (!get_varint(q, qe, &x)) return false;
+                    ++c;
+                }
+            } else {
+                return false;
+            }
+        }
+    }
+    *count = c;
+    *nbytes = b;
+    return true;
+}
+
+// Writes the values of an already-validated list.
+// Returns the byte cursor after the list.
+inline int64_t write_bytes(const Span& s, uint8_t* tok_bytes, int32_t* tok_off, int64_t byte_cursor) {
+    const uint8_t* p = s.p;
+    const uint8_t* e = p + s.n;
+    int64_t t = 0;
+    while (p < e) {
+        uint64_t tag = 0;
+        get_varint(p, e, &tag);
+        if ((tag >> 3) != 1) { skip_field(p, e, tag & 7); continue; }
+        const uint8_t* v = nullptr;
+        uint32_t n = 0;
+        get_span(p, e, &v, &n);
+        std::memcpy(tok_bytes + byte_cursor, v, n);
+        tok_off[t++] = static_cast<int32_t>(byte_cursor);
+        byte_cursor += n;
+    }
+    return byte_cursor;
+}
+inline void write_floats(const Span& s, float* dst) {
+    const uint8_t* p = s.p;
+    const uint8_t* e = p + s.n;
+    while (p < e) {
+        uint64_t tag = 0;
+        get_varint(p, e, &tag);
+        if ((tag >> 3) != 1) { skip_field(p, e, tag & 7); continue; }
+        if ((tag & 7) == 5) {
+            std::memcpy(dst++, p, 4);
+            p += 4;
+        } else {
+            const uint8_t* v = nullptr;
+            uint32_t n = 0;
+            get_span(p, e, &v, &n);
+            std::memcpy(dst, v, n);
+            dst += n / 4;
+        }
+    }
+}
+inline void write_int64s(const Span& s, int64_t* dst) {
+    const uint8_t* p = s.p;
+    const uint8_t* e = p + s.n;
+    while (p < e) {
+        uint64_t tag = 0;
+        get_varint(p, e, &tag);
+        if ((tag >> 3) != 1) { skip_field(p, e, tag & 7); continue; }
+        uint64_t x = 0;
+        if ((tag & 7) == 0) {
+            get_varint(p, e, &x);
+            *dst++ = static_cast<int64_t>(x);
+        } else {
+            const uint8_t* v = nullptr;
+            uint32_t n = 0;
+            get_span(p, e, &v, &n);
+            const uint8_t* qe = v + n;
+            while (v < qe) {
+                get_varint(v, qe, &x);
+                *dst++ = static_cast<int64_t>(x);
+            }
+        }
+    }
+}
+
+// Compiled schema: map key -> feature index, and each feature's group and position.
+struct Schema {
+    std::vector<std::string> names;
+    std::vector<int32_t> kind, shape, group_pos;  // group_pos: index within its output group
+    std::vector<int64_t> def_i;
+    std::vector<float> def_f;
+    std::unordered_map<std::string_view, int32_t> index;
+    int32_t n_bytes = 0, n_iseq = 0, n_fseq = 0, n_iscalar = 0, n_fscalar = 0;
+
+    Status build(const rf_tfr_feature* f, int32_t n) {
+        names.reserve(n);
+        for (int32_t j = 0; j < n; ++j) {
+            if (!f[j].name) return fail(RF_EINVAL, "feature " + std::to_string(j) + " has no name");
+            if (f[j].kind < RF_TFR_BYTES || f[j].kind > RF_TFR_FLOAT)
+                return fail(RF_EINVAL, std::string("feature ") + f[j].name + ": bad kind");
+            if (f[j].shape != RF_TFR_SEQ && f[j].shape != RF_TFR_SCALAR)
+                return fail(RF_EINVAL, std::string("feature ") + f[j].name + ": bad shape");
+            names.emplace_back(f[j].name);
+            kind.push_back(f[j].kind);
+            shape.push_back(f[j].shape);
+            def_i.push_back(f[j].default_i);
+            def_f.push_back(static_cast<float>(f[j].default_f));
+            int32_t pos;
+            if (f[j].kind == RF_TFR_BYTES) pos = n_bytes++;
+            else if (f[j].shape == RF_TFR_SEQ) pos = f[j].kind == RF_TFR_INT64 ? n_iseq++ : n_fseq++;
+            else pos = f[j].kind == RF_TFR_INT64 ? n_iscalar++ : n_fscalar++;
+            group_pos.push_back(pos);
+        }
+        for (int32_t j = 0; j < n; ++j) {
+            if (!index.emplace(std::string_view(names[j]), j).second)
+                return fail(RF_EINVAL, "duplicate feature name " + names[j]);
+        }
+        return {};
+    }
+    int32_t size() const { return static_cast<int32_t>(names.size()); }
+};
+
+// Locates every schema key of one Example: spans[j] (kind -1 = absent). Last map entry wins.
+bool locate(const Schema& sc, const uint8_t* p, uint32_t n, Span* spans) {
+    const int32_t F = sc.size();
+    for (int32_t j = 0; j < F; ++j) spans[j].kind = -1;
+    const uint8_t* e = p + n;
+    int32_t guess = 0;
+    while (p < e) {  // Example
+        uint64_t tag;
+        if (!get_varint(p, e, &tag)) return false;
+        if (tag != ((1u << 3) | 2)) {
+            if (!skip_field(p, e, tag & 7)) return false;
+            continue;
+        }
+        const uint8_t* fs;
+        uint32_t fn;
+        if (!get_span(p, e, &fs, &fn)) return false;
+        const uint8_t* fe = fs + fn;
+        while (fs < fe) {  // Features: repeated map entry (field 1)
+            if (!get_varint(fs, fe, &tag)) return false;
+            if (tag != ((1u << 3) | 2)) {
+                if (!skip_field(fs, fe, tag & 7)) return false;
+                continue;
+            }
+            const uint8_t* es;
+            uint32_t en;
+            if (!get_span(fs, fe, &es, &en)) return false;
+            const uint8_t* ee = es + en;
+            const uint8_t* key = nullptr;
+            uint32_t key_n = 0;
+            const uint8_t* val = nullptr;
+            uint32_t val_n = 0;
+            bool has_val = false;
+            while (es < ee) {  // map entry {1: key, 2: Feature}
+                uint64_t t2;
+                if (!get_varint(es, ee, &t2)) return false;
+                if (t2 == ((1u << 3) | 2)) {
+                    if (!get_span(es, ee, &key, &key_n)) return false;
+                } else if (t2 == ((2u << 3) | 2)) {
+                    if (!get_span(es, ee, &val, &val_n)) return false;
+                    has_val = true;
+                } else if (!skip_field(es, ee, t2 & 7)) {
+                    return false;
+                }
+            }
+            // fast path: examples written by one writer list keys in schema order
+            int32_t j = -1;
+            if (guess < F && sc.names[guess].size() == key_n && std::memcmp(sc.names[guess].data(), key, key_n) == 0) {
+                j = guess;
+            } else {
+                auto it = sc.index.find(std::string_view(reinterpret_cast<const char*>(key), key_n));
+                if (it != sc.index.end()) j = it->second;
+            }
+            if (j < 0) continue;  // not in the feature description: ignored, as parse_example does
+            guess = j + 1;
+            if (has_val) {
+                if (!decode_feature(val, val_n, &spans[j])) return false;
+            } else {
+                spans[j].kind = -2;
+                spans[j].p = nullptr;
+                spans[j].n = 0;
+            }
+        }
+    }
+    return true;
+}
+
+const char* kind_name(int32_t k) { return k == RF_TFR_BYTES ? "bytes" : k == RF_TFR_INT64 ? "int64" : "float"; }
+
+// ------------------------------------------------------------------------------------------------
+// Reader
+// ------------------------------------------------------------------------------------------------
+struct Rec {
+    const uint8_t* p;
+    uint32_t n;
+};
+
+class Reader {
+  public:
+    Reader(std::vector<std::string> paths, bool gz, int n_threads)
+        : paths_(std::move(paths)), gz_(gz), pool_(std::max(1, n_threads)) {
+        cycle_.resize(std::max<size_t>(1, std::min<size_t>(paths_.size(), static_cast<size_t>(std::max(1, n_threads)))));
+    }
+
+    Status next_batch(const Schema& sc, int32_t batch, rf_tfr_columns* cols) {
+        Status s = fill(batch);
+        if (!s.ok()) return s;
+        const int32_t B = static_cast<int32_t>(std::min<size_t>(batch, pend_.size()));
+        s = parse(sc, B, cols);
+        if (!s.ok()) return s;
+        if (cols->batch == B) {  // consumed: drop the records (and the chunks that held them)
+            pend_.erase(pend_.begin(), pend_.begin() + B);
+            hold_.erase(hold_.begin(), hold_.begin() + B);
+            handed_ += B;
+        }
+        return {};
+    }
+    int64_t handed() const { return handed_; }
+
+  private:
+    // Interleave (tf.data InterleaveDataset order, block_length 1) until `batch` records are pending.
+    Status fill(int32_t batch) {
+        while (pend_.size() < static_cast<size_t>(batch)) {
+            if (!any_open_ && next_path_ >= paths_.size()) return {};
+            auto& slot = cycle_[cursor_];
+            if (!slot) {
+                if (next_path_ < paths_.size()) {
+                    slot = std::make_unique<FileProducer>(paths_[next_path_++], gz_);
+                    ++n_open_;
+                    any_open_ = true;
+                    continue;  // the new file produces in this same turn
+                }
+                cursor_ = (cursor_ + 1) % cycle_.size();
+                continue;
+            }
+            const uint8_t* p;
+            uint32_t n;
+            std::shared_ptr<Chunk> hold;
+            const int r = slot->next(&p, &n, &hold);
+            if (r == 1) {
+                pend_.push_back({p, n});
+                hold_.push_back(std::move(hold));
+                cursor_ = (cursor_ + 1) % cycle_.size();
+            } else if (r == 0) {
+                slot.reset();
+                any_open_ = --n_open_ > 0;
+                cursor_ = (cursor_ + 1) % cycle_.size();
+            } else {
+                Status st = slot->status();
+                return st;
+            }
+        }
+        return {};
+    }
+
+    Status parse(const Schema& sc, int32_t B, rf_tfr_columns* c) {
+        const int32_t F = sc.size();
+        c->batch = 0;
+        if (B == 0) {
+            c->n_tok = c->n_tok_bytes = c->n_ival = c->n_fval = 0;
+            return {};
+        }
+        spans_.resize(static_cast<size_t>(B) * F);
+        const int T = std::min(pool_.size() * 4, std::max(1, B / 16));
+        struct Part {
+            int64_t tok = 0, bytes = 0, ival = 0, fval = 0;
+            std::vector<int32_t> lmax;
+            Status st;
+        };
+        std::vector<Part> parts(T);
+        const int32_t Sb = sc.n_bytes, Si = sc.n_iseq, Sf = sc.n_fseq;
+        auto range = [&](int t, int32_t* b0, int32_t* b1) {
+            *b0 = static_cast<int32_t>(static_cast<int64_t>(B) * t / T);
+            *b1 = static_cast<int32_t>(static_cast<int64_t>(B) * (t + 1) / T);
+        };
+        // counts[b*F + j] = value count (bytes: token count); byte totals per (b, j) are not needed
+        counts_.resize(static_cast<size_t>(B) * F);
+        pool_.run(T, [&](int t) {
+            Part& pt = parts[t];
+            pt.lmax.assign(static_cast<size_t>(Sb + Si + Sf), 0);
+            int32_t b0, b1;
+            range(t, &b0, &b1);
+            for (int32_t b = b0; b < b1; ++b) {
+                Span* sp = &spans_[static_cast<size_t>(b) * F];
+                if (!locate(sc, pend_[b].p, pend_[b].n, sp)) {
+                    pt.st = fail(RF_EDATA, "malformed tf.train.Example at batch position " + std::to_string(b) +
+                                               " (record " + std::to_string(handed_ + b) + ")");
+                    return;
+                }
+                for (int32_t j = 0; j < F; ++j) {
+                    Span& s = sp[j];
+                    int64_t cnt = 0, nb = 0;
+                    if (s.kind >= 0) {
+                        if (s.kind != sc.kind[j]) {
+                            pt.st = fail(RF_EDATA, "Key: " + sc.names[j] + ". Data types don't match. Expected " +
+                                                       kind_name(sc.kind[j]) + ", got " + kind_name(s.kind) +
+                                                       " (record " + std::to_string(handed_ + b) + ")");
+                            return;
+                        }
+                        if (!count_list(s, &cnt, &nb)) {
+                            pt.st = fail(RF_EDATA, "Key: " + sc.names[j] + ". malformed " + kind_name(s.kind) +
+                                                       " list (record " + std::to_string(handed_ + b) + ")");
+                            return;
+                        }
+                    } else if (s.kind == -2) {
+                        s.kind = sc.kind[j];  // Feature with no kind: an empty list
+                        s.p = nullptr;
+                        s.n = 0;
+                    }
+                    if (sc.shape[j] == RF_TFR_SCALAR) {
+                        if (s.kind == -1) {
+                            cnt = sc.kind[j] == RF_TFR_BYTES ? 1 : 0;  // missing -> default ("" is one empty token)
+                        } else if (cnt != 1) {
+                            pt.st = fail(RF_EDATA, "Key: " + sc.names[j] + ". Number of values != expected. Values size: " +
+                                                       std::to_string(cnt) + " but output shape: [] (record " +
+                                                       std::to_string(handed_ + b) + ")");
+                            return;
+                        }
+                    }
+                    if (cnt > INT32_MAX) {
+                        pt.st = fail(RF_EDATA, "Key: " + sc.names[j] + ": list too long");
+                        return;
+                    }
+                    counts_[static_cast<size_t>(b) * F + j] = static_cast<int32_t>(cnt);
+                    const int32_t g = sc.group_pos[j];
+                    if (sc.kind[j] == RF_TFR_BYTES) {
+                        pt.tok += cnt;
+                        pt.bytes += nb;
+                        pt.lmax[g] = std::max<int32_t>(pt.lmax[g], static_cast<int32_t>(cnt));
+                    } else if (sc.shape[j] == RF_TFR_SEQ) {
+                        if (sc.kind[j] == RF_TFR_INT64) {
+                            pt.ival += cnt;
+                            pt.lmax[Sb + g] = std::max<int32_t>(pt.lmax[Sb + g], static_cast<int32_t>(cnt));
+                        } else {
+                            pt.fval += cnt;
+                            pt.lmax[Sb + Si + g] = std::max<int32_t>(pt.lmax[Sb + Si + g], static_cast<int32_t>(cnt));
+                        }
+                    }
+                }
+            }
+        });
+        for (auto& pt : parts)
+            if (!pt.st.ok()) return pt.st;
+        // exclusive scan over ranges
+        std::vector<int64_t> tok0(T + 1, 0), bytes0(T + 1, 0), ival0(T + 1, 0), fval0(T + 1, 0);
+        for (int t = 0; t < T; ++t) {
+            tok0[t + 1] = tok0[t] + parts[t].tok;
+            bytes0[t + 1] = bytes0[t] + parts[t].bytes;
+            ival0[t + 1] = ival0[t] + parts[t].ival;
+            fval0[t + 1] = fval0[t] + parts[t].fval;
+        }
+        c->n_tok = tok0[T];
+        c->n_tok_bytes = bytes0[T];
+        c->n_ival = ival0[T];
+        c->n_fval = fval0[T];
+        if (c->n_tok_bytes > INT32_MAX || c->n_tok > INT32_MAX || c->n_ival > INT32_MAX || c->n_fval > INT32_MAX)
+            return fail(RF_EINVAL, "batch too large for int32 CSR offsets; use a smaller batch");
+        if (c->n_tok > c->tok_cap || c->n_tok_bytes > c->tok_bytes_cap || c->n_ival > c->ival_cap || c->n_fval > c->fval_cap)
+            return fail(RF_ENOSPC, "column capacity too small: need tok " + std::to_string(c->n_tok) + " bytes " +
+                                       std::to_string(c->n_tok_bytes) + " ival " + std::to_string(c->n_ival) + " fval " +
+                                       std::to_string(c->n_fval));
+        if ((Sb && (!c->tok_off || !c->bag_off || !c->lmax || (c->n_tok_bytes && !c->tok_bytes))) ||
+            (Si && (!c->ibag_off || !c->ilmax || (c->n_ival && !c->ival))) ||
+            (Sf && (!c->fbag_off || !c->flmax || (c->n_fval && !c->fval))) || (sc.n_iscalar && !c->iscalar) ||
+            (sc.n_fscalar && !c->fscalar))
+            return fail(RF_EINVAL, "a column buffer the schema needs is NULL");
+        pool_.run(T, [&](int t) {
+            int32_t b0, b1;
+            range(t, &b0, &b1);
+            int64_t tok = tok0[t], byt = bytes0[t], iv = ival0[t], fv = fval0[t];
+            for (int32_t b = b0; b < b1; ++b) {
+                const Span* sp = &spans_[static_cast<size_t>(b) * F];
+                const int32_t* cn = &counts_[static_cast<size_t>(b) * F];
+                for (int32_t j = 0; j < F; ++j) {
+                    const int32_t g = sc.group_pos[j];
+                    const Span& s = sp[j];
+                    const int32_t cnt = cn[j];
+                    if (sc.kind[j] == RF_TFR_BYTES) {
+                        c->bag_off[static_cast<int64_t>(b) * Sb + g] = static_cast<int32_t>(tok);
+                        if (s.kind >= 0) {
+                            byt = write_bytes(s, c->tok_bytes, c->tok_off + tok, byt);
+                        } else if (cnt == 1) {  // missing SCALAR bytes -> default b""
+                            c->tok_off[tok] = static_cast<int32_t>(byt);
+                        }
+                        tok += cnt;
+                    } else if (sc.shape[j] == RF_TFR_SEQ) {
+                        if (sc.kind[j] == RF_TFR_INT64) {
+                            c->ibag_off[static_cast<int64_t>(b) * Si + g] = static_cast<int32_t>(iv);
+                            if (s.kind >= 0) write_int64s(s, c->ival + iv);
+                            iv += cnt;
+                        } else {
+                            c->fbag_off[static_cast<int64_t>(b) * Sf + g] = static_cast<int32_t>(fv);
+                            if (s.kind >= 0) write_floats(s, c->fval + fv);
+                            fv += cnt;
+                        }
+                    } else if (sc.kind[j] == RF_TFR_INT64) {
+                        int64_t v = sc.def_i[j];
+                        if (s.kind >= 0) write_int64s(s, &v);
+                        c->iscalar[static_cast<int64_t>(b) * sc.n_iscalar + g] = v;
+                    } else {
+                        float v = sc.def_f[j];
+                        if (s.kind >= 0) write_floats(s, &v);
+                        c->fscalar[static_cast<int64_t>(b) * sc.n_fscalar + g] = v;
+                    }
+                }
+            }
+        });
+        if (Sb) {
+            c->bag_off[static_cast<int64_t>(B) * Sb] = static_cast<int32_t>(c->n_tok);
+            c->tok_off[c->n_tok] = static_cast<int32_t>(c->n_tok_bytes);
+            for (int32_t g = 0; g < Sb; ++g) {
+                int32_t m = 0;
+                for (auto& pt : parts) m = std::max(m, pt.lmax[g]);
+                c->lmax[g] = m;
+            }
+        }
+        if (Si) {
+            c->ibag_off[static_cast<int64_t>(B) * Si] = static_cast<int32_t>(c->n_ival);
+            for (int32_t g = 0; g < Si; ++g) {
+                int32_t m = 0;
+                for (auto& pt : parts) m = std::max(m, pt.lmax[Sb + g]);
+                c->ilmax[g] = m;
+            }
+        }
+        if (Sf) {
+            c->fbag_off[static_cast<int64_t>(B) * Sf] = static_cast<int32_t>(c->n_fval);
+            for (int32_t g = 0; g < Sf; ++g) {
+                int32_t m = 0;
+                for (auto& pt : parts) m = std::max(m, pt.lmax[Sb + Si + g]);
+                c->flmax[g] = m;
+            }
+        }
+        c->batch = B;
+        return {};
+    }
+
+    std::vector<std::string> paths_;
+    bool gz_;
+    Pool pool_;
+    std::vector<std::unique_ptr<FileProducer>> cycle_;
+    size_t cursor_ = 0, next_path_ = 0;
+    int n_open_ = 0;
+    bool any_open_ = false;
+    std::vector<Rec> pend_;
+    std::vector<std::shared_ptr<Chunk>> hold_;
+    std::vector<Span> spans_;
+    std::vector<int32_t> counts_;
+    int64_t handed_ = 0;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Writer
+// ------------------------------------------------------------------------------------------------
+class Writer {
+  public:
+    Writer(FILE* f, bool gz) : f_(f), gz_(gz) {}
+    Status init(int level) {
+        if (!gz_) return {};
+        std::memset(&zs_, 0, sizeof(zs_));
+        if (deflateInit2(&zs_, level, Z_DEFLATED, 16 + MAX_WBITS, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+            return fail(RF_EINVAL, "deflateInit2 failed (level " + std::to_string(level) + ")");
+        z_init_ = true;
+        out_.resize(1 << 18);
+        return {};
+    }
+    Status write(const uint8_t* p, size_t n) {
+        if (failed_) return fail(RF_EIO, "an earlier write failed");
+        if (!gz_) {
+            if (std::fwrite(p, 1, n, f_) != n) { failed_ = true; return fail(RF_EIO, "fwrite failed"); }
+            return {};
+        }
+        zs_.next_in = const_cast<uint8_t*>(p);
+        zs_.avail_in = static_cast<uInt>(n);
+        while (zs_.avail_in) {
+            Status s = pump(Z_NO_FLUSH);
+            if (!s.ok()) return s;
+        }
+        return {};
+    }
+    Status close() {
+        Status s;
+        if (gz_ && z_init_) {
+            int rc;
+            do {
+                zs_.next_out = out_.data();
+                zs_.avail_out = static_cast<uInt>(out_.size());
+                rc = deflate(&zs_, Z_FINISH);
+                const size_t k = out_.size() - zs_.avail_out;
+                if (k && std::fwrite(out_.data(), 1, k, f_) != k) failed_ = true;
+            } while (rc == Z_OK);
+            if (rc != Z_STREAM_END) failed_ = true;
+            deflateEnd(&zs_);
+            z_init_ = false;
+        }
+        if (std::fclose(f_) != 0) failed_ = true;
+        f_ = nullptr;
+        if (failed_) s = fail(RF_EIO, "write/close failed");
+        return s;
+    }
+    ~Writer() {
+        if (z_init_) deflateEnd(&zs_);
+        if (f_) std::fclose(f_);
+    }
+
+  private:
+    Status pump(int flush) {
+        zs_.next_out = out_.data();
+        zs_.avail_out = static_cast<uInt>(out_.size());
+        const int rc = deflate(&zs_, flush);
+        if (rc == Z_STREAM_ERROR) { failed_ = true; return fail(RF_EIO, "deflate failed"); }
+        const size_t k = out_.size() - zs_.avail_out;
+        if (k && std::fwrite(out_.data(), 1, k, f_) != k) { failed_ = true; return fail(RF_EIO, "fwrite failed"); }
+        return {};
+    }
+    FILE* f_;
+    bool gz_;
+    z_stream zs_;
+    bool z_init_ = false, failed_ = false;
+    std::vector<uint8_t> out_;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Example encoding
+// ------------------------------------------------------------------------------------------------
+inline size_t varint_size(uint64_t v) {
+    size_t n = 1;
+    while (v >= 0x80) { v >>= 7; ++n; }
+    return n;
+}
+inline uint8_t* put_varint(uint8_t* p, uint64_t v) {
+    while (v >= 0x80) { *p++ = static_cast<uint8_t>(v | 0x80); v >>= 7; }
+    *p++ = static_cast<uint8_t>(v);
+    return p;
+}
+
+struct ListView {  // one (example, feature) value list of the input columns
+    int32_t kind;
+    int64_t begin, end;  // element range in its group's value array (bytes: token range)
+    int64_t scalar_i;
+    float scalar_f;
+    bool scalar;
+};
+
+struct Encoder {
+    const Schema& sc;
+    const rf_tfr_columns& c;
+
+    ListView view(int32_t b, int32_t j) const {
+        ListView v{sc.kind[j], 0, 0, 0, 0.f, false};
+        const int32_t g = sc.group_pos[j];
+        if (sc.kind[j] == RF_TFR_BYTES) {
+            v.begin = c.bag_off[static_cast<int64_t>(b) * sc.n_bytes + g];
+            v.end = c.bag_off[static_cast<int64_t>(b) * sc.n_bytes + g + 1];
+        } else if (sc.shape[j] == RF_TFR_SEQ) {
+            const int32_t* bo = sc.kind[j] == RF_TFR_INT64 ? c.ibag_off : c.fbag_off;
+            const int32_t S = sc.kind[j] == RF_TFR_INT64 ? sc.n_iseq : sc.n_fseq;
+            v.begin = bo[static_cast<int64_t>(b) * S + g];
+            v.end = bo[static_cast<int64_t>(b) * S + g + 1];
+        } else {
+            v.scalar = true;
+            if (sc.kind[j] == RF_TFR_INT64) v.scalar_i = c.iscalar[static_cast<int64_t>(b) * sc.n_iscalar + g];
+            else v.scalar_f = c.fscalar[static_cast<int64_t>(b) * sc.n_fscalar + g];
+        }
+        return v;
+    }
+    // payload size of the {Bytes,Float,Int64}List message
+    size_t list_size(const ListView& v) const {
+        if (v.kind == RF_TFR_BYTES) {
+            size_t s = 0;
+            for (int64_t t = v.begin; t < v.end; ++t) {
+                const uint64_t n = static_cast<uint64_t>(c.tok_off[t + 1] - c.tok_off[t]);
+                s += 1 + varint_size(n) + n;
+            }
+            return s;
+        }
+        if (v.kind == RF_TFR_FLOAT) {
+            const uint64_t n = v.scalar ? 1 : static_cast<uint64_t>(v.end - v.begin);
+            return n ? 1 + varint_size(4 * n) + 4 * n : 0;
+        }
+        uint64_t n = 0;
+        if (v.scalar) n = varint_size(static_cast<uint64_t>(v.scalar_i));
+        else for (int64_t t = v.begin; t < v.end; ++t) n += varint_size(static_cast<uint64_t>(c.ival[t]));
+        const bool empty = v.scalar ? false : v.end == v.begin;
+        return empty ? 0 : 1 + varint_size(n) + n;
+    }
+    uint8_t* put_list(uint8_t* p, const ListView& v) const {
+        if (v.kind == RF_TFR_BYTES) {
+            for (int64_t t = v.begin; t < v.end; ++t) {
+                const uint64_t n = static_cast<uint64_t>(c.tok_off[t + 1] - c.tok_off[t]);
+                *p++ = 0x0a;
+                p = put_varint(p, n);
+                std::memcpy(p, c.tok_bytes + c.tok_off[t], n);
+                p += n;
+            }
+            return p;
+        }
+        if (v.kind == RF_TFR_FLOAT) {
+            const uint64_t n = v.scalar ? 1 : static_cast<uint64_t>(v.end - v.begin);
+            if (!n) return p;
+            *p++ = 0x0a;
+            p = put_varint(p, 4 * n);
+            const float* src = v.scalar ? &v.scalar_f : c.fval + v.begin;
+            std::memcpy(p, src, 4 * n);
+            return p + 4 * n;
+        }
+        if (!v.scalar && v.end == v.begin) return p;
+        uint64_t n = 0;
+        if (v.scalar) n = varint_size(static_cast<uint64_t>(v.scalar_i));
+        else for (int64_t t = v.begin; t < v.end; ++t) n += varint_size(static_cast<uint64_t>(c.ival[t]));
+        *p++ = 0x0a;
+        p = put_varint(p, n);
+        if (v.scalar) return put_varint(p, static_cast<uint64_t>(v.scalar_i));
+        for (int64_t t = v.begin; t < v.end; ++t) p = put_varint(p, static_cast<uint64_t>(c.ival[t]));
+        return p;
+    }
+    // Feature = {field kind+1... : list}; entry = {1: key, 2: Feature}
+    size_t feature_size(const ListView& v) const {
+        const size_t l = list_size(v);
+        return 1 + varint_size(l) + l;
+    }
+    size_t entry_size(int32_t j, const ListView& v) const {
+        const size_t k = sc.names[j].size(), f = feature_size(v);
+        return 1 + varint_size(k) + k + 1 + varint_size(f) + f;
+    }
+    size_t features_size(int32_t b) const {
+        size_t s = 0;
+        for (int32_t j = 0; j < sc.size(); ++j) {
+            const size_t e = entry_size(j, view(b, j));
+            s += 1 + varint_size(e) + e;
+        }
+        return s;
+    }
+    size_t example_size(int32_t b) const {
+        const size_t f = features_size(b);
+        return 1 + varint_size(f) + f;
+    }
+    uint8_t* put_example(uint8_t* p, int32_t b) const {
+        *p++ = 0x0a;
+        p = put_varint(p, features_size(b));
+        for (int32_t j = 0; j < sc.size(); ++j) {
+            const ListView v = view(b, j);
+            *p++ = 0x0a;
+            p = put_varint(p, entry_size(j, v));
+            *p++ = 0x0a;
+            p = put_varint(p, sc.names[j].size());
+            std::memcpy(p, sc.names[j].data(), sc.names[j].size());
+            p += sc.names[j].size();
+            *p++ = 0x12;
+            p = put_varint(p, feature_size(v));
+            *p++ = static_cast<uint8_t>(v.kind == RF_TFR_BYTES ? 0x0a : v.kind == RF_TFR_FLOAT ? 0x12 : 0x1a);
+            p = put_varint(p, list_size(v));
+            p = put_list(p, v);
+        }
+        return p;
+    }
+};
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" uint32_t rf_crc32c(uint32_t crc, const void* data, size_t n) { return crc32c(crc, data, n); }
+
+extern "C" uint32_t rf_crc32c_masked(const void* data, size_t n) { return mask_crc(crc32c(0, data, n)); }
+
+extern "C" int rf_tfw_open(const char* path, int32_t compression, int32_t level, void** out_writer) {
+    if (!path || !out_writer) return rf_set_error(RF_EINVAL, "rf_tfw_open: NULL argument");
+    if (compression != RF_TFR_NONE && compression != RF_TFR_GZIP)
+        return rf_set_error(RF_EINVAL, "rf_tfw_open: compression must be RF_TFR_NONE or RF_TFR_GZIP");
+    if (level < -1 || level > 9) return rf_set_error(RF_EINVAL, "rf_tfw_open: level must be -1..9");
+    *out_writer = nullptr;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return rf_set_error(RF_EIO, "rf_tfw_open: cannot open %s: %s", path, std::strerror(errno));
+    auto* w = new (std::nothrow) Writer(f, compression == RF_TFR_GZIP);
+    if (!w) {
+        std::fclose(f);
+        return rf_set_error(RF_EIO, "rf_tfw_open: out of memory");
+    }
+    Status s = w->init(level);
+    if (!s.ok()) {
+        delete w;
+        return rf_set_error(s.code, "rf_tfw_open: %s", s.msg.c_str());
+    }
+    *out_writer = w;
+    return RF_OK;
+}
+
+extern "C" int rf_tfw_write(void* writer, const void* record, int64_t len) {
+    if (!writer || (len && !record) || len < 0) return rf_set_error(RF_EINVAL, "rf_tfw_write: bad argument");
+    auto* w = static_cast<Writer*>(writer);
+    uint8_t hdr[12];
+    const uint64_t n = static_cast<uint64_t>(len);
+    std::memcpy(hdr, &n, 8);
+    const uint32_t hc = mask_crc(crc32c(0, hdr, 8));
+    std::memcpy(hdr + 8, &hc, 4);
+    const uint32_t dc = mask_crc(crc32c(0, record, static_cast<size_t>(len)));
+    Status s = w->write(hdr, 12);
+    if (s.ok() && len) s = w->write(static_cast<const uint8_t*>(record), static_cast<size_t>(len));
+    if (s.ok()) s = w->write(reinterpret_cast<const uint8_t*>(&dc), 4);
+    if (!s.ok()) return rf_set_error(s.code, "rf_tfw_write: %s", s.msg.c_str());
+    return RF_OK;
+}
+
+extern "C" int rf_tfw_close(void* writer) {
+    if (!writer) return rf_set_error(RF_EINVAL, "rf_tfw_close: NULL writer");
+    auto* w = static_cast<Writer*>(writer);
+    Status s = w->close();
+    delete w;
+    if (!s.ok()) return rf_set_error(s.code, "rf_tfw_close: %s", s.msg.c_str());
+    return RF_OK;
+}
+
+extern "C" int rf_tfr_encode_examples(const rf_tfr_feature* feats, int32_t n_feats, const rf_tfr_columns* cols,
+                                      uint8_t* out, int64_t out_cap, int64_t* rec_off, int64_t* needed) {
+    if (!feats || n_feats <= 0 || !cols || !rec_off || !needed || cols->batch < 0)
+        return rf_set_error(RF_EINVAL, "rf_tfr_encode_examples: bad argument");
+    Schema sc;
+    Status s = sc.build(feats, n_feats);
+    if (!s.ok()) return rf_set_error(s.code, "rf_tfr_encode_examples: %s", s.msg.c_str());
+    const rf_tfr_columns& c = *cols;
+    if ((sc.n_bytes && (!c.bag_off || !c.tok_off)) || (sc.n_iseq && !c.ibag_off) || (sc.n_fseq && !c.fbag_off) ||
+        (sc.n_iscalar && !c.iscalar) || (sc.n_fscalar && !c.fscalar))
+        return rf_set_error(RF_EINVAL, "rf_tfr_encode_examples: a column buffer the schema needs is NULL");
+    Encoder enc{sc, c};
+    int64_t total = 0;
+    rec_off[0] = 0;
+    for (int32_t b = 0; b < c.batch; ++b) {
+        total += static_cast<int64_t>(enc.example_size(b));
+        rec_off[b + 1] = total;
+    }
+    *needed = total;
+    if (total > out_cap || (total && !out))
+        return rf_set_error(RF_ENOSPC, "rf_tfr_encode_examples: need %lld bytes, have %lld", (long long)total,
+                            (long long)out_cap);
+    for (int32_t b = 0; b < c.batch; ++b) {
+        uint8_t* e = enc.put_example(out + rec_off[b], b);
+        if (e != out + rec_off[b + 1]) return rf_set_error(RF_EINVAL, "rf_tfr_encode_examples: internal size mismatch");
+    }
+    return RF_OK;
+}
+
+extern "C" int rf_tfr_open(const char* const* paths, int32_t n_paths, int32_t compression, int32_t n_threads,
+                           void** out_reader) {
+    if (!paths || n_paths <= 0 || !out_reader) return rf_set_error(RF_EINVAL, "rf_tfr_open: need at least one path");
+    if (compression != RF_TFR_NONE && compression != RF_TFR_GZIP)
+        return rf_set_error(RF_EINVAL, "rf_tfr_open: compression must be RF_TFR_NONE or RF_TFR_GZIP");
+    if (n_threads <= 0 || n_threads > 256) return rf_set_error(RF_EINVAL, "rf_tfr_open: n_threads must be 1..256");
+    std::vector<std::string> ps;
+    for (int32_t i = 0; i < n_paths; ++i) {
+        if (!paths[i]) return rf_set_error(RF_EINVAL, "rf_tfr_open: path %d is NULL", i);
+        FILE* f = std::fopen(paths[i], "rb");  // fail at open time, as TFRecordDataset does on iteration
+        if (!f) return rf_set_error(RF_EIO, "rf_tfr_open: cannot open %s: %s", paths[i], std::strerror(errno));
+        std::fclose(f);
+        ps.emplace_back(paths[i]);
+    }
+    *out_reader = new Reader(std::move(ps), compression == RF_TFR_GZIP, n_threads);
+    return RF_OK;
+}
+
+extern "C" int rf_tfr_next_batch(void* reader, const rf_tfr_feature* feats, int32_t n_feats, int32_t batch,
+                                 rf_tfr_columns* cols) {
+    if (!reader || !feats || n_feats <= 0 || !cols || batch <= 0 || cols->reserved != 0)
+        return rf_set_error(RF_EINVAL, "rf_tfr_next_batch: bad argument");
+    Schema sc;
+    Status s = sc.build(feats, n_feats);
+    if (s.ok()) s = static_cast<Reader*>(reader)->next_batch(sc, batch, cols);
+    if (!s.ok()) return rf_set_error(s.code, "rf_tfr_next_batch: %s", s.msg.c_str());
+    return RF_OK;
+}
+
+extern "C" int64_t rf_tfr_records_read(void* reader) {
+    return reader ? static_cast<Reader*>(reader)->handed() : -1;
+}
+
+extern "C" int rf_tfr_close(void* reader) {
+    if (!reader) return rf_set_error(RF_EINVAL, "rf_tfr_close: NULL reader");
+    delete static_cast<Reader*>(reader);
+    return RF_OK;
+}
