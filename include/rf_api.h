@@ -239,6 +239,45 @@ int rf_route_rows(const int64_t* rows, int64_t n, int32_t nranks, int64_t table_
 int rf_gather_rows(const int64_t* rows, int64_t n, const void* table, int32_t dtype, int64_t table_rows,
                    int32_t dim, void* out, void* stream);
 
+/* ---- training backward of the sparse path (rf_train.hip) ------------------------ */
+/*
+ * Backward of rf_fused_hash_embed_fwd for an fp32 table and fp32 output/gradient: the deduplicated
+ * sparse gradient Keras hands its optimizer. Reference: the Embedding gather gradient is an
+ * IndexedSlices over every position of the padded [B, Lmax] ids (preprocess_layers.py:67; padding
+ * positions gather bin 0, dataloader.py:32-33) shaped by the combiner's gradient (:44-64:
+ * reduce_sum -> g, reduce_mean -> g / L, reduce_max/min -> (x == y) / num_selected * g, first/last ->
+ * g at that position and 0 elsewhere); OptimizerV2._deduplicate_indexed_slices sums it per row
+ * (unsorted_segment_sum, (b, l) order on CPU). Outputs: uniq_rows[u] ascending distinct fused-table rows,
+ * uniq_grad[u][dim] their summed gradients (same order of additions as the reference, bit-exact),
+ * *n_uniq (DEVICE int32) = number of distinct rows, or -(error bits) for an invalid batch (1: a row
+ * outside the table, 2: n_positions wrong, 4: a bag longer than lmax). Rows beyond uniq_cap are dropped
+ * (n_uniq > uniq_cap tells the caller). n_positions = batch * sum_s 2 * lmax[s] (host-known).
+ * out (the forward output) and minmax_count (int32 scratch shaped like out) are needed iff a slot pools
+ * max/min, else may be NULL. dout and out share out_stride. ws: rf_embed_bwd_ws_bytes bytes.
+ */
+size_t rf_embed_bwd_ws_bytes(int64_t n_positions, int32_t n_slots, int64_t table_rows);
+int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                            const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
+                            int64_t n_positions, const float* table, int64_t table_rows, int32_t dim,
+                            const float* out, const float* dout, int64_t out_stride, int32_t flags,
+                            int32_t* minmax_count, int64_t* uniq_rows, float* uniq_grad, int64_t uniq_cap,
+                            int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * One tf.keras.optimizers.Adam step on an fp32 table from a deduplicated sparse gradient
+ * (Adam._resource_apply_sparse, example/ranking_search/train.py:97):
+ *   m = m * beta1 (every row); m[r] += g_r * (1 - beta1) (listed rows); v likewise with g_r * g_r * (1 - beta2);
+ *   table -= lr * m / (sqrt(v) + epsilon) (every row).
+ * lr must already carry Keras' bias correction: lr_t * sqrt(1 - beta2^t) / (1 - beta1^t) (fp32).
+ * lazy != 0: only the listed rows are decayed and updated (TF-Addons LazyAdam semantics; a deviation,
+ * much less HBM traffic). n_uniq is the DEVICE count written by rf_fused_hash_embed_bwd.
+ * ws: rf_adam_ws_bytes(table_rows, lazy) bytes (dense mode: a row -> gradient map).
+ */
+size_t rf_adam_ws_bytes(int64_t table_rows, int32_t lazy);
+int rf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                  const float* uniq_grad, const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1,
+                  float beta2, float epsilon, int32_t lazy, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

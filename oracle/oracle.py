@@ -79,6 +79,11 @@ def lib():
         L.orf_hash_rows.argtypes = [vp, i32, vp, vp, vp, i32, vp]
         L.orf_pool_rows_fwd.restype = ctypes.c_int
         L.orf_pool_rows_fwd.argtypes = [vp, i32, vp, vp, i32, i64, vp, vp, i32, i32, vp, i32, i64, i32]
+        L.orf_fused_hash_embed_bwd.restype = i64
+        L.orf_fused_hash_embed_bwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i64, i32, vp, vp, i64, i32, vp, vp]
+        L.orf_adam_apply.restype = None
+        L.orf_adam_apply.argtypes = [vp, vp, vp, i64, i32, vp, vp, i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_float, i32]
         L.orf_bucketize_owner.restype = None
         L.orf_bucketize_owner.argtypes = [vp, i64, i32, vp, vp, vp, vp]
         _lib = L
@@ -141,6 +146,48 @@ def fused_hash_embed(slots: np.ndarray, tok_bytes: np.ndarray, tok_off: np.ndarr
     if rc != 0:
         raise RuntimeError(f"oracle fused_hash_embed failed rc={rc}")
     return out, (idx[:n_tok] if emit_idx else None)
+
+
+def fused_hash_embed_bwd(slots, tok_bytes, tok_off, bag_off, lmax, batch, table, dim, out, dout, flags=0):
+    """Restatement of rf_fused_hash_embed_bwd (fp32): returns (uniq_rows int64 [U], uniq_grad f32 [U, dim])."""
+    slots = np.ascontiguousarray(slots, dtype=SLOT_DTYPE)
+    tok_bytes = np.ascontiguousarray(tok_bytes, dtype=np.uint8)
+    if tok_bytes.size == 0:
+        tok_bytes = np.zeros(1, np.uint8)
+    tok_off = np.ascontiguousarray(tok_off, dtype=np.int32)
+    bag_off = np.ascontiguousarray(bag_off, dtype=np.int32)
+    lmax = np.ascontiguousarray(lmax, dtype=np.int32)
+    table = np.ascontiguousarray(table, dtype=np.float32)
+    out = np.ascontiguousarray(out, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    n_pos = int(batch) * int(2 * lmax.astype(np.int64).sum())
+    cap = max(min(n_pos, table.shape[0]), 1)
+    rows = np.zeros(cap, np.int64)
+    grad = np.zeros((cap, dim), np.float32)
+    nu = lib().orf_fused_hash_embed_bwd(_p(slots), len(slots), _p(tok_bytes), _p(tok_off), _p(bag_off), _p(lmax), batch,
+                                        _p(table), table.shape[0], dim, _p(out), _p(dout), dout.shape[1], flags,
+                                        _p(rows), _p(grad))
+    if nu < 0:
+        raise RuntimeError("oracle fused_hash_embed_bwd: row out of range")
+    return rows[:nu], grad[:nu]
+
+
+def adam_apply(table, m, v, uniq_rows, uniq_grad, lr, beta1, beta2, eps, lazy=False):
+    """Restatement of rf_adam_apply, in place on fp32 numpy arrays."""
+    for a in (table, m, v):
+        assert a.dtype == np.float32 and a.flags.c_contiguous
+    uniq_rows = np.ascontiguousarray(uniq_rows, dtype=np.int64)
+    uniq_grad = np.ascontiguousarray(uniq_grad, dtype=np.float32)
+    lib().orf_adam_apply(_p(table), _p(m), _p(v), table.shape[0], table.shape[1], _p(uniq_rows), _p(uniq_grad),
+                         len(uniq_rows), lr, beta1, beta2, eps, int(lazy))
+
+
+def keras_adam_lr(lr: float, beta1: float, beta2: float, step: int) -> float:
+    """Keras Adam's bias-corrected step size in float32: lr * (sqrt(1 - b2^t) / (1 - b1^t))."""
+    f = np.float32
+    t = f(step)
+    b1p, b2p = np.power(f(beta1), t), np.power(f(beta2), t)
+    return float(f(lr) * (np.sqrt(f(1) - b2p) / (f(1) - b1p)))
 
 
 def embedding_bag(ids: np.ndarray, table: np.ndarray, combiner: str, row_base: int = 0, out_dtype: int = DT_F32):

@@ -365,3 +365,148 @@ int orf_pool_rows_fwd(const rf_slot_desc* slots, int32_t n_slots, const int32_t*
     free(acc);
     return status;
 }
+
+/* ============================================================================================
+ * Training backward, restated sequentially:
+ *   the Embedding gradient of each (slot, table) is an IndexedSlices over every gathered position of
+ *   the padded [B, Lmax] ids (preprocess_layers.py:67 + the combiner gradient of :44-64:
+ *   reduce_sum -> g; reduce_mean -> g / L; reduce_max/min -> (x == y) / num_selected * g
+ *   (tf _MinOrMaxGrad); t[0] / t[-1] -> g at that position, 0 elsewhere);
+ *   Keras _deduplicate_indexed_slices = unique + unsorted_segment_sum, which on CPU adds the values
+ *   of one row into a zero-initialised accumulator in (b, l) order.
+ * Output: distinct rows ascending, their summed gradients. Returns n_uniq, or -1 on a bad row.
+ * ============================================================================================ */
+static int cmp_u64(const void* a, const void* b) {
+    uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+int64_t orf_fused_hash_embed_bwd(const rf_slot_desc* slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                 const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
+                                 const float* table, int64_t table_rows, int32_t dim, const float* out,
+                                 const float* dout, int64_t out_stride, int32_t flags, int64_t* uniq_rows,
+                                 float* uniq_grad) {
+    const int masked = (flags & RF_FLAG_MASK_PADDING) != 0;
+    int64_t per = 0;
+    int64_t* pos_off = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_slots + 1));
+    for (int32_t s = 0; s < n_slots; ++s) { pos_off[s] = per; per += 2 * (int64_t)lmax[s]; }
+    pos_off[n_slots] = per;
+    const int64_t n = per * batch;
+    uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n > 0 ? n : 1));
+    int64_t m = 0;
+    int status = 0;
+    /* positions p in (b, s, k, l) order; key = row << 32 | p */
+    for (int32_t b = 0; b < batch; ++b)
+        for (int32_t s = 0; s < n_slots; ++s) {
+            const rf_slot_desc* sd = &slots[s];
+            const int64_t u = (int64_t)b * n_slots + s;
+            const int32_t t0 = bag_off[u], len = bag_off[u + 1] - t0;
+            for (int k = 0; k < 2; ++k)
+                for (int32_t l = 0; l < lmax[s]; ++l) {
+                    const int64_t p = (int64_t)b * per + pos_off[s] + (int64_t)k * lmax[s] + l;
+                    int64_t row;
+                    if (l < len) {
+                        const int32_t t = t0 + l;
+                        row = sd->row_base[k] + orf_hash_bucket(sd->salt[k], sd->salt[k], tok_bytes + tok_off[t],
+                                                                tok_off[t + 1] - tok_off[t], sd->num_bins, sd->mask_empty);
+                    } else if (masked) {
+                        continue;
+                    } else {
+                        row = sd->row_base[k] + (sd->mask_empty ? 0 : orf_hash_bucket(sd->salt[k], sd->salt[k],
+                                                                                       (const uint8_t*)"", 0, sd->num_bins, 0));
+                    }
+                    if (row < 0 || row >= table_rows) { status = -1; continue; }
+                    keys[m++] = ((uint64_t)row << 32) | (uint64_t)p;
+                }
+        }
+    qsort(keys, (size_t)m, sizeof(uint64_t), cmp_u64);
+    int64_t nu = 0;
+    for (int64_t i = 0; i < m;) {
+        const uint64_t row = keys[i] >> 32;
+        float* acc = uniq_grad + nu * dim;
+        for (int32_t d = 0; d < dim; ++d) acc[d] = 0.0f;
+        const float* tr = table + (int64_t)row * dim;
+        for (; i < m && (keys[i] >> 32) == row; ++i) {
+            const int64_t p = (int64_t)(keys[i] & 0xffffffffu);
+            const int32_t b = (int32_t)(p / per);
+            const int64_t r = p - (int64_t)b * per;
+            int32_t s = 0;
+            while (s + 1 < n_slots && pos_off[s + 1] <= r) ++s;
+            const int32_t k = (int32_t)((r - pos_off[s]) / lmax[s]);
+            const int32_t l = (int32_t)(r - pos_off[s] - (int64_t)k * lmax[s]);
+            const rf_slot_desc* sd = &slots[s];
+            const int64_t u = (int64_t)b * n_slots + s;
+            const int32_t t0 = bag_off[u], len = bag_off[u + 1] - t0;
+            const int32_t L = masked ? len : (lmax[s] > len ? lmax[s] : len);
+            const int64_t col = (int64_t)b * out_stride + sd->out_off + (int64_t)k * dim;
+            for (int32_t d = 0; d < dim; ++d) {
+                const float g = dout[col + d];
+                float v = 0.0f;
+                switch (sd->combiner) {
+                    case RF_COMB_SUM: v = g; break;
+                    case RF_COMB_AVG: v = g / (float)L; break;
+                    case RF_COMB_MAX:
+                    case RF_COMB_MIN: {
+                        /* num_selected over the bag's L positions (pads included unless masked) */
+                        int32_t c = 0;
+                        for (int32_t l2 = 0; l2 < L; ++l2) {
+                            int64_t r2;
+                            if (l2 < len) {
+                                const int32_t t = t0 + l2;
+                                r2 = sd->row_base[k] + orf_hash_bucket(sd->salt[k], sd->salt[k], tok_bytes + tok_off[t],
+                                                                       tok_off[t + 1] - tok_off[t], sd->num_bins, sd->mask_empty);
+                            } else {
+                                r2 = sd->row_base[k] + (sd->mask_empty ? 0 : orf_hash_bucket(sd->salt[k], sd->salt[k],
+                                                                                              (const uint8_t*)"", 0, sd->num_bins, 0));
+                            }
+                            if (r2 >= 0 && r2 < table_rows && table[r2 * dim + d] == out[col + d]) ++c;
+                        }
+                        v = ((tr[d] == out[col + d] ? 1.0f : 0.0f) / (float)c) * g;
+                        break;
+                    }
+                    case RF_COMB_FIRST: v = l == 0 ? g : 0.0f; break;
+                    case RF_COMB_LAST: v = l == L - 1 ? g : 0.0f; break;
+                    default: break;
+                }
+                acc[d] += v;
+            }
+        }
+        uniq_rows[nu++] = (int64_t)row;
+    }
+    free(keys);
+    free(pos_off);
+    return status ? -1 : nu;
+}
+
+/* Keras Adam (OptimizerV2 Adam._resource_apply_sparse after dedup), fp32, one step:
+ *   m = m * b1 (every row); m[r] = m[r] + g_r * (1 - b1) (touched rows); likewise v with g_r * g_r;
+ *   var = var - lr * m / (sqrt(v) + eps) (every row); lr = lr_t * sqrt(1 - b2^t) / (1 - b1^t) (host).
+ * lazy != 0: touched rows only (TF-Addons LazyAdam). uniq_rows must be distinct. */
+void orf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                    const float* uniq_grad, int64_t n_uniq, float lr, float b1, float b2, float eps, int32_t lazy) {
+    const float omb1 = 1.0f - b1, omb2 = 1.0f - b2;
+    int32_t* map = NULL;
+    if (!lazy) {
+        map = (int32_t*)malloc(sizeof(int32_t) * (size_t)table_rows);
+        for (int64_t r = 0; r < table_rows; ++r) map[r] = -1;
+        for (int64_t u = 0; u < n_uniq; ++u) map[uniq_rows[u]] = (int32_t)u;
+    }
+    const int64_t nrows = lazy ? n_uniq : table_rows;
+    for (int64_t i = 0; i < nrows; ++i) {
+        const int64_t row = lazy ? uniq_rows[i] : i;
+        const int64_t u = lazy ? i : map[i];
+        for (int32_t d = 0; d < dim; ++d) {
+            const int64_t e = row * dim + d;
+            float mt = m[e] * b1, vt = v[e] * b2;
+            if (u >= 0) {
+                const float g = uniq_grad[u * dim + d];
+                mt = mt + g * omb1;
+                vt = vt + (g * g) * omb2;
+            }
+            m[e] = mt;
+            v[e] = vt;
+            table[e] = table[e] - (lr * mt) / (sqrtf(vt) + eps);
+        }
+    }
+    free(map);
+}

@@ -76,6 +76,24 @@ def init_table(table: torch.Tensor, row0: int = 0, row_stride: int = 1, seed: in
     return table
 
 
+@dataclass
+class SparseGrad:
+    """Deduplicated gradient of a fused table (device): rows[:n] ascending, grad[:n] [n, dim]; n = n_uniq
+    (a device int32; negative = invalid batch, see rf_fused_hash_embed_bwd)."""
+    rows: torch.Tensor
+    grad: torch.Tensor
+    n_uniq: torch.Tensor
+    cap: int
+
+    def count(self) -> int:
+        n = int(self.n_uniq.item())
+        if n < 0:
+            raise ValueError(f"invalid batch for the embedding backward (error bits {-n})")
+        if n > self.cap:
+            raise ValueError(f"{n} distinct rows exceed uniq_cap {self.cap}")
+        return n
+
+
 class FusedSparseEncoder(torch.nn.Module):
     """All hashing slots of one tower -> [B, sum_s 2*D] with one rf_fused_hash_embed_fwd launch."""
 
@@ -147,6 +165,42 @@ class FusedSparseEncoder(torch.nn.Module):
         if emit_idx:
             return out, idx[: batch.n_tokens]
         return out
+
+    # ---- training -------------------------------------------------------------
+    def backward(self, batch: SparseBatch, dout: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 uniq_cap: Optional[int] = None, stream=None) -> "SparseGrad":
+        """Deduplicated sparse gradient of the fused table from dout [B, out_width] (fp32), exactly the
+        IndexedSlices Keras' optimizer sums per row (rf_fused_hash_embed_bwd). `out` (the forward
+        output) is needed when a slot pools max/min."""
+        if self.table.dtype != torch.float32 or dout.dtype != torch.float32:
+            raise ValueError("backward needs an fp32 table and an fp32 output gradient")
+        if batch.n_slots != len(self.slots):
+            raise ValueError(f"batch has {batch.n_slots} slots, encoder {len(self.slots)}")
+        lm = batch.lmax_numpy()
+        if not batch.is_device():
+            batch = batch.to(self.table.device)
+        B = batch.batch
+        dev = self.table.device
+        n_pos = B * int(2 * np.asarray(lm, np.int64).sum())
+        cap = int(uniq_cap) if uniq_cap is not None else max(1, min(n_pos, self.table.shape[0]))
+        rows = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        grad = torch.empty((max(cap, 1), self.dim), dtype=torch.float32, device=dev)
+        n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+        need_mm = any(sp.combiner in ("max", "min") for sp in self.slots)
+        if need_mm and out is None:
+            raise ValueError("max/min pooling: backward needs the forward output `out`")
+        dout = dout.contiguous()
+        if out is not None and (out.stride(0) != dout.stride(0) or out.dtype != torch.float32):
+            out = out.contiguous().float()
+        cnt = torch.empty(dout.shape, dtype=torch.int32, device=dev) if need_mm else None
+        wsb = L.load().rf_embed_bwd_ws_bytes(n_pos, len(self.slots), self.table.shape[0])
+        ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=dev)
+        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        L.call("rf_fused_hash_embed_bwd", L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes), L.ptr(batch.tok_off),
+               L.ptr(batch.bag_off), L.ptr(batch.lmax), B, n_pos, L.ptr(self.table), self.table.shape[0], self.dim,
+               L.ptr(out) if need_mm else None, L.ptr(dout), dout.stride(0), flags, L.ptr(cnt), L.ptr(rows), L.ptr(grad),
+               cap, L.ptr(n_uniq), L.ptr(ws), ws.numel(), L.stream_ptr(stream))
+        return SparseGrad(rows, grad, n_uniq, cap)
 
     def algorithmic_bytes(self, batch: SparseBatch) -> int:
         """HBM bytes one forward must move: rows read (every occurrence, padding positions

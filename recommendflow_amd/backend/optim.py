@@ -1,0 +1,48 @@
+"""Optimizers for the fused embedding tables.
+
+Reference: ``tf.keras.optimizers.Adam(learning_rate=args.learning_rate)`` compiled into every training
+script (example/ranking_search/train.py:97, example/recall_search/train.py:97, finetune.py:78); Keras'
+defaults beta_1 = 0.9, beta_2 = 0.999, epsilon = 1e-7. For an Embedding variable Keras applies
+Adam._resource_apply_sparse to the deduplicated IndexedSlices gradient: m and v decay over the whole
+variable, the scaled gradient is scatter-added, and every row moves (dense semantics). ``lazy=True``
+touches only the rows in the gradient (TF-Addons LazyAdam; deviation D-lazy-adam, opt-in).
+
+Dense parameters (towers, attention) use torch.optim.Adam with the same hyper-parameters.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..runtime import lib as L
+from .encoder.sparse_encoder import SparseGrad
+
+
+class SparseAdam:
+    """tf.keras.optimizers.Adam for an fp32 fused embedding table, driven by SparseGrad (rf_adam_apply)."""
+
+    def __init__(self, table: torch.Tensor, learning_rate: float = 0.001, beta_1: float = 0.9, beta_2: float = 0.999,
+                 epsilon: float = 1e-7, lazy: bool = False):
+        if table.dtype != torch.float32 or table.dim() != 2 or not table.is_contiguous():
+            raise ValueError("SparseAdam needs a contiguous fp32 [rows, dim] table")
+        self.table = table
+        self.learning_rate, self.beta_1, self.beta_2, self.epsilon = learning_rate, beta_1, beta_2, epsilon
+        self.lazy = bool(lazy)
+        self.m = torch.zeros_like(table)
+        self.v = torch.zeros_like(table)
+        self.iterations = 0
+        wsb = int(L.load().rf_adam_ws_bytes(table.shape[0], int(self.lazy)))
+        self._ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=table.device)
+
+    def step_lr(self) -> float:
+        """lr_t * sqrt(1 - beta_2^t) / (1 - beta_1^t) in float32, t = iterations + 1 (Keras local_step)."""
+        f = np.float32
+        t = f(self.iterations + 1)
+        b1p, b2p = np.power(f(self.beta_1), t), np.power(f(self.beta_2), t)
+        return float(f(self.learning_rate) * (np.sqrt(f(1) - b2p) / (f(1) - b1p)))
+
+    def apply(self, g: SparseGrad, stream=None):
+        L.call("rf_adam_apply", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0], self.table.shape[1],
+               L.ptr(g.rows), L.ptr(g.grad), L.ptr(g.n_uniq), g.cap, self.step_lr(), self.beta_1, self.beta_2,
+               self.epsilon, int(self.lazy), L.ptr(self._ws), self._ws.numel(), L.stream_ptr(stream))
+        self.iterations += 1

@@ -1,0 +1,495 @@
+// rf_train.hip — training backward of the sparse hot path.
+//
+// Reference: model.fit with tf.keras.optimizers.Adam (example/ranking_search/train.py:96-104). The
+// gradient of every Keras Embedding gather is an IndexedSlices over ALL gathered positions of the
+// padded [B, Lmax] id tensor (padding positions gather bin 0, dataloader.py:32-33 + Hashing
+// mask_value=""), shaped by the pooling combiner's gradient (EmbeddingBag.get_combiner,
+// backend/layers/preprocess_layers.py:44-64: reduce_sum / reduce_mean / reduce_max / reduce_min /
+// t[0] / t[-1]). OptimizerV2 first deduplicates it (_deduplicate_indexed_slices: unique +
+// unsorted_segment_sum, summing in (b, l) order on CPU), then Adam._resource_apply_sparse decays m and v
+// over the WHOLE variable, scatter-adds the scaled gradient, and updates every row.
+//
+// Here (one fused table, all slots of a tower):
+//   1. enum      thread per position p -> key = fused-table row (SipHash of its token, or the slot's pad
+//                row), value = p; positions are enumerated example-major, so within one row they are
+//                already in the reference's (b, l) order
+//   2. sort      hipcub radix sort of (row, p) pairs over the row's significant bits (stable)
+//   3. heads     segment heads + inclusive scan -> distinct rows (ascending) and segment starts
+//   4. reduce    a team of D/4 lanes per distinct row walks its segment IN ORDER, recomputes each
+//                position's gradient vector from dout (and, for max/min, from the forward output and
+//                the tie counts), and accumulates acc = 0; acc += v like unsorted_segment_sum
+//   5. adam      rf_adam_apply: Keras-exact dense Adam (map row -> distinct id, one fused pass over the
+//                table: var, m, v read + written once) or lazy (touched rows only; TF-Addons LazyAdam)
+// No atomics anywhere: the result is deterministic and bit-identical to oracle/rf_oracle.c.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <hipcub/hipcub.hpp>
+
+#include "rf_common.h"
+
+namespace {
+
+size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int key_bits(uint64_t max_key) {
+    int b = 1;
+    while (b < 32 && (max_key >> b) != 0) ++b;
+    return b;
+}
+
+struct BwdLayout {
+    int64_t n;
+    int end_bit;
+    size_t sort_bytes, scan_bytes;
+    size_t off_kin, off_kout, off_vin, off_vout, off_scan, off_seg, off_posoff, off_flag, off_tmp, total;
+};
+
+BwdLayout bwd_layout(int64_t n_positions, int32_t n_slots, int64_t table_rows) {
+    BwdLayout L{};
+    L.n = std::max<int64_t>(n_positions, 1);
+    L.end_bit = key_bits((uint64_t)table_rows);  // sentinel key = table_rows (masked padding / bad rows)
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, L.sort_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)L.n, 0, L.end_bit);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, L.scan_bytes, (const int32_t*)nullptr, (int32_t*)nullptr, (int)L.n);
+    size_t o = 0;
+    const size_t v = a256((size_t)L.n * 4);
+    L.off_kin = o; o += v;
+    L.off_kout = o; o += v;
+    L.off_vin = o; o += v;
+    L.off_vout = o; o += v;
+    L.off_scan = o; o += v;
+    L.off_seg = o; o += a256((size_t)(L.n + 1) * 4);
+    L.off_posoff = o; o += a256((size_t)(n_slots + 2) * 8);
+    L.off_flag = o; o += 256;
+    L.off_tmp = o; o += a256(std::max(L.sort_bytes, L.scan_bytes));
+    L.total = o;
+    return L;
+}
+
+// pos_off[s] = sum_{s' < s} 2 * lmax[s'] (int64), pos_off[S] = positions per example; one block
+__global__ __launch_bounds__(1024) void posoff_kernel(const int32_t* __restrict__ lmax, int S, int64_t* __restrict__ pos_off) {
+    __shared__ int64_t s_carry;
+    __shared__ int64_t s_wave[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < S; c0 += 1024) {
+        const int s = c0 + threadIdx.x;
+        const int64_t x = s < S ? 2 * (int64_t)max(lmax[s], 0) : 0;
+        int64_t incl = x;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) s_wave[wave] = incl;
+        __syncthreads();
+        int64_t base = s_carry;
+        for (int w = 0; w < wave; ++w) base += s_wave[w];
+        if (s < S) pos_off[s] = base + incl - x;
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = base + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) pos_off[S] = s_carry;
+}
+
+// last s with pos_off[s] <= r (pos_off strictly increasing except for lmax == 0 slots, which own no positions)
+__device__ __forceinline__ int find_slot(const int64_t* __restrict__ pos_off, int S, int64_t r) {
+    int lo = 0, hi = S - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pos_off[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+struct Pos {
+    int b, s, k, l, L, len;
+};
+
+__device__ __forceinline__ Pos decode_pos(uint32_t p, const int64_t* __restrict__ pos_off, int S,
+                                          const int32_t* __restrict__ lmax, const int32_t* __restrict__ bag_off) {
+    Pos q;
+    const int64_t per = pos_off[S];
+    q.b = (int)((int64_t)p / per);
+    const int64_t r = (int64_t)p - (int64_t)q.b * per;
+    q.s = find_slot(pos_off, S, r);
+    const int lm = lmax[q.s];
+    const int64_t w = r - pos_off[q.s];
+    q.k = (int)(w / lm);
+    q.l = (int)(w - (int64_t)q.k * lm);
+    const int64_t u = (int64_t)q.b * S + q.s;
+    const int t0 = bag_off[u];
+    q.len = bag_off[u + 1] - t0;
+    q.L = lm;
+    return q;
+}
+
+__global__ __launch_bounds__(256) void enum_kernel(const rf_slot_desc* __restrict__ slots, int S,
+                                                   const uint8_t* __restrict__ tok_bytes,
+                                                   const int32_t* __restrict__ tok_off,
+                                                   const int32_t* __restrict__ bag_off,
+                                                   const int32_t* __restrict__ lmax, int batch, int64_t n_pos,
+                                                   const int64_t* __restrict__ pos_off, int64_t table_rows, int masked,
+                                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                   int32_t* __restrict__ flag) {
+    const uint32_t sentinel = (uint32_t)table_rows;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_pos; p += (int64_t)gridDim.x * blockDim.x) {
+        vals[p] = (uint32_t)p;
+        const int64_t per = pos_off[S];
+        if (p == 0 && n_pos != (int64_t)batch * per) atomicOr(flag, 2);  // caller's n_positions is wrong
+        if (per == 0 || p / per >= batch) {
+            keys[p] = sentinel;
+            continue;
+        }
+        const Pos q = decode_pos((uint32_t)p, pos_off, S, lmax, bag_off);
+        const rf_slot_desc* sd = slots + q.s;
+        if (q.len > q.L) atomicOr(flag, 4);  // a bag longer than its lmax: invalid batch
+        int64_t row;
+        if (q.l < q.len) {
+            const int t = bag_off[(int64_t)q.b * S + q.s] + q.l;
+            const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
+            row = sd->row_base[q.k] +
+                  hash_bucket_dev(sd->salt[q.k], sd->salt[q.k], tok_bytes + b0, n, sd->num_bins, sd->mask_empty);
+        } else if (masked) {
+            keys[p] = sentinel;
+            continue;
+        } else {
+            row = sd->row_base[q.k] +
+                  (sd->mask_empty ? 0 : hash_bucket_dev(sd->salt[q.k], sd->salt[q.k], tok_bytes, 0, sd->num_bins, 0));
+        }
+        if (row < 0 || row >= table_rows) {
+            atomicOr(flag, 1);
+            keys[p] = sentinel;
+        } else {
+            keys[p] = (uint32_t)row;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void heads_kernel(const uint32_t* __restrict__ keys, int64_t n, int32_t* __restrict__ head) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void emit_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ scan,
+                                                   int64_t n, uint32_t sentinel, int64_t cap,
+                                                   int64_t* __restrict__ uniq_rows, int32_t* __restrict__ seg) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i != 0 && keys[i] == keys[i - 1]) continue;
+        const int64_t u = scan[i] - 1;
+        seg[u] = (int32_t)i;  // the sentinel segment (if any) starts where the real ones end
+        if (keys[i] != sentinel && u < cap) uniq_rows[u] = keys[i];
+    }
+}
+
+// n_uniq = distinct rows, or -(error bits) for an invalid batch: 1 row out of range, 2 n_positions !=
+// batch * sum_s 2 * lmax[s], 4 a bag longer than its lmax (then the reduce and Adam kernels do nothing)
+__global__ void count_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ scan, int64_t n,
+                             uint32_t sentinel, const int32_t* __restrict__ flag, int32_t* __restrict__ seg,
+                             int32_t* __restrict__ n_uniq) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int32_t total = scan[n - 1];
+    const bool has_sentinel = keys[n - 1] == sentinel;
+    const int32_t nu = has_sentinel ? total - 1 : total;
+    if (!has_sentinel) seg[nu] = (int32_t)n;
+    *n_uniq = *flag ? -*flag : nu;
+}
+
+// max/min tie counts: cnt[b][col + d] = #{l < L : T[row_l][d] == out[b][col + d]} (tf _MinOrMaxGrad num_selected)
+__global__ __launch_bounds__(256) void minmax_count_kernel(const rf_slot_desc* __restrict__ slots, int S,
+                                                           const uint8_t* __restrict__ tok_bytes,
+                                                           const int32_t* __restrict__ tok_off,
+                                                           const int32_t* __restrict__ bag_off,
+                                                           const int32_t* __restrict__ lmax, int batch, int masked,
+                                                           const float* __restrict__ table, int64_t table_rows, int D,
+                                                           const float* __restrict__ out, int64_t stride,
+                                                           int32_t* __restrict__ cnt) {
+    const int64_t n = (int64_t)batch * S * 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(i & 1);
+        const int64_t u = i >> 1;
+        const int s = (int)(u % S), b = (int)(u / S);
+        const rf_slot_desc* sd = slots + s;
+        if (sd->combiner != RF_COMB_MAX && sd->combiner != RF_COMB_MIN) continue;
+        const int t0 = bag_off[u], len = bag_off[u + 1] - t0;
+        const int L = masked ? len : max(lmax[s], len);
+        const int64_t pad = sd->row_base[k] + (sd->mask_empty ? 0 : hash_bucket_dev(sd->salt[k], sd->salt[k], tok_bytes, 0, sd->num_bins, 0));
+        const float* o = out + (int64_t)b * stride + sd->out_off + (int64_t)k * D;
+        int32_t* c = cnt + (int64_t)b * stride + sd->out_off + (int64_t)k * D;
+        for (int d = 0; d < D; ++d) c[d] = 0;
+        for (int l = 0; l < L; ++l) {
+            int64_t row = pad;
+            if (l < len) {
+                const int bb = tok_off[t0 + l], nb = tok_off[t0 + l + 1] - bb;
+                row = sd->row_base[k] + hash_bucket_dev(sd->salt[k], sd->salt[k], tok_bytes + bb, nb, sd->num_bins, sd->mask_empty);
+            }
+            if (row < 0 || row >= table_rows) continue;
+            const float* tr = table + row * D;
+            for (int d = 0; d < D; ++d) c[d] += tr[d] == o[d] ? 1 : 0;
+        }
+    }
+}
+
+// The gradient of position q (table row `row`) at column d of its [slot, k] block.
+__device__ __forceinline__ float pos_grad(const rf_slot_desc* sd, const Pos& q, int masked, float g, float t, float o, int32_t c) {
+    const int L = masked ? q.len : max(q.L, q.len);
+    switch (sd->combiner) {
+        case RF_COMB_SUM: return g;
+        case RF_COMB_AVG: return g / (float)L;
+        case RF_COMB_MAX:
+        case RF_COMB_MIN: return ((t == o ? 1.0f : 0.0f) / (float)c) * g;
+        case RF_COMB_FIRST: return q.l == 0 ? g : 0.0f;
+        case RF_COMB_LAST: return q.l == L - 1 ? g : 0.0f;
+        default: return 0.0f;
+    }
+}
+
+// Team of TPR = D/4 lanes per distinct row; lanes own 4 consecutive columns. Walks the segment in
+// order (the reference's summation order); the row's own table values are loaded once (max/min).
+template <int TPR>
+__global__ __launch_bounds__(256) void reduce_kernel(const rf_slot_desc* __restrict__ slots, int S,
+                                                     const int32_t* __restrict__ bag_off,
+                                                     const int32_t* __restrict__ lmax,
+                                                     const int64_t* __restrict__ pos_off, int masked,
+                                                     const uint32_t* __restrict__ vals,
+                                                     const int32_t* __restrict__ seg,
+                                                     const int32_t* __restrict__ n_uniq_p, int64_t cap,
+                                                     const int64_t* __restrict__ uniq_rows,
+                                                     const float* __restrict__ table, int D,
+                                                     const float* __restrict__ out, const float* __restrict__ dout,
+                                                     int64_t stride, const int32_t* __restrict__ cnt,
+                                                     float* __restrict__ uniq_grad) {
+    constexpr int TEAMS = 256 / TPR;
+    const int team = threadIdx.x / TPR, lane = threadIdx.x % TPR;
+    const int64_t nu = min<int64_t>(*n_uniq_p, cap);
+    const int d0 = lane * 4;
+    const bool active_lane = d0 < D;
+    for (int64_t u = (int64_t)blockIdx.x * TEAMS + team; u < nu; u += (int64_t)gridDim.x * TEAMS) {
+        const int64_t row = uniq_rows[u];
+        const int i0 = seg[u], i1 = seg[u + 1];
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 trow = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (active_lane) trow = *reinterpret_cast<const float4*>(table + row * D + d0);
+        for (int i = i0; i < i1; ++i) {
+            const Pos q = decode_pos(vals[i], pos_off, S, lmax, bag_off);
+            const rf_slot_desc* sd = slots + q.s;
+            if (!active_lane) continue;
+            const int64_t col = (int64_t)q.b * stride + sd->out_off + (int64_t)q.k * D + d0;
+            const float4 g = *reinterpret_cast<const float4*>(dout + col);
+            float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+            int4 c = make_int4(1, 1, 1, 1);
+            if (sd->combiner == RF_COMB_MAX || sd->combiner == RF_COMB_MIN) {
+                o = *reinterpret_cast<const float4*>(out + col);
+                c = *reinterpret_cast<const int4*>(cnt + col);
+            }
+            acc.x += pos_grad(sd, q, masked, g.x, trow.x, o.x, c.x);
+            acc.y += pos_grad(sd, q, masked, g.y, trow.y, o.y, c.y);
+            acc.z += pos_grad(sd, q, masked, g.z, trow.z, o.z, c.z);
+            acc.w += pos_grad(sd, q, masked, g.w, trow.w, o.w, c.w);
+        }
+        if (active_lane) *reinterpret_cast<float4*>(uniq_grad + u * D + d0) = acc;
+    }
+}
+
+// ---- Adam --------------------------------------------------------------------------------------
+struct AdamCoef {
+    float lr, b1, b2, omb1, omb2, eps;
+};
+
+__device__ __forceinline__ void adam_elem(float& w, float& m, float& v, bool touched, float g, const AdamCoef& c) {
+    // Adam._resource_apply_sparse: m_t = m * beta_1; m_t = scatter_add(m_t, g * (1 - beta_1)); likewise v
+    // with g * g; var -= lr * m_t / (sqrt(v_t) + epsilon)   (lr already carries sqrt(1-b2^t)/(1-b1^t))
+    float mt = m * c.b1;
+    float vt = v * c.b2;
+    if (touched) {
+        mt = mt + g * c.omb1;
+        vt = vt + (g * g) * c.omb2;
+    }
+    m = mt;
+    v = vt;
+    w = w - (c.lr * mt) / (sqrtf(vt) + c.eps);
+}
+
+__global__ __launch_bounds__(256) void map_fill_kernel(const int64_t* __restrict__ uniq_rows, const int32_t* __restrict__ n_uniq_p,
+                                                       int64_t cap, int32_t* __restrict__ map) {
+    const int64_t nu = min<int64_t>(*n_uniq_p, cap);
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x)
+        map[uniq_rows[u]] = (int32_t)u;
+}
+
+// dense: every element of the table (float4 granules); row -> distinct id through `map`
+__global__ __launch_bounds__(256) void adam_dense_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                                         int64_t n4, int D4, const int32_t* __restrict__ map,
+                                                         const float* __restrict__ grad, AdamCoef c) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / D4;
+        const int j = (int)(i - row * D4);
+        const int32_t u = map[row];
+        float4 wv = reinterpret_cast<float4*>(w)[i];
+        float4 mv = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+        float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool t = u >= 0;
+        if (t) g = reinterpret_cast<const float4*>(grad)[(int64_t)u * D4 + j];
+        adam_elem(wv.x, mv.x, vv.x, t, g.x, c);
+        adam_elem(wv.y, mv.y, vv.y, t, g.y, c);
+        adam_elem(wv.z, mv.z, vv.z, t, g.z, c);
+        adam_elem(wv.w, mv.w, vv.w, t, g.w, c);
+        reinterpret_cast<float4*>(w)[i] = wv;
+        reinterpret_cast<float4*>(m)[i] = mv;
+        reinterpret_cast<float4*>(v)[i] = vv;
+    }
+}
+
+// lazy: touched rows only
+__global__ __launch_bounds__(256) void adam_lazy_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                                        int D4, const int64_t* __restrict__ uniq_rows,
+                                                        const int32_t* __restrict__ n_uniq_p, int64_t cap,
+                                                        const float* __restrict__ grad, AdamCoef c) {
+    const int64_t nu = min<int64_t>(*n_uniq_p, cap);
+    const int64_t n4 = nu * D4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = i / D4;
+        const int j = (int)(i - u * D4);
+        const int64_t e = uniq_rows[u] * D4 + j;
+        float4 wv = reinterpret_cast<float4*>(w)[e];
+        float4 mv = reinterpret_cast<float4*>(m)[e];
+        float4 vv = reinterpret_cast<float4*>(v)[e];
+        const float4 g = reinterpret_cast<const float4*>(grad)[i];
+        adam_elem(wv.x, mv.x, vv.x, true, g.x, c);
+        adam_elem(wv.y, mv.y, vv.y, true, g.y, c);
+        adam_elem(wv.z, mv.z, vv.z, true, g.z, c);
+        adam_elem(wv.w, mv.w, vv.w, true, g.w, c);
+        reinterpret_cast<float4*>(w)[e] = wv;
+        reinterpret_cast<float4*>(m)[e] = mv;
+        reinterpret_cast<float4*>(v)[e] = vv;
+    }
+}
+
+int grid_of(int64_t n, int cap = 256 * 64) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)); }
+
+}  // namespace
+
+extern "C" size_t rf_embed_bwd_ws_bytes(int64_t n_positions, int32_t n_slots, int64_t table_rows) {
+    if (n_positions < 0 || n_slots < 1 || table_rows < 1) return 0;
+    return bwd_layout(n_positions, n_slots, table_rows).total;
+}
+
+extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                       const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                                       int32_t batch, int64_t n_positions, const float* table, int64_t table_rows,
+                                       int32_t dim, const float* out, const float* dout, int64_t out_stride,
+                                       int32_t flags, int32_t* minmax_count, int64_t* uniq_rows, float* uniq_grad,
+                                       int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream) {
+    RF_REQUIRE(n_slots >= 1 && batch >= 0 && n_positions >= 0, "rf_fused_hash_embed_bwd: need n_slots >= 1, batch >= 0, n_positions >= 0");
+    RF_REQUIRE(n_positions < ((int64_t)1 << 32) - 1, "rf_fused_hash_embed_bwd: n_positions must be < 2^32 - 1");
+    RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 32) - 1, "rf_fused_hash_embed_bwd: table_rows must be in [1, 2^32 - 1)");
+    RF_REQUIRE(dim >= 4 && dim <= 256 && dim % 4 == 0, "rf_fused_hash_embed_bwd: dim must be a multiple of 4 in [4, 256]");
+    RF_REQUIRE(out_stride % 4 == 0 && out_stride >= 2 * (int64_t)dim, "rf_fused_hash_embed_bwd: out_stride must be a multiple of 4");
+    RF_REQUIRE((flags & ~RF_FLAG_MASK_PADDING) == 0, "rf_fused_hash_embed_bwd: only RF_FLAG_MASK_PADDING is accepted");
+    RF_REQUIRE(uniq_cap >= 0 && n_uniq && ws, "rf_fused_hash_embed_bwd: null pointer");
+    const BwdLayout lay = bwd_layout(n_positions, n_slots, table_rows);
+    RF_REQUIRE(ws_bytes >= lay.total, "rf_fused_hash_embed_bwd: workspace too small (%zu < %zu)", ws_bytes, lay.total);
+    hipStream_t st = rf_stream(stream);
+    if (n_positions == 0 || batch == 0) {
+        if (hipMemsetAsync(n_uniq, 0, sizeof(int32_t), st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
+        return RF_OK;
+    }
+    RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && lmax && table && dout && uniq_rows && uniq_grad,
+               "rf_fused_hash_embed_bwd: null pointer");
+    RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)dout & 15) == 0 && ((uintptr_t)uniq_grad & 15) == 0 &&
+               (!out || ((uintptr_t)out & 15) == 0) && (!minmax_count || ((uintptr_t)minmax_count & 15) == 0),
+               "rf_fused_hash_embed_bwd: buffers must be 16-byte aligned");
+    const int masked = (flags & RF_FLAG_MASK_PADDING) ? 1 : 0;
+    char* w = static_cast<char*>(ws);
+    auto* kin = reinterpret_cast<uint32_t*>(w + lay.off_kin);
+    auto* kout = reinterpret_cast<uint32_t*>(w + lay.off_kout);
+    auto* vin = reinterpret_cast<uint32_t*>(w + lay.off_vin);
+    auto* vout = reinterpret_cast<uint32_t*>(w + lay.off_vout);
+    auto* scan = reinterpret_cast<int32_t*>(w + lay.off_scan);
+    auto* seg = reinterpret_cast<int32_t*>(w + lay.off_seg);
+    auto* pos_off = reinterpret_cast<int64_t*>(w + lay.off_posoff);
+    auto* flag = reinterpret_cast<int32_t*>(w + lay.off_flag);
+    void* tmp = w + lay.off_tmp;
+    const int64_t n = n_positions;
+    const uint32_t sentinel = (uint32_t)table_rows;
+    if (hipMemsetAsync(flag, 0, 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
+    hipLaunchKernelGGL(posoff_kernel, dim3(1), dim3(1024), 0, st, lmax, n_slots, pos_off);
+    hipLaunchKernelGGL(enum_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_slots, n_slots, tok_bytes, tok_off, bag_off,
+                       lmax, batch, n, pos_off, table_rows, masked, kin, vin, flag);
+    size_t sb = lay.sort_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp, sb, kin, kout, vin, vout, (int)n, 0, lay.end_bit, st) != hipSuccess)
+        return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: radix sort failed");
+    hipLaunchKernelGGL(heads_kernel, dim3(grid_of(n)), dim3(256), 0, st, kout, n, scan);
+    size_t cb = lay.scan_bytes;
+    if (hipcub::DeviceScan::InclusiveSum(tmp, cb, scan, scan, (int)n, st) != hipSuccess)
+        return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: scan failed");
+    hipLaunchKernelGGL(emit_kernel, dim3(grid_of(n)), dim3(256), 0, st, kout, scan, n, sentinel, uniq_cap, uniq_rows, seg);
+    hipLaunchKernelGGL(count_kernel, dim3(1), dim3(64), 0, st, kout, scan, n, sentinel, flag, seg, n_uniq);
+    if (minmax_count) {
+        RF_REQUIRE(out, "rf_fused_hash_embed_bwd: max/min pooling needs the forward output");
+        hipLaunchKernelGGL(minmax_count_kernel, dim3(grid_of((int64_t)batch * n_slots * 2)), dim3(256), 0, st, d_slots,
+                           n_slots, tok_bytes, tok_off, bag_off, lmax, batch, masked, table, table_rows, dim, out,
+                           out_stride, minmax_count);
+    }
+    // teams of D/4 lanes; grid sized for the worst case (every position distinct), capped
+    const int64_t max_u = std::min<int64_t>(std::min<int64_t>(n, table_rows), uniq_cap);
+    auto launch = [&](auto tpr) {
+        constexpr int TPR = decltype(tpr)::value;
+        const int teams = 256 / TPR;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((max_u + teams - 1) / teams, 256 * 64));
+        hipLaunchKernelGGL(reduce_kernel<TPR>, dim3(grid), dim3(256), 0, st, d_slots, n_slots, bag_off, lmax, pos_off,
+                           masked, vout, seg, n_uniq, uniq_cap, uniq_rows, table, dim, out, dout, out_stride,
+                           minmax_count, uniq_grad);
+    };
+    const int d4 = dim / 4;
+    if (d4 <= 1) launch(std::integral_constant<int, 1>{});
+    else if (d4 <= 2) launch(std::integral_constant<int, 2>{});
+    else if (d4 <= 4) launch(std::integral_constant<int, 4>{});
+    else if (d4 <= 8) launch(std::integral_constant<int, 8>{});
+    else if (d4 <= 16) launch(std::integral_constant<int, 16>{});
+    else if (d4 <= 32) launch(std::integral_constant<int, 32>{});
+    else launch(std::integral_constant<int, 64>{});
+    return rf_check_launch("rf_fused_hash_embed_bwd");
+}
+
+extern "C" size_t rf_adam_ws_bytes(int64_t table_rows, int32_t lazy) {
+    if (table_rows < 1) return 0;
+    return lazy ? 256 : a256((size_t)table_rows * 4);
+}
+
+extern "C" int rf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                             const float* uniq_grad, const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1,
+                             float beta2, float epsilon, int32_t lazy, void* ws, size_t ws_bytes, void* stream) {
+    RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 31), "rf_adam_apply: table_rows must be in [1, 2^31)");
+    RF_REQUIRE(dim >= 4 && dim % 4 == 0, "rf_adam_apply: dim must be a multiple of 4");
+    RF_REQUIRE(table && m && v && n_uniq && (uniq_cap == 0 || (uniq_rows && uniq_grad)), "rf_adam_apply: null pointer");
+    RF_REQUIRE((((uintptr_t)table | (uintptr_t)m | (uintptr_t)v | (uintptr_t)uniq_grad) & 15) == 0,
+               "rf_adam_apply: buffers must be 16-byte aligned");
+    RF_REQUIRE(ws_bytes >= rf_adam_ws_bytes(table_rows, lazy) && (lazy || ws), "rf_adam_apply: workspace too small");
+    hipStream_t st = rf_stream(stream);
+    AdamCoef c;
+    c.lr = lr;
+    c.b1 = beta1;
+    c.b2 = beta2;
+    c.omb1 = 1.0f - beta1;  // one_minus_beta_1_t (fp32, as Keras computes it)
+    c.omb2 = 1.0f - beta2;
+    c.eps = epsilon;
+    const int D4 = dim / 4;
+    if (lazy) {
+        if (uniq_cap > 0)
+            hipLaunchKernelGGL(adam_lazy_kernel, dim3(grid_of(uniq_cap * D4)), dim3(256), 0, st, table, m, v, D4, uniq_rows,
+                               n_uniq, uniq_cap, uniq_grad, c);
+        return rf_check_launch("adam_lazy_kernel");
+    }
+    auto* map = static_cast<int32_t*>(ws);
+    if (hipMemsetAsync(map, 0xff, (size_t)table_rows * 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_adam_apply: memset failed");
+    if (uniq_cap > 0)
+        hipLaunchKernelGGL(map_fill_kernel, dim3(grid_of(uniq_cap)), dim3(256), 0, st, uniq_rows, n_uniq, uniq_cap, map);
+    hipLaunchKernelGGL(adam_dense_kernel, dim3(grid_of(table_rows * D4, 256 * 256)), dim3(256), 0, st, table, m, v,
+                       table_rows * D4, D4, map, uniq_grad, c);
+    return rf_check_launch("adam_dense_kernel");
+}

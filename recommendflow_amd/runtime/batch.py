@@ -28,6 +28,7 @@ class SparseBatch:
     lmax: object
     batch: int
     n_slots: int
+    host_lmax: object = None  # numpy copy of lmax kept with a device batch (n_positions of the backward)
 
     @property
     def n_tokens(self) -> int:
@@ -54,7 +55,17 @@ class SparseBatch:
         tb = self.tok_bytes
         if isinstance(tb, np.ndarray) and tb.size == 0:
             tb = np.zeros(16, np.uint8)  # never hand a zero-sized buffer to the kernel
-        return SparseBatch(cv(tb), cv(self.tok_off), cv(self.bag_off), cv(self.lmax), self.batch, self.n_slots)
+        hl = self.lmax if isinstance(self.lmax, np.ndarray) else self.host_lmax
+        return SparseBatch(cv(tb), cv(self.tok_off), cv(self.bag_off), cv(self.lmax), self.batch, self.n_slots,
+                           None if hl is None else np.array(hl, np.int32))
+
+    def lmax_numpy(self) -> np.ndarray:
+        """lmax on the host (no device sync when the batch came from host memory)."""
+        if isinstance(self.lmax, np.ndarray):
+            return self.lmax
+        if self.host_lmax is None:
+            self.host_lmax = self.lmax.cpu().numpy()
+        return self.host_lmax
 
     def slot(self, s: int) -> "SparseBatch":
         """Host-side single-slot view (re-based CSR) for per-feature operators."""

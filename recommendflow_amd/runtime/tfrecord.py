@@ -539,6 +539,7 @@ class FeaturePipe:
                     dev = {k: v.to(self.device, non_blocking=True) for k, v in host.items()}
                     ev = torch.cuda.Event()
                     ev.record(self.stream)
+                dev["_host_lmax"] = np.array(host["lmax"].numpy(), np.int32)
                 self._ready.put((dev, c.batch, ev, cols))
         except BaseException as e:  # surfaced to the consumer
             self._err = e
@@ -554,12 +555,16 @@ class FeaturePipe:
                     raise self._err
                 return
             dev, B, ev, cols = item
+            host_lmax = dev.pop("_host_lmax")
             cur = torch.cuda.current_stream(self.device)
             cur.wait_event(ev)
             for t in dev.values():
                 t.record_stream(cur)
             self._free.put((cols, ev))
-            yield _make_batch(self.groups, B, dev)
+            fb = _make_batch(self.groups, B, dev)
+            if fb.sparse is not None:
+                fb.sparse.host_lmax = host_lmax
+            yield fb
 
     def close(self):
         self._stop = True

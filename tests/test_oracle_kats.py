@@ -128,3 +128,99 @@ def test_bucketize_owner(O):
     assert counts.tolist() == [4, 2, 2]  # owners 2 2 1 1 0 0 0 0
     assert perm.tolist() == [4, 5, 6, 7, 2, 3, 0, 1]  # owner-major, stable
     np.testing.assert_array_equal(local, rows[perm] // 3)
+
+
+def _ref_embedding_grad(O, desc, rows_tok, lmax, table, out, dout, dim, masked):
+    """Keras restatement, written independently of rf_oracle.c: per (slot, table k) build the padded
+    [B, Lmax] id matrix, the combiner's gradient per position, then unsorted_segment_sum over the
+    flattened positions into a zero-initialised accumulator (CPU kernel order)."""
+    f32 = np.float32
+    acc = {}
+    order = []
+    B = len(rows_tok)
+    for b in range(B):
+        for s, sd in enumerate(desc):
+            toks = rows_tok[b][s]
+            for k in range(2):
+                base = int(sd["row_base"][k])
+                salt = int(sd["salt"][k])
+                ids = [base + O.hash_bucket(t, int(sd["num_bins"]), salt, True) for t in toks]
+                L = len(toks) if masked else int(lmax[s])
+                ids += [base] * (L - len(toks))  # b"" padding -> bin 0
+                col = int(sd["out_off"]) + k * dim
+                comb = int(sd["combiner"])
+                for l, r in enumerate(ids):
+                    g = dout[b, col:col + dim].astype(f32)
+                    if comb == 0:
+                        v = g
+                    elif comb == 1:
+                        v = (g / f32(L)).astype(f32)
+                    elif comb in (2, 3):
+                        y = out[b, col:col + dim]
+                        ind = (table[r] == y).astype(f32)
+                        num = sum((table[r2] == y).astype(np.int64) for r2 in ids).astype(f32)
+                        v = ((ind / num).astype(f32) * g).astype(f32)
+                    elif comb == 4:
+                        v = g if l == 0 else np.zeros(dim, f32)
+                    else:
+                        v = g if l == L - 1 else np.zeros(dim, f32)
+                    if r not in acc:
+                        acc[r] = np.zeros(dim, f32)
+                        order.append(r)
+                    acc[r] = (acc[r] + v).astype(f32)
+    rows = np.array(sorted(acc), np.int64)
+    return rows, np.stack([acc[r] for r in rows]) if len(rows) else np.zeros((0, dim), f32)
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_oracle_embedding_backward_matches_keras_restatement(O, masked):
+    from recommendflow_amd.runtime.batch import from_lists
+
+    rng = np.random.default_rng(7)
+    S, B, D = 6, 12, 4
+    rows_tok = [[[rng.choice([b"a", b"b", b"cc", b"", b"a"]) for _ in range(int(rng.integers(0, 4)))] for _ in range(S)]
+                for _ in range(B)]
+    hb = from_lists(rows_tok, lmax=[4, 3, 5, 3, 3, 4])
+    desc = np.zeros(S, O.SLOT_DTYPE)
+    base = 0
+    for s in range(S):
+        nb = 5 + s
+        desc[s]["row_base"] = (base, base + nb)
+        desc[s]["num_bins"] = nb
+        desc[s]["salt"] = (11 + s, 13 + s)
+        desc[s]["out_off"] = 2 * D * s
+        desc[s]["dim"] = D
+        desc[s]["combiner"] = s
+        desc[s]["mask_empty"] = 1
+        base += 2 * nb
+    # coarse table values make max/min ties likely
+    table = (rng.integers(-2, 3, (base, D)) * 0.25).astype(np.float32)
+    flags = O.FLAG_MASK_PADDING if masked else 0
+    out, _ = O.fused_hash_embed(desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, B, table, D, 2 * D * S, flags=flags)
+    dout = rng.normal(size=out.shape).astype(np.float32)
+    got_r, got_g = O.fused_hash_embed_bwd(desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, B, table, D, out, dout, flags)
+    want_r, want_g = _ref_embedding_grad(O, desc, rows_tok, hb.lmax, table, out, dout, D, masked)
+    np.testing.assert_array_equal(got_r, want_r)
+    assert np.array_equal(got_g.view(np.uint32), want_g.view(np.uint32))
+
+
+def test_oracle_adam_matches_keras_formula(O):
+    rng = np.random.default_rng(3)
+    R, D = 20, 4
+    t = rng.normal(size=(R, D)).astype(np.float32)
+    m = rng.normal(size=(R, D)).astype(np.float32) * np.float32(0.1)
+    v = np.abs(rng.normal(size=(R, D))).astype(np.float32) * np.float32(0.01)
+    rows = np.array([1, 4, 7, 19], np.int64)
+    g = rng.normal(size=(4, D)).astype(np.float32)
+    f = np.float32
+    lr = O.keras_adam_lr(0.001, 0.9, 0.999, 3)
+    # Adam._resource_apply_sparse, spelled out in numpy float32
+    m2 = (m * f(0.9)).astype(f)
+    m2[rows] = m2[rows] + g * (f(1) - f(0.9))
+    v2 = (v * f(0.999)).astype(f)
+    v2[rows] = v2[rows] + (g * g) * (f(1) - f(0.999))
+    t2 = (t - (f(lr) * m2) / (np.sqrt(v2) + f(1e-7))).astype(f)
+    O.adam_apply(t, m, v, rows, g, lr, 0.9, 0.999, 1e-7)
+    assert np.array_equal(m.view(np.uint32), m2.view(np.uint32))
+    assert np.array_equal(v.view(np.uint32), v2.view(np.uint32))
+    assert np.array_equal(t.view(np.uint32), t2.view(np.uint32))

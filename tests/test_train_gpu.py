@@ -1,0 +1,122 @@
+"""GPU parity of the sparse training backward (rf_fused_hash_embed_bwd) and the Keras Adam step
+(rf_adam_apply) against the C oracle, through the C ABI. Bar: bit-exact (same order of fp32 additions
+as Keras' unsorted_segment_sum on CPU; same fp32 Adam expression)."""
+import numpy as np
+import pytest
+import torch
+
+from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
+from recommendflow_amd.backend.optim import SparseAdam
+from recommendflow_amd.runtime.batch import from_lists, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+COMBS = ["sum", "avg", "max", "min", "first", "last"]
+
+
+def bits(x):
+    return np.ascontiguousarray(x).view(np.uint32)
+
+
+def run_bwd(O, enc, hb, seed=0):
+    dev = hb.to("cuda")
+    out = enc(dev)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dout = torch.randn(out.shape, generator=g).cuda()
+    sg = enc.backward(dev, dout, out=out)
+    n = sg.count()
+    got_rows = sg.rows[:n].cpu().numpy()
+    got_grad = sg.grad[:n].cpu().numpy()
+    flags = O.FLAG_MASK_PADDING if enc.mask_padding else 0
+    want_rows, want_grad = O.fused_hash_embed_bwd(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax,
+                                                  hb.batch, enc.table.cpu().numpy(), enc.dim, out.cpu().numpy(),
+                                                  dout.cpu().numpy(), flags)
+    return sg, got_rows, got_grad, want_rows, want_grad
+
+
+@pytest.mark.parametrize("dim", [4, 16, 64, 128])
+@pytest.mark.parametrize("masked", [False, True])
+def test_bwd_every_combiner(O, cuda, dim, masked):
+    S, B = 12, 96
+    specs = [SlotSpec(f"f{s}", 50 + 7 * s, (2022 + s, 2023), COMBS[s % 6]) for s in range(S)]
+    enc = FusedSparseEncoder(specs, dim, seed=3, mask_padding=masked)
+    hb = synthetic_batch(B, [s % 2 == 0 for s in range(S)], seed=11, id_max=40)  # small vocab: many collisions
+    _, gr, gg, wr, wg = run_bwd(O, enc, hb, seed=1)
+    np.testing.assert_array_equal(gr, wr)
+    assert np.array_equal(bits(gg), bits(wg)), np.abs(gg - wg).max()
+
+
+def test_bwd_ties_empty_tokens_and_empty_bags(O, cuda):
+    # duplicate tokens in one bag (max/min ties), b"" tokens (= the pad row), empty bags, lmax padding
+    rows = []
+    rng = np.random.default_rng(4)
+    for b in range(40):
+        r = []
+        for s in range(6):
+            n = int(rng.integers(0, 5))
+            r.append([rng.choice([b"", b"a", b"b", b"a", b"zz"]) for _ in range(n)])
+        rows.append(r)
+    hb = from_lists(rows, lmax=[6, 4, 5, 4, 4, 7])
+    specs = [SlotSpec(f"f{s}", 3 + s, (7, 9), c) for s, c in enumerate(["max", "min", "sum", "avg", "first", "last"])]
+    for masked in (False, True):
+        enc = FusedSparseEncoder(specs, 8, seed=5, mask_padding=masked)
+        _, gr, gg, wr, wg = run_bwd(O, enc, hb, seed=2)
+        np.testing.assert_array_equal(gr, wr)
+        assert np.array_equal(bits(gg), bits(wg))
+
+
+def test_bwd_cfg2_full_size(O, cuda):
+    """base_recall_sdpa.yaml: 229 slots, 10M x 64 fp32 fused table, B = 4096 — bit-exact."""
+    import os
+
+    from recommendflow_amd.config_parser.configuration import Configuration
+
+    conf = Configuration(os.path.join(os.path.dirname(__file__), "golden", "conf", "base_recall_sdpa.yaml"))
+    feats = conf.features.hashing_features
+    nb = 10_000_000 // (2 * len(feats))
+    specs = [SlotSpec(f.name, nb, tuple(f.hash_seeds), f.pooling.value) for f in feats]
+    enc = FusedSparseEncoder(specs, 64, seed=2023)
+    hb = synthetic_batch(4096, [bool(f.multivalued) for f in feats], seed=1234)
+    sg, gr, gg, wr, wg = run_bwd(O, enc, hb, seed=3)
+    np.testing.assert_array_equal(gr, wr)
+    assert np.array_equal(bits(gg), bits(wg))
+    assert len(gr) > 100_000
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_adam_matches_keras_restatement(O, cuda, lazy):
+    S, B, D = 8, 64, 16
+    specs = [SlotSpec(f"f{s}", 97, (2022, 2023), COMBS[s % 4]) for s in range(S)]
+    enc = FusedSparseEncoder(specs, D, seed=9)
+    opt = SparseAdam(enc.table, learning_rate=0.01, lazy=lazy)
+    t_ref = enc.table.cpu().numpy().copy()
+    m_ref = np.zeros_like(t_ref)
+    v_ref = np.zeros_like(t_ref)
+    for step in range(3):
+        hb = synthetic_batch(B, [s % 3 == 0 for s in range(S)], seed=100 + step, id_max=200)
+        dev = hb.to("cuda")
+        out = enc(dev)
+        dout = torch.randn(out.shape, generator=torch.Generator().manual_seed(step)).cuda()
+        sg = enc.backward(dev, dout, out=out)
+        n = sg.count()
+        wr, wg = O.fused_hash_embed_bwd(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, B, t_ref, D,
+                                        out.cpu().numpy(), dout.cpu().numpy())
+        np.testing.assert_array_equal(sg.rows[:n].cpu().numpy(), wr)
+        lr = O.keras_adam_lr(0.01, 0.9, 0.999, step + 1)
+        assert lr == opt.step_lr()
+        opt.apply(sg)
+        O.adam_apply(t_ref, m_ref, v_ref, wr, wg, lr, 0.9, 0.999, 1e-7, lazy=lazy)
+        assert np.array_equal(bits(enc.table.cpu().numpy()), bits(t_ref)), step
+        assert np.array_equal(bits(opt.m.cpu().numpy()), bits(m_ref))
+        assert np.array_equal(bits(opt.v.cpu().numpy()), bits(v_ref))
+
+
+def test_bwd_rejects_wrong_positions(O, cuda):
+    specs = [SlotSpec("a", 10, (1, 2))]
+    enc = FusedSparseEncoder(specs, 8, seed=1)
+    hb = synthetic_batch(8, [True], seed=1)
+    dev = hb.to("cuda")
+    dev.host_lmax = np.array([int(hb.lmax[0]) + 1], np.int32)  # inconsistent host lmax -> n_positions wrong
+    out = enc(dev)
+    sg = enc.backward(dev, torch.ones_like(out))
+    with pytest.raises(ValueError, match="error bits 2"):
+        sg.count()
