@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--shard-rows", type=int, default=125_000_000, help="cfg4 weak scaling: fused-table rows per GPU")
     p.add_argument("--shard-dim", type=int, default=128)
     p.add_argument("--shard-batch", type=int, default=8192, help="cfg4: examples per GPU (65536 at P=8)")
+    p.add_argument("--no-train", action="store_true", help="skip the cfg2 DSSM training-step extra")
     p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
     p.add_argument("--pipe-examples", type=int, default=16384, help="feature pipe: examples written and read back")
     p.add_argument("--pipe-threads", type=int, default=16, help="feature pipe: reader threads (the box's CPU share)")
@@ -138,6 +139,8 @@ def main():
             del dev, out
         torch.cuda.empty_cache()
         extras = {"cfg3_esim_forward": bench_esim(args), "cfg2_dssm_forward": bench_dssm(args, enc, host)}
+    if world == 1 and not args.no_train:
+        extras = dict(extras or {}, cfg2_dssm_train_step=bench_train(args, specs, multi))
     if world == 1 and not args.no_pipe:
         extras = dict(extras or {}, feature_pipe=bench_pipe(args, enc, specs, multi))
 
@@ -376,6 +379,78 @@ def bench_sharded(args, specs, multi, rank, world):
                      f"({enc.local_rows} rows/GPU), {B} examples/GPU (global {B * P}), owner = row mod P, "
                      f"per-step row dedup, RCCL all_to_all_single for ids and rows"}
     del enc, batches, out
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_train(args, specs, multi):
+    """one DSSM training step on cfg2 (base_recall_sdpa.yaml: 229 slots, 10M x 64 fp32 fused
+    table, B = 4096, towers [1024, 512, 256], cosent_loss): fused encoder forward -> torch towers + our
+    cosent kernel -> backward -> rf_fused_hash_embed_bwd (dedup sort-reduce) -> rf_adam_apply (Keras
+    dense Adam over the whole table + m + v) and torch Adam on the towers. Also times the sparse stages
+    alone, and the lazy-Adam variant of the table update."""
+    import numpy as np
+    import torch
+
+    from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder
+    from recommendflow_amd.config_parser.configuration import Configuration
+    from recommendflow_amd.models.matching.dssm import TrainableDssm
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "base_recall_sdpa.yaml"))
+    n_user = sum(1 for f in conf.features.hashing_features if f.tower.value == "user")
+    B = args.batch
+    enc = FusedSparseEncoder(specs, args.dim, seed=2023)
+    model = TrainableDssm(enc, n_user, learning_rate=1e-3, seed=7)
+    batches = [synthetic_batch(B, multi, seed=555 + i).to("cuda") for i in range(2)]
+    y = (torch.rand(B, generator=torch.Generator().manual_seed(0)) < 0.3).float().cuda()
+    steps = max(5, args.steps // 5)
+    for i in range(2):
+        model.step(batches[i % 2], y)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = model.step(batches[i % 2], y)
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / steps * 1e3
+    # sparse stages alone (HIP events on the launch stream)
+    dout = torch.randn((B, enc.out_width), device="cuda")
+    out = torch.empty((B, enc.out_width), device="cuda")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    acc = np.zeros(4)
+    for i in range(steps):
+        ev[0].record()
+        enc(batches[i % 2], out=out)
+        ev[1].record()
+        g = enc.backward(batches[i % 2], dout, out=out)
+        ev[2].record()
+        model.sparse_opt.apply(g)
+        ev[3].record()
+        torch.cuda.synchronize()
+        acc += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3]), 0]
+    acc /= steps
+    n_uniq = g.count()
+    from recommendflow_amd.backend.optim import SparseAdam
+
+    lazy = SparseAdam(enc.table, lazy=True)
+    for i in range(2):
+        lazy.apply(g)
+    torch.cuda.synchronize()
+    ev[0].record()
+    for i in range(steps):
+        lazy.apply(g)
+    ev[1].record()
+    torch.cuda.synchronize()
+    lazy_ms = ev[0].elapsed_time(ev[1]) / steps
+    adam_bytes = enc.table.numel() * 4 * 6 + enc.table.shape[0] * 4 + n_uniq * (args.dim * 4 + 8)
+    res = {"examples_per_s": round(B / step_ms * 1e3, 1), "ms_per_step": round(step_ms, 4), "loss": round(float(loss), 4),
+           "sparse_stage_ms": {"fwd": round(acc[0], 4), "bwd_dedup": round(acc[1], 4), "adam_dense": round(acc[2], 4),
+                               "adam_lazy": round(lazy_ms, 4)},
+           "distinct_rows_per_step": n_uniq,
+           "adam_dense_GBs": round(adam_bytes / acc[2] / 1e6, 1),
+           "config": "cfg2 DSSM train step: 229 slots, 9999972x64 fp32 table (+ m, v), B=4096, towers [1024,512,256] "
+                     "BN/selu/dropout (torch, library GEMMs), cosent_loss (HIP), Keras Adam (dense, exact) on the table"}
+    del model, enc, batches
     torch.cuda.empty_cache()
     return res
 

@@ -278,6 +278,24 @@ int rf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t 
                   const float* uniq_grad, const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1,
                   float beta2, float epsilon, int32_t lazy, void* ws, size_t ws_bytes, void* stream);
 
+/* ---- two-tower training losses (rf_loss.hip), forward + gradient ---------------- */
+/* Workspace of both loss entry points (bytes). */
+size_t rf_loss_ws_bytes(int32_t batch);
+/*
+ * cosent_loss (backend/losses/match_losses.py:42-56) on precomputed scores s_i = <query_i, doc_i>:
+ * *loss (device f32) = logsumexp([0] ++ [scale * (s_i - s_j) for y_i < y_j]); dscore[i] = dloss/ds_i
+ * (may be NULL).
+ */
+int rf_cosent_loss(const float* score, const float* label, int32_t batch, float scale, float* loss, float* dscore,
+                   void* ws, size_t ws_bytes, void* stream);
+/*
+ * batch_neg_sample_scaled_multi_class_ce_loss (match_losses.py:150-165) on logits P = query . doc^T
+ * ([batch][ld], a library GEMM): *loss = mean_i(-log softmax(scale * P_i.)_i * y_i);
+ * dlogits[i][j] = dloss/dP_ij (may be NULL).
+ */
+int rf_inbatch_ce_loss(const float* logits, int64_t ld, const float* label, int32_t batch, float scale, float* loss,
+                       float* dlogits, int64_t ldd, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

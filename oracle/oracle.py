@@ -371,3 +371,35 @@ def l2_normalize(x, eps=1e-12):
     """K.l2_normalize (dssm.py:35-36): x / sqrt(max(sum x^2, eps))."""
     x = np.asarray(x, np.float64)
     return x / np.sqrt(np.maximum((x * x).sum(axis=-1, keepdims=True), eps))
+
+
+# ----------------------------------------------------------------------------------------------
+# training losses (float64), backend/losses/match_losses.py
+# ----------------------------------------------------------------------------------------------
+def cosent_loss(y: np.ndarray, s: np.ndarray, scale: float = 20.0):
+    """match_losses.py:42-56 on scores s_i = <q_i, d_i>: returns (loss, dloss/ds)."""
+    y = np.asarray(y, np.float64)
+    s = np.asarray(s, np.float64)
+    valid = y[:, None] < y[None, :]
+    x = scale * (s[:, None] - s[None, :])
+    xs = np.where(valid, x, -np.inf)
+    m = max(0.0, float(xs.max()) if valid.any() else 0.0)
+    e = np.where(valid, np.exp(x - m), 0.0)
+    z = np.exp(-m) + e.sum()
+    loss = m + np.log(z)
+    p = e / z
+    ds = scale * (p.sum(axis=1) - p.sum(axis=0))
+    return loss, ds
+
+
+def inbatch_ce_loss(y: np.ndarray, logits: np.ndarray, scale: float = 20.0):
+    """match_losses.py:150-165 on logits P = q . d^T: returns (loss, dloss/dP)."""
+    y = np.asarray(y, np.float64)
+    P = np.asarray(logits, np.float64) * scale
+    m = P.max(axis=1, keepdims=True)
+    e = np.exp(P - m)
+    sm = e / e.sum(axis=1, keepdims=True)
+    B = len(y)
+    loss = float(np.mean(-np.log(np.diag(sm)) * y))
+    d = scale * y[:, None] / B * (sm - np.eye(B))
+    return loss, d

@@ -1,0 +1,69 @@
+"""Two-tower training losses (reference: backend/losses/match_losses.py), forward + gradient in one HIP
+call each (rf_cosent_loss, rf_inbatch_ce_loss). Same names and (y_true, query, doc, scale) signatures as
+the reference; they are torch autograd functions so the towers' backward flows through them.
+
+* cosent_loss (match_losses.py:42-56) — the loss of base_recall_sdpa.yaml (Networks.loss).
+* batch_neg_sample_scaled_multi_class_ce_loss (match_losses.py:150-165) — Que2Search in-batch softmax;
+  the [B, B] logits are one library GEMM (query . doc^T), the softmax/CE and its gradient are ours.
+"""
+from __future__ import annotations
+
+import torch
+
+from ...runtime import lib as L
+
+
+def _ws(batch: int, device) -> torch.Tensor:
+    return torch.empty(max(int(L.load().rf_loss_ws_bytes(batch)), 256), dtype=torch.uint8, device=device)
+
+
+class _Cosent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, score, label, scale):
+        score = score.float().contiguous()
+        label = label.float().contiguous()
+        B = score.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=score.device)
+        ds = torch.empty_like(score)
+        ws = _ws(B, score.device)
+        L.call("rf_cosent_loss", L.ptr(score), L.ptr(label), B, float(scale), L.ptr(loss), L.ptr(ds), L.ptr(ws),
+               ws.numel(), L.stream_ptr())
+        ctx.save_for_backward(ds)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (ds,) = ctx.saved_tensors
+        return ds * g, None, None
+
+
+class _InBatchCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, label, scale):
+        logits = logits.float().contiguous()
+        label = label.float().contiguous()
+        B = logits.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        dl = torch.empty_like(logits)
+        ws = _ws(B, logits.device)
+        L.call("rf_inbatch_ce_loss", L.ptr(logits), logits.stride(0), L.ptr(label), B, float(scale), L.ptr(loss),
+               L.ptr(dl), dl.stride(0), L.ptr(ws), ws.numel(), L.stream_ptr())
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return dl * g, None, None
+
+
+def cosent_loss(y_true, query, doc, scale=20):
+    """logsumexp([0] ++ [scale*(s_i - s_j) : y_i < y_j]), s = <query_i, doc_i> (match_losses.py:42-56)."""
+    L.require_gpu()
+    return _Cosent.apply((query * doc).sum(dim=1), y_true.reshape(-1), scale)
+
+
+def batch_neg_sample_scaled_multi_class_ce_loss(y_true, query, doc, scale=20):
+    """mean_i(-log(exp(s<q_i,d_i>) / sum_j exp(s<q_i,d_j>)) * y_i) (match_losses.py:150-165)."""
+    L.require_gpu()
+    return _InBatchCE.apply(query @ doc.t(), y_true.reshape(-1), scale)

@@ -1,0 +1,39 @@
+"""Training step plumbing for the sparse hot path.
+
+The fused encoder joins torch autograd through `embed()`: forward = rf_fused_hash_embed_fwd, backward =
+rf_fused_hash_embed_bwd, whose deduplicated row gradient is parked on the encoder (`enc.grad`) for
+SparseAdam (rf_adam_apply) — the table is never a dense torch gradient. Dense parameters (towers) train
+with torch autograd + torch.optim.Adam using Keras' Adam defaults (reference: model.fit with
+tf.keras.optimizers.Adam, example/recall_search/train.py:96-104).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..backend.encoder.sparse_encoder import FusedSparseEncoder, SparseGrad
+from .batch import SparseBatch
+
+
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, enc: FusedSparseEncoder, batch: SparseBatch):
+        out = enc(batch)
+        ctx.enc, ctx.batch = enc, batch
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (out,) = ctx.saved_tensors
+        ctx.enc.grad = ctx.enc.backward(ctx.batch, dout.float().contiguous(), out=out)
+        return None, None, None
+
+
+def embed(enc: FusedSparseEncoder, batch: SparseBatch) -> torch.Tensor:
+    """enc(batch) with a sparse backward: after loss.backward(), enc.grad holds the SparseGrad."""
+    if not hasattr(enc, "_anchor"):
+        enc._anchor = torch.zeros(1, device=enc.table.device, requires_grad=True)
+    enc.grad: Optional[SparseGrad] = None
+    return _EmbedFn.apply(enc._anchor, enc, batch)
