@@ -198,6 +198,11 @@ __global__ void count_kernel(const uint32_t* __restrict__ keys, const int32_t* _
     *n_uniq = *flag ? -*flag : nu;
 }
 
+// flags raised after count_kernel (prep's alignment check) reach the caller through n_uniq too
+__global__ void flag_kernel(const int32_t* __restrict__ flag, int32_t* __restrict__ n_uniq) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && *flag) *n_uniq = -*flag;
+}
+
 // max/min tie counts: cnt[b][col + d] = #{l < L : T[row_l][d] == out[b][col + d]} (tf _MinOrMaxGrad num_selected)
 __global__ __launch_bounds__(256) void minmax_count_kernel(const rf_slot_desc* __restrict__ slots, int S,
                                                            const uint8_t* __restrict__ tok_bytes,
@@ -233,64 +238,176 @@ __global__ __launch_bounds__(256) void minmax_count_kernel(const rf_slot_desc* _
     }
 }
 
-// The gradient of position q (table row `row`) at column d of its [slot, k] block.
-__device__ __forceinline__ float pos_grad(const rf_slot_desc* sd, const Pos& q, int masked, float g, float t, float o, int32_t c) {
-    const int L = masked ? q.len : max(q.L, q.len);
-    switch (sd->combiner) {
-        case RF_COMB_SUM: return g;
-        case RF_COMB_AVG: return g / (float)L;
-        case RF_COMB_MAX:
-        case RF_COMB_MIN: return ((t == o ? 1.0f : 0.0f) / (float)c) * g;
-        case RF_COMB_FIRST: return q.l == 0 ? g : 0.0f;
-        case RF_COMB_LAST: return q.l == L - 1 ? g : 0.0f;
-        default: return 0.0f;
+// ---- ordered segment reduce -------------------------------------------------------------------
+// After the sort, a parallel prep pass turns every position into (src, aux): src = the float4 index of
+// its [slot, k] block in dout (kZero for the exact-zero gradients of first/last at other positions),
+// aux = combiner << 24 | L. The reduce then only streams dout rows and adds them in order; no decode
+// sits on the serial chain. An accumulator that starts at +0.0 can never become -0.0 under round-to-
+// nearest, so adding +0.0 changes nothing: kZero positions add nothing (their row still counts as touched).
+constexpr uint32_t kZero = 0xffffffffu;
+constexpr int kLong = 256;  // segments longer than this go to the block-per-segment kernel
+
+__global__ __launch_bounds__(256) void prep_kernel(const rf_slot_desc* __restrict__ slots, int S,
+                                                   const int32_t* __restrict__ bag_off,
+                                                   const int32_t* __restrict__ lmax,
+                                                   const int64_t* __restrict__ pos_off, int masked,
+                                                   const uint32_t* __restrict__ vals,
+                                                   const int32_t* __restrict__ seg,
+                                                   const int32_t* __restrict__ n_uniq_p, int D, int64_t stride,
+                                                   uint32_t* __restrict__ src, uint32_t* __restrict__ aux,
+                                                   int32_t* __restrict__ flag) {
+    const int32_t nu = *n_uniq_p;
+    if (nu <= 0) return;
+    const int64_t n = seg[nu];  // positions of real rows (the sentinel segment, if any, follows)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const Pos q = decode_pos(vals[i], pos_off, S, lmax, bag_off);
+        const rf_slot_desc* sd = slots + q.s;
+        const int L = masked ? q.len : max(q.L, q.len);
+        const int64_t col = (int64_t)q.b * stride + sd->out_off + (int64_t)q.k * D;
+        if (col & 3) atomicOr(flag, 8);
+        const int comb = sd->combiner;
+        const bool zero = (comb == RF_COMB_FIRST && q.l != 0) || (comb == RF_COMB_LAST && q.l != L - 1);
+        src[i] = zero ? kZero : (uint32_t)(col >> 2);
+        aux[i] = ((uint32_t)comb << 24) | ((uint32_t)L & 0xffffffu);
     }
 }
 
-// Team of TPR = D/4 lanes per distinct row; lanes own 4 consecutive columns. Walks the segment in
-// order (the reference's summation order); the row's own table values are loaded once (max/min).
+__global__ __launch_bounds__(256) void classify_kernel(const int32_t* __restrict__ seg, const int32_t* __restrict__ n_uniq_p,
+                                                       int64_t cap, int32_t* __restrict__ long_list,
+                                                       int32_t* __restrict__ long_cnt) {
+    const int64_t nu = min<int64_t>(*n_uniq_p, cap);
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x)
+        if (seg[u + 1] - seg[u] > kLong) long_list[atomicAdd(long_cnt, 1)] = (int32_t)u;
+}
+
+// gradient contribution of one position to the lane's 4 columns
+__device__ __forceinline__ float4 pos_value(uint32_t s4, uint32_t a, int lane, const float4& trow,
+                                            const float4* __restrict__ dout4, const float4* __restrict__ out4,
+                                            const int4* __restrict__ cnt4) {
+    if (s4 == kZero) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g = dout4[(int64_t)s4 + lane];
+    const int comb = (int)(a >> 24);
+    if (comb == RF_COMB_AVG) {  // tf.reduce_mean gradient: g / L
+        const float L = (float)(a & 0xffffffu);
+        return make_float4(g.x / L, g.y / L, g.z / L, g.w / L);
+    }
+    if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) {  // tf _MinOrMaxGrad: (x == y) / num_selected * grad
+        const float4 o = out4[(int64_t)s4 + lane];
+        const int4 c = cnt4[(int64_t)s4 + lane];
+        return make_float4(((trow.x == o.x ? 1.f : 0.f) / (float)c.x) * g.x, ((trow.y == o.y ? 1.f : 0.f) / (float)c.y) * g.y,
+                           ((trow.z == o.z ? 1.f : 0.f) / (float)c.z) * g.z, ((trow.w == o.w ? 1.f : 0.f) / (float)c.w) * g.w);
+    }
+    return g;  // sum, and first/last at their position
+}
+
+__device__ __forceinline__ void add4(float4& a, const float4& v) {
+    a.x += v.x;
+    a.y += v.y;
+    a.z += v.z;
+    a.w += v.w;
+}
+
+// Short segments: a team of TPR lanes (>= D/4) per row, 4 positions' loads in flight per step.
 template <int TPR>
-__global__ __launch_bounds__(256) void reduce_kernel(const rf_slot_desc* __restrict__ slots, int S,
-                                                     const int32_t* __restrict__ bag_off,
-                                                     const int32_t* __restrict__ lmax,
-                                                     const int64_t* __restrict__ pos_off, int masked,
-                                                     const uint32_t* __restrict__ vals,
-                                                     const int32_t* __restrict__ seg,
-                                                     const int32_t* __restrict__ n_uniq_p, int64_t cap,
-                                                     const int64_t* __restrict__ uniq_rows,
-                                                     const float* __restrict__ table, int D,
-                                                     const float* __restrict__ out, const float* __restrict__ dout,
-                                                     int64_t stride, const int32_t* __restrict__ cnt,
-                                                     float* __restrict__ uniq_grad) {
+__global__ __launch_bounds__(256) void reduce_short_kernel(const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux,
+                                                           const int32_t* __restrict__ seg,
+                                                           const int32_t* __restrict__ n_uniq_p, int64_t cap,
+                                                           const int64_t* __restrict__ uniq_rows,
+                                                           const float* __restrict__ table, int D,
+                                                           const float* __restrict__ out, const float* __restrict__ dout,
+                                                           const int32_t* __restrict__ cnt, float* __restrict__ uniq_grad) {
     constexpr int TEAMS = 256 / TPR;
     const int team = threadIdx.x / TPR, lane = threadIdx.x % TPR;
     const int64_t nu = min<int64_t>(*n_uniq_p, cap);
-    const int d0 = lane * 4;
-    const bool active_lane = d0 < D;
+    const bool active = lane * 4 < D;
+    const auto* dout4 = reinterpret_cast<const float4*>(dout);
+    const auto* out4 = reinterpret_cast<const float4*>(out);
+    const auto* cnt4 = reinterpret_cast<const int4*>(cnt);
     for (int64_t u = (int64_t)blockIdx.x * TEAMS + team; u < nu; u += (int64_t)gridDim.x * TEAMS) {
-        const int64_t row = uniq_rows[u];
         const int i0 = seg[u], i1 = seg[u + 1];
+        if (i1 - i0 > kLong || !active) continue;
+        const int64_t row = uniq_rows[u];
+        const float4 trow = reinterpret_cast<const float4*>(table + row * D)[lane];
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 trow = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (active_lane) trow = *reinterpret_cast<const float4*>(table + row * D + d0);
-        for (int i = i0; i < i1; ++i) {
-            const Pos q = decode_pos(vals[i], pos_off, S, lmax, bag_off);
-            const rf_slot_desc* sd = slots + q.s;
-            if (!active_lane) continue;
-            const int64_t col = (int64_t)q.b * stride + sd->out_off + (int64_t)q.k * D + d0;
-            const float4 g = *reinterpret_cast<const float4*>(dout + col);
-            float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-            int4 c = make_int4(1, 1, 1, 1);
-            if (sd->combiner == RF_COMB_MAX || sd->combiner == RF_COMB_MIN) {
-                o = *reinterpret_cast<const float4*>(out + col);
-                c = *reinterpret_cast<const int4*>(cnt + col);
+        int i = i0;
+        for (; i + 4 <= i1; i += 4) {
+            uint32_t s4[4], a[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                s4[k] = src[i + k];
+                a[k] = aux[i + k];
             }
-            acc.x += pos_grad(sd, q, masked, g.x, trow.x, o.x, c.x);
-            acc.y += pos_grad(sd, q, masked, g.y, trow.y, o.y, c.y);
-            acc.z += pos_grad(sd, q, masked, g.z, trow.z, o.z, c.z);
-            acc.w += pos_grad(sd, q, masked, g.w, trow.w, o.w, c.w);
+            float4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = pos_value(s4[k], a[k], lane, trow, dout4, out4, cnt4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) add4(acc, v[k]);
         }
-        if (active_lane) *reinterpret_cast<float4*>(uniq_grad + u * D + d0) = acc;
+        for (; i < i1; ++i) add4(acc, pos_value(src[i], aux[i], lane, trow, dout4, out4, cnt4));
+        reinterpret_cast<float4*>(uniq_grad + u * D)[lane] = acc;
+    }
+}
+
+// value of chunk c of a long segment for this thread (position i0 + c * P + pi); zero past the end
+__device__ __forceinline__ float4 long_value(const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux, int i0,
+                                             int i1, int c, int nch, int P, int pi, int lane, bool active,
+                                             const float4& trow, const float4* __restrict__ dout4,
+                                             const float4* __restrict__ out4, const int4* __restrict__ cnt4) {
+    const int i = i0 + c * P + pi;
+    if (c >= nch || i >= i1 || !active) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return pos_value(src[i], aux[i], lane, trow, dout4, out4, cnt4);
+}
+
+// Long segments (Zipf-hot tokens, the padding rows of multi-valued slots): one 1024-thread block per
+// row. Every thread computes one (position, float4) value of a chunk of P = 1024 / TPR positions, with
+// kDepth chunks in flight in registers; a chunk goes through LDS and the first team adds it in order.
+// Only the adds are serial.
+template <int TPR>
+__global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux,
+                                                           const int32_t* __restrict__ seg,
+                                                           const int32_t* __restrict__ long_list,
+                                                           const int32_t* __restrict__ long_cnt,
+                                                           const int64_t* __restrict__ uniq_rows,
+                                                           const float* __restrict__ table, int D,
+                                                           const float* __restrict__ out, const float* __restrict__ dout,
+                                                           const int32_t* __restrict__ cnt, float* __restrict__ uniq_grad) {
+    constexpr int P = 1024 / TPR;
+    constexpr int kDepth = 4;
+    __shared__ float4 buf[1024];
+    const int t = threadIdx.x, pi = t / TPR, lane = t % TPR;
+    const bool active = lane * 4 < D;
+    const auto* dout4 = reinterpret_cast<const float4*>(dout);
+    const auto* out4 = reinterpret_cast<const float4*>(out);
+    const auto* cnt4 = reinterpret_cast<const int4*>(cnt);
+    const int nl = *long_cnt;
+    for (int j = blockIdx.x; j < nl; j += gridDim.x) {
+        const int32_t u = long_list[j];
+        const int i0 = seg[u], i1 = seg[u + 1];
+        const int64_t row = uniq_rows[u];
+        const float4 trow = active ? reinterpret_cast<const float4*>(table + row * D)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int nch = (i1 - i0 + P - 1) / P;
+        float4 ring[kDepth];
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) ring[k] = long_value(src, aux, i0, i1, k, nch, P, pi, lane, active, trow, dout4, out4, cnt4);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int c0 = 0; c0 < nch; c0 += kDepth) {
+#pragma unroll
+            for (int k = 0; k < kDepth; ++k) {
+                const int c = c0 + k;
+                if (c < nch) {  // block-uniform
+                    buf[t] = ring[k];
+                    __syncthreads();
+                    ring[k] = long_value(src, aux, i0, i1, c + kDepth, nch, P, pi, lane, active, trow, dout4, out4, cnt4);
+                    if (t < TPR && active) {
+                        const int np = min(P, i1 - (i0 + c * P));
+                        for (int q = 0; q < np; ++q) add4(acc, buf[q * TPR + t]);
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+        if (t < TPR && active) reinterpret_cast<float4*>(uniq_grad + (int64_t)u * D)[t] = acc;
+        __syncthreads();
     }
 }
 
@@ -435,15 +552,25 @@ extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_sl
                            n_slots, tok_bytes, tok_off, bag_off, lmax, batch, masked, table, table_rows, dim, out,
                            out_stride, minmax_count);
     }
-    // teams of D/4 lanes; grid sized for the worst case (every position distinct), capped
+    // prep (src/aux into the now-free pre-sort buffers) and the long-segment list (into the free scan buffer)
+    uint32_t* src = kin;
+    uint32_t* aux = vin;
+    int32_t* long_list = scan;
+    int32_t* long_cnt = flag + 1;
+    if (hipMemsetAsync(long_cnt, 0, 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
+    hipLaunchKernelGGL(prep_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_slots, n_slots, bag_off, lmax, pos_off, masked,
+                       vout, seg, n_uniq, dim, out_stride, src, aux, flag);
     const int64_t max_u = std::min<int64_t>(std::min<int64_t>(n, table_rows), uniq_cap);
+    hipLaunchKernelGGL(classify_kernel, dim3(grid_of(max_u)), dim3(256), 0, st, seg, n_uniq, uniq_cap, long_list, long_cnt);
     auto launch = [&](auto tpr) {
         constexpr int TPR = decltype(tpr)::value;
         const int teams = 256 / TPR;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((max_u + teams - 1) / teams, 256 * 64));
-        hipLaunchKernelGGL(reduce_kernel<TPR>, dim3(grid), dim3(256), 0, st, d_slots, n_slots, bag_off, lmax, pos_off,
-                           masked, vout, seg, n_uniq, uniq_cap, uniq_rows, table, dim, out, dout, out_stride,
-                           minmax_count, uniq_grad);
+        hipLaunchKernelGGL(reduce_short_kernel<TPR>, dim3(grid), dim3(256), 0, st, src, aux, seg, n_uniq, uniq_cap,
+                           uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
+        const int lgrid = (int)std::max<int64_t>(1, std::min<int64_t>(n / kLong + 1, 1024));
+        hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
+                           uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
     };
     const int d4 = dim / 4;
     if (d4 <= 1) launch(std::integral_constant<int, 1>{});
@@ -453,6 +580,7 @@ extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_sl
     else if (d4 <= 16) launch(std::integral_constant<int, 16>{});
     else if (d4 <= 32) launch(std::integral_constant<int, 32>{});
     else launch(std::integral_constant<int, 64>{});
+    hipLaunchKernelGGL(flag_kernel, dim3(1), dim3(64), 0, st, flag, n_uniq);  // prep's alignment flag
     return rf_check_launch("rf_fused_hash_embed_bwd");
 }
 
