@@ -348,20 +348,12 @@ __global__ __launch_bounds__(256) void reduce_short_kernel(const uint32_t* __res
     }
 }
 
-// value of chunk c of a long segment for this thread (position i0 + c * P + pi); zero past the end
-__device__ __forceinline__ float4 long_value(const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux, int i0,
-                                             int i1, int c, int nch, int P, int pi, int lane, bool active,
-                                             const float4& trow, const float4* __restrict__ dout4,
-                                             const float4* __restrict__ out4, const int4* __restrict__ cnt4) {
-    const int i = i0 + c * P + pi;
-    if (c >= nch || i >= i1 || !active) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return pos_value(src[i], aux[i], lane, trow, dout4, out4, cnt4);
-}
-
 // Long segments (Zipf-hot tokens, the padding rows of multi-valued slots): one 1024-thread block per
-// row. Every thread computes one (position, float4) value of a chunk of P = 1024 / TPR positions, with
-// kDepth chunks in flight in registers; a chunk goes through LDS and the first team adds it in order.
-// Only the adds are serial.
+// row. Every thread computes one (position, float4) value of a chunk of P = 1024 / TPR positions. Two
+// register rings keep kDepth chunks in flight: the (src, aux) pairs of chunk c + 2 kDepth and the dout
+// values of chunk c + kDepth, so a dout load never waits on its index load. A chunk goes through a
+// double-buffered LDS image (one barrier per chunk) and the first team adds it in order: only the adds
+// are serial.
 template <int TPR>
 __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux,
                                                            const int32_t* __restrict__ seg,
@@ -372,8 +364,9 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
                                                            const float* __restrict__ out, const float* __restrict__ dout,
                                                            const int32_t* __restrict__ cnt, float* __restrict__ uniq_grad) {
     constexpr int P = 1024 / TPR;
-    constexpr int kDepth = 4;
-    __shared__ float4 buf[1024];
+    constexpr int kDepth = 8;
+    constexpr int G = 8;  // LDS reads per add group
+    __shared__ float4 buf[2][1024];
     const int t = threadIdx.x, pi = t / TPR, lane = t % TPR;
     const bool active = lane * 4 < D;
     const auto* dout4 = reinterpret_cast<const float4*>(dout);
@@ -386,23 +379,61 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
         const int64_t row = uniq_rows[u];
         const float4 trow = active ? reinterpret_cast<const float4*>(table + row * D)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
         const int nch = (i1 - i0 + P - 1) / P;
-        float4 ring[kDepth];
+        // index of this thread's position in chunk c, or -1 past the segment
+        auto pos_of = [&](int c) -> int {
+            const int i = i0 + c * P + pi;
+            return (c < nch && i < i1 && active) ? i : -1;
+        };
+        uint32_t rs[kDepth], ra[kDepth];
+        float4 rv[kDepth];
 #pragma unroll
-        for (int k = 0; k < kDepth; ++k) ring[k] = long_value(src, aux, i0, i1, k, nch, P, pi, lane, active, trow, dout4, out4, cnt4);
+        for (int k = 0; k < kDepth; ++k) {
+            const int i = pos_of(k);
+            rs[k] = i >= 0 ? src[i] : kZero;
+            ra[k] = i >= 0 ? aux[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) {
+            rv[k] = pos_value(rs[k], ra[k], lane, trow, dout4, out4, cnt4);
+            const int i = pos_of(k + kDepth);
+            rs[k] = i >= 0 ? src[i] : kZero;
+            ra[k] = i >= 0 ? aux[i] : 0u;
+        }
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int c0 = 0; c0 < nch; c0 += kDepth) {
 #pragma unroll
             for (int k = 0; k < kDepth; ++k) {
                 const int c = c0 + k;
                 if (c < nch) {  // block-uniform
-                    buf[t] = ring[k];
+                    float4* b = buf[c & 1];
+                    b[t] = rv[k];
                     __syncthreads();
-                    ring[k] = long_value(src, aux, i0, i1, c + kDepth, nch, P, pi, lane, active, trow, dout4, out4, cnt4);
+                    rv[k] = pos_value(rs[k], ra[k], lane, trow, dout4, out4, cnt4);  // chunk c + kDepth
+                    const int i = pos_of(c + 2 * kDepth);
+                    rs[k] = i >= 0 ? src[i] : kZero;
+                    ra[k] = i >= 0 ? aux[i] : 0u;
                     if (t < TPR && active) {
                         const int np = min(P, i1 - (i0 + c * P));
-                        for (int q = 0; q < np; ++q) add4(acc, buf[q * TPR + t]);
+                        int q = 0;
+                        if (np == P) {  // full chunk: reads of group g + 1 in flight while group g is added
+                            float4 cur[G], nxt[G];
+#pragma unroll
+                            for (int r = 0; r < G; ++r) cur[r] = b[r * TPR + t];
+#pragma unroll
+                            for (int g = 0; g < P / G; ++g) {
+                                if (g + 1 < P / G) {
+#pragma unroll
+                                    for (int r = 0; r < G; ++r) nxt[r] = b[((g + 1) * G + r) * TPR + t];
+                                }
+#pragma unroll
+                                for (int r = 0; r < G; ++r) add4(acc, cur[r]);
+#pragma unroll
+                                for (int r = 0; r < G; ++r) cur[r] = nxt[r];
+                            }
+                            q = P;
+                        }
+                        for (; q < np; ++q) add4(acc, b[q * TPR + t]);
                     }
-                    __syncthreads();
                 }
             }
         }

@@ -92,8 +92,9 @@ class TrainableDssm(torch.nn.Module):
         from ...runtime.train import embed
 
         x = embed(self.enc, batch)
-        u = torch.nn.functional.normalize(self.user_tower(x[:, : self.wu]), dim=-1, eps=1e-6)
-        v = torch.nn.functional.normalize(self.ad_tower(x[:, self.wu:]), dim=-1, eps=1e-6)
+        # contiguous column blocks: BatchNorm's backward on a strided view falls off torch's fast path
+        u = torch.nn.functional.normalize(self.user_tower(x[:, : self.wu].contiguous()), dim=-1, eps=1e-6)
+        v = torch.nn.functional.normalize(self.ad_tower(x[:, self.wu:].contiguous()), dim=-1, eps=1e-6)
         return u, v
 
     def step(self, batch: SparseBatch, labels: torch.Tensor) -> torch.Tensor:
