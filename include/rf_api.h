@@ -296,6 +296,43 @@ int rf_cosent_loss(const float* score, const float* label, int32_t batch, float 
 int rf_inbatch_ce_loss(const float* logits, int64_t ld, const float* label, int32_t batch, float scale, float* loss,
                        float* dlogits, int64_t ldd, void* ws, size_t ws_bytes, void* stream);
 
+/* ---- Lookup / Discrete embeddings: GPU index producers (rf_lookup.hip) ----------- */
+/*
+ * StringLookup / IntegerLookup (backend/layers/preprocess_layers.py:135-169, Keras TF >= 2.6 defaults:
+ * num_oov_indices = 1, mask_token = None): vocab[i] -> i + 1, any other value -> 0. The vocabulary is an
+ * open-addressing table (linear probing) of `cap` entries, cap a power of two >= 2 * n_vocab
+ * (rf_vocab_capacity); string keys are a SipHash-2-4 of the bytes (hits are verified against the
+ * vocabulary bytes), integer keys the value itself.
+ */
+#define RF_VOCAB_BYTES 0
+#define RF_VOCAB_INT64 1
+typedef struct rf_vocab_entry {
+    uint64_t key; /* SipHash of the term (bytes) or the term (int64) */
+    int32_t id;   /* i + 1 for vocabulary entry i; -1 = empty slot */
+    int32_t ref;  /* vocabulary index i (bytes: for the byte-for-byte check) */
+} rf_vocab_entry; /* 16 bytes */
+int64_t rf_vocab_capacity(int64_t n_vocab);
+/* HOST function: fills a HOST table (copy it to the device). values: bytes + off[n_vocab + 1] for
+ * RF_VOCAB_BYTES, int64[n_vocab] for RF_VOCAB_INT64. A repeated term -> RF_EINVAL (Keras raises too). */
+int rf_vocab_build(int32_t kind, const void* values, const int32_t* off, int64_t n_vocab, rf_vocab_entry* table,
+                   int64_t cap);
+/*
+ * Padded ids of one slot of a batched CSR group (bag_off[B * n_slots + 1], example-major):
+ * ids[b][l] (int64, [batch][lmax]) = lookup(value l of bag (b, slot)) for l < len, lookup(default) for
+ * padding (b"" / 0: the value parse_example pads with, dataloader.py:32-33). values = token bytes (+ tok_off)
+ * for RF_VOCAB_BYTES, int64 values for RF_VOCAB_INT64. Feed ids to rf_embedding_bag_fwd.
+ */
+int rf_lookup_ids(int32_t kind, const rf_vocab_entry* table, int64_t cap, const uint8_t* vocab_bytes,
+                  const int32_t* vocab_off, const void* values, const int32_t* tok_off, const int32_t* bag_off,
+                  int32_t n_slots, int32_t slot, int32_t batch, int32_t lmax, int64_t* ids, void* stream);
+/*
+ * Discretization(bin_boundaries) (preprocess_layers.py:172-200) = tf Bucketize: ids[b][l] = number of
+ * boundaries <= x (upper bound; NaN -> n_boundaries), padding x = pad_value (the float default 0.0).
+ */
+int rf_bucketize_ids(const float* values, const int32_t* bag_off, int32_t n_slots, int32_t slot, int32_t batch,
+                     int32_t lmax, const float* boundaries, int32_t n_boundaries, float pad_value, int64_t* ids,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -403,3 +403,25 @@ def inbatch_ce_loss(y: np.ndarray, logits: np.ndarray, scale: float = 20.0):
     loss = float(np.mean(-np.log(np.diag(sm)) * y))
     d = scale * y[:, None] / B * (sm - np.eye(B))
     return loss, d
+
+
+# ----------------------------------------------------------------------------------------------
+# Lookup / Discrete index producers (preprocess_layers.py:135-200), pure Python
+# ----------------------------------------------------------------------------------------------
+def lookup_ids(vocab, rows, pad):
+    """StringLookup/IntegerLookup(vocabulary, num_oov_indices=1, mask_token=None) on padded rows:
+    vocab[i] -> i + 1, else 0; rows shorter than the batch max are padded with `pad` first."""
+    index = {v: i + 1 for i, v in enumerate(vocab)}
+    width = max((len(r) for r in rows), default=0)
+    return np.array([[index.get(v, 0) for v in list(r) + [pad] * (width - len(r))] for r in rows], np.int64).reshape(len(rows), width)
+
+
+def bucketize_ids(boundaries, rows, pad=0.0):
+    """tf Bucketize / Keras Discretization: number of boundaries <= x (bisect_right; NaN -> len). The
+    boundaries are a list(float) op attribute, i.e. float32, like the inputs."""
+    import bisect
+
+    b = [float(np.float32(x)) for x in boundaries]
+    width = max((len(r) for r in rows), default=0)
+    return np.array([[bisect.bisect_right(b, float(np.float32(v))) for v in list(r) + [pad] * (width - len(r))]
+                     for r in rows], np.int64).reshape(len(rows), width)

@@ -8,8 +8,8 @@ Operator                 reference (file:line)          device entry point
 Hashing                  keras Hashing (:89-90)         rf_siphash_bucket
 EmbeddingBag             :16-76                          rf_embedding_bag_fwd
 DoubleHashingEmbedding   :79-106                         rf_fused_hash_embed_fwd (one slot)
-LookupEmbedding          :135-169                        host Lookup -> rf_embedding_bag_fwd
-DiscreteEmbedding        :172-200                        Discretization (torch.bucketize) -> rf_embedding_bag_fwd
+LookupEmbedding          :135-169                        rf_lookup_ids (vocab hash table) -> rf_embedding_bag_fwd
+DiscreteEmbedding        :172-200                        rf_bucketize_ids -> rf_embedding_bag_fwd
 BertEncode               :109-132                        out of scope (BERT), raises
 """
 from __future__ import annotations
@@ -207,13 +207,46 @@ class DoubleHashingEmbedding(torch.nn.Module):
         return {"name": self.name, "combiner": self.combiner, "seeds": self.seeds, "num_bins": self.num_bins}
 
 
+VOCAB_DTYPE = np.dtype([("key", "<u8"), ("id", "<i4"), ("ref", "<i4")])  # rf_vocab_entry, 16 bytes
+assert VOCAB_DTYPE.itemsize == 16
+
+
+def _ragged_slot(inputs, slot: int, dtype, device):
+    """(values, bag_off, n_slots, lmax) of one slot of a ragged group, on `device`. Accepts
+    runtime.tfrecord.RaggedColumns (the pipe's int64/float list features) or padded dense host rows
+    [B][L] (the parse_example form; every position is a value, padding included)."""
+    if hasattr(inputs, "bag_off") and hasattr(inputs, "values"):
+        S = len(inputs.names) if getattr(inputs, "names", None) else 1
+        lm = inputs.lmax
+        lmax = int(lm[slot]) if isinstance(lm, np.ndarray) else int(lm[slot].item())
+        vals = inputs.values if isinstance(inputs.values, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(inputs.values))
+        bo = inputs.bag_off if isinstance(inputs.bag_off, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(inputs.bag_off))
+        vals = vals.to(device=device, dtype=dtype)
+        if vals.numel() == 0:
+            vals = torch.zeros(1, dtype=dtype, device=device)
+        return vals.contiguous(), bo.to(device=device, dtype=torch.int32).contiguous(), S, lmax
+    rows = [list(r) if isinstance(r, (list, tuple, np.ndarray)) else [r] for r in inputs]
+    L_ = max((len(r) for r in rows), default=0)
+    flat = [v for r in rows for v in r]
+    bo = np.zeros(len(rows) + 1, np.int32)
+    np.cumsum([len(r) for r in rows], out=bo[1:])
+    np_dt = np.int64 if dtype == torch.int64 else np.float32
+    vals = torch.from_numpy(np.asarray(flat if flat else [0], np_dt)).to(device)
+    return vals, torch.from_numpy(bo).to(device), 1, L_
+
+
 class LookupEmbedding(torch.nn.Module):
-    """StringLookup / IntegerLookup + EmbeddingBag (preprocess_layers.py:135-169).
+    """StringLookup / IntegerLookup + EmbeddingBag (preprocess_layers.py:135-169), index producer on the GPU
+    (rf_lookup_ids over a vocabulary hash table).
 
     Index rule of Keras StringLookup/IntegerLookup (num_oov_indices=1, mask_token=None): vocab[i] -> i+1,
-    anything else (including the padding default "" / 0) -> 0. Deviation D-lookup: the reference calls a
-    missing update_lookup_layer (:158) and compares a TF dtype with a type name (:148); its table has
-    len(vocabs) rows for len(vocabs)+1 ids — the build sizes it max(vocab_size, len(vocabs)+1).
+    anything else (including the padding default "" / 0) -> 0. A repeated vocabulary term raises ValueError,
+    as Keras does. Deviation D-lookup: the reference calls a missing update_lookup_layer (:158) and compares a
+    TF dtype with a type name (:148); its table has len(vocabs) rows for len(vocabs)+1 ids — the build sizes it
+    max(vocab_size, len(vocabs)+1).
+
+    forward(inputs, slot=0): inputs = a SparseBatch (string features; `slot` picks the feature of a
+    multi-slot group), a RaggedColumns (int features from the TFRecord pipe), or padded dense host rows.
     """
 
     def __init__(self, embedding_dim: int, dtype: str, vocabs: List[Any], vocab_size: Optional[int] = None,
@@ -221,26 +254,61 @@ class LookupEmbedding(torch.nn.Module):
         super().__init__()
         if dtype not in (TYPE_STR, TYPE_INT):
             raise ValueError(f"Unsupported type for lookup feature: {dtype}")
+        L.load()
+        L.require_gpu()
         self.vocabulary = list(vocabs)
         self.pooling = pooling
         self.dtype_name = dtype
-        conv = str if dtype == TYPE_STR else int
-        self.index = {conv(v): i + 1 for i, v in enumerate(self.vocabulary)}
-        rows = max(int(vocab_size or 0), len(self.vocabulary) + 1)
+        self.device = torch.device(device)
+        self.kind = 0 if dtype == TYPE_STR else 1  # RF_VOCAB_BYTES / RF_VOCAB_INT64
+        n = len(self.vocabulary)
+        cap = int(L.load().rf_vocab_capacity(n))
+        tab = np.zeros(cap, VOCAB_DTYPE)
+        if self.kind == 0:
+            terms = [v if isinstance(v, bytes) else str(v).encode() for v in self.vocabulary]
+            vb = np.frombuffer(b"".join(terms), np.uint8).copy() if terms else np.zeros(0, np.uint8)
+            voff = np.zeros(n + 1, np.int32)
+            np.cumsum([len(t) for t in terms], out=voff[1:])
+            vbuf = vb if vb.size else np.zeros(1, np.uint8)
+            L.call("rf_vocab_build", 0, vbuf.ctypes.data, voff.ctypes.data, n, tab.ctypes.data, cap)
+            self.vocab_bytes = torch.from_numpy(vbuf).to(self.device)
+            self.vocab_off = torch.from_numpy(voff).to(self.device)
+        else:
+            iv = np.asarray([int(v) for v in self.vocabulary] or [0], np.int64)
+            L.call("rf_vocab_build", 1, iv.ctypes.data, None, n, tab.ctypes.data, cap)
+            self.vocab_bytes = self.vocab_off = None
+        self.cap = cap
+        self.vocab_table = torch.from_numpy(tab.view(np.uint8).copy()).to(self.device)
+        rows = max(int(vocab_size or 0), n + 1)
         self.embedding = EmbeddingBag(rows, embedding_dim, True, combiner=pooling, name=(name or "lookup") + "_embedding",
                                       dtype=table_dtype, device=device)
 
-    def lookup(self, rows) -> np.ndarray:
-        conv = (lambda v: v.decode() if isinstance(v, bytes) else str(v)) if self.dtype_name == TYPE_STR else int
-        width = max((len(r) for r in rows), default=0)
-        ids = np.zeros((len(rows), width), np.int64)
-        for b, r in enumerate(rows):
-            for j, v in enumerate(r):
-                ids[b, j] = self.index.get(conv(v), 0)
+    def lookup_ids(self, inputs, slot: int = 0) -> torch.Tensor:
+        """Padded [B, Lmax] int64 ids (the StringLookup/IntegerLookup output)."""
+        st = L.stream_ptr()
+        if self.kind == 0:
+            sb = inputs if isinstance(inputs, SparseBatch) else from_dense([inputs])
+            lmax = int(sb.lmax_numpy()[slot])
+            if not sb.is_device():
+                sb = sb.to(self.device)
+            ids = torch.empty((sb.batch, lmax), dtype=torch.int64, device=self.device)
+            L.call("rf_lookup_ids", 0, L.ptr(self.vocab_table), self.cap, L.ptr(self.vocab_bytes), L.ptr(self.vocab_off),
+                   L.ptr(sb.tok_bytes), L.ptr(sb.tok_off), L.ptr(sb.bag_off), sb.n_slots, slot, sb.batch, lmax,
+                   L.ptr(ids), st)
+            return ids
+        vals, bo, S, lmax = _ragged_slot(inputs, slot, torch.int64, self.device)
+        B = (bo.numel() - 1) // S
+        ids = torch.empty((B, lmax), dtype=torch.int64, device=self.device)
+        L.call("rf_lookup_ids", 1, L.ptr(self.vocab_table), self.cap, None, None, L.ptr(vals), None, L.ptr(bo), S, slot, B,
+               lmax, L.ptr(ids), st)
         return ids
 
-    def forward(self, inputs):
-        ids = inputs if isinstance(inputs, torch.Tensor) else torch.from_numpy(self.lookup(inputs))
+    def lookup(self, rows) -> np.ndarray:
+        """Host convenience: padded ids of host rows."""
+        return self.lookup_ids(rows).cpu().numpy()
+
+    def forward(self, inputs, slot: int = 0):
+        ids = inputs if isinstance(inputs, torch.Tensor) else self.lookup_ids(inputs, slot)
         return self.embedding(ids)
 
     def get_vocabulary(self):
@@ -248,23 +316,32 @@ class LookupEmbedding(torch.nn.Module):
 
 
 class DiscreteEmbedding(torch.nn.Module):
-    """Discretization(bin_boundaries) + EmbeddingBag (preprocess_layers.py:172-200).
-    bin = number of boundaries <= x (Keras Discretization / np.digitize right=False)."""
+    """Discretization(bin_boundaries) + EmbeddingBag (preprocess_layers.py:172-200), index producer on the GPU
+    (rf_bucketize_ids): bin = number of boundaries <= x (tf Bucketize); padding = the float default 0.0."""
 
     def __init__(self, embedding_dim: int, vocabs: List[float], vocab_size: Optional[int] = None,
                  pooling: str = "sum", name: Optional[str] = None, device="cuda", table_dtype=torch.float32):
         super().__init__()
+        L.load()
+        L.require_gpu()
         self.vocabulary = [float(v) for v in vocabs]
         self.pooling = pooling
+        self.device = torch.device(device)
         rows = max(int(vocab_size or 0), len(self.vocabulary) + 1)
-        self.register_buffer("boundaries", torch.tensor(self.vocabulary, dtype=torch.float32, device=device), persistent=False)
+        self.boundaries = torch.tensor(self.vocabulary or [0.0], dtype=torch.float32, device=self.device)
         self.embedding = EmbeddingBag(rows, embedding_dim, True, combiner=pooling,
                                       name=(name or "discrete") + "_disc_lookup_embedding", dtype=table_dtype, device=device)
 
-    def forward(self, inputs):
-        x = inputs if isinstance(inputs, torch.Tensor) else torch.tensor(np.asarray(inputs, np.float32))
-        x = x.to(self.boundaries.device, torch.float32)
-        ids = torch.bucketize(x, self.boundaries, right=True)
+    def bucket_ids(self, inputs, slot: int = 0) -> torch.Tensor:
+        vals, bo, S, lmax = _ragged_slot(inputs, slot, torch.float32, self.device)
+        B = (bo.numel() - 1) // S
+        ids = torch.empty((B, lmax), dtype=torch.int64, device=self.device)
+        L.call("rf_bucketize_ids", L.ptr(vals), L.ptr(bo), S, slot, B, lmax, L.ptr(self.boundaries), len(self.vocabulary),
+               0.0, L.ptr(ids), L.stream_ptr())
+        return ids
+
+    def forward(self, inputs, slot: int = 0):
+        ids = inputs if (isinstance(inputs, torch.Tensor) and inputs.dtype == torch.int64) else self.bucket_ids(inputs, slot)
         return self.embedding(ids)
 
     def get_vocabulary(self):

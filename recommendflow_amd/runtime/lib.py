@@ -50,6 +50,10 @@ _SIGS = {
     "rf_loss_ws_bytes": (ctypes.c_size_t, [_i32]),
     "rf_cosent_loss": (ctypes.c_int, [_vp, _vp, _i32, _f32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_inbatch_ce_loss": (ctypes.c_int, [_vp, _i64, _vp, _i32, _f32, _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "rf_vocab_capacity": (_i64, [_i64]),
+    "rf_vocab_build": (ctypes.c_int, [_i32, _vp, _vp, _i64, _vp, _i64]),
+    "rf_lookup_ids": (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "rf_bucketize_ids": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _i32, _f32, _vp, _vp]),
 }
 EXPORTED = tuple(_SIGS)
 
