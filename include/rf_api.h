@@ -333,6 +333,19 @@ int rf_bucketize_ids(const float* values, const int32_t* bag_off, int32_t n_slot
                      int32_t lmax, const float* boundaries, int32_t n_boundaries, float pad_value, int64_t* ids,
                      void* stream);
 
+/* ---- recall search: exact top-k (rf_topk.hip) ------------------------------------ */
+/*
+ * FaissSearcher Flat search (faiss_searcher.py:141-204) in blocks of items: for each of `rows` queries,
+ * the best k of { scores[row][0 .. cols) with item index col_base + c } U { prev_val/prev_idx[row][0 .. k_prev) }
+ * -> out_val/out_idx[row][0 .. k), sorted by score descending, ties by smaller item index; NaN scores
+ * never selected; missing entries are (-inf, -1). Chain calls over item blocks (scores of a block =
+ * rf_linear_fwd(queries, items_block)) with out as the next call's prev (double-buffered).
+ * cols <= 32768, 1 <= k <= 1024, k_prev <= 1024, item indices < 2^32. out must not alias prev.
+ */
+int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int32_t cols, int32_t k, int64_t col_base,
+                  const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld, float* out_val,
+                  int64_t* out_idx, int64_t out_ld, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -425,3 +425,18 @@ def bucketize_ids(boundaries, rows, pad=0.0):
     width = max((len(r) for r in rows), default=0)
     return np.array([[bisect.bisect_right(b, float(np.float32(v))) for v in list(r) + [pad] * (width - len(r))]
                      for r in rows], np.int64).reshape(len(rows), width)
+
+
+# ----------------------------------------------------------------------------------------------
+# exact top-k search (faiss IndexFlatIP semantics), float64
+# ----------------------------------------------------------------------------------------------
+def flat_search(queries, items, k, cos=False):
+    """(scores float64 [B, k], indexes int64 [B, k]): inner products, descending, ties by smaller index."""
+    q = np.asarray(queries, np.float64)
+    x = np.asarray(items, np.float64)
+    if cos:
+        q = q / np.sqrt((q * q).sum(1, keepdims=True))
+        x = x / np.sqrt((x * x).sum(1, keepdims=True))
+    s = q @ x.T
+    idx = np.argsort(-s, axis=1, kind="stable")[:, :k]
+    return np.take_along_axis(s, idx, 1), idx

@@ -1,0 +1,107 @@
+"""FaissSearcher on the GPU: exact (Flat) inner-product / cosine search (reference:
+backend/third_party_components/faiss_searcher.py:23-225, which wraps faiss.index_factory).
+
+Only the exact index is rebuilt (index_param "Flat", measurement "ip" | "cos"): the item matrix stays
+resident in HBM (fp32, l2-normalised for "cos" like __normvec__ :104-105), each query batch is scored
+block by block with the MFMA GEMM (rf_linear_fwd: queries . items_block^T, 32768 items per block) and
+the running top-k is merged after every block (rf_topk_merge: radix select + bitonic merge, ties by
+smaller item index). Approximate faiss indexes (IVF / HNSW / PQ) are out of scope.
+
+search() returns what the reference returns without an encoder: (item_list[indexes], directories) for
+an int topK, {k: (items, sims)} for a list of topK (:178-204).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from ...runtime import lib as L
+
+BLOCK = 32768
+
+
+class FaissSearcher:
+    def __init__(self, encoder=None, items=None, item_list: Optional[Sequence] = None, index_param: str = None,
+                 measurement: Union[str, int] = None, norm_vec: bool = False, use_gpu: bool = True,
+                 dtype=torch.float32, device="cuda", **kwargs):
+        if encoder is not None:
+            raise NotImplementedError("FaissSearcher(encoder=...) (text encoders) is outside the hot path; pass vectors")
+        if items is None or index_param is None or measurement is None:
+            raise AssertionError("Args 'items' 'index_param' 'measurement' must be given.")
+        items = items.detach().cpu().numpy() if isinstance(items, torch.Tensor) else items
+        if not isinstance(items, np.ndarray):
+            raise ReferenceError("如果不传入encoder，则item只能输入numpy.array类型")
+        if len(items.shape) != 2:
+            raise AssertionError(f"encoder=None, 输入只能是二维矩阵[(n, dim)]，当前维度为[{items.shape}]")
+        if item_list is not None:
+            assert len(item_list) == len(items), f"len(item_list)={len(item_list)} != len(items)={len(items)}"
+        if str(index_param).lower() != "flat":
+            raise NotImplementedError(f"index_param {index_param!r}: only the exact 'Flat' index is implemented")
+        if measurement not in ("ip", "cos"):
+            raise NotImplementedError(f"measurement {measurement!r}: only 'ip' and 'cos' are implemented")
+        L.load()
+        L.require_gpu()
+        self.index_param, self.measurement = index_param, measurement
+        self.norm_vec = True if measurement == "cos" else norm_vec
+        self.items = items
+        self.item_list = np.array(item_list if item_list is not None else np.arange(len(items)))
+        self.vec_dim = items.shape[1]
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.index = None
+
+    def get_vecs(self, items) -> torch.Tensor:
+        x = items if isinstance(items, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(items))
+        x = x.to(self.device, torch.float32)
+        if self.norm_vec:
+            x = x / (x * x).sum(dim=1, keepdim=True).sqrt()
+        return x.to(self.dtype).contiguous()
+
+    def train(self):
+        self.index = self.get_vecs(self.items)  # [N, E] resident in HBM
+        return self
+
+    def search_index(self, target, k: int):
+        """(directories [B, k] fp32, indexes [B, k] int64) on the device — faiss index.search."""
+        if self.index is None:
+            raise Exception("Faiss dose not train, please use train method before search or load a trained index...")
+        if not 1 <= k <= 1024:
+            raise ValueError("topK must be in [1, 1024]")
+        q = self.get_vecs(target)
+        B, E = q.shape
+        N = self.index.shape[0]
+        dev = self.device
+        vals = [torch.empty((B, k), dtype=torch.float32, device=dev) for _ in range(2)]
+        idxs = [torch.empty((B, k), dtype=torch.int64, device=dev) for _ in range(2)]
+        scores = torch.empty((B, min(BLOCK, max(N, 1))), dtype=torch.float32, device=dev)
+        st = L.stream_ptr()
+        dt = L.torch_dtype_code(self.dtype)
+        cur, k_prev = 0, 0
+        for c0 in range(0, N, BLOCK):
+            n = min(BLOCK, N - c0)
+            blk = self.index[c0:c0 + n]
+            L.call("rf_linear_fwd", L.ptr(q), dt, B, E, q.stride(0), L.ptr(blk), n, None, 0, L.ptr(scores), scores.stride(0), st)
+            nxt = 1 - cur
+            L.call("rf_topk_merge", L.ptr(scores), scores.stride(0), B, n, k, c0, L.ptr(vals[cur]), L.ptr(idxs[cur]), k_prev,
+                   k, L.ptr(vals[nxt]), L.ptr(idxs[nxt]), k, st)
+            cur, k_prev = nxt, k
+        if k_prev == 0:
+            vals[cur].fill_(-float("inf"))
+            idxs[cur].fill_(-1)
+        return vals[cur], idxs[cur]
+
+    def search(self, target, topK: Union[int, List[int]], keep_rank_no=False):
+        if isinstance(topK, int):
+            d, i = self.search_index(target, topK)
+            i = i.cpu().numpy()
+            return (self.item_list[i], d.cpu().numpy(), i) if keep_rank_no else (self.item_list[i], d.cpu().numpy())
+        if isinstance(topK, list):
+            d, i = self.search_index(target, max(topK))
+            d, i = d.cpu().numpy(), i.cpu().numpy()
+            res = {}
+            for k in topK:
+                res[k] = (self.item_list[i[:, :k]], d[:, :k], i[:, :k]) if keep_rank_no else (self.item_list[i[:, :k]], d[:, :k])
+            return res
+        raise TypeError(f"TopK dose not support type: {type(topK)}")

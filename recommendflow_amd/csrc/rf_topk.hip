@@ -1,0 +1,201 @@
+// rf_topk.hip — exact top-k over a block of scores, merged with a running top-k (the
+// FaissSearcher Flat inner-product search, backend/third_party_components/faiss_searcher.py:141-204, and
+// the recall evaluation on top of it, backend/utils/eval_utils.py:85-147).
+//
+// One 1024-thread workgroup per query row. Every candidate becomes a unique 64-bit key
+//   (orderable(score) << 32) | ~index
+// so "larger key" = higher score, then smaller index (a deterministic tie order). The row's keys stay in
+// registers (IPT per thread, columns t + 1024 j: coalesced loads); a radix select (8 bits a pass, per-wave
+// LDS histograms, early exit once the boundary bin holds exactly the missing count) finds the k-th
+// largest key, the selected keys and the previous top-k are written to LDS and bitonic-sorted, and the
+// best k are the new running top-k. NaN scores are never selected.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "rf_common.h"
+
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kWavesTopk = kThreads / 64;
+constexpr int kMaxK = 1024;
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <int IPT>
+__global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict__ scores, int64_t ld, int cols, int k,
+                                                        int64_t col_base, const float* __restrict__ prev_val,
+                                                        const int64_t* __restrict__ prev_idx, int k_prev, int64_t prev_ld,
+                                                        float* __restrict__ out_val, int64_t* __restrict__ out_idx,
+                                                        int64_t out_ld) {
+    __shared__ uint32_t hist[kWavesTopk][256];
+    __shared__ uint32_t tot[256];
+    __shared__ uint64_t cand[2 * kMaxK];
+    __shared__ uint64_t s_prefix, s_mask;
+    __shared__ int s_need, s_bin_cnt, s_cnt, s_valid;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const int64_t row = blockIdx.x;
+    const float* srow = scores + row * ld;
+
+    uint64_t key[IPT];
+    int nvalid = 0;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const int c = t + kThreads * j;
+        const float s = c < cols ? srow[c] : __builtin_nanf("");
+        const bool ok = !isnan(s);
+        key[j] = ok ? ((uint64_t)f2key(s) << 32) | (uint64_t)(~(uint32_t)(col_base + c)) : 0ull;
+        nvalid += ok;
+    }
+    // valid count (block reduction)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nvalid += __shfl_xor(nvalid, o, 64);
+    if (t == 0) s_valid = 0;
+    __syncthreads();
+    if (lane == 0) atomicAdd(&s_valid, nvalid);
+    if (t == 0) {
+        s_prefix = 0;
+        s_mask = 0;
+        s_cnt = 0;
+    }
+    __syncthreads();
+    const int total = s_valid;
+    const int kk = min(k, total);
+    if (t == 0) s_need = kk;
+    __syncthreads();
+    if (kk > 0 && kk < total) {
+#pragma unroll 1
+        for (int pass = 0; pass < 8; ++pass) {
+            const int shift = 56 - 8 * pass;
+            for (int i = t; i < kWavesTopk * 256; i += kThreads) (&hist[0][0])[i] = 0;
+            __syncthreads();
+            const uint64_t prefix = s_prefix, mask = s_mask;
+#pragma unroll
+            for (int j = 0; j < IPT; ++j)
+                if (key[j] != 0ull && (key[j] & mask) == prefix) atomicAdd(&hist[wave][(key[j] >> shift) & 255], 1u);
+            __syncthreads();
+            if (t < 256) {
+                uint32_t s = 0;
+                for (int w = 0; w < kWavesTopk; ++w) s += hist[w][t];
+                tot[t] = s;
+            }
+            __syncthreads();
+            if (wave == 0) {
+                // lane owns bins 4*(63-lane) .. +3 (lane 0 the top bins): suffix counts from the top
+                uint32_t c[4], loc = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    c[q] = tot[4 * (63 - lane) + (3 - q)];  // descending bin order inside the lane
+                    loc += c[q];
+                }
+                uint32_t incl = loc;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += y;
+                }
+                const uint32_t above = incl - loc;  // keys in bins above this lane's bins
+                const int need = s_need;
+                uint32_t run = above;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (run < (uint32_t)need && run + c[q] >= (uint32_t)need) {
+                        const int bin = 4 * (63 - lane) + (3 - q);
+                        s_prefix = prefix | ((uint64_t)bin << shift);
+                        s_mask = mask | ((uint64_t)0xff << shift);
+                        s_need = need - (int)run;
+                        s_bin_cnt = (int)c[q];
+                    }
+                    run += c[q];
+                }
+            }
+            __syncthreads();
+            if (s_need == s_bin_cnt) break;  // every key of the boundary bin is selected
+            __syncthreads();
+        }
+    }
+    // select: keys whose masked bits are >= the boundary prefix (exactly kk of them)
+    const uint64_t prefix = s_prefix, mask = s_mask;
+    const bool all = kk >= total;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        if (key[j] != 0ull && (all || (key[j] & mask) >= prefix)) cand[atomicAdd(&s_cnt, 1)] = key[j];
+    }
+    __syncthreads();
+    const int nsel = s_cnt;
+    // previous running top-k (entries with index -1 are empty)
+    for (int i = t; i < k_prev; i += kThreads) {
+        const int64_t pidx = prev_idx[row * prev_ld + i];
+        const float pv = prev_val[row * prev_ld + i];
+        const bool ok = pidx >= 0 && !isnan(pv);
+        cand[nsel + i] = ok ? ((uint64_t)f2key(pv) << 32) | (uint64_t)(~(uint32_t)pidx) : 0ull;
+    }
+    int m = nsel + k_prev;
+    int p2 = 1;
+    while (p2 < m) p2 <<= 1;
+    for (int i = m + t; i < p2; i += kThreads) cand[i] = 0ull;
+    __syncthreads();
+    // bitonic sort, descending
+#pragma unroll 1
+    for (int size = 2; size <= p2; size <<= 1) {
+#pragma unroll 1
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = t; i < p2 / 2; i += kThreads) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const uint64_t a = cand[lo], b = cand[hi];
+                if ((a < b) == desc) {
+                    cand[lo] = b;
+                    cand[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = t; i < k; i += kThreads) {
+        const uint64_t kv = i < m ? cand[i] : 0ull;
+        float v = -INFINITY;
+        int64_t idx = -1;
+        if (kv != 0ull) {
+            v = key2f((uint32_t)(kv >> 32));
+            idx = (int64_t)(~(uint32_t)kv);
+        }
+        out_val[row * out_ld + i] = v;
+        out_idx[row * out_ld + i] = idx;
+    }
+}
+
+}  // namespace
+
+extern "C" int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int32_t cols, int32_t k, int64_t col_base,
+                             const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld,
+                             float* out_val, int64_t* out_idx, int64_t out_ld, void* stream) {
+    RF_REQUIRE(rows >= 0 && cols >= 0 && cols <= 32 * kThreads, "rf_topk_merge: cols must be in [0, 32768]");
+    RF_REQUIRE(k >= 1 && k <= kMaxK && k_prev >= 0 && k_prev <= kMaxK, "rf_topk_merge: k and k_prev must be in [1, 1024]");
+    RF_REQUIRE(ld >= cols && out_ld >= k && (k_prev == 0 || prev_ld >= k_prev), "rf_topk_merge: bad leading dimension");
+    RF_REQUIRE(col_base >= 0 && col_base + cols <= ((int64_t)1 << 32) - 1, "rf_topk_merge: item index must fit 32 bits");
+    if (rows == 0) return RF_OK;
+    RF_REQUIRE((cols == 0 || scores) && out_val && out_idx && (k_prev == 0 || (prev_val && prev_idx)),
+               "rf_topk_merge: null pointer");
+    const int ipt = std::max(1, (cols + kThreads - 1) / kThreads);
+    hipStream_t st = rf_stream(stream);
+#define RF_TOPK(N)                                                                                                  \
+    hipLaunchKernelGGL(topk_kernel<N>, dim3(rows), dim3(kThreads), 0, st, scores, ld, cols, k, col_base, prev_val, \
+                       prev_idx, k_prev, prev_ld, out_val, out_idx, out_ld)
+    if (ipt <= 1) RF_TOPK(1);
+    else if (ipt <= 2) RF_TOPK(2);
+    else if (ipt <= 4) RF_TOPK(4);
+    else if (ipt <= 8) RF_TOPK(8);
+    else if (ipt <= 16) RF_TOPK(16);
+    else RF_TOPK(32);
+#undef RF_TOPK
+    return rf_check_launch("rf_topk_merge");
+}

@@ -1,0 +1,112 @@
+"""Recall search: rf_topk_merge exact selection, FaissSearcher Flat ip/cos vs the float64
+oracle, recall metrics (eval_utils.py:85-147)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from recommendflow_amd.backend.utils.eval_utils import MISS, get_click_index
+
+
+def test_click_index_intended_semantics():
+    rec = np.array([[5, 7, 9], [1, 2, 3], [4, 4, 8], [2, 1, 0]])
+    lab = np.array([5, 3, 8, 1])
+    assert get_click_index(rec, lab).tolist() == [0, 2, 2, 1]
+    assert get_click_index(rec, np.array([6, 6, 6, 6])).tolist() == [MISS] * 4
+
+
+def test_recall_metrics_formula():
+    from recommendflow_amd.backend.utils import eval_utils as E
+
+    class Fake:
+        def search(self, t, k):
+            return (np.array([[1, 2, 3]] * len(t))[:, :k], None)
+
+    hit, mrr, ndcg = E.batch_compute_recall_score(Fake(), np.zeros((4, 2)), np.array([1, 2, 3, 9]), [1, 3], np.ones(4), 2)
+    assert np.allclose(hit, [0.25, 0.75])
+    assert np.isclose(mrr[0], (1 + 1 / 2 + 1 / 3 + 1 / (MISS + 1)) / 4)
+    # click ids [0, 1, 2, MISS]; the reference's simplified idcg = 1 / log2(3) for every hit
+    assert np.isclose(ndcg[1], (np.log2(3) + 1 + 0.5 * np.log2(3)) / 4, rtol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cols,k", [(1, 1), (100, 10), (5000, 100), (32768, 1024), (700, 1024)])
+def test_topk_merge_exact(cuda, cols, k):
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    rng = np.random.default_rng(cols + k)
+    B = 37
+    s = (rng.integers(-50, 50, (B, cols)) * 0.25).astype(np.float32)  # many exact ties
+    s[3, : min(cols, 5)] = np.nan
+    prev_v = np.sort((rng.integers(-50, 50, (B, k)) * 0.25).astype(np.float32), axis=1)[:, ::-1].copy()
+    prev_i = rng.permutation(10 ** 6)[: B * k].reshape(B, k).astype(np.int64) + 10 ** 7
+    prev_i[5, k // 2:] = -1
+    base = 123456
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ov = torch.empty((B, k), device="cuda")
+    oi = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    ds, pv, pi = dev(s), dev(prev_v), dev(prev_i)
+    L.call("rf_topk_merge", L.ptr(ds), cols, B, cols, k, base, L.ptr(pv), L.ptr(pi), k, k, L.ptr(ov), L.ptr(oi), k, L.stream_ptr())
+    gv, gi = ov.cpu().numpy(), oi.cpu().numpy()
+    for b in range(B):
+        cand = [(float(s[b, c]), base + c) for c in range(cols) if not np.isnan(s[b, c])]
+        cand += [(float(prev_v[b, j]), int(prev_i[b, j])) for j in range(k) if prev_i[b, j] >= 0]
+        cand.sort(key=lambda x: (-x[0], x[1]))
+        want = cand[:k] + [(-np.inf, -1)] * (k - len(cand[:k]))
+        assert gi[b].tolist() == [w[1] for w in want], b
+        assert gv[b].tolist() == [w[0] for w in want], b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("measurement", ["ip", "cos"])
+def test_flat_searcher_vs_oracle(cuda, measurement):
+    from recommendflow_amd.backend.third_party_components.faiss_searcher import FaissSearcher
+
+    rng = np.random.default_rng(7)
+    N, E, B, k = 70000, 64, 300, 50  # 3 item blocks
+    items = rng.normal(size=(N, E)).astype(np.float32)
+    q = rng.normal(size=(B, E)).astype(np.float32)
+    names = np.array([f"item{i}" for i in range(N)])
+    s = FaissSearcher(items=items, item_list=names, index_param="Flat", measurement=measurement).train()
+    got_items, got_d = s.search(q, k)
+    want_d, want_i = O.flat_search(q, items, k, cos=measurement == "cos")
+    np.testing.assert_allclose(got_d, want_d, rtol=1e-4, atol=1e-4)
+    # identical lists except where two oracle scores are closer than the fp32 GEMM error
+    tol = 1e-4 * np.abs(want_d).max()
+    for b in range(B):
+        g = [int(x[4:]) for x in got_items[b]]
+        if g != want_i[b].tolist():
+            gaps = np.diff(want_d[b])
+            assert np.abs(gaps).min() < tol or abs(want_d[b, -1] - O.flat_search(q[b:b + 1], items, k + 1)[0][0, -1]) < tol, b
+    res = s.search(q, [5, 20], keep_rank_no=True)
+    assert res[5][0].shape == (B, 5) and res[20][2].shape == (B, 20)
+
+
+@pytest.mark.gpu
+def test_searcher_fewer_items_than_k(cuda):
+    from recommendflow_amd.backend.third_party_components.faiss_searcher import FaissSearcher
+
+    items = np.eye(4, 8, dtype=np.float32)
+    s = FaissSearcher(items=items, index_param="Flat", measurement="ip").train()
+    d, i = s.search_index(np.ones((2, 8), np.float32), 6)
+    assert i.cpu().tolist() == [[0, 1, 2, 3, -1, -1]] * 2
+    assert d[0, 4].item() == -np.inf
+
+
+@pytest.mark.gpu
+def test_recall_score_on_gpu_searcher(cuda):
+    from recommendflow_amd.backend.third_party_components.faiss_searcher import FaissSearcher
+    from recommendflow_amd.backend.utils.eval_utils import batch_compute_recall_score
+
+    rng = np.random.default_rng(3)
+    items = rng.normal(size=(5000, 32)).astype(np.float32)
+    labels = rng.integers(0, 5000, 400)
+    q = items[labels] + 0.5 * rng.normal(size=(400, 32)).astype(np.float32)
+    s = FaissSearcher(items=items, index_param="Flat", measurement="cos").train()
+    hit, mrr, ndcg = batch_compute_recall_score(s, q, labels, [1, 10, 50], np.ones(400), 128)
+    _, idx = O.flat_search(q, items, 50, cos=True)
+    ci = get_click_index(idx, labels)
+    for j, kk in enumerate([1, 10, 50]):
+        assert abs(hit[j] - (ci < kk).mean()) <= 2 / 400
+    assert 0 < hit[0] <= hit[1] <= hit[2] <= 1
