@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--shard-dim", type=int, default=128)
     p.add_argument("--shard-batch", type=int, default=8192, help="cfg4: examples per GPU (65536 at P=8)")
     p.add_argument("--no-train", action="store_true", help="skip the cfg2 DSSM training-step extra")
+    p.add_argument("--no-cascade", action="store_true", help="skip the cfg5 recall->prerank->rank extra")
+    p.add_argument("--catalog", type=int, default=1_000_000, help="cfg5: items in the catalog")
     p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
     p.add_argument("--pipe-examples", type=int, default=16384, help="feature pipe: examples written and read back")
     p.add_argument("--pipe-threads", type=int, default=16, help="feature pipe: reader threads (the box's CPU share)")
@@ -139,6 +141,8 @@ def main():
             del dev, out
         torch.cuda.empty_cache()
         extras = {"cfg3_esim_forward": bench_esim(args), "cfg2_dssm_forward": bench_dssm(args, enc, host)}
+    if world == 1 and not args.no_cascade:
+        extras = dict(extras or {}, cfg5_cascade=bench_cascade(args, enc))
     if world == 1 and not args.no_train:
         extras = dict(extras or {}, cfg2_dssm_train_step=bench_train(args, specs, multi))
     if world == 1 and not args.no_pipe:
@@ -381,6 +385,67 @@ def bench_sharded(args, specs, multi, rank, world):
     del enc, batches, out
     torch.cuda.empty_cache()
     return res
+
+
+def bench_cascade(args, enc):
+    """cfg5 on one GPU: recall (cfg2 towers: 69 user + 160 ad slots over the 10M x 64
+    fp32 table, [1024, 512, 256]) over a catalog of `--catalog` items (Flat inner-product top-200,
+    MFMA score blocks + rf_topk_merge) -> prerank (light interaction MLP, top-50) -> rank (cfg3 ESIM,
+    100 + 100 slots x 1M bins, bf16 tables, fp16 MFMA attention) -> top-10, for 1024 users per step."""
+    import numpy as np
+    import torch
+
+    from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
+    from recommendflow_amd.config_parser.configuration import Configuration
+    from recommendflow_amd.models.cascade import Cascade
+    from recommendflow_amd.models.matching.dssm import Dssm
+    from recommendflow_amd.models.ranking.esim import Esim
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "base_recall_sdpa.yaml"))
+    feats = conf.features.hashing_features
+    users = [i for i, f in enumerate(feats) if f.tower.value == "user"]
+    ads = [i for i, f in enumerate(feats) if f.tower.value == "ad"]
+    mv = [bool(f.multivalued) for f in feats]
+    eu = FusedSparseEncoder([enc.slots[i] for i in users], enc.dim, table=enc.table, row_base0=0)
+    ea = FusedSparseEncoder([enc.slots[i] for i in ads], enc.dim, table=enc.table,
+                            row_base0=int(enc.host_desc[ads[0]]["row_base"][0]))
+    dssm = Dssm(eu, ea, seed=5)
+    Ls = 100
+    esim = Esim([SlotSpec(f"u{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)],
+                [SlotSpec(f"a{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)], n_dense=16, dim=64,
+                table_dtype=torch.bfloat16, seed=3)
+    cas = Cascade(dssm, esim, k_recall=200, k_prerank=50, k_final=10, seed=9)
+    N, CB = args.catalog, 8192
+    t0 = time.perf_counter()
+    rb = [synthetic_batch(CB, [mv[i] for i in ads], seed=600 + j, slot_ids=ads).to("cuda") for j in range(2)]
+    kb = [synthetic_batch(CB, [False] * Ls, seed=700 + j, slot_ids=range(Ls, 2 * Ls)).to("cuda") for j in range(2)]
+    nb = (N + CB - 1) // CB
+    cas.index_catalog([rb[j % 2] for j in range(nb)], [kb[j % 2] for j in range(nb)])
+    cas.searcher.index = cas.searcher.index[:N].contiguous()
+    cas.a_item = cas.a_item[:N].contiguous()
+    torch.cuda.synchronize()
+    index_s = time.perf_counter() - t0
+    B = 1024
+    ur = [synthetic_batch(B, [mv[i] for i in users], seed=800 + j, slot_ids=users).to("cuda") for j in range(2)]
+    uk = [synthetic_batch(B, [False] * Ls, seed=900 + j, slot_ids=range(Ls)).to("cuda") for j in range(2)]
+    dense = torch.randn(B, 16, device="cuda")
+    for j in range(2):
+        cas(ur[j % 2], uk[j % 2], dense)
+    steps = max(3, args.steps // 10)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(steps):
+        res = cas(ur[j % 2], uk[j % 2], dense)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    out = {"users_per_s": round(B / ms * 1e3, 1), "ms_per_step": round(ms, 3), "catalog_items": N,
+           "catalog_index_s": round(index_s, 2), "pairs_ranked_per_s": round(B * 50 / ms * 1e3, 1),
+           "config": f"1024 users/step; recall: cfg2 towers, Flat IP top-200 over {N} items (fp32 MFMA + rf_topk_merge); "
+                     "prerank: u*v -> Dense(64, relu) -> Dense(1), top-50; rank: cfg3 ESIM (fp16 attention) top-10"}
+    del cas, esim, dssm, rb, kb, ur, uk
+    torch.cuda.empty_cache()
+    return out
 
 
 def bench_train(args, specs, multi):

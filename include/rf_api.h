@@ -346,6 +346,15 @@ int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int32_t cols, i
                   const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld, float* out_val,
                   int64_t* out_idx, int64_t out_ld, void* stream);
 
+/*
+ * Que2Search AttentionFusion forward (backend/layers/fusion_layers.py:35-46), fp32:
+ * x: [batch][channels * dim] (the K.concatenate of the channel inputs, row stride ldx); W: [channels*dim][channels]
+ * (Keras layout). att = softmax(x @ W); out[b] = sum_c att[b][c] * x_c[b] (l2-normalised if is_norm,
+ * tf.nn.l2_normalize eps 1e-12) -> out [batch][dim] (stride ldo); att_out [batch][channels] optional.
+ */
+int rf_attention_fusion_fwd(const float* x, int32_t batch, int32_t channels, int32_t dim, int64_t ldx, const float* W,
+                            int32_t is_norm, float* out, int64_t ldo, float* att_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

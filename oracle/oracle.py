@@ -440,3 +440,15 @@ def flat_search(queries, items, k, cos=False):
     s = q @ x.T
     idx = np.argsort(-s, axis=1, kind="stable")[:, :k]
     return np.take_along_axis(s, idx, 1), idx
+
+
+def attention_fusion(inputs, W, is_norm=True):
+    """fusion_layers.py:35-46 in float64: (out, att)."""
+    x = np.concatenate([np.asarray(t, np.float64) for t in inputs], axis=1)
+    logits = x @ np.asarray(W, np.float64)
+    e = np.exp(logits - logits.max(axis=1, keepdims=True))
+    att = e / e.sum(axis=1, keepdims=True)
+    out = sum(att[:, c:c + 1] * np.asarray(inputs[c], np.float64) for c in range(len(inputs)))
+    if is_norm:
+        out = out / np.sqrt(np.maximum((out * out).sum(axis=1, keepdims=True), 1e-12))
+    return out, att

@@ -110,3 +110,20 @@ def test_recall_score_on_gpu_searcher(cuda):
     for j, kk in enumerate([1, 10, 50]):
         assert abs(hit[j] - (ci < kk).mean()) <= 2 / 400
     assert 0 < hit[0] <= hit[1] <= hit[2] <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,d,norm", [(1, 8, True), (3, 256, True), (4, 100, False), (16, 64, True)])
+def test_attention_fusion_vs_oracle(cuda, C, d, norm):
+    import torch
+
+    from recommendflow_amd.backend.layers.fusion_layers import AttentionFusion
+
+    rng = np.random.default_rng(C * d)
+    xs = [torch.tensor(rng.normal(size=(333, d)), dtype=torch.float32).cuda() for _ in range(C)]
+    af = AttentionFusion(d, C, is_norm=norm, seed=C)
+    out = af(xs).cpu().numpy()
+    want, att = O.attention_fusion([x.cpu().numpy() for x in xs], af.W.cpu().numpy(), norm)
+    np.testing.assert_allclose(out, want, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(af.attention.cpu().numpy(), att, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(af.get_fusion_weights(), att.sum(0, keepdims=True) / att.sum(), rtol=1e-5)
