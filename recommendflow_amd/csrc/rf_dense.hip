@@ -72,7 +72,8 @@ __global__ __launch_bounds__(256) void norm_kernel(const float* __restrict__ x, 
 // ---------------------------------------------------------------------------------------------
 // GEMM y[M,N] = act(x[M,K] W[N,K]^T + b)
 // ---------------------------------------------------------------------------------------------
-constexpr int BM = 128, BN = 128;
+// block tile BT x BT (128, or 64 when the 128-tile grid would leave CUs idle), 4 waves in 2 x 2, each
+// wave BT/2 x BT/2 = FR x FR fragments of 16 x 16
 
 // bf16: BK = 64 (128-byte rows), LDS rows padded to 72 elements (144 B): conflict-free ds_read_b128
 // for the 16 rows a 16-lane group reads.
@@ -80,22 +81,23 @@ constexpr int BKH = 64, RSH = BKH + 8;
 // f32: BK = 32 (128-byte rows), rows padded to 36 floats (144 B).
 constexpr int BKF = 32, RSF = BKF + 4;
 
-template <bool BF16>
+template <bool BF16, int BT>
 struct GemmCfg {
     static constexpr int BK = BF16 ? BKH : BKF;
     static constexpr int RS = BF16 ? RSH : RSF;          // elements
     static constexpr int ESZ = BF16 ? 2 : 4;
     static constexpr int EPC = 16 / ESZ;                  // elements per 16-byte chunk
     static constexpr int CPR = BK / EPC;                  // chunks per tile row (8)
-    static constexpr int CHUNKS = BM * CPR;               // per operand tile (1024)
-    static constexpr int PER_THREAD = CHUNKS / 256;       // 4
+    static constexpr int CHUNKS = BT * CPR;               // per operand tile (1024 at BT = 128)
+    static constexpr int PER_THREAD = CHUNKS / 256;       // 4 at BT = 128
+    static constexpr int FR = BT / 32;                    // 16x16 fragments per wave and dimension
 };
 
-template <bool BF16>
-__device__ __forceinline__ void load_tile(uint4 (&rg)[2][GemmCfg<BF16>::PER_THREAD], const char* __restrict__ x,
+template <bool BF16, int BT>
+__device__ __forceinline__ void load_tile(uint4 (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], const char* __restrict__ x,
                                           const char* __restrict__ w, int64_t M, int N, int K, int64_t ldx, int64_t m0,
                                           int n0, int k0, int tid) {
-    using C = GemmCfg<BF16>;
+    using C = GemmCfg<BF16, BT>;
 #pragma unroll
     for (int i = 0; i < C::PER_THREAD; ++i) {
         const int c = tid + i * 256;
@@ -109,10 +111,10 @@ __device__ __forceinline__ void load_tile(uint4 (&rg)[2][GemmCfg<BF16>::PER_THRE
     }
 }
 
-template <bool BF16>
+template <bool BF16, int BT>
 __device__ __forceinline__ void store_tile(char* __restrict__ As, char* __restrict__ Bs,
-                                           const uint4 (&rg)[2][GemmCfg<BF16>::PER_THREAD], int tid) {
-    using C = GemmCfg<BF16>;
+                                           const uint4 (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], int tid) {
+    using C = GemmCfg<BF16, BT>;
 #pragma unroll
     for (int i = 0; i < C::PER_THREAD; ++i) {
         const int c = tid + i * 256;
@@ -122,93 +124,94 @@ __device__ __forceinline__ void store_tile(char* __restrict__ As, char* __restri
     }
 }
 
-template <bool BF16>
+template <bool BF16, int BT>
 __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
                                                    const float* __restrict__ bias, float* __restrict__ y, int64_t M,
                                                    int N, int K, int64_t ldx, int64_t ldy, int act) {
-    using C = GemmCfg<BF16>;
-    __shared__ __attribute__((aligned(16))) char smem[2][2][BM * C::RS * C::ESZ];
+    using C = GemmCfg<BF16, BT>;
+    constexpr int FR = C::FR, WT = BT / 2;
+    __shared__ __attribute__((aligned(16))) char smem[2][2][BT * C::RS * C::ESZ];
     const char* x = reinterpret_cast<const char*>(xv);
     const char* w = reinterpret_cast<const char*>(wv);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int wm = wave >> 1, wn = wave & 1;
     // XCD-aware tile order: consecutive tiles of one M row-panel on one XCD (guide T1)
-    const int tiles_n = (N + BN - 1) / BN;
+    const int tiles_n = (N + BT - 1) / BT;
     const int64_t tid_lin = blockIdx.x;
-    const int64_t m0 = (tid_lin / tiles_n) * BM;
-    const int n0 = (int)(tid_lin % tiles_n) * BN;
-    f4 acc[4][4];
+    const int64_t m0 = (tid_lin / tiles_n) * BT;
+    const int n0 = (int)(tid_lin % tiles_n) * BT;
+    f4 acc[FR][FR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FR; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     uint4 rg[2][C::PER_THREAD];
     const int nk = (K + C::BK - 1) / C::BK;
-    load_tile<BF16>(rg, x, w, M, N, K, ldx, m0, n0, 0, tid);
-    store_tile<BF16>(smem[0][0], smem[0][1], rg, tid);
+    load_tile<BF16, BT>(rg, x, w, M, N, K, ldx, m0, n0, 0, tid);
+    store_tile<BF16, BT>(smem[0][0], smem[0][1], rg, tid);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) load_tile<BF16>(rg, x, w, M, N, K, ldx, m0, n0, (kt + 1) * C::BK, tid);
+        if (kt + 1 < nk) load_tile<BF16, BT>(rg, x, w, M, N, K, ldx, m0, n0, (kt + 1) * C::BK, tid);
         const char* As = smem[cur][0];
         const char* Bs = smem[cur][1];
         if constexpr (BF16) {
 #pragma unroll
             for (int ks = 0; ks < C::BK; ks += 32) {
-                bf16x8 af[4], bfr[4];
+                bf16x8 af[FR], bfr[FR];
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    af[i] = *reinterpret_cast<const bf16x8*>(As + ((wm * 64 + i * 16 + lr) * C::RS + ks + lg * 8) * 2);
+                for (int i = 0; i < FR; ++i)
+                    af[i] = *reinterpret_cast<const bf16x8*>(As + ((wm * WT + i * 16 + lr) * C::RS + ks + lg * 8) * 2);
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ((wn * 64 + j * 16 + lr) * C::RS + ks + lg * 8) * 2);
+                for (int j = 0; j < FR; ++j)
+                    bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + ((wn * WT + j * 16 + lr) * C::RS + ks + lg * 8) * 2);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < FR; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < FR; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
         } else {
             // 16x16x4 f32: lane (lr, lg) supplies A[lr][k], B[k][lr] for k = lg*8 + s at step s (the k order is
             // permuted consistently for A and B, so the dot product is over all 32 k of the tile)
-            f4 a0[4], a1[4], b0[4], b1[4];
+            f4 a0[FR], a1[FR], b0[FR], b1[FR];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float* p = reinterpret_cast<const float*>(As) + (wm * 64 + i * 16 + lr) * C::RS + lg * 8;
+            for (int i = 0; i < FR; ++i) {
+                const float* p = reinterpret_cast<const float*>(As) + (wm * WT + i * 16 + lr) * C::RS + lg * 8;
                 a0[i] = *reinterpret_cast<const f4*>(p);
                 a1[i] = *reinterpret_cast<const f4*>(p + 4);
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float* p = reinterpret_cast<const float*>(Bs) + (wn * 64 + j * 16 + lr) * C::RS + lg * 8;
+            for (int j = 0; j < FR; ++j) {
+                const float* p = reinterpret_cast<const float*>(Bs) + (wn * WT + j * 16 + lr) * C::RS + lg * 8;
                 b0[j] = *reinterpret_cast<const f4*>(p);
                 b1[j] = *reinterpret_cast<const f4*>(p + 4);
             }
 #pragma unroll
             for (int s = 0; s < 8; ++s)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < FR; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < FR; ++j) {
                         const float av = s < 4 ? a0[i][s] : a1[i][s - 4];
                         const float bv = s < 4 ? b0[j][s] : b1[j][s - 4];
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
                     }
         }
-        if (kt + 1 < nk) store_tile<BF16>(smem[cur ^ 1][0], smem[cur ^ 1][1], rg, tid);
+        if (kt + 1 < nk) store_tile<BF16, BT>(smem[cur ^ 1][0], smem[cur ^ 1][1], rg, tid);
         __syncthreads();
     }
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + j * 16 + lr;
+    for (int j = 0; j < FR; ++j) {
+        const int col = n0 + wn * WT + j * 16 + lr;
         if (col >= N) continue;
         const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FR; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int64_t row = m0 + wm * 64 + i * 16 + lg * 4 + r;
+                const int64_t row = m0 + wm * WT + i * 16 + lg * 4 + r;
                 if (row < M) y[row * ldy + col] = act_apply(act, acc[i][j][r] + bv);
             }
     }
@@ -297,11 +300,17 @@ extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t 
     }
     RF_REQUIRE(K % epc == 0 && ldx % epc == 0, "rf_linear_fwd: K and ldx must be multiples of %d (16-byte rows)", epc);
     RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0, "rf_linear_fwd: x/W must be 16-byte aligned");
-    const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    // 128-tiles unless that grid would give fewer than 2 workgroups per CU (256 CUs): then 64-tiles
+    // (4x the workgroups; same per-element accumulation order, so identical results)
+    const int64_t tiles128 = ((M + 127) / 128) * ((N + 127) / 128);
+    const bool small = tiles128 < 512;
+    const int bt = small ? 64 : 128;
+    const int64_t tiles = ((M + bt - 1) / bt) * ((N + bt - 1) / bt);
     RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_linear_fwd: too many tiles");
-    if (bf)
-        hipLaunchKernelGGL(gemm_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
-    else
-        hipLaunchKernelGGL(gemm_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+    const dim3 g((unsigned)tiles);
+    if (bf && small) hipLaunchKernelGGL((gemm_kernel<true, 64>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+    else if (bf) hipLaunchKernelGGL((gemm_kernel<true, 128>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+    else if (small) hipLaunchKernelGGL((gemm_kernel<false, 64>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+    else hipLaunchKernelGGL((gemm_kernel<false, 128>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
     return rf_check_launch("gemm_kernel");
 }
