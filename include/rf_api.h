@@ -264,6 +264,28 @@ int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const 
                             int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
 
 /*
+ * Backward of rf_pool_rows_fwd (the requester side of the sharded lookup): the same
+ * per-position gradients and (b, l) summation order as rf_fused_hash_embed_bwd, keyed by the distinct
+ * gathered row each logical row maps to (row_map, as in the forward; n_rows = number of gathered rows).
+ * uniq_rows are gathered-row indices, i.e. positions in the all-to-all receive buffer = the request order.
+ * gathered (the received rows) is read for max/min only.
+ */
+int rf_pool_rows_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
+                     int32_t batch, int64_t n_tok, int64_t n_positions, const int32_t* row_map, const float* gathered,
+                     int64_t n_rows, int32_t dim, const float* out, const float* dout, int64_t out_stride, int32_t flags,
+                     int32_t* minmax_count, int64_t* uniq_rows, float* uniq_grad, int64_t uniq_cap, int32_t* n_uniq,
+                     void* ws, size_t ws_bytes, void* stream);
+/*
+ * Owner side of the sharded backward: rows vals[i] (f32 [n][dim]) with ids[i] in [0, id_range) are summed
+ * per id in input order (the concatenation of the requesters' gradients in rank order): uniq_ids ascending,
+ * uniq_vals their sums (acc = 0; acc += v in order). Ids outside the range are dropped. n_uniq: DEVICE int32.
+ * ws: rf_segment_sum_ws_bytes(n, id_range).
+ */
+size_t rf_segment_sum_ws_bytes(int64_t n, int64_t id_range);
+int rf_segment_sum_rows(const int64_t* ids, const float* vals, int64_t n, int32_t dim, int64_t id_range, int64_t* uniq_ids,
+                        float* uniq_vals, int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
+
+/*
  * One tf.keras.optimizers.Adam step on an fp32 table from a deduplicated sparse gradient
  * (Adam._resource_apply_sparse, example/ranking_search/train.py:97):
  *   m = m * beta1 (every row); m[r] += g_r * (1 - beta1) (listed rows); v likewise with g_r * g_r * (1 - beta2);

@@ -81,6 +81,8 @@ def lib():
         L.orf_pool_rows_fwd.argtypes = [vp, i32, vp, vp, i32, i64, vp, vp, i32, i32, vp, i32, i64, i32]
         L.orf_fused_hash_embed_bwd.restype = i64
         L.orf_fused_hash_embed_bwd.argtypes = [vp, i32, vp, vp, vp, vp, i32, vp, i64, i32, vp, vp, i64, i32, vp, vp]
+        L.orf_pool_rows_bwd.restype = i64
+        L.orf_pool_rows_bwd.argtypes = [vp, i32, vp, vp, i32, i64, vp, vp, i64, i32, vp, vp, i64, i32, vp, vp]
         L.orf_adam_apply.restype = None
         L.orf_adam_apply.argtypes = [vp, vp, vp, i64, i32, vp, vp, i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_float, i32]
@@ -170,6 +172,45 @@ def fused_hash_embed_bwd(slots, tok_bytes, tok_off, bag_off, lmax, batch, table,
     if nu < 0:
         raise RuntimeError("oracle fused_hash_embed_bwd: row out of range")
     return rows[:nu], grad[:nu]
+
+
+def pool_rows_bwd(slots, bag_off, lmax, batch, n_tok, row_map, gathered, dim, out, dout, flags=0):
+    """Restatement of rf_pool_rows_bwd (the sharded requester's backward, rf_oracle.c orf_pool_rows_bwd):
+    rows index `gathered`; returns (uniq_rows int64 [U], uniq_grad f32 [U, dim])."""
+    slots = np.ascontiguousarray(slots, dtype=SLOT_DTYPE)
+    bag_off = np.ascontiguousarray(bag_off, dtype=np.int32)
+    lmax = np.ascontiguousarray(lmax, dtype=np.int32)
+    row_map = np.ascontiguousarray(row_map, dtype=np.int32)
+    gathered = np.ascontiguousarray(gathered, dtype=np.float32)
+    out = np.ascontiguousarray(out, dtype=np.float32)
+    dout = np.ascontiguousarray(dout, dtype=np.float32)
+    n_pos = int(batch) * int(2 * lmax.astype(np.int64).sum())
+    cap = max(min(n_pos, gathered.shape[0]), 1)
+    rows = np.zeros(cap, np.int64)
+    grad = np.zeros((cap, dim), np.float32)
+    nu = lib().orf_pool_rows_bwd(_p(slots), len(slots), _p(bag_off), _p(lmax), batch, n_tok, _p(row_map), _p(gathered),
+                                 gathered.shape[0], dim, _p(out), _p(dout), dout.shape[1], flags, _p(rows), _p(grad))
+    if nu < 0:
+        raise RuntimeError("oracle pool_rows_bwd: row out of range")
+    return rows[:nu], grad[:nu]
+
+
+def segment_sum_rows(ids, vals):
+    """Restatement of rf_segment_sum_rows: distinct ids ascending, each with the fp32 sum of its rows taken
+    in input order starting from +0.0 (the owner side of the sharded backward: the senders' rows arrive
+    rank-major, so a row's gradient is the sum over ranks r = 0..P-1 in that order)."""
+    ids = np.asarray(ids, np.int64)
+    vals = np.asarray(vals, np.float32).reshape(len(ids), -1)
+    order = np.argsort(ids, kind="stable")
+    uid, start = np.unique(ids[order], return_index=True)
+    out = np.zeros((len(uid), vals.shape[1]), np.float32)
+    bounds = list(start) + [len(ids)]
+    for u in range(len(uid)):
+        acc = np.zeros(vals.shape[1], np.float32)
+        for i in order[bounds[u]: bounds[u + 1]]:
+            acc = acc + vals[i]
+        out[u] = acc
+    return uid, out
 
 
 def adam_apply(table, m, v, uniq_rows, uniq_grad, lr, beta1, beta2, eps, lazy=False):

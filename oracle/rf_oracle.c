@@ -381,11 +381,25 @@ static int cmp_u64(const void* a, const void* b) {
     return x < y ? -1 : x > y;
 }
 
-int64_t orf_fused_hash_embed_bwd(const rf_slot_desc* slots, int32_t n_slots, const uint8_t* tok_bytes,
-                                 const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
-                                 const float* table, int64_t table_rows, int32_t dim, const float* out,
-                                 const float* dout, int64_t out_stride, int32_t flags, int64_t* uniq_rows,
-                                 float* uniq_grad) {
+/* Row read at (slot s, table k, bag position l) of an example whose bag starts at token t0 and holds len
+ * tokens: the hashed row (row_map == NULL), or — the sharded requester — the slot in the receive buffer
+ * of logical row 2t + k (real token) / 2 n_tok + 2 s + k (padding), as rf_pool_rows_fwd reads it. */
+static int64_t bwd_row(const rf_slot_desc* sd, int32_t s, int k, int32_t l, int32_t t0, int32_t len,
+                       const uint8_t* tok_bytes, const int32_t* tok_off, const int32_t* row_map, int64_t n_tok) {
+    if (row_map) return l < len ? row_map[2 * (int64_t)(t0 + l) + k] : row_map[2 * n_tok + 2 * (int64_t)s + k];
+    if (l < len) {
+        const int32_t t = t0 + l;
+        return sd->row_base[k] + orf_hash_bucket(sd->salt[k], sd->salt[k], tok_bytes + tok_off[t],
+                                                 tok_off[t + 1] - tok_off[t], sd->num_bins, sd->mask_empty);
+    }
+    return sd->row_base[k] + (sd->mask_empty ? 0 : orf_hash_bucket(sd->salt[k], sd->salt[k], (const uint8_t*)"", 0,
+                                                                     sd->num_bins, 0));
+}
+
+static int64_t embed_bwd(const rf_slot_desc* slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                         const int32_t* bag_off, const int32_t* lmax, int32_t batch, const int32_t* row_map,
+                         int64_t n_tok, const float* table, int64_t table_rows, int32_t dim, const float* out,
+                         const float* dout, int64_t out_stride, int32_t flags, int64_t* uniq_rows, float* uniq_grad) {
     const int masked = (flags & RF_FLAG_MASK_PADDING) != 0;
     int64_t per = 0;
     int64_t* pos_off = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n_slots + 1));
@@ -404,17 +418,8 @@ int64_t orf_fused_hash_embed_bwd(const rf_slot_desc* slots, int32_t n_slots, con
             for (int k = 0; k < 2; ++k)
                 for (int32_t l = 0; l < lmax[s]; ++l) {
                     const int64_t p = (int64_t)b * per + pos_off[s] + (int64_t)k * lmax[s] + l;
-                    int64_t row;
-                    if (l < len) {
-                        const int32_t t = t0 + l;
-                        row = sd->row_base[k] + orf_hash_bucket(sd->salt[k], sd->salt[k], tok_bytes + tok_off[t],
-                                                                tok_off[t + 1] - tok_off[t], sd->num_bins, sd->mask_empty);
-                    } else if (masked) {
-                        continue;
-                    } else {
-                        row = sd->row_base[k] + (sd->mask_empty ? 0 : orf_hash_bucket(sd->salt[k], sd->salt[k],
-                                                                                       (const uint8_t*)"", 0, sd->num_bins, 0));
-                    }
+                    if (l >= len && masked) continue;
+                    const int64_t row = bwd_row(sd, s, k, l, t0, len, tok_bytes, tok_off, row_map, n_tok);
                     if (row < 0 || row >= table_rows) { status = -1; continue; }
                     keys[m++] = ((uint64_t)row << 32) | (uint64_t)p;
                 }
@@ -450,15 +455,7 @@ int64_t orf_fused_hash_embed_bwd(const rf_slot_desc* slots, int32_t n_slots, con
                         /* num_selected over the bag's L positions (pads included unless masked) */
                         int32_t c = 0;
                         for (int32_t l2 = 0; l2 < L; ++l2) {
-                            int64_t r2;
-                            if (l2 < len) {
-                                const int32_t t = t0 + l2;
-                                r2 = sd->row_base[k] + orf_hash_bucket(sd->salt[k], sd->salt[k], tok_bytes + tok_off[t],
-                                                                       tok_off[t + 1] - tok_off[t], sd->num_bins, sd->mask_empty);
-                            } else {
-                                r2 = sd->row_base[k] + (sd->mask_empty ? 0 : orf_hash_bucket(sd->salt[k], sd->salt[k],
-                                                                                              (const uint8_t*)"", 0, sd->num_bins, 0));
-                            }
+                            const int64_t r2 = bwd_row(sd, s, k, l2, t0, len, tok_bytes, tok_off, row_map, n_tok);
                             if (r2 >= 0 && r2 < table_rows && table[r2 * dim + d] == out[col + d]) ++c;
                         }
                         v = ((tr[d] == out[col + d] ? 1.0f : 0.0f) / (float)c) * g;
@@ -476,6 +473,25 @@ int64_t orf_fused_hash_embed_bwd(const rf_slot_desc* slots, int32_t n_slots, con
     free(keys);
     free(pos_off);
     return status ? -1 : nu;
+}
+
+int64_t orf_fused_hash_embed_bwd(const rf_slot_desc* slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                 const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
+                                 const float* table, int64_t table_rows, int32_t dim, const float* out,
+                                 const float* dout, int64_t out_stride, int32_t flags, int64_t* uniq_rows,
+                                 float* uniq_grad) {
+    return embed_bwd(slots, n_slots, tok_bytes, tok_off, bag_off, lmax, batch, NULL, 0, table, table_rows, dim, out,
+                     dout, out_stride, flags, uniq_rows, uniq_grad);
+}
+
+/* rf_pool_rows_bwd: the same gradient with rows read through row_map from gathered [n_rows][dim]
+ * (uniq_rows index the gathered rows). */
+int64_t orf_pool_rows_bwd(const rf_slot_desc* slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
+                          int32_t batch, int64_t n_tok, const int32_t* row_map, const float* gathered, int64_t n_rows,
+                          int32_t dim, const float* out, const float* dout, int64_t out_stride, int32_t flags,
+                          int64_t* uniq_rows, float* uniq_grad) {
+    return embed_bwd(slots, n_slots, NULL, NULL, bag_off, lmax, batch, row_map, n_tok, gathered, n_rows, dim, out,
+                     dout, out_stride, flags, uniq_rows, uniq_grad);
 }
 
 /* Keras Adam (OptimizerV2 Adam._resource_apply_sparse after dedup), fp32, one step:

@@ -132,6 +132,45 @@ class GpuShardOps:
         return out
 
 
+    # -- training -------------------------------------------------------------
+    def pool_bwd(self, desc, n_slots: int, batch: SparseBatch, row_map: torch.Tensor, gathered: torch.Tensor,
+                 out: torch.Tensor, dout: torch.Tensor, flags: int, need_minmax: bool):
+        """rf_pool_rows_bwd -> (rows into `gathered` [U] ascending, grads [U, D])."""
+        lm = batch.lmax_numpy()
+        n_pos = batch.batch * int(2 * np.asarray(lm, np.int64).sum())
+        R = gathered.shape[0]
+        cap = max(1, min(n_pos, R))
+        D = gathered.shape[1]
+        rows = torch.empty(cap, dtype=torch.int64, device=self.device)
+        grad = torch.empty((cap, D), dtype=torch.float32, device=self.device)
+        n_uniq = torch.zeros(1, dtype=torch.int32, device=self.device)
+        cnt = torch.empty(dout.shape, dtype=torch.int32, device=self.device) if need_minmax else None
+        wsb = int(L.load().rf_embed_bwd_ws_bytes(n_pos, n_slots, max(R, 1)))
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=self.device)
+        L.call("rf_pool_rows_bwd", L.ptr(desc), n_slots, L.ptr(batch.bag_off), L.ptr(batch.lmax), batch.batch,
+               batch.n_tokens, n_pos, L.ptr(row_map), L.ptr(gathered), R, D, L.ptr(out) if need_minmax else None,
+               L.ptr(dout), dout.stride(0), flags, L.ptr(cnt), L.ptr(rows), L.ptr(grad), cap, L.ptr(n_uniq), L.ptr(ws),
+               ws.numel(), L.stream_ptr(None))
+        n = int(n_uniq.item())
+        if n < 0:
+            raise ValueError(f"rf_pool_rows_bwd: invalid batch (error bits {-n})")
+        return rows[:n], grad[:n]
+
+    def segment_sum(self, ids: torch.Tensor, vals: torch.Tensor, id_range: int):
+        """rf_segment_sum_rows -> (distinct ids ascending, per-id sums in input order)."""
+        n = ids.numel()
+        D = vals.shape[1]
+        cap = max(1, min(n, id_range))
+        uid = torch.empty(cap, dtype=torch.int64, device=self.device)
+        uval = torch.empty((cap, D), dtype=torch.float32, device=self.device)
+        n_uniq = torch.zeros(1, dtype=torch.int32, device=self.device)
+        wsb = int(L.load().rf_segment_sum_ws_bytes(n, id_range))
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=self.device)
+        L.call("rf_segment_sum_rows", L.ptr(ids.contiguous()), L.ptr(vals.contiguous()), n, D, id_range, L.ptr(uid),
+               L.ptr(uval), cap, L.ptr(n_uniq), L.ptr(ws), ws.numel(), L.stream_ptr(None))
+        return uid, uval, n_uniq, cap
+
+
 class TorchDistComm:
     """Exchange over torch.distributed: RCCL on MI355X (xGMI point-to-point), gloo in the CPU tests."""
 
@@ -246,6 +285,97 @@ class ShardedFusedEncoder(torch.nn.Module):
         vec = self.serve(wanted)
         back = self.comm.exchange(vec, recv_counts, st.counts)               # my rows, owner-major
         return self.combine(batch, st, back, out)
+
+
+@dataclass
+class TrainCtx:
+    batch: SparseBatch
+    st: RouteState
+    wanted: torch.Tensor   # local ids the other ranks requested from this shard, rank-major
+    recv_counts: List[int]
+    back: torch.Tensor     # the rows this rank received (request order)
+    out: torch.Tensor
+
+
+def _grad_exchange_plan(enc, st: RouteState, rows: torch.Tensor):
+    """Per-owner counts of the touched requested rows (rows index the owner-major request order)."""
+    bounds = torch.tensor(np.cumsum(st.counts), dtype=torch.int64, device=rows.device)
+    owner = torch.bucketize(rows, bounds, right=True)
+    return [int(c) for c in torch.bincount(owner, minlength=enc.nranks).cpu().tolist()]
+
+
+def _shard_training_methods():
+    def forward_train(self, batch: SparseBatch, out: Optional[torch.Tensor] = None) -> TrainCtx:
+        """forward() that keeps what the backward needs (route state, received rows, served ids)."""
+        batch = self.ops.prepare_batch(batch)
+        st = self.route(batch)
+        counts_t = torch.tensor(st.counts, dtype=torch.int64, device=st.local.device)
+        recv_counts = [int(c) for c in self.comm.exchange_counts(counts_t).cpu().tolist()]
+        wanted = self.comm.exchange(st.local, st.counts, recv_counts)
+        back = self.comm.exchange(self.serve(wanted), recv_counts, st.counts)
+        out = self.combine(batch, st, back, out)
+        return TrainCtx(batch, st, wanted, recv_counts, back, out)
+
+    def requester_grad(self, ctx: TrainCtx, dout: torch.Tensor):
+        """(local ids at their owners, grads, per-owner counts) of the rows this rank touched."""
+        if self.table_dtype != torch.float32:
+            raise ValueError("sharded training needs an fp32 table")
+        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        mm = any(sp.combiner in ("max", "min") for sp in self.slots)
+        rows, grad = self.ops.pool_bwd(self.desc, len(self.slots), ctx.batch, ctx.st.row_map, ctx.back, ctx.out,
+                                       dout.float().contiguous(), flags, mm)
+        return ctx.st.local[rows], grad, _grad_exchange_plan(self, ctx.st, rows)
+
+    def owner_grad(self, ids: torch.Tensor, grads: torch.Tensor):
+        """Sum the gradients other ranks sent for this shard's rows (rank order) -> SparseGrad."""
+        from .sparse_encoder import SparseGrad
+
+        uid, uval, n_uniq, cap = self.ops.segment_sum(ids, grads, max(self.local_rows, 1))
+        return SparseGrad(uid, uval, n_uniq, cap)
+
+    def backward(self, ctx: TrainCtx, dout: torch.Tensor):
+        """Reverse all-to-all of row gradients; returns the SparseGrad of the local shard (feed SparseAdam(shard))."""
+        ids, grad, send = self.requester_grad(ctx, dout)
+        recv = [int(c) for c in self.comm.exchange_counts(torch.tensor(send, dtype=torch.int64, device=ids.device)).cpu().tolist()]
+        r_ids = self.comm.exchange(ids, send, recv)
+        r_grad = self.comm.exchange(grad, send, recv)
+        return self.owner_grad(r_ids, r_grad)
+
+    return forward_train, requester_grad, owner_grad, backward
+
+
+(ShardedFusedEncoder.forward_train, ShardedFusedEncoder.requester_grad, ShardedFusedEncoder.owner_grad,
+ ShardedFusedEncoder.backward) = _shard_training_methods()
+
+
+def simulate_sharded_backward(encoders: Sequence[ShardedFusedEncoder], batches: Sequence[SparseBatch], douts):
+    """All P ranks in one process: forward, requester gradients, the reverse exchange by slicing, owner sums.
+    Returns (outputs, [SparseGrad per shard])."""
+    P = len(encoders)
+    ctxs = []
+    batches = [enc.ops.prepare_batch(b) for enc, b in zip(encoders, batches)]
+    states = [enc.route(b) for enc, b in zip(encoders, batches)]
+    offs = [np.concatenate([[0], np.cumsum(st.counts)]) for st in states]
+    vec = []
+    for o in range(P):
+        wanted = torch.cat([states[r].local[offs[r][o]: offs[r][o + 1]] for r in range(P)])
+        vec.append(encoders[o].serve(wanted))
+    for r in range(P):
+        pos = [int(sum(states[q].counts[o] for q in range(r))) for o in range(P)]
+        back = torch.cat([vec[o][pos[o]: pos[o] + states[r].counts[o]] for o in range(P)])
+        out = encoders[r].combine(batches[r], states[r], back)
+        ctxs.append(TrainCtx(batches[r], states[r], None, None, back, out))
+    sent = [encoders[r].requester_grad(ctxs[r], douts[r]) for r in range(P)]
+    grads = []
+    for o in range(P):
+        ids, gs = [], []
+        for r in range(P):
+            _, _, cnt = sent[r]
+            a = int(sum(cnt[:o]))
+            ids.append(sent[r][0][a: a + cnt[o]])
+            gs.append(sent[r][1][a: a + cnt[o]])
+        grads.append(encoders[o].owner_grad(torch.cat(ids), torch.cat(gs)))
+    return [c.out for c in ctxs], grads
 
 
 def simulate_sharded_forward(encoders: Sequence[ShardedFusedEncoder], batches: Sequence[SparseBatch]):

@@ -127,12 +127,27 @@ __device__ __forceinline__ Pos decode_pos(uint32_t p, const int64_t* __restrict_
     return q;
 }
 
+// Row of table k for bag position l of (b, s): the hashed token (or the slot's pad row) — or, for pooled
+// pre-gathered rows (rf_pool_rows_bwd), the distinct-row index row_map gives the logical row 2t + k
+// (pad rows: 2 n_tok + 2 s + k), exactly the rows rf_pool_rows_fwd read.
+__device__ __forceinline__ int64_t position_row(const rf_slot_desc* sd, int s, int k, int t, bool real,
+                                                const uint8_t* __restrict__ tok_bytes, const int32_t* __restrict__ tok_off,
+                                                const int32_t* __restrict__ row_map, int64_t n_tok) {
+    if (row_map) return real ? (int64_t)row_map[2 * (int64_t)t + k] : (int64_t)row_map[2 * n_tok + 2 * s + k];
+    if (real) {
+        const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
+        return sd->row_base[k] + hash_bucket_dev(sd->salt[k], sd->salt[k], tok_bytes + b0, n, sd->num_bins, sd->mask_empty);
+    }
+    return sd->row_base[k] + (sd->mask_empty ? 0 : hash_bucket_dev(sd->salt[k], sd->salt[k], tok_bytes, 0, sd->num_bins, 0));
+}
+
 __global__ __launch_bounds__(256) void enum_kernel(const rf_slot_desc* __restrict__ slots, int S,
                                                    const uint8_t* __restrict__ tok_bytes,
                                                    const int32_t* __restrict__ tok_off,
                                                    const int32_t* __restrict__ bag_off,
                                                    const int32_t* __restrict__ lmax, int batch, int64_t n_pos,
                                                    const int64_t* __restrict__ pos_off, int64_t table_rows, int masked,
+                                                   const int32_t* __restrict__ row_map, int64_t n_tok,
                                                    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                    int32_t* __restrict__ flag) {
     const uint32_t sentinel = (uint32_t)table_rows;
@@ -147,19 +162,12 @@ __global__ __launch_bounds__(256) void enum_kernel(const rf_slot_desc* __restric
         const Pos q = decode_pos((uint32_t)p, pos_off, S, lmax, bag_off);
         const rf_slot_desc* sd = slots + q.s;
         if (q.len > q.L) atomicOr(flag, 4);  // a bag longer than its lmax: invalid batch
-        int64_t row;
-        if (q.l < q.len) {
-            const int t = bag_off[(int64_t)q.b * S + q.s] + q.l;
-            const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
-            row = sd->row_base[q.k] +
-                  hash_bucket_dev(sd->salt[q.k], sd->salt[q.k], tok_bytes + b0, n, sd->num_bins, sd->mask_empty);
-        } else if (masked) {
+        if (q.l >= q.len && masked) {
             keys[p] = sentinel;
             continue;
-        } else {
-            row = sd->row_base[q.k] +
-                  (sd->mask_empty ? 0 : hash_bucket_dev(sd->salt[q.k], sd->salt[q.k], tok_bytes, 0, sd->num_bins, 0));
         }
+        const int t = bag_off[(int64_t)q.b * S + q.s] + q.l;
+        const int64_t row = position_row(sd, q.s, q.k, t, q.l < q.len, tok_bytes, tok_off, row_map, n_tok);
         if (row < 0 || row >= table_rows) {
             atomicOr(flag, 1);
             keys[p] = sentinel;
@@ -209,6 +217,7 @@ __global__ __launch_bounds__(256) void minmax_count_kernel(const rf_slot_desc* _
                                                            const int32_t* __restrict__ tok_off,
                                                            const int32_t* __restrict__ bag_off,
                                                            const int32_t* __restrict__ lmax, int batch, int masked,
+                                                           const int32_t* __restrict__ row_map, int64_t n_tok,
                                                            const float* __restrict__ table, int64_t table_rows, int D,
                                                            const float* __restrict__ out, int64_t stride,
                                                            int32_t* __restrict__ cnt) {
@@ -221,16 +230,12 @@ __global__ __launch_bounds__(256) void minmax_count_kernel(const rf_slot_desc* _
         if (sd->combiner != RF_COMB_MAX && sd->combiner != RF_COMB_MIN) continue;
         const int t0 = bag_off[u], len = bag_off[u + 1] - t0;
         const int L = masked ? len : max(lmax[s], len);
-        const int64_t pad = sd->row_base[k] + (sd->mask_empty ? 0 : hash_bucket_dev(sd->salt[k], sd->salt[k], tok_bytes, 0, sd->num_bins, 0));
+        const int64_t pad = position_row(sd, s, k, 0, false, tok_bytes, tok_off, row_map, n_tok);
         const float* o = out + (int64_t)b * stride + sd->out_off + (int64_t)k * D;
         int32_t* c = cnt + (int64_t)b * stride + sd->out_off + (int64_t)k * D;
         for (int d = 0; d < D; ++d) c[d] = 0;
         for (int l = 0; l < L; ++l) {
-            int64_t row = pad;
-            if (l < len) {
-                const int bb = tok_off[t0 + l], nb = tok_off[t0 + l + 1] - bb;
-                row = sd->row_base[k] + hash_bucket_dev(sd->salt[k], sd->salt[k], tok_bytes + bb, nb, sd->num_bins, sd->mask_empty);
-            }
+            const int64_t row = l < len ? position_row(sd, s, k, t0 + l, true, tok_bytes, tok_off, row_map, n_tok) : pad;
             if (row < 0 || row >= table_rows) continue;
             const float* tr = table + row * D;
             for (int d = 0; d < D; ++d) c[d] += tr[d] == o[d] ? 1 : 0;
@@ -327,7 +332,7 @@ __global__ __launch_bounds__(256) void reduce_short_kernel(const uint32_t* __res
         const int i0 = seg[u], i1 = seg[u + 1];
         if (i1 - i0 > kLong || !active) continue;
         const int64_t row = uniq_rows[u];
-        const float4 trow = reinterpret_cast<const float4*>(table + row * D)[lane];
+        const float4 trow = table ? reinterpret_cast<const float4*>(table + row * D)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         int i = i0;
         for (; i + 4 <= i1; i += 4) {
@@ -377,7 +382,7 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
         const int32_t u = long_list[j];
         const int i0 = seg[u], i1 = seg[u + 1];
         const int64_t row = uniq_rows[u];
-        const float4 trow = active ? reinterpret_cast<const float4*>(table + row * D)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 trow = (active && table) ? reinterpret_cast<const float4*>(table + row * D)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
         const int nch = (i1 - i0 + P - 1) / P;
         // index of this thread's position in chunk c, or -1 past the segment
         auto pos_of = [&](int c) -> int {
@@ -439,6 +444,28 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
         }
         if (t < TPR && active) reinterpret_cast<float4*>(uniq_grad + (int64_t)u * D)[t] = acc;
         __syncthreads();
+    }
+}
+
+// ---- owner-side gradient sum (sharded training) ------------------------------------------------
+__global__ __launch_bounds__(256) void ids_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t range,
+                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t id = ids[i];
+        keys[i] = (id >= 0 && id < range) ? (uint32_t)id : (uint32_t)range;
+        vals[i] = (uint32_t)i;
+    }
+}
+
+__global__ __launch_bounds__(256) void prep_sum_kernel(const uint32_t* __restrict__ vals, const int32_t* __restrict__ seg,
+                                                       const int32_t* __restrict__ n_uniq_p, int D4,
+                                                       uint32_t* __restrict__ src, uint32_t* __restrict__ aux) {
+    const int32_t nu = *n_uniq_p;
+    if (nu <= 0) return;
+    const int64_t n = seg[nu];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        src[i] = vals[i] * (uint32_t)D4;
+        aux[i] = ((uint32_t)RF_COMB_SUM << 24) | 1u;
     }
 }
 
@@ -526,12 +553,14 @@ extern "C" size_t rf_embed_bwd_ws_bytes(int64_t n_positions, int32_t n_slots, in
     return bwd_layout(n_positions, n_slots, table_rows).total;
 }
 
-extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
-                                       const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
-                                       int32_t batch, int64_t n_positions, const float* table, int64_t table_rows,
-                                       int32_t dim, const float* out, const float* dout, int64_t out_stride,
-                                       int32_t flags, int32_t* minmax_count, int64_t* uniq_rows, float* uniq_grad,
-                                       int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream) {
+namespace {
+// shared by rf_fused_hash_embed_bwd (rows = hashed tokens) and rf_pool_rows_bwd (rows = row_map of the
+// pre-gathered logical rows; `table` = the gathered rows, table_rows = their count)
+int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                   const int32_t* row_map, int64_t n_tok, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
+                   int64_t n_positions, const float* table, int64_t table_rows, int32_t dim, const float* out,
+                   const float* dout, int64_t out_stride, int32_t flags, int32_t* minmax_count, int64_t* uniq_rows,
+                   float* uniq_grad, int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream) {
     RF_REQUIRE(n_slots >= 1 && batch >= 0 && n_positions >= 0, "rf_fused_hash_embed_bwd: need n_slots >= 1, batch >= 0, n_positions >= 0");
     RF_REQUIRE(n_positions < ((int64_t)1 << 32) - 1, "rf_fused_hash_embed_bwd: n_positions must be < 2^32 - 1");
     RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 32) - 1, "rf_fused_hash_embed_bwd: table_rows must be in [1, 2^32 - 1)");
@@ -546,7 +575,7 @@ extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_sl
         if (hipMemsetAsync(n_uniq, 0, sizeof(int32_t), st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
         return RF_OK;
     }
-    RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && lmax && table && dout && uniq_rows && uniq_grad,
+    RF_REQUIRE(d_slots && (row_map || (tok_bytes && tok_off)) && bag_off && lmax && table && dout && uniq_rows && uniq_grad,
                "rf_fused_hash_embed_bwd: null pointer");
     RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)dout & 15) == 0 && ((uintptr_t)uniq_grad & 15) == 0 &&
                (!out || ((uintptr_t)out & 15) == 0) && (!minmax_count || ((uintptr_t)minmax_count & 15) == 0),
@@ -567,7 +596,7 @@ extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_sl
     if (hipMemsetAsync(flag, 0, 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
     hipLaunchKernelGGL(posoff_kernel, dim3(1), dim3(1024), 0, st, lmax, n_slots, pos_off);
     hipLaunchKernelGGL(enum_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_slots, n_slots, tok_bytes, tok_off, bag_off,
-                       lmax, batch, n, pos_off, table_rows, masked, kin, vin, flag);
+                       lmax, batch, n, pos_off, table_rows, masked, row_map, n_tok, kin, vin, flag);
     size_t sb = lay.sort_bytes;
     if (hipcub::DeviceRadixSort::SortPairs(tmp, sb, kin, kout, vin, vout, (int)n, 0, lay.end_bit, st) != hipSuccess)
         return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: radix sort failed");
@@ -580,7 +609,7 @@ extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_sl
     if (minmax_count) {
         RF_REQUIRE(out, "rf_fused_hash_embed_bwd: max/min pooling needs the forward output");
         hipLaunchKernelGGL(minmax_count_kernel, dim3(grid_of((int64_t)batch * n_slots * 2)), dim3(256), 0, st, d_slots,
-                           n_slots, tok_bytes, tok_off, bag_off, lmax, batch, masked, table, table_rows, dim, out,
+                           n_slots, tok_bytes, tok_off, bag_off, lmax, batch, masked, row_map, n_tok, table, table_rows, dim, out,
                            out_stride, minmax_count);
     }
     // prep (src/aux into the now-free pre-sort buffers) and the long-segment list (into the free scan buffer)
@@ -613,6 +642,100 @@ extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_sl
     else launch(std::integral_constant<int, 64>{});
     hipLaunchKernelGGL(flag_kernel, dim3(1), dim3(64), 0, st, flag, n_uniq);  // prep's alignment flag
     return rf_check_launch("rf_fused_hash_embed_bwd");
+}
+}  // namespace
+
+extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                       const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                                       int32_t batch, int64_t n_positions, const float* table, int64_t table_rows,
+                                       int32_t dim, const float* out, const float* dout, int64_t out_stride,
+                                       int32_t flags, int32_t* minmax_count, int64_t* uniq_rows, float* uniq_grad,
+                                       int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream) {
+    return embed_bwd_impl(d_slots, n_slots, tok_bytes, tok_off, nullptr, 0, bag_off, lmax, batch, n_positions, table,
+                          table_rows, dim, out, dout, out_stride, flags, minmax_count, uniq_rows, uniq_grad, uniq_cap,
+                          n_uniq, ws, ws_bytes, stream);
+}
+
+extern "C" int rf_pool_rows_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
+                                int32_t batch, int64_t n_tok, int64_t n_positions, const int32_t* row_map,
+                                const float* gathered, int64_t n_rows, int32_t dim, const float* out, const float* dout,
+                                int64_t out_stride, int32_t flags, int32_t* minmax_count, int64_t* uniq_rows,
+                                float* uniq_grad, int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes,
+                                void* stream) {
+    RF_REQUIRE(row_map, "rf_pool_rows_bwd: row_map is required");
+    return embed_bwd_impl(d_slots, n_slots, nullptr, nullptr, row_map, n_tok, bag_off, lmax, batch, n_positions, gathered,
+                          n_rows, dim, out, dout, out_stride, flags, minmax_count, uniq_rows, uniq_grad, uniq_cap, n_uniq,
+                          ws, ws_bytes, stream);
+}
+
+extern "C" size_t rf_segment_sum_ws_bytes(int64_t n, int64_t id_range) {
+    if (n < 0 || id_range < 1) return 0;
+    return bwd_layout(n, 1, id_range).total;
+}
+
+extern "C" int rf_segment_sum_rows(const int64_t* ids, const float* vals, int64_t n, int32_t dim, int64_t id_range,
+                                   int64_t* uniq_ids, float* uniq_vals, int64_t uniq_cap, int32_t* n_uniq, void* ws,
+                                   size_t ws_bytes, void* stream) {
+    RF_REQUIRE(n >= 0 && n < ((int64_t)1 << 31), "rf_segment_sum_rows: n must be in [0, 2^31)");
+    RF_REQUIRE(id_range >= 1 && id_range < ((int64_t)1 << 32) - 1, "rf_segment_sum_rows: id_range must be in [1, 2^32 - 1)");
+    RF_REQUIRE(dim >= 4 && dim <= 256 && dim % 4 == 0, "rf_segment_sum_rows: dim must be a multiple of 4 in [4, 256]");
+    RF_REQUIRE(n_uniq && ws && uniq_cap >= 0, "rf_segment_sum_rows: null pointer");
+    const BwdLayout lay = bwd_layout(n, 1, id_range);
+    RF_REQUIRE(ws_bytes >= lay.total, "rf_segment_sum_rows: workspace too small (%zu < %zu)", ws_bytes, lay.total);
+    hipStream_t st = rf_stream(stream);
+    if (n == 0) {
+        if (hipMemsetAsync(n_uniq, 0, 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_segment_sum_rows: memset failed");
+        return RF_OK;
+    }
+    RF_REQUIRE(ids && vals && uniq_ids && uniq_vals, "rf_segment_sum_rows: null pointer");
+    RF_REQUIRE((((uintptr_t)vals | (uintptr_t)uniq_vals) & 15) == 0, "rf_segment_sum_rows: buffers must be 16-byte aligned");
+    char* w = static_cast<char*>(ws);
+    auto* kin = reinterpret_cast<uint32_t*>(w + lay.off_kin);
+    auto* kout = reinterpret_cast<uint32_t*>(w + lay.off_kout);
+    auto* vin = reinterpret_cast<uint32_t*>(w + lay.off_vin);
+    auto* vout = reinterpret_cast<uint32_t*>(w + lay.off_vout);
+    auto* scan = reinterpret_cast<int32_t*>(w + lay.off_scan);
+    auto* seg = reinterpret_cast<int32_t*>(w + lay.off_seg);
+    auto* flag = reinterpret_cast<int32_t*>(w + lay.off_flag);
+    void* tmp = w + lay.off_tmp;
+    const uint32_t sentinel = (uint32_t)id_range;
+    if (hipMemsetAsync(flag, 0, 8, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_segment_sum_rows: memset failed");
+    hipLaunchKernelGGL(ids_kernel, dim3(grid_of(n)), dim3(256), 0, st, ids, n, id_range, kin, vin);
+    size_t sb = lay.sort_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp, sb, kin, kout, vin, vout, (int)n, 0, lay.end_bit, st) != hipSuccess)
+        return rf_set_error(RF_EHIP, "rf_segment_sum_rows: radix sort failed");
+    hipLaunchKernelGGL(heads_kernel, dim3(grid_of(n)), dim3(256), 0, st, kout, n, scan);
+    size_t cb = lay.scan_bytes;
+    if (hipcub::DeviceScan::InclusiveSum(tmp, cb, scan, scan, (int)n, st) != hipSuccess)
+        return rf_set_error(RF_EHIP, "rf_segment_sum_rows: scan failed");
+    hipLaunchKernelGGL(emit_kernel, dim3(grid_of(n)), dim3(256), 0, st, kout, scan, n, sentinel, uniq_cap, uniq_ids, seg);
+    hipLaunchKernelGGL(count_kernel, dim3(1), dim3(64), 0, st, kout, scan, n, sentinel, flag, seg, n_uniq);
+    uint32_t* src = kin;
+    uint32_t* aux = vin;
+    int32_t* long_list = scan;
+    int32_t* long_cnt = flag + 1;
+    hipLaunchKernelGGL(prep_sum_kernel, dim3(grid_of(n)), dim3(256), 0, st, vout, seg, n_uniq, dim / 4, src, aux);
+    const int64_t max_u = std::min<int64_t>(std::min<int64_t>(n, id_range), uniq_cap);
+    hipLaunchKernelGGL(classify_kernel, dim3(grid_of(max_u)), dim3(256), 0, st, seg, n_uniq, uniq_cap, long_list, long_cnt);
+    auto launch = [&](auto tpr) {
+        constexpr int TPR = decltype(tpr)::value;
+        const int teams = 256 / TPR;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((max_u + teams - 1) / teams, 256 * 64));
+        hipLaunchKernelGGL(reduce_short_kernel<TPR>, dim3(grid), dim3(256), 0, st, src, aux, seg, n_uniq, uniq_cap,
+                           uniq_ids, nullptr, dim, nullptr, vals, nullptr, uniq_vals);
+        const int lgrid = (int)std::max<int64_t>(1, std::min<int64_t>(n / kLong + 1, 1024));
+        hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
+                           uniq_ids, nullptr, dim, nullptr, vals, nullptr, uniq_vals);
+    };
+    const int d4 = dim / 4;
+    if (d4 <= 1) launch(std::integral_constant<int, 1>{});
+    else if (d4 <= 2) launch(std::integral_constant<int, 2>{});
+    else if (d4 <= 4) launch(std::integral_constant<int, 4>{});
+    else if (d4 <= 8) launch(std::integral_constant<int, 8>{});
+    else if (d4 <= 16) launch(std::integral_constant<int, 16>{});
+    else if (d4 <= 32) launch(std::integral_constant<int, 32>{});
+    else launch(std::integral_constant<int, 64>{});
+    return rf_check_launch("rf_segment_sum_rows");
 }
 
 extern "C" size_t rf_adam_ws_bytes(int64_t table_rows, int32_t lazy) {

@@ -44,6 +44,10 @@ _SIGS = {
     "rf_embed_bwd_ws_bytes": (ctypes.c_size_t, [_i64, _i32, _i64]),
     "rf_fused_hash_embed_bwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _vp, _vp, _i64,
                                                _i32, _vp, _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "rf_pool_rows_bwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i64, _i64, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _i32,
+                                        _vp, _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "rf_segment_sum_ws_bytes": (ctypes.c_size_t, [_i64, _i64]),
+    "rf_segment_sum_rows": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_adam_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
     "rf_adam_apply": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _i32, _vp,
                                      ctypes.c_size_t, _vp]),

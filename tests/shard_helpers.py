@@ -47,6 +47,39 @@ class OracleShardOps:
         out.copy_(torch.from_numpy(res))
         return out
 
+    def pool_bwd(self, desc, n_slots, batch, row_map, gathered, out, dout, flags, need_minmax):
+        r, g = O.pool_rows_bwd(desc, batch.bag_off, batch.lmax, batch.batch, batch.n_tokens, row_map.numpy(),
+                               gathered.numpy(), gathered.shape[1], out.numpy(), dout.numpy(), flags)
+        return torch.from_numpy(r), torch.from_numpy(g)
+
+    def segment_sum(self, ids, vals, id_range):
+        uid, uval = O.segment_sum_rows(ids.numpy(), vals.numpy())
+        n = len(uid)
+        return torch.from_numpy(uid), torch.from_numpy(uval), torch.tensor([n], dtype=torch.int32), max(n, 1)
+
+
+def sharded_grad_oracle(O, desc, table, dim, batches, outs, douts, nranks, flags=0):
+    """Expected owner-side gradients of a row-sharded step: every rank's unsharded backward on its own batch
+    (rows = global rows), then per global row g the fp32 sum over ranks 0..P-1 in order, starting at +0.0.
+    Returns {owner: (local ids ascending, grads)}."""
+    per_rank = []
+    for b, out, dout in zip(batches, outs, douts):
+        rows, g = O.fused_hash_embed_bwd(desc, b.tok_bytes, b.tok_off, b.bag_off, b.lmax, b.batch, table, dim, out,
+                                         dout, flags)
+        per_rank.append(dict(zip(rows.tolist(), g)))
+    res = {}
+    for o in range(nranks):
+        rows = sorted({g for d in per_rank for g in d if g % nranks == o})
+        grads = np.zeros((len(rows), dim), np.float32)
+        for i, g in enumerate(rows):
+            acc = np.zeros(dim, np.float32)
+            for d in per_rank:
+                if g in d:
+                    acc = acc + d[g]
+            grads[i] = acc
+        res[o] = (np.array([g // nranks for g in rows], np.int64), grads)
+    return res
+
 
 def small_slots(n=12, seed=0):
     rng = np.random.default_rng(seed)
@@ -70,5 +103,13 @@ def dist_worker(rank, world, port, dim, seed, result_dir):
                                   seed=seed, device="cpu")
         out = enc(rank_batch(rank))
         np.save(os.path.join(result_dir, f"out{rank}.npy"), out.numpy())
+        # one training step: forward_train, requester grads, reverse all-to-all, owner segment sum
+        ctx = enc.forward_train(rank_batch(rank))
+        dout = torch.from_numpy(np.random.default_rng(50 + rank).standard_normal(ctx.out.shape).astype(np.float32))
+        sg = enc.backward(ctx, dout)
+        n = sg.count()
+        np.save(os.path.join(result_dir, f"dout{rank}.npy"), dout.numpy())
+        np.save(os.path.join(result_dir, f"gid{rank}.npy"), sg.rows[:n].numpy())
+        np.save(os.path.join(result_dir, f"gval{rank}.npy"), sg.grad[:n].numpy())
     finally:
         dist.destroy_process_group()

@@ -12,8 +12,8 @@ import torch
 import torch.multiprocessing as mp
 
 from recommendflow_amd.backend.encoder.sharded_encoder import (ShardedFusedEncoder, build_slot_desc, shard_rows,
-                                                               simulate_sharded_forward)
-from shard_helpers import OracleShardOps, dist_worker, rank_batch, small_slots
+                                                               simulate_sharded_backward, simulate_sharded_forward)
+from shard_helpers import OracleShardOps, dist_worker, rank_batch, sharded_grad_oracle, small_slots
 
 DIM, SEED = 8, 11
 
@@ -57,6 +57,36 @@ def test_simulated_shards_bit_exact(O, P, dedup):
         np.testing.assert_array_equal(outs[r].numpy(), unsharded(O, r))
 
 
+def expected_grads(O, P, douts, mask_padding=False):
+    desc, rows = build_slot_desc(small_slots(), DIM)
+    table = O.table_init_uniform(rows, DIM, seed=SEED)
+    flags = O.FLAG_MASK_PADDING if mask_padding else 0
+    batches = [rank_batch(r) for r in range(P)]
+    outs = []
+    for b in batches:
+        out, _ = O.fused_hash_embed(desc, b.tok_bytes, b.tok_off, b.bag_off, b.lmax, b.batch, table, DIM,
+                                    2 * DIM * len(desc), flags=flags)
+        outs.append(out)
+    return sharded_grad_oracle(O, desc, table, DIM, batches, outs, douts, P, flags)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+@pytest.mark.parametrize("mask_padding", [False, True])
+def test_simulated_backward(O, P, mask_padding):
+    """Sharded training gradient: requester pool_rows_bwd + reverse exchange + owner segment sum equals each
+    rank's unsharded backward summed over ranks in rank order (DESIGN D-sharded-grad-order)."""
+    encs = [ShardedFusedEncoder(small_slots(), DIM, r, P, ops=OracleShardOps(), seed=SEED, device="cpu",
+                                mask_padding=mask_padding) for r in range(P)]
+    rng = np.random.default_rng(7)
+    douts = [torch.from_numpy(rng.standard_normal((24, 2 * DIM * 12)).astype(np.float32)) for _ in range(P)]
+    outs, grads = simulate_sharded_backward(encs, [rank_batch(r) for r in range(P)], douts)
+    want = expected_grads(O, P, [d.numpy() for d in douts], mask_padding)
+    for o in range(P):
+        n = grads[o].count()
+        np.testing.assert_array_equal(grads[o].rows[:n].numpy(), want[o][0])
+        assert np.array_equal(grads[o].grad[:n].numpy().view(np.uint32), want[o][1].view(np.uint32))
+
+
 def test_gloo_world2_bit_exact(O, tmp_path):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -64,3 +94,7 @@ def test_gloo_world2_bit_exact(O, tmp_path):
     mp.spawn(dist_worker, args=(2, port, DIM, SEED, str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         np.testing.assert_array_equal(np.load(tmp_path / f"out{r}.npy"), unsharded(O, r))
+    want = expected_grads(O, 2, [np.load(tmp_path / f"dout{r}.npy") for r in range(2)])
+    for o in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"gid{o}.npy"), want[o][0])
+        np.testing.assert_array_equal(np.load(tmp_path / f"gval{o}.npy").view(np.uint32), want[o][1].view(np.uint32))

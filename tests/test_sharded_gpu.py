@@ -124,3 +124,49 @@ def test_sharded_cfg2_layout(cuda):
     outs = simulate_sharded_forward(encs, batches)
     for r in range(P):
         np.testing.assert_array_equal(bits(outs[r]), bits(full(batches[r].to("cuda"))))
+
+
+def full_table(encs):
+    P = len(encs)
+    rows = encs[0].table_rows
+    t = np.zeros((rows, encs[0].dim), np.float32)
+    for r, e in enumerate(encs):
+        t[r::P] = e.shard.cpu().numpy()
+    return t
+
+
+@pytest.mark.parametrize("P", [1, 2, 4])
+@pytest.mark.parametrize("mask_padding", [False, True])
+def test_simulated_backward_and_adam(O, cuda, P, mask_padding):
+    """Sharded training step (DESIGN D-sharded-grad-order): rf_pool_rows_bwd on every requester, the reverse
+    exchange, rf_segment_sum_rows on every owner, SparseAdam on every shard — bit-exact vs the oracle's
+    per-rank unsharded backward summed in rank order, and the dense Keras Adam on the logical table."""
+    from shard_helpers import sharded_grad_oracle
+
+    from recommendflow_amd.backend.encoder.sharded_encoder import simulate_sharded_backward
+    from recommendflow_amd.backend.optim import SparseAdam
+
+    sp = slots(18, seed=10 + P)
+    encs = [ShardedFusedEncoder(sp, 16, r, P, seed=5, mask_padding=mask_padding) for r in range(P)]
+    batches = [synthetic_batch(64 + 9 * r, [i % 3 == 0 for i in range(len(sp))], seed=70 + r, id_max=300)
+               for r in range(P)]
+    table0 = full_table(encs)
+    g = torch.Generator().manual_seed(P)
+    douts = [torch.randn((b.batch, encs[0].out_width), generator=g).cuda() for b in batches]
+    outs, grads = simulate_sharded_backward(encs, batches, douts)
+    flags = O.FLAG_MASK_PADDING if mask_padding else 0
+    want = sharded_grad_oracle(O, encs[0].host_desc, table0, 16, batches, [o.cpu().numpy() for o in outs],
+                               [d.cpu().numpy() for d in douts], P, flags)
+    for o in range(P):
+        n = grads[o].count()
+        np.testing.assert_array_equal(grads[o].rows[:n].cpu().numpy(), want[o][0])
+        assert np.array_equal(bits(grads[o].grad[:n]), want[o][1].view(np.uint32))
+    # Adam on every shard == dense Keras Adam on the logical table with the summed gradient
+    for o in range(P):
+        SparseAdam(encs[o].shard, learning_rate=0.01).apply(grads[o])
+    t, m, v = table0.copy(), np.zeros_like(table0), np.zeros_like(table0)
+    rows = np.concatenate([want[o][0] * P + o for o in range(P)])
+    gr = np.concatenate([want[o][1] for o in range(P)])
+    order = np.argsort(rows)
+    O.adam_apply(t, m, v, rows[order], gr[order], O.keras_adam_lr(0.01, 0.9, 0.999, 1), 0.9, 0.999, 1e-7)
+    assert np.array_equal(full_table(encs).view(np.uint32), t.view(np.uint32))
