@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "rf_common.h"
 
@@ -90,6 +91,17 @@ __device__ __forceinline__ float rows4_sum(float v) {
     const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
     const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// IEEE-754 maximum (NaN-propagating): v_maximum3_f32 on gfx950, no operand canonicalisation
+// (fmaxf costs an extra v_max_f32 per non-canonical operand: loads, MFMA results, bit casts)
+__device__ __forceinline__ float fmx(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float fmx3(float a, float b, float c) { return fmx(fmx(a, b), c); }
+
+__device__ __forceinline__ float rows4_maximum(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float s = __builtin_elementwise_maximum(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+    return __builtin_elementwise_maximum(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 __device__ __forceinline__ float rows4_max(float v) {
     const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -299,6 +311,265 @@ __global__ __launch_bounds__(kEsimWaves * 64) void esim_kernel(const uint16_t* _
 }
 
 // ---------------------------------------------------------------------------------------------
+// ESIM v2: 4-wave workgroups, two per CU (LDS <= 80 KB each), so two examples are in flight per CU and
+// one workgroup's barriers / softmax / statistics overlap the other's MFMA and LDS phases. Wave w owns
+// the score stripes w and w + 4 and runs them jointly: every q fragment (scores) and every transposed V
+// fragment (P @ V) read from LDS feeds both stripes' MFMAs, halving the LDS read traffic per example.
+// The LDS images stop at the 16-row tile edge (not the 32-row k-step): the upper half of a P @ V k-step
+// past the last tile reads zeros instead of LDS.
+// ---------------------------------------------------------------------------------------------
+constexpr int kEsim2Waves = 4;
+
+template <typename frag>
+__device__ __forceinline__ frag v_frag_tr_acc_h(const uint16_t* V, int rs, int k0, int n0, int lane, bool hi_ok) {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+    const uint16_t* base = V + (k0 + 4 * g + qq) * rs + n0 + 4 * p;
+    const s4v lo = tr_read(base);
+    s4v hi = s4v{0, 0, 0, 0};
+    if (hi_ok) hi = tr_read(base + 16 * rs);
+    const s8v x = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(frag, x);
+}
+
+// column softmax of one E^T stripe held in accumulators (j on (lane >> 4, register), i on lane & 15),
+// rounded once to the MFMA dtype as the A operand of P @ V (k order of v_frag_tr_acc). VALU-lean: the
+// padding mask touches only the last tile, exp is v_exp_f32 on a pre-scaled argument (one fma + one
+// exp per score), and P is packed with the hardware round-to-nearest-even conversions.
+template <typename M, typename frag>
+__device__ __forceinline__ void stripe_softmax(f4 (&ev)[8], int nt, int L, int lg, frag (&pa)[4]) {
+    using elem = decltype(frag{}[0]);
+    constexpr float kL2E = 1.4426950408889634f;
+    const bool partial = (L & 15) != 0;
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt)
+        if (partial && jt == nt - 1)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (jt * 16 + lg * 4 + r >= L) ev[jt][r] = -INFINITY;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt)
+        if (jt < nt) mx = fmx3(fmx3(mx, ev[jt][0], ev[jt][1]), ev[jt][2], ev[jt][3]);
+    mx = rows4_maximum(mx);
+    const float mo = -mx * kL2E;
+    float sm = 0.f;
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt)
+        if (jt < nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                ev[jt][r] = __builtin_amdgcn_exp2f(fmaf(ev[jt][r], kL2E, mo));
+                sm += ev[jt][r];
+            }
+    const float inv = 1.0f / rows4_sum(sm);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+        frag f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            f[r] = (elem)(2 * kt < nt ? ev[2 * kt][r] * inv : 0.f);
+            f[4 + r] = (elem)(2 * kt + 1 < nt ? ev[2 * kt + 1][r] * inv : 0.f);
+        }
+        pa[kt] = f;
+    }
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// ESIM combine statistics of 4 rows of one column: sum x, sum x*att, max of [x, att, x - att, x*att].
+// Pairs of rows go through packed f32 math (v_pk_mul/add_f32); CHECK masks rows >= L (last stripe only).
+template <typename M, bool CHECK>
+__device__ __forceinline__ void esim_rows(s4v xv, f4 at, int row0, int L, float& s_x, float& s_mul, float& m_all) {
+    f2v sx = {0.f, 0.f}, sm = {0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        f2v x = {M::to_f((uint16_t)xv[2 * p]), M::to_f((uint16_t)xv[2 * p + 1])};
+        f2v t = {at[2 * p], at[2 * p + 1]};
+        if (CHECK) {
+            const bool v0 = row0 + 2 * p < L, v1 = row0 + 2 * p + 1 < L;
+            x = f2v{v0 ? x[0] : 0.f, v1 ? x[1] : 0.f};
+            t = f2v{v0 ? t[0] : 0.f, v1 ? t[1] : 0.f};
+            const f2v ml = x * t, d = x - t;
+            sx += x;
+            sm += ml;
+            const float r0 = fmx(fmx3(x[0], t[0], d[0]), ml[0]), r1 = fmx(fmx3(x[1], t[1], d[1]), ml[1]);
+            m_all = fmx3(m_all, v0 ? r0 : -INFINITY, v1 ? r1 : -INFINITY);
+        } else {
+            const f2v ml = x * t, d = x - t;
+            sx += x;
+            sm += ml;
+            m_all = fmx3(m_all, x[0], t[0]);
+            m_all = fmx3(m_all, d[0], ml[0]);
+            m_all = fmx3(m_all, x[1], t[1]);
+            m_all = fmx3(m_all, d[1], ml[1]);
+        }
+    }
+    s_x += sx[0] + sx[1];
+    s_mul += sm[0] + sm[1];
+}
+
+template <bool F16, int D>
+__global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
+                                                                     const uint16_t* __restrict__ a, int batch, int L,
+                                                                     int64_t ex_stride, int64_t ld, float* __restrict__ out,
+                                                                     int64_t out_stride, int64_t out_off,
+                                                                     float* __restrict__ att_out) {
+    using M = Mfma<F16>;
+    using frag = typename M::frag;
+    constexpr int NTH = kEsim2Waves * 64;
+    constexpr int RS = D + 8;
+    constexpr int DK = D / 32;
+    constexpr int NT = D / 16;
+    constexpr int CPR = D / 8;
+    constexpr int NCH = 2 * 128 * CPR / NTH;
+    constexpr int HALF = NCH / 2;
+    constexpr int LOG_CPR = D == 128 ? 4 : 3;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int L16 = (L + 15) & ~15;  // LDS rows per image
+    const int nt = L16 >> 4;         // 16-row tiles (<= 8)
+    uint16_t* qs = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* as = qs + L16 * RS;
+    float* st = reinterpret_cast<float*>(as + L16 * RS);  // [wave][stat 3][side*D + n]
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+
+    uint4 pre[NCH];
+    auto prefetch = [&](int64_t e) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int cm = tid + (i % HALF) * NTH;
+            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
+            pre[i] = make_uint4(0, 0, 0, 0);
+            if (r < L) pre[i] = *reinterpret_cast<const uint4*>((i < HALF ? q : a) + e * ex_stride + (int64_t)r * ld + ch * 8);
+        }
+    };
+    int64_t e = blockIdx.x;
+    if (e < batch) prefetch(e);
+    for (; e < batch; e += gridDim.x) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int cm = tid + (i % HALF) * NTH;
+            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
+            if (r < L16) *reinterpret_cast<uint4*>((i < HALF ? qs : as) + r * RS + ch * 8) = pre[i];
+        }
+        __syncthreads();
+        if (e + gridDim.x < batch) prefetch(e + gridDim.x);
+
+        const int sp0 = wave, sp1 = wave + kEsim2Waves;
+        const bool h1 = sp1 < nt;
+        if (sp0 < nt) {
+            float* wst = st + wave * 3 * 2 * D;
+            frag pa0[4], pa1[4];
+            {
+                // E^T stripes (attention_layers.py:44-47); each q fragment feeds both stripes
+                frag b0[DK], b1[DK];
+#pragma unroll
+                for (int kk = 0; kk < DK; ++kk) {
+                    b0[kk] = lds_frag<frag>(as + (sp0 * 16 + lr) * RS + kk * 32 + lg * 8);
+                    b1[kk] = b0[kk];
+                    if (h1) b1[kk] = lds_frag<frag>(as + (sp1 * 16 + lr) * RS + kk * 32 + lg * 8);
+                }
+                f4 e0[8], e1[8];
+#pragma unroll
+                for (int jt = 0; jt < 8; ++jt) {
+                    e0[jt] = f4{0.f, 0.f, 0.f, 0.f};
+                    e1[jt] = f4{0.f, 0.f, 0.f, 0.f};
+                    if (jt < nt) {
+#pragma unroll
+                        for (int kk = 0; kk < DK; ++kk) {
+                            const frag qf = lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8);
+                            e0[jt] = M::mma(qf, b0[kk], e0[jt]);
+                            if (h1) e1[jt] = M::mma(qf, b1[kk], e1[jt]);
+                        }
+                    }
+                }
+                stripe_softmax<M>(e0, nt, L, lg, pa0);
+                if (h1) stripe_softmax<M>(e1, nt, L, lg, pa1);
+            }
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const uint16_t* V = side ? as : qs;
+                f4 c0[NT], c1[NT];
+#pragma unroll
+                for (int nn = 0; nn < NT; ++nn) {
+                    c0[nn] = f4{0.f, 0.f, 0.f, 0.f};
+                    c1[nn] = f4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt) {
+                    if (2 * kt < nt) {
+                        const bool hi_ok = 2 * kt + 1 < nt;
+#pragma unroll
+                        for (int nn = 0; nn < NT; ++nn) {
+                            const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, nn * 16, lane, hi_ok);
+                            c0[nn] = M::mma(pa0[kt], vf, c0[nn]);
+                            if (h1) c1[nn] = M::mma(pa1[kt], vf, c1[nn]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int nn = 0; nn < NT; ++nn) {
+                    // ESIM combine statistics (esim.py:79-82) over this wave's rows of both stripes:
+                    // sum x, sum x*att and max of [x, att, x - att, x*att]
+                    const int n = nn * 16 + lr;
+                    float s_x = 0.f, s_mul = 0.f, m_all = -INFINITY;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if (h == 1 && !h1) break;
+                        const int sp = h ? sp1 : sp0;
+                        const int row0 = sp * 16 + lg * 4;
+                        const s4v xv = tr_read(V + (row0 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3));
+                        const f4 at = h ? c1[nn] : c0[nn];
+                        if ((L & 15) && sp == nt - 1) esim_rows<M, true>(xv, at, row0, L, s_x, s_mul, m_all);
+                        else esim_rows<M, false>(xv, at, row0, L, s_x, s_mul, m_all);
+                        if (att_out) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (row0 + r < L) att_out[((e * 2 + side) * L + row0 + r) * D + n] = at[r];
+                        }
+                    }
+                    s_x = rows4_sum(s_x);
+                    s_mul = rows4_sum(s_mul);
+                    m_all = rows4_maximum(m_all);
+                    if (lg == 0) {
+                        float* w = wst + side * D + n;
+                        w[0] = s_x;
+                        w[2 * D] = s_mul;
+                        w[4 * D] = m_all;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84)
+        const int nw = min(nt, kEsim2Waves);
+        for (int n = tid; n < D; n += NTH) {
+            float avg[2], mxv[2];
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                float sx = 0.f, smul = 0.f, m3 = -INFINITY;
+                for (int w = 0; w < nw; ++w) {
+                    const float* ws = st + w * 3 * 2 * D + side * D + n;
+                    sx += ws[0];
+                    smul += ws[2 * D];
+                    m3 = fmx(m3, ws[4 * D]);
+                }
+                avg[side] = (2.0f * sx + smul) / (float)(4 * L);
+                mxv[side] = m3;
+            }
+            float* o = out + e * out_stride + out_off + n;
+            o[0] = avg[0];
+            o[D] = mxv[0];
+            o[2 * D] = avg[1];
+            o[3 * D] = mxv[1];
+            o[4 * D] = avg[0] - avg[1];
+            o[5 * D] = mxv[0] - mxv[1];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // masked multi-head SDPA: one workgroup per (example, head)
 // ---------------------------------------------------------------------------------------------
 template <bool F16, int DEP>
@@ -438,11 +709,37 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)a & 15) == 0, "rf_esim_soft_attention_fwd: q/a must be 16-byte aligned");
     if (batch == 0) return RF_OK;
     RF_REQUIRE(q && a && out, "rf_esim_soft_attention_fwd: null pointer");
-    const int Lk = (L + 31) & ~31;
-    const size_t lds = (size_t)2 * Lk * (d + 8) * 2 + (size_t)kEsimWaves * 3 * 2 * d * 4;
     hipStream_t st = rf_stream(stream);
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    // v2 (default): 4-wave workgroups, two per CU. RF_ESIM_V1=1 selects the 8-wave one-per-CU kernel (A/B only).
+    static const bool v1 = [] {
+        const char* e = getenv("RF_ESIM_V1");
+        return e && e[0] == '1';
+    }();
+    if (!v1) {
+        const int L16 = (L + 15) & ~15;
+        const size_t lds2 = (size_t)2 * L16 * (d + 8) * 2 + (size_t)kEsim2Waves * 3 * 2 * d * 4;
+        const int per_cu = lds2 <= 80 * 1024 ? 2 : 1;
+        const int grid2 = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
+#define RF_ESIM2_LAUNCH(F16, D)                                                                                    \
+    {                                                                                                              \
+        auto kern = esim2_kernel<F16, D>;                                                                          \
+        int rc = launch_big_lds(kern, grid2, lds2, st, "esim2_kernel");                                            \
+        if (rc) return rc;                                                                                         \
+        hipLaunchKernelGGL(kern, dim3(grid2), dim3(kEsim2Waves * 64), lds2, st, (const uint16_t*)q, (const uint16_t*)a, \
+                           batch, L, ex_stride, ld, out, out_stride, out_off, att_out);                            \
+    }
+        if (dtype == RF_DTYPE_BF16) {
+            if (d == 64) RF_ESIM2_LAUNCH(false, 64) else RF_ESIM2_LAUNCH(false, 128)
+        } else {
+            if (d == 64) RF_ESIM2_LAUNCH(true, 64) else RF_ESIM2_LAUNCH(true, 128)
+        }
+#undef RF_ESIM2_LAUNCH
+        return rf_check_launch("rf_esim_soft_attention_fwd");
+    }
+    const int Lk = (L + 31) & ~31;
+    const size_t lds = (size_t)2 * Lk * (d + 8) * 2 + (size_t)kEsimWaves * 3 * 2 * d * 4;
     const int grid = (int)std::min<int64_t>(batch, cus);  // persistent: one 8-wave workgroup per CU
 #define RF_ESIM_LAUNCH(F16, D)                                                                                     \
     {                                                                                                              \
