@@ -335,8 +335,8 @@ __device__ __forceinline__ frag v_frag_tr_acc_h(const uint16_t* V, int rs, int k
 // rounded once to the MFMA dtype as the A operand of P @ V (k order of v_frag_tr_acc). VALU-lean: the
 // padding mask touches only the last tile, exp is v_exp_f32 on a pre-scaled argument (one fma + one
 // exp per score), and P is packed with the hardware round-to-nearest-even conversions.
-template <typename M, typename frag>
-__device__ __forceinline__ void stripe_softmax(f4 (&ev)[8], int nt, int L, int lg, frag (&pa)[4]) {
+template <typename M, int nt, typename frag>
+__device__ __forceinline__ void stripe_softmax(f4 (&ev)[8], int L, int lg, frag (&pa)[4]) {
     using elem = decltype(frag{}[0]);
     constexpr float kL2E = 1.4426950408889634f;
     const bool partial = (L & 15) != 0;
@@ -408,29 +408,113 @@ __device__ __forceinline__ void esim_rows(s4v xv, f4 at, int row0, int L, float&
     s_mul += sm[0] + sm[1];
 }
 
-template <bool F16, int D>
-__global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
-                                                                     const uint16_t* __restrict__ a, int batch, int L,
-                                                                     int64_t ex_stride, int64_t ld, float* __restrict__ out,
-                                                                     int64_t out_stride, int64_t out_off,
-                                                                     float* __restrict__ att_out) {
-    using M = Mfma<F16>;
+// one wave's share of an ESIM example: score stripes sp0 (and sp1 when TWO), softmax, P @ [q | a] and the
+// combine statistics of its rows -> wst[stat][side*D + n]; NTT = 16-row tiles (compile time: no selects on the tile count)
+template <typename M, int D, int NTT, bool TWO>
+__device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
+                                           int lane) {
+    constexpr int nt = NTT;
     using frag = typename M::frag;
-    constexpr int NTH = kEsim2Waves * 64;
     constexpr int RS = D + 8;
     constexpr int DK = D / 32;
     constexpr int NT = D / 16;
+    const int lr = lane & 15, lg = lane >> 4;
+    frag pa0[4], pa1[4];
+    {
+        // E^T stripes (attention_layers.py:44-47); each q fragment feeds both stripes
+        frag b0[DK], b1[DK];
+#pragma unroll
+        for (int kk = 0; kk < DK; ++kk) {
+            b0[kk] = lds_frag<frag>(as + (sp0 * 16 + lr) * RS + kk * 32 + lg * 8);
+            b1[kk] = b0[kk];
+            if (TWO) b1[kk] = lds_frag<frag>(as + (sp1 * 16 + lr) * RS + kk * 32 + lg * 8);
+        }
+        f4 e0[8], e1[8];
+#pragma unroll
+        for (int jt = 0; jt < 8; ++jt) {
+            e0[jt] = f4{0.f, 0.f, 0.f, 0.f};
+            e1[jt] = f4{0.f, 0.f, 0.f, 0.f};
+            if (jt < nt) {
+#pragma unroll
+                for (int kk = 0; kk < DK; ++kk) {
+                    const frag qf = lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8);
+                    e0[jt] = M::mma(qf, b0[kk], e0[jt]);
+                    if (TWO) e1[jt] = M::mma(qf, b1[kk], e1[jt]);
+                }
+            }
+        }
+        stripe_softmax<M, NTT>(e0, L, lg, pa0);
+        if (TWO) stripe_softmax<M, NTT>(e1, L, lg, pa1);
+    }
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        const uint16_t* V = side ? as : qs;
+        f4 c0[NT], c1[NT];
+#pragma unroll
+        for (int nn = 0; nn < NT; ++nn) {
+            c0[nn] = f4{0.f, 0.f, 0.f, 0.f};
+            c1[nn] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            if (2 * kt < nt) {
+                const bool hi_ok = 2 * kt + 1 < nt;
+#pragma unroll
+                for (int nn = 0; nn < NT; ++nn) {
+                    const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, nn * 16, lane, hi_ok);
+                    c0[nn] = M::mma(pa0[kt], vf, c0[nn]);
+                    if (TWO) c1[nn] = M::mma(pa1[kt], vf, c1[nn]);
+                }
+            }
+        }
+#pragma unroll
+        for (int nn = 0; nn < NT; ++nn) {
+            // ESIM combine statistics (esim.py:79-82) over this wave's rows of both stripes:
+            // sum x, sum x*att and max of [x, att, x - att, x*att]
+            const int n = nn * 16 + lr;
+            float s_x = 0.f, s_mul = 0.f, m_all = -INFINITY;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (h == 1 && !TWO) break;
+                const int sp = h ? sp1 : sp0;
+                const int row0 = sp * 16 + lg * 4;
+                const s4v xv = tr_read(V + (row0 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3));
+                const f4 at = h ? c1[nn] : c0[nn];
+                if ((L & 15) && sp == nt - 1) esim_rows<M, true>(xv, at, row0, L, s_x, s_mul, m_all);
+                else esim_rows<M, false>(xv, at, row0, L, s_x, s_mul, m_all);
+            }
+            s_x = rows4_sum(s_x);
+            s_mul = rows4_sum(s_mul);
+            m_all = rows4_maximum(m_all);
+            if (lg == 0) {
+                float* w = wst + side * D + n;
+                w[0] = s_x;
+                w[2 * D] = s_mul;
+                w[4 * D] = m_all;
+            }
+        }
+    }
+}
+
+template <bool F16, int D, int NTT>
+__global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
+                                                                     const uint16_t* __restrict__ a, int batch, int L,
+                                                                     int64_t ex_stride, int64_t ld, float* __restrict__ out,
+                                                                     int64_t out_stride, int64_t out_off) {
+    using M = Mfma<F16>;
+    constexpr int NTH = kEsim2Waves * 64;
+    constexpr int RS = D + 8;
     constexpr int CPR = D / 8;
     constexpr int NCH = 2 * 128 * CPR / NTH;
     constexpr int HALF = NCH / 2;
     constexpr int LOG_CPR = D == 128 ? 4 : 3;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int L16 = (L + 15) & ~15;  // LDS rows per image
-    const int nt = L16 >> 4;         // 16-row tiles (<= 8)
+    constexpr int L16 = NTT * 16;  // LDS rows per image
+    constexpr int nt = NTT;        // 16-row tiles (<= 8)
     uint16_t* qs = reinterpret_cast<uint16_t*>(smem);
     uint16_t* as = qs + L16 * RS;
     float* st = reinterpret_cast<float*>(as + L16 * RS);  // [wave][stat 3][side*D + n]
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
     uint4 pre[NCH];
     auto prefetch = [&](int64_t e) {
@@ -456,89 +540,11 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         if (e + gridDim.x < batch) prefetch(e + gridDim.x);
 
         const int sp0 = wave, sp1 = wave + kEsim2Waves;
-        const bool h1 = sp1 < nt;
         if (sp0 < nt) {
             float* wst = st + wave * 3 * 2 * D;
-            frag pa0[4], pa1[4];
-            {
-                // E^T stripes (attention_layers.py:44-47); each q fragment feeds both stripes
-                frag b0[DK], b1[DK];
-#pragma unroll
-                for (int kk = 0; kk < DK; ++kk) {
-                    b0[kk] = lds_frag<frag>(as + (sp0 * 16 + lr) * RS + kk * 32 + lg * 8);
-                    b1[kk] = b0[kk];
-                    if (h1) b1[kk] = lds_frag<frag>(as + (sp1 * 16 + lr) * RS + kk * 32 + lg * 8);
-                }
-                f4 e0[8], e1[8];
-#pragma unroll
-                for (int jt = 0; jt < 8; ++jt) {
-                    e0[jt] = f4{0.f, 0.f, 0.f, 0.f};
-                    e1[jt] = f4{0.f, 0.f, 0.f, 0.f};
-                    if (jt < nt) {
-#pragma unroll
-                        for (int kk = 0; kk < DK; ++kk) {
-                            const frag qf = lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8);
-                            e0[jt] = M::mma(qf, b0[kk], e0[jt]);
-                            if (h1) e1[jt] = M::mma(qf, b1[kk], e1[jt]);
-                        }
-                    }
-                }
-                stripe_softmax<M>(e0, nt, L, lg, pa0);
-                if (h1) stripe_softmax<M>(e1, nt, L, lg, pa1);
-            }
-#pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                const uint16_t* V = side ? as : qs;
-                f4 c0[NT], c1[NT];
-#pragma unroll
-                for (int nn = 0; nn < NT; ++nn) {
-                    c0[nn] = f4{0.f, 0.f, 0.f, 0.f};
-                    c1[nn] = f4{0.f, 0.f, 0.f, 0.f};
-                }
-#pragma unroll
-                for (int kt = 0; kt < 4; ++kt) {
-                    if (2 * kt < nt) {
-                        const bool hi_ok = 2 * kt + 1 < nt;
-#pragma unroll
-                        for (int nn = 0; nn < NT; ++nn) {
-                            const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, nn * 16, lane, hi_ok);
-                            c0[nn] = M::mma(pa0[kt], vf, c0[nn]);
-                            if (h1) c1[nn] = M::mma(pa1[kt], vf, c1[nn]);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int nn = 0; nn < NT; ++nn) {
-                    // ESIM combine statistics (esim.py:79-82) over this wave's rows of both stripes:
-                    // sum x, sum x*att and max of [x, att, x - att, x*att]
-                    const int n = nn * 16 + lr;
-                    float s_x = 0.f, s_mul = 0.f, m_all = -INFINITY;
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        if (h == 1 && !h1) break;
-                        const int sp = h ? sp1 : sp0;
-                        const int row0 = sp * 16 + lg * 4;
-                        const s4v xv = tr_read(V + (row0 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3));
-                        const f4 at = h ? c1[nn] : c0[nn];
-                        if ((L & 15) && sp == nt - 1) esim_rows<M, true>(xv, at, row0, L, s_x, s_mul, m_all);
-                        else esim_rows<M, false>(xv, at, row0, L, s_x, s_mul, m_all);
-                        if (att_out) {
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                if (row0 + r < L) att_out[((e * 2 + side) * L + row0 + r) * D + n] = at[r];
-                        }
-                    }
-                    s_x = rows4_sum(s_x);
-                    s_mul = rows4_sum(s_mul);
-                    m_all = rows4_maximum(m_all);
-                    if (lg == 0) {
-                        float* w = wst + side * D + n;
-                        w[0] = s_x;
-                        w[2 * D] = s_mul;
-                        w[4 * D] = m_all;
-                    }
-                }
-            }
+            // both-stripe / one-stripe waves are separate instantiations: no predicated MFMAs
+            if (sp1 < nt) esim2_wave<M, D, NTT, true>(qs, as, wst, sp0, sp1, L, lane);
+            else esim2_wave<M, D, NTT, false>(qs, as, wst, sp0, sp1, L, lane);
         }
         __syncthreads();
 
@@ -696,7 +702,31 @@ int launch_big_lds(K kernel, int grid, size_t lds, hipStream_t st, const char* n
     return RF_OK;
 }
 
+template <bool F16, int D, int NTT>
+int launch_esim2_nt(int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L, int64_t ex_stride,
+                    int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
+    auto kern = esim2_kernel<F16, D, NTT>;
+    const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, (const uint16_t*)q, (const uint16_t*)a, batch, L,
+                       ex_stride, ld, out, out_stride, out_off);
+    return RF_OK;
+}
+
+template <bool F16, int D>
+int launch_esim2(int nt, int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L,
+                 int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
+    switch (nt) {
+#define RF_NT(N) \
+    case N: return launch_esim2_nt<F16, D, N>(grid, lds, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
+        RF_NT(1) RF_NT(2) RF_NT(3) RF_NT(4) RF_NT(5) RF_NT(6) RF_NT(7) RF_NT(8)
+#undef RF_NT
+        default: return rf_set_error(RF_EINVAL, "esim2: bad tile count %d", nt);
+    }
+}
+
 }  // namespace
+
 
 extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d,
                                           int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
@@ -717,27 +747,23 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
         const char* e = getenv("RF_ESIM_V1");
         return e && e[0] == '1';
     }();
-    if (!v1) {
-        const int L16 = (L + 15) & ~15;
-        const size_t lds2 = (size_t)2 * L16 * (d + 8) * 2 + (size_t)kEsim2Waves * 3 * 2 * d * 4;
+    if (!v1 && !att_out) {
+        const int nt = (L + 15) >> 4;
+        const size_t lds2 = (size_t)2 * nt * 16 * (d + 8) * 2 + (size_t)kEsim2Waves * 3 * 2 * d * 4;
         const int per_cu = lds2 <= 80 * 1024 ? 2 : 1;
         const int grid2 = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
-#define RF_ESIM2_LAUNCH(F16, D)                                                                                    \
-    {                                                                                                              \
-        auto kern = esim2_kernel<F16, D>;                                                                          \
-        int rc = launch_big_lds(kern, grid2, lds2, st, "esim2_kernel");                                            \
-        if (rc) return rc;                                                                                         \
-        hipLaunchKernelGGL(kern, dim3(grid2), dim3(kEsim2Waves * 64), lds2, st, (const uint16_t*)q, (const uint16_t*)a, \
-                           batch, L, ex_stride, ld, out, out_stride, out_off, att_out);                            \
-    }
+        int rc = RF_OK;
         if (dtype == RF_DTYPE_BF16) {
-            if (d == 64) RF_ESIM2_LAUNCH(false, 64) else RF_ESIM2_LAUNCH(false, 128)
+            rc = d == 64 ? launch_esim2<false, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
+                         : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
         } else {
-            if (d == 64) RF_ESIM2_LAUNCH(true, 64) else RF_ESIM2_LAUNCH(true, 128)
+            rc = d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
+                         : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
         }
-#undef RF_ESIM2_LAUNCH
+        if (rc) return rc;
         return rf_check_launch("rf_esim_soft_attention_fwd");
     }
+    // the attention-output variant (tests, diagnostics) and RF_ESIM_V1=1 run the 8-wave kernel
     const int Lk = (L + 31) & ~31;
     const size_t lds = (size_t)2 * Lk * (d + 8) * 2 + (size_t)kEsimWaves * 3 * 2 * d * 4;
     const int grid = (int)std::min<int64_t>(batch, cus);  // persistent: one 8-wave workgroup per CU

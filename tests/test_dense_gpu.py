@@ -36,6 +36,21 @@ def test_esim_pool_vs_oracle(O, cuda, L, d, dt):
         np.testing.assert_allclose(got, want, atol=tol * (scale + 1), rtol=0)
 
 
+@pytest.mark.parametrize("L", [1, 15, 16, 17, 33, 48, 64, 65, 80, 97, 100, 112, 113, 127, 128])
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_esim_pool_fast_path(O, cuda, L, d, dt):
+    """The pooled-only path (no attention output: the 4-wave two-per-CU kernel, one instantiation per
+    16-row tile count) against the float64 oracle; B spans more than one persistent pass of the grid."""
+    B = 600 if L in (100, 128) else 37
+    for scale in (0.1, 2.0):
+        q, a = rnd((B, L, d), L * 13 + d, scale, dt), rnd((B, L, d), L * 17 + d + 3, scale, dt)
+        got = esim_soft_attention_pool(q.cuda(), a.cuda()).cpu().numpy()
+        want = O.esim_pool(q.float().numpy(), a.float().numpy())
+        tol = (2 ** -7 if dt == torch.bfloat16 else 2 ** -10) * scale
+        np.testing.assert_allclose(got, want, atol=tol * (scale + 1), rtol=0)
+
+
 def test_esim_strided_views(O, cuda):
     """q and a as slices of one [B, 200, 128] token tensor (cfg3: 100 user + 100 ad slots)."""
     x = rnd((6, 200, 128), 5, 0.1).cuda()
