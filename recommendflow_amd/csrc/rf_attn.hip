@@ -379,8 +379,7 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // ESIM combine statistics of 4 rows of one column: sum x, sum x*att, max of [x, att, x - att, x*att].
 // Pairs of rows go through packed f32 math (v_pk_mul/add_f32); CHECK masks rows >= L (last stripe only).
 template <typename M, bool CHECK>
-__device__ __forceinline__ void esim_rows(s4v xv, f4 at, int row0, int L, float& s_x, float& s_mul, float& m_all) {
-    f2v sx = {0.f, 0.f}, sm = {0.f, 0.f};
+__device__ __forceinline__ void esim_rows(s4v xv, f4 at, int row0, int L, f2v& sx, f2v& sm, float& m_all) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
         f2v x = {M::to_f((uint16_t)xv[2 * p]), M::to_f((uint16_t)xv[2 * p + 1])};
@@ -404,8 +403,16 @@ __device__ __forceinline__ void esim_rows(s4v xv, f4 at, int row0, int L, float&
             m_all = fmx3(m_all, d[1], ml[1]);
         }
     }
-    s_x += sx[0] + sx[1];
-    s_mul += sm[0] + sm[1];
+}
+
+// LDS row stride (elements) of the ESIM v2 images: D + 16 puts the 8 rows of a ds_read_b64_tr_b16 lane
+// group (and the 16 rows of a ds_read_b128 fragment) on disjoint banks; D + 8 (2-way conflicts) only
+// where the wider images would push the workgroup past 80 KB (two per CU)
+__host__ __device__ constexpr size_t esim2_lds_bytes(int D, int ntt, int rs) {
+    return (size_t)2 * ntt * 16 * rs * 2 + (size_t)kEsim2Waves * 3 * 2 * D * 4;
+}
+__host__ __device__ constexpr int esim2_rs(int D, int ntt) {
+    return esim2_lds_bytes(D, ntt, D + 16) <= 80 * 1024 ? D + 16 : D + 8;
 }
 
 // one wave's share of an ESIM example: score stripes sp0 (and sp1 when TWO), softmax, P @ [q | a] and the
@@ -415,7 +422,7 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
                                            int lane) {
     constexpr int nt = NTT;
     using frag = typename M::frag;
-    constexpr int RS = D + 8;
+    constexpr int RS = esim2_rs(D, NTT);
     constexpr int DK = D / 32;
     constexpr int NT = D / 16;
     const int lr = lane & 15, lg = lane >> 4;
@@ -434,7 +441,22 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
         for (int jt = 0; jt < 8; ++jt) {
             e0[jt] = f4{0.f, 0.f, 0.f, 0.f};
             e1[jt] = f4{0.f, 0.f, 0.f, 0.f};
-            if (jt < nt) {
+        }
+        if constexpr (NTT < 8) {
+            // k-step outer, tiles inner: consecutive MFMAs are independent (no accumulator RAW stalls)
+#pragma unroll
+            for (int kk = 0; kk < DK; ++kk) {
+#pragma unroll
+                for (int jt = 0; jt < nt; ++jt) {
+                    const frag qf = lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8);
+                    e0[jt] = M::mma(qf, b0[kk], e0[jt]);
+                    if (TWO) e1[jt] = M::mma(qf, b1[kk], e1[jt]);
+                }
+            }
+        } else {
+            // 8 tiles: tile-outer keeps fewer q fragments live (measured faster at L = 128)
+#pragma unroll
+            for (int jt = 0; jt < nt; ++jt) {
 #pragma unroll
                 for (int kk = 0; kk < DK; ++kk) {
                     const frag qf = lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8);
@@ -472,7 +494,8 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
             // ESIM combine statistics (esim.py:79-82) over this wave's rows of both stripes:
             // sum x, sum x*att and max of [x, att, x - att, x*att]
             const int n = nn * 16 + lr;
-            float s_x = 0.f, s_mul = 0.f, m_all = -INFINITY;
+            f2v sx = {0.f, 0.f}, sm = {0.f, 0.f};
+            float m_all = -INFINITY;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (h == 1 && !TWO) break;
@@ -480,11 +503,11 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
                 const int row0 = sp * 16 + lg * 4;
                 const s4v xv = tr_read(V + (row0 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3));
                 const f4 at = h ? c1[nn] : c0[nn];
-                if ((L & 15) && sp == nt - 1) esim_rows<M, true>(xv, at, row0, L, s_x, s_mul, m_all);
-                else esim_rows<M, false>(xv, at, row0, L, s_x, s_mul, m_all);
+                if ((L & 15) && sp == nt - 1) esim_rows<M, true>(xv, at, row0, L, sx, sm, m_all);
+                else esim_rows<M, false>(xv, at, row0, L, sx, sm, m_all);
             }
-            s_x = rows4_sum(s_x);
-            s_mul = rows4_sum(s_mul);
+            const float s_x = rows4_sum(sx[0] + sx[1]);
+            const float s_mul = rows4_sum(sm[0] + sm[1]);
             m_all = rows4_maximum(m_all);
             if (lg == 0) {
                 float* w = wst + side * D + n;
@@ -503,7 +526,7 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                                                                      int64_t out_stride, int64_t out_off) {
     using M = Mfma<F16>;
     constexpr int NTH = kEsim2Waves * 64;
-    constexpr int RS = D + 8;
+    constexpr int RS = esim2_rs(D, NTT);
     constexpr int CPR = D / 8;
     constexpr int NCH = 2 * 128 * CPR / NTH;
     constexpr int HALF = NCH / 2;
@@ -549,28 +572,34 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         __syncthreads();
 
         // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84)
-        const int nw = min(nt, kEsim2Waves);
-        for (int n = tid; n < D; n += NTH) {
-            float avg[2], mxv[2];
+        // every thread of the workgroup: lane l of wave w reduces side l >> 5 of the columns
+        // n = (w * 32 + (l & 31)) + j * 128; the two sides of a column meet with one lane swap (l ^ 32)
+        constexpr int nw = nt < kEsim2Waves ? nt : kEsim2Waves;
+        const int side = lane >> 5;
 #pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                float sx = 0.f, smul = 0.f, m3 = -INFINITY;
+        for (int n0 = 0; n0 < D; n0 += NTH / 2) {
+            const int n = n0 + wave * 32 + (lane & 31);
+            float sx = 0.f, smul = 0.f, m3 = -INFINITY;
+            if (n < D) {
+#pragma unroll
                 for (int w = 0; w < nw; ++w) {
                     const float* ws = st + w * 3 * 2 * D + side * D + n;
                     sx += ws[0];
                     smul += ws[2 * D];
                     m3 = fmx(m3, ws[4 * D]);
                 }
-                avg[side] = (2.0f * sx + smul) / (float)(4 * L);
-                mxv[side] = m3;
             }
-            float* o = out + e * out_stride + out_off + n;
-            o[0] = avg[0];
-            o[D] = mxv[0];
-            o[2 * D] = avg[1];
-            o[3 * D] = mxv[1];
-            o[4 * D] = avg[0] - avg[1];
-            o[5 * D] = mxv[0] - mxv[1];
+            const float avg = (2.0f * sx + smul) / (float)(4 * L);
+            const float avg_o = __shfl_xor(avg, 32, 64), mx_o = __shfl_xor(m3, 32, 64);
+            if (n < D) {
+                float* o = out + e * out_stride + out_off + n;
+                o[2 * side * D] = avg;
+                o[(2 * side + 1) * D] = m3;
+                if (side == 0) {
+                    o[4 * D] = avg - avg_o;
+                    o[5 * D] = m3 - mx_o;
+                }
+            }
         }
     }
 }
@@ -749,7 +778,7 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     }();
     if (!v1 && !att_out) {
         const int nt = (L + 15) >> 4;
-        const size_t lds2 = (size_t)2 * nt * 16 * (d + 8) * 2 + (size_t)kEsim2Waves * 3 * 2 * d * 4;
+        const size_t lds2 = esim2_lds_bytes(d, nt, esim2_rs(d, nt));
         const int per_cu = lds2 <= 80 * 1024 ? 2 : 1;
         const int grid2 = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
         int rc = RF_OK;
