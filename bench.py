@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--shard-dim", type=int, default=128)
     p.add_argument("--shard-batch", type=int, default=8192, help="cfg4: examples per GPU (65536 at P=8)")
     p.add_argument("--no-train", action="store_true", help="skip the cfg2 DSSM training-step extra")
+    p.add_argument("--no-shard-train", action="store_true", help="skip the cfg4 sharded training-step extra")
     p.add_argument("--no-cascade", action="store_true", help="skip the cfg5 recall->prerank->rank extra")
     p.add_argument("--catalog", type=int, default=1_000_000, help="cfg5: items in the catalog")
     p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
@@ -382,9 +383,65 @@ def bench_sharded(args, specs, multi, rank, world):
            "config": f"cfg2 slots ({S}) over a {enc.table_rows}x{D} fp32 fused table row-sharded over {P} GPU(s) "
                      f"({enc.local_rows} rows/GPU), {B} examples/GPU (global {B * P}), owner = row mod P, "
                      f"per-step row dedup, RCCL all_to_all_single for ids and rows"}
+    if not args.no_shard_train:
+        res["train_step"] = bench_sharded_train(args, enc, batches, out, world)
     del enc, batches, out
     torch.cuda.empty_cache()
     return res
+
+
+def bench_sharded_train(args, enc, batches, out, world):
+    """cfg4 training step: forward_train (route, ids/rows all-to-all, pool) ->
+    backward (rf_pool_rows_bwd on the requester, reverse all-to-all of (local id, grad) pairs,
+    rf_segment_sum_rows on the owner) -> lazy Keras Adam on the shard (rf_adam_apply, touched rows).
+    Bit-exact vs the oracle (tests/test_sharded_gpu.py::test_simulated_backward_and_adam)."""
+    import torch
+    import torch.distributed as dist
+
+    from recommendflow_amd.backend.optim import SparseAdam
+
+    B = batches[0].batch
+    opt = SparseAdam(enc.shard, learning_rate=1e-4, lazy=True)
+    g = torch.Generator(device="cuda").manual_seed(5 + enc.rank)
+    dout = torch.randn((B, enc.out_width), generator=g, device="cuda") * 1e-3
+    names = ["forward", "backward", "adam"]
+    st = {}
+
+    def step(i, ev=None):
+        ctx = enc.forward_train(batches[i % 2], out=out)
+        if ev: ev[1].record()
+        sg = enc.backward(ctx, dout)
+        if ev: ev[2].record()
+        opt.apply(sg)
+        if ev: ev[3].record()
+        st["rows"] = sg.cap
+
+    steps = max(5, args.steps // 5)
+    for i in range(2):
+        step(i)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record()
+        step(i, evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    stage = {n: round(sum(e[k].elapsed_time(e[k + 1]) for e in evs) / steps, 4) for k, n in enumerate(names)}
+    n_rows = int(opt.m.shape[0])
+    del opt
+    torch.cuda.empty_cache()
+    return {"examples_per_s": round(B * enc.nranks * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
+            "stage_ms_rank0": stage, "shard_rows": n_rows,
+            "optimizer": "Keras Adam, lazy (touched rows only; DESIGN D-lazy-adam)"}
 
 
 def bench_cascade(args, enc):
