@@ -368,10 +368,12 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
                                                            const float* __restrict__ table, int D,
                                                            const float* __restrict__ out, const float* __restrict__ dout,
                                                            const int32_t* __restrict__ cnt, float* __restrict__ uniq_grad) {
-    constexpr int P = 1024 / TPR;
-    constexpr int kDepth = 8;
+    constexpr int PPT = TPR >= 32 ? 2 : 1;  // positions per thread per chunk (register budget: 1024 threads)
+    constexpr int PT = 1024 / TPR;     // positions per pass of the block
+    constexpr int P = PPT * PT;        // positions per chunk (one barrier)
+    constexpr int kDepth = 8 / PPT;
     constexpr int G = 8;  // LDS reads per add group
-    __shared__ float4 buf[2][1024];
+    __shared__ float4 buf[2][PPT * 1024];
     const int t = threadIdx.x, pi = t / TPR, lane = t % TPR;
     const bool active = lane * 4 < D;
     const auto* dout4 = reinterpret_cast<const float4*>(dout);
@@ -384,26 +386,30 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
         const int64_t row = uniq_rows[u];
         const float4 trow = (active && table) ? reinterpret_cast<const float4*>(table + row * D)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
         const int nch = (i1 - i0 + P - 1) / P;
-        // index of this thread's position in chunk c, or -1 past the segment
-        auto pos_of = [&](int c) -> int {
-            const int i = i0 + c * P + pi;
+        // index of this thread's h-th position in chunk c (chunk-local q = h * PT + pi), or -1
+        auto pos_of = [&](int c, int h) -> int {
+            const int i = i0 + c * P + h * PT + pi;
             return (c < nch && i < i1 && active) ? i : -1;
         };
-        uint32_t rs[kDepth], ra[kDepth];
-        float4 rv[kDepth];
+        uint32_t rs[kDepth][PPT], ra[kDepth][PPT];
+        float4 rv[kDepth][PPT];
 #pragma unroll
-        for (int k = 0; k < kDepth; ++k) {
-            const int i = pos_of(k);
-            rs[k] = i >= 0 ? src[i] : kZero;
-            ra[k] = i >= 0 ? aux[i] : 0u;
-        }
+        for (int k = 0; k < kDepth; ++k)
 #pragma unroll
-        for (int k = 0; k < kDepth; ++k) {
-            rv[k] = pos_value(rs[k], ra[k], lane, trow, dout4, out4, cnt4);
-            const int i = pos_of(k + kDepth);
-            rs[k] = i >= 0 ? src[i] : kZero;
-            ra[k] = i >= 0 ? aux[i] : 0u;
-        }
+            for (int h = 0; h < PPT; ++h) {
+                const int i = pos_of(k, h);
+                rs[k][h] = i >= 0 ? src[i] : kZero;
+                ra[k][h] = i >= 0 ? aux[i] : 0u;
+            }
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k)
+#pragma unroll
+            for (int h = 0; h < PPT; ++h) {
+                rv[k][h] = pos_value(rs[k][h], ra[k][h], lane, trow, dout4, out4, cnt4);
+                const int i = pos_of(k + kDepth, h);
+                rs[k][h] = i >= 0 ? src[i] : kZero;
+                ra[k][h] = i >= 0 ? aux[i] : 0u;
+            }
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int c0 = 0; c0 < nch; c0 += kDepth) {
 #pragma unroll
@@ -411,12 +417,16 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
                 const int c = c0 + k;
                 if (c < nch) {  // block-uniform
                     float4* b = buf[c & 1];
-                    b[t] = rv[k];
+#pragma unroll
+                    for (int h = 0; h < PPT; ++h) b[h * 1024 + t] = rv[k][h];  // = b[q * TPR + lane]
                     __syncthreads();
-                    rv[k] = pos_value(rs[k], ra[k], lane, trow, dout4, out4, cnt4);  // chunk c + kDepth
-                    const int i = pos_of(c + 2 * kDepth);
-                    rs[k] = i >= 0 ? src[i] : kZero;
-                    ra[k] = i >= 0 ? aux[i] : 0u;
+#pragma unroll
+                    for (int h = 0; h < PPT; ++h) {
+                        rv[k][h] = pos_value(rs[k][h], ra[k][h], lane, trow, dout4, out4, cnt4);  // chunk c + kDepth
+                        const int i = pos_of(c + 2 * kDepth, h);
+                        rs[k][h] = i >= 0 ? src[i] : kZero;
+                        ra[k][h] = i >= 0 ? aux[i] : 0u;
+                    }
                     if (t < TPR && active) {
                         const int np = min(P, i1 - (i0 + c * P));
                         int q = 0;
