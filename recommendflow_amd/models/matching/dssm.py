@@ -97,12 +97,19 @@ class TrainableDssm(torch.nn.Module):
         v = torch.nn.functional.normalize(self.ad_tower(x[:, self.wu:].contiguous()), dim=-1, eps=1e-6)
         return u, v
 
-    def step(self, batch: SparseBatch, labels: torch.Tensor) -> torch.Tensor:
+    def step(self, batch: SparseBatch, labels: torch.Tensor, dp=None) -> torch.Tensor:
+        """One training step; `dp` (runtime.dist.DataParallel) = MirroredStrategy-style replicas: the
+        loss is scaled by 1/P, dense gradients are SUM-all-reduced in buckets and the table's sparse
+        gradients all-gathered and summed in rank order before the (identical) optimizer steps."""
         self.train()
         self.dense_opt.zero_grad(set_to_none=True)
         u, v = self(batch)
         loss = self.loss_fn(labels, u, v)
-        loss.backward()
-        self.sparse_opt.apply(self.enc.grad)
+        (loss * dp.loss_scale() if dp is not None else loss).backward()
+        sg = self.enc.grad
+        if dp is not None:
+            dp.allreduce_dense(list(self.user_tower.parameters()) + list(self.ad_tower.parameters()))
+            sg = dp.allgather_sparse(sg, self.enc.table_rows)
+        self.sparse_opt.apply(sg)
         self.dense_opt.step()
         return loss.detach()

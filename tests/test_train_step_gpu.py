@@ -50,3 +50,33 @@ def test_loss_decreases(cuda, loss, lazy):
     assert min(losses[-5:]) < losses[0] * 0.8, losses
     assert not torch.equal(t0, model.enc.table)  # the table trained
     assert model.sparse_opt.iterations == 30
+
+
+def test_data_parallel_world1_matches_single(cuda):
+    """runtime.dist.DataParallel over RCCL with one rank: the bucketed all-reduce, the sparse all-gather and
+    the rank-ordered segment sum are identities, so three steps give bit-identical tables and towers."""
+    import socket
+
+    import torch.distributed as dist
+
+    from recommendflow_amd.runtime.dist import DataParallel
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        dp = DataParallel(bucket_bytes=1 << 16)
+        S = 16
+        hb = synthetic_batch(128, [s % 4 == 0 for s in range(S)], seed=9, id_max=400).to("cuda")
+        y = (torch.arange(128, device="cuda") % 2).float()
+        models = [_model()[0] for _ in range(2)]
+        for _ in range(3):
+            models[0].step(hb, y)
+            models[1].step(hb, y, dp=dp)
+        torch.cuda.synchronize()
+        assert torch.equal(models[0].enc.table, models[1].enc.table)
+        for a, b in zip(models[0].parameters(), models[1].parameters()):
+            assert torch.equal(a, b)
+    finally:
+        dist.destroy_process_group()
