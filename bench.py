@@ -32,8 +32,8 @@ TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=50, help="untimed launches: the clocks and the hot-row cache settle over ~50")
     p.add_argument("--batch", type=int, default=4096)
     p.add_argument("--batches", type=int, default=4, help="distinct resident batches cycled through")
     p.add_argument("--table-rows", type=int, default=10_000_000)

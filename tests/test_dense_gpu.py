@@ -94,6 +94,35 @@ def test_dense_fp32_exact_mfma(O, cuda, M, K, N):
     np.testing.assert_allclose(y, want, rtol=1e-5, atol=1e-6 * np.sqrt(K))
 
 
+@pytest.mark.parametrize("cols", [16, 200, 256, 1024, 1280, 2048, 2050, 3000])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+def test_norm_rows(O, cuda, cols, mode, odt):
+    """rf_norm_fwd: the register-resident float4 path (cols % 4 == 0, <= 2048) and the scalar path
+    (2050, 3000, and a misaligned column offset) against float64 LayerNorm / BatchNorm-inference."""
+    from recommendflow_amd.backend.layers.core import Norm
+
+    spec = LayerNormalization(epsilon=1e-6) if mode == 0 else BatchNormalization(epsilon=1e-3)
+    nm = Norm(spec, cols)
+    g = torch.Generator().manual_seed(cols + mode)
+    nm.gamma.copy_(torch.rand(cols, generator=g) + 0.5)
+    nm.beta.copy_(torch.randn(cols, generator=g))
+    if mode == 1:
+        nm.mean.copy_(torch.randn(cols, generator=g))
+        nm.var.copy_(torch.rand(cols, generator=g) + 0.1)
+    base = (torch.randn(67, cols + 4, generator=g) * 3 + 1).cuda()
+    for x in (base[:, :cols], base[:, 1: cols + 1]):  # 16-byte aligned rows, then a misaligned view
+        y = nm(x, out_dtype=odt).float().cpu().numpy()
+        xn = x.cpu().numpy().astype(np.float64)
+        if mode == 0:
+            want = O.layer_norm(xn, nm.gamma.cpu().numpy(), nm.beta.cpu().numpy(), 1e-6)
+        else:
+            want = O.batch_norm_infer(xn, nm.gamma.cpu().numpy(), nm.beta.cpu().numpy(), nm.mean.cpu().numpy(),
+                                      nm.var.cpu().numpy(), 1e-3)
+        tol = 1e-4 if odt == torch.float32 else 2e-2
+        np.testing.assert_allclose(y, want, rtol=tol, atol=tol)
+
+
 @pytest.mark.parametrize("norm", ["ln", "bn"])
 def test_create_mlp(O, cuda, norm):
     spec = LayerNormalization(epsilon=1e-6) if norm == "ln" else BatchNormalization(epsilon=1e-6)
