@@ -1,0 +1,44 @@
+"""cfg3 sparse-encoder ablations (diagnostics): one tower = 100 single-valued slots x 1M bins x 2 tables,
+D = 64 bf16, B = 4096, through rf_fused_hash_embed_fwd with the kernel's ablation flags
+(1<<12: rows from a cheap formula instead of SipHash; 1<<13: hash only, no gather/pool)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch
+
+from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
+from recommendflow_amd.runtime.batch import synthetic_batch
+
+
+def main():
+    B, Ls = 4096, 100
+    specs = [SlotSpec(f"u{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)]
+    enc = FusedSparseEncoder(specs, 64, table_dtype=torch.bfloat16, seed=3)
+    hb = synthetic_batch(B, [False] * Ls, seed=77, slot_ids=range(Ls)).to("cuda")
+    out = torch.empty((B, enc.out_width), dtype=torch.bfloat16, device="cuda")
+    res = {}
+    for name, fl in (("full", 0), ("no_hash", 1 << 12), ("hash_only", 1 << 13)):
+        enc.extra_flags = fl
+
+        def run():
+            enc(hb, out=out)
+
+        for _ in range(20):
+            run()
+        s = [torch.cuda.Event(enable_timing=True) for _ in range(30)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(30)]
+        for i in range(30):
+            s[i].record()
+            run()
+            e[i].record()
+        torch.cuda.synchronize()
+        res[name] = round(sorted(a.elapsed_time(b) for a, b in zip(s, e))[15], 4)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
