@@ -147,6 +147,7 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
     const bool emit = (flags & RF_FLAG_EMIT_IDX) != 0 && idx_out != nullptr;
     const bool abl_nohash = (flags & (1 << 12)) != 0, abl_nopool = (flags & (1 << 13)) != 0,
                abl_nopad = (flags & (1 << 14)) != 0;  // diagnostic ablations (tools/kbench.py)
+    const bool no_lean = (flags & (1 << 15)) != 0;  // A/B: force the general phase 2 on single-token items
     // rf_pool_rows_fwd: `table` holds pre-gathered rows (token t, table k -> row 2t + k; pad rows after)
     constexpr bool pregathered = PRE;
     // PRE: tok_bytes is unused and tok_off carries the optional row map (logical row j of the pre-gathered
@@ -212,6 +213,10 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         }
         if (lane == 0) s_loc[wave][0] = 0;
         const int ntok = __shfl(incl, 63, 64);
+        // single-token items (Lmax = 1, every bag 0 or 1 token): phase 2 is one row pair per bag, so the
+        // lean path below issues every team's loads up front instead of running the pooling pipeline
+        const bool lean = !no_lean && lm == 1 && comb != RF_COMB_NULL && !emit && !pregathered && !abl_nohash &&
+                          !abl_nopad && __all(len <= 1);
         wave_lds_sync();
 
         // ---- phase 1b: lane-per-token double hashing into the LDS bucket ----
@@ -260,6 +265,60 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         }
         wave_lds_sync();
         if (abl_nopool) continue;
+
+        // ---- lean phase 2 (single-token items): a team per bag, GU bags' row pairs in flight per team.
+        // Same values as the general path with Lu = 1: sum/avg = 0 + x (avg / 1 is exact), max/min =
+        // comb_step(init, x), first/last = x; an empty bag reads the pad rows, or is zeros when masked.
+        if (lean) {
+            constexpr int UPT = kUnits / TEAMS;     // bags per team
+            constexpr int GU = CPL >= 2 ? 2 : 4;    // bags per load group
+            const float initv = comb_init(comb);
+#pragma unroll 1
+            for (int q0 = 0; q0 < UPT; q0 += GU) {
+                uint4 v[GU][2][CPL];
+                bool has[GU];
+#pragma unroll
+                for (int g = 0; g < GU; ++g) {
+                    const int jj = min(team + TEAMS * (q0 + g), nu - 1);
+                    const int i = s_loc[wave][jj];
+                    has[g] = s_loc[wave][jj + 1] - i == 1;
+                    const uint32_t r0 = has[g] ? s_row[wave][0][i] : pad0;
+                    const uint32_t r1 = has[g] ? s_row[wave][1][i] : pad1;
+#pragma unroll
+                    for (int cc = 0; cc < CPL; ++cc) {
+                        v[g][0][cc] = row_chunk(table, r0, dim, cidx[cc]);
+                        v[g][1][cc] = row_chunk(table, r1, dim, cidx[cc]);
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < GU; ++g) {
+                    const int j = team + TEAMS * (q0 + g);
+                    if (j >= nu) continue;
+                    const int64_t ob = (int64_t)(b0 + j) * out_stride + out_off;
+                    const bool zero = !has[g] && mask_pad;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+#pragma unroll
+                        for (int cc = 0; cc < CPL; ++cc) {
+                            float f[EPV], a[EPV];
+                            unpack16<TT>(v[g][k][cc], f);
+#pragma unroll
+                            for (int e = 0; e < EPV; ++e) {
+                                if (zero) a[e] = 0.0f;
+                                else if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) a[e] = __fadd_rn(0.0f, f[e]);
+                                else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) a[e] = comb_step(comb, initv, f[e]);
+                                else a[e] = f[e];
+                            }
+                            if (!ok) {
+#pragma unroll
+                                for (int e = 0; e < EPV; ++e) a[e] = __builtin_nanf("");
+                            }
+                            if (cown[cc]) store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + cidx[cc] * EPV, a);
+                        }
+                }
+            }
+            continue;
+        }
 
         // ---- phase 2: token-balanced teams, pipelined gather + pool ----
         auto bound = [&](int tm) -> int {  // first unit j whose first token lies in team tm's share

@@ -95,6 +95,35 @@ def test_fused_embed_edge_cases(O, cuda, mask_padding):
     np.testing.assert_array_equal(bits(got), bits(ref))
 
 
+@pytest.mark.parametrize("tdt,odt", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
+                                     (torch.bfloat16, torch.float32)])
+@pytest.mark.parametrize("dim", [8, 64, 128])
+@pytest.mark.parametrize("mask_padding", [False, True])
+def test_fused_embed_single_token_items(O, cuda, tdt, odt, dim, mask_padding):
+    """Items whose bags hold 0 or 1 token with Lmax = 1 take the lean phase 2 (no emit_idx): bit-exact vs
+    the oracle and vs the general path (flag bit 15), every combiner, empty bags, b"" tokens, and a slot
+    with one 2-token bag (Lmax = 2: general path) beside them; B spans several 64-example items."""
+    rng = np.random.default_rng(dim)
+    S, B = 7, 150
+    rows = []
+    for b in range(B):
+        r = []
+        for s in range(S):
+            n = 2 if (s == 6 and b == 77) else int(rng.random() < 0.8)
+            r.append([b"" if rng.random() < 0.05 else b"t%d" % rng.integers(0, 400) for _ in range(n)])
+        rows.append(r)
+    hb = from_lists(rows)
+    assert list(hb.lmax[:6]) == [1] * 6 and hb.lmax[6] == 2
+    for comb in COMBS:
+        specs = [SlotSpec(f"f{s}", 40 + 13 * s, (s, 7 + s), comb, mask_empty=s != 3) for s in range(S)]
+        enc = FusedSparseEncoder(specs, dim, table_dtype=tdt, out_dtype=odt, seed=dim + 1, mask_padding=mask_padding)
+        got, ref, _, _ = run_both(O, enc, hb, emit=False)
+        np.testing.assert_array_equal(bits(got), bits(ref), err_msg=comb)
+        enc.extra_flags = 1 << 15
+        gen, _, _, _ = run_both(O, enc, hb, emit=False)
+        np.testing.assert_array_equal(bits(got), bits(gen), err_msg=comb)
+
+
 def test_double_hashing_embedding_api(O, cuda):
     with pytest.raises(ValueError):
         DoubleHashingEmbedding(0, 8, [1, 2], "sum")
