@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--no-cascade", action="store_true", help="skip the cfg5 recall->prerank->rank extra")
     p.add_argument("--catalog", type=int, default=1_000_000, help="cfg5: items in the catalog")
     p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
-    p.add_argument("--pipe-examples", type=int, default=16384, help="feature pipe: examples written and read back")
+    p.add_argument("--pipe-examples", type=int, default=65536, help="feature pipe: examples written and read back")
     p.add_argument("--pipe-threads", type=int, default=16, help="feature pipe: reader threads (the box's CPU share)")
     return p.parse_args()
 
@@ -593,7 +593,7 @@ def bench_pipe(args, enc, specs, multi):
     from recommendflow_amd.runtime import tfrecord as T
     from recommendflow_amd.runtime.batch import synthetic_batch
 
-    n_files = 8
+    n_files = max(1, min(16, args.pipe_threads))  # one GZIP part file per reader thread (tf.data interleave)
     per = max(1, args.pipe_examples // n_files)
     fspecs = [T.FeatureSpec(s.name, T.BYTES, T.SEQ, "") for s in specs] + [T.FeatureSpec("label", T.FLOAT, T.SCALAR, 0.0)]
     tmp = tempfile.mkdtemp(prefix="rf_pipe_", dir="/tmp")
