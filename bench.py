@@ -136,18 +136,27 @@ def main():
     if world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(enc, host[0], args.cpu_seconds)
 
+    def guarded(fn, *a):
+        # an extra line must never cost the headline: report its failure in place of its numbers
+        try:
+            return fn(*a)
+        except Exception as e:  # noqa: BLE001
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            return {"error": f"{type(e).__name__}: {e}"[:300]}
+
     extras = None
     if world == 1 and not args.no_extras:
         if args.no_sharded:
             del dev, out
         torch.cuda.empty_cache()
-        extras = {"cfg3_esim_forward": bench_esim(args), "cfg2_dssm_forward": bench_dssm(args, enc, host)}
+        extras = {"cfg3_esim_forward": guarded(bench_esim, args), "cfg2_dssm_forward": guarded(bench_dssm, args, enc, host)}
     if world == 1 and not args.no_cascade:
-        extras = dict(extras or {}, cfg5_cascade=bench_cascade(args, enc))
+        extras = dict(extras or {}, cfg5_cascade=guarded(bench_cascade, args, enc))
     if world == 1 and not args.no_train:
-        extras = dict(extras or {}, cfg2_dssm_train_step=bench_train(args, specs, multi))
+        extras = dict(extras or {}, cfg2_dssm_train_step=guarded(bench_train, args, specs, multi))
     if world == 1 and not args.no_pipe:
-        extras = dict(extras or {}, feature_pipe=bench_pipe(args, enc, specs, multi))
+        extras = dict(extras or {}, feature_pipe=guarded(bench_pipe, args, enc, specs, multi))
 
     value = args.batch * world * args.steps / elapsed
     line = {
