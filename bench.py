@@ -119,7 +119,15 @@ def main():
     if not args.no_sharded:
         del dev, out
         torch.cuda.empty_cache()
-        sharded = bench_sharded(args, specs, multi, rank, world)
+        if world == 1:
+            try:
+                sharded = bench_sharded(args, specs, multi, rank, world)
+            except Exception as e:  # noqa: BLE001 — the headline line must still print
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+                sharded = {"error": f"{type(e).__name__}: {e}"[:300]}
+        else:
+            sharded = bench_sharded(args, specs, multi, rank, world)
 
     if rank != 0:
         if world > 1:
