@@ -146,6 +146,8 @@ int rf_table_init_uniform(void* table, int32_t dtype, int64_t rows, int32_t dim,
  * stride ex_stride (elements). out: F32 [batch][out_stride], pooled written at out_off.
  * Optional att_out (F32 [batch][2][L][d], may be NULL): att_q then att_a, for tests.
  * Constraints: 1 <= L <= 128, d in {64, 128}.
+ * The max statistic uses IEEE maximum (a NaN element propagates; DESIGN D-esim-max-nan). Without att_out
+ * the 4-wave two-per-CU kernel runs; with it, the 8-wave one.
  */
 int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L,
                                int32_t d, int64_t ex_stride, int64_t ld, float* out, int64_t out_stride,
