@@ -8,7 +8,9 @@
 // registers (IPT per thread, columns t + 1024 j: coalesced loads); a radix select (8 bits a pass, per-wave
 // LDS histograms, early exit once the boundary bin holds exactly the missing count) finds the k-th
 // largest key, the selected keys and the previous top-k are written to LDS and bitonic-sorted, and the
-// best k are the new running top-k. NaN scores are never selected.
+// best k are the new running top-k. NaN scores are never selected. With a full running top-k, keys at or
+// below its k-th entry are dropped on load (they cannot enter), which skips the radix passes for most
+// rows of a long scan.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,15 +46,24 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     const int64_t row = blockIdx.x;
     const float* srow = scores + row * ld;
 
+    // a full running top-k bounds the block: only keys above its k-th entry can enter (keys are unique),
+    // so after the first blocks of a scan most rows select a handful of keys and skip the radix passes
+    uint64_t floor_key = 0ull;
+    if (k_prev >= k) {
+        const int64_t pidx = prev_idx[row * prev_ld + k - 1];
+        const float pv = prev_val[row * prev_ld + k - 1];
+        if (pidx >= 0 && !isnan(pv)) floor_key = ((uint64_t)f2key(pv) << 32) | (uint64_t)(~(uint32_t)pidx);
+    }
     uint64_t key[IPT];
     int nvalid = 0;
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
         const int c = t + kThreads * j;
         const float s = c < cols ? srow[c] : __builtin_nanf("");
-        const bool ok = !isnan(s);
-        key[j] = ok ? ((uint64_t)f2key(s) << 32) | (uint64_t)(~(uint32_t)(col_base + c)) : 0ull;
-        nvalid += ok;
+        uint64_t kv = !isnan(s) ? ((uint64_t)f2key(s) << 32) | (uint64_t)(~(uint32_t)(col_base + c)) : 0ull;
+        if (kv <= floor_key) kv = 0ull;
+        key[j] = kv;
+        nvalid += kv != 0ull;
     }
     // valid count (block reduction)
 #pragma unroll
