@@ -40,6 +40,8 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     __shared__ uint32_t hist[kWavesTopk][256];
     __shared__ uint32_t tot[256];
     __shared__ uint64_t cand[2 * kMaxK];
+    __shared__ uint64_t pk[kMaxK];  // the running top-k as keys
+    __shared__ int s_unsorted;
     __shared__ uint64_t s_prefix, s_mask;
     __shared__ int s_need, s_bin_cnt, s_cnt, s_valid;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -146,42 +148,77 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
         const int64_t pidx = prev_idx[row * prev_ld + i];
         const float pv = prev_val[row * prev_ld + i];
         const bool ok = pidx >= 0 && !isnan(pv);
-        cand[nsel + i] = ok ? ((uint64_t)f2key(pv) << 32) | (uint64_t)(~(uint32_t)pidx) : 0ull;
+        pk[i] = ok ? ((uint64_t)f2key(pv) << 32) | (uint64_t)(~(uint32_t)pidx) : 0ull;
     }
-    int m = nsel + k_prev;
-    int p2 = 1;
-    while (p2 < m) p2 <<= 1;
-    for (int i = m + t; i < p2; i += kThreads) cand[i] = 0ull;
+    if (t == 0) s_unsorted = 0;
+    int p2n = 1;
+    while (p2n < nsel) p2n <<= 1;
+    for (int i = nsel + t; i < p2n; i += kThreads) cand[i] = 0ull;
     __syncthreads();
-    // bitonic sort, descending
-#pragma unroll 1
-    for (int size = 2; size <= p2; size <<= 1) {
-#pragma unroll 1
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = t; i < p2 / 2; i += kThreads) {
-                const int lo = 2 * i - (i & (stride - 1));
-                const int hi = lo + stride;
-                const bool desc = (lo & size) == 0;
-                const uint64_t a = cand[lo], b = cand[hi];
-                if ((a < b) == desc) {
-                    cand[lo] = b;
-                    cand[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int i = t; i < k; i += kThreads) {
-        const uint64_t kv = i < m ? cand[i] : 0ull;
+    for (int i = t; i + 1 < k_prev; i += kThreads)
+        if (pk[i] < pk[i + 1]) s_unsorted = 1;
+    __syncthreads();
+    auto emit = [&](int r, uint64_t kv) {
         float v = -INFINITY;
         int64_t idx = -1;
         if (kv != 0ull) {
             v = key2f((uint32_t)(kv >> 32));
             idx = (int64_t)(~(uint32_t)kv);
         }
-        out_val[row * out_ld + i] = v;
-        out_idx[row * out_ld + i] = idx;
+        out_val[row * out_ld + r] = v;
+        out_idx[row * out_ld + r] = idx;
+    };
+    auto bitonic = [&](uint64_t* a, int n2) {  // descending, n2 a power of two
+#pragma unroll 1
+        for (int size = 2; size <= n2; size <<= 1) {
+#pragma unroll 1
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = t; i < n2 / 2; i += kThreads) {
+                    const int lo = 2 * i - (i & (stride - 1));
+                    const int hi = lo + stride;
+                    const bool desc = (lo & size) == 0;
+                    const uint64_t x = a[lo], y = a[hi];
+                    if ((x < y) == desc) {
+                        a[lo] = y;
+                        a[hi] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    };
+    if (!s_unsorted) {
+        // the running top-k is sorted (this kernel writes it so): sort only the new keys, then every key's
+        // output position is its index plus the number of keys above it in the other list (merge path)
+        bitonic(cand, p2n);
+        auto above = [](const uint64_t* a, int n, uint64_t x) {  // entries of descending a[0..n) above x
+            int lo = 0, hi = n;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (a[mid] > x) lo = mid + 1; else hi = mid;
+            }
+            return lo;
+        };
+        for (int i = t; i < nsel; i += kThreads) {
+            const int r = i + above(pk, k_prev, cand[i]);
+            if (r < k) emit(r, cand[i]);
+        }
+        for (int i = t; i < k_prev; i += kThreads) {
+            const int r = i + above(cand, nsel, pk[i]);
+            if (r < k) emit(r, pk[i]);
+        }
+        for (int i = nsel + k_prev + t; i < k; i += kThreads) emit(i, 0ull);
+        return;
     }
+    // general case: one bitonic sort over the new keys and the running top-k
+    const int m = nsel + k_prev;
+    for (int i = t; i < k_prev; i += kThreads) cand[nsel + i] = pk[i];
+    int p2 = 1;
+    while (p2 < m) p2 <<= 1;
+    for (int i = m + t; i < p2; i += kThreads) cand[i] = 0ull;
+    __syncthreads();
+    bitonic(cand, p2);
+    for (int i = t; i < k; i += kThreads) emit(i, i < m ? cand[i] : 0ull);
 }
 
 }  // namespace

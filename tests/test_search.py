@@ -59,6 +59,39 @@ def test_topk_merge_exact(cuda, cols, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cols,k", [(100, 10), (5000, 100), (32768, 200), (32768, 1024), (3000, 1024)])
+def test_topk_merge_chained(cuda, cols, k):
+    """A running top-k written by the kernel itself (sorted keys: the merge-path branch) folded with a
+    second block, including a row whose second block holds nothing above the running k-th entry."""
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    rng = np.random.default_rng(cols * 7 + k)
+    B = 29
+    s1 = (rng.integers(-50, 50, (B, cols)) * 0.25).astype(np.float32)
+    s2 = (rng.integers(-60, 50, (B, cols)) * 0.25).astype(np.float32)
+    s2[4] = -1e30  # nothing enters
+    s2[7, : min(cols, 9)] = np.nan
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    v1 = torch.empty((B, k), device="cuda")
+    i1 = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    v2, i2 = torch.empty_like(v1), torch.empty_like(i1)
+    d1, d2 = dev(s1), dev(s2)
+    L.call("rf_topk_merge", L.ptr(d1), cols, B, cols, k, 0, None, None, 0, k, L.ptr(v1), L.ptr(i1), k, L.stream_ptr())
+    L.call("rf_topk_merge", L.ptr(d2), cols, B, cols, k, cols, L.ptr(v1), L.ptr(i1), k, k, L.ptr(v2), L.ptr(i2), k,
+           L.stream_ptr())
+    gv, gi = v2.cpu().numpy(), i2.cpu().numpy()
+    for b in range(B):
+        cand = [(float(s1[b, c]), c) for c in range(cols)] + \
+               [(float(s2[b, c]), cols + c) for c in range(cols) if not np.isnan(s2[b, c])]
+        cand.sort(key=lambda x: (-x[0], x[1]))
+        want = cand[:k] + [(-np.inf, -1)] * (k - len(cand[:k]))
+        assert gi[b].tolist() == [w[1] for w in want], b
+        assert gv[b].tolist() == [w[0] for w in want], b
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("measurement", ["ip", "cos"])
 def test_flat_searcher_vs_oracle(cuda, measurement):
     from recommendflow_amd.backend.third_party_components.faiss_searcher import FaissSearcher
