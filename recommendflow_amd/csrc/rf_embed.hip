@@ -233,7 +233,7 @@ extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_sl
     RF_REQUIRE(dim > 0 && dim % epv == 0, "rf_fused_hash_embed_fwd: dim (%d) must be a positive multiple of %d (16-byte rows chunks)", dim, epv);
     RF_REQUIRE(out_stride % epv == 0, "rf_fused_hash_embed_fwd: out_stride must be a multiple of %d", epv);
     RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)out & 15) == 0, "rf_fused_hash_embed_fwd: table/out must be 16-byte aligned");
-    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | 0xF000)) == 0, "rf_fused_hash_embed_fwd: unknown flags");  // 0xF000: reserved diagnostic bits (ablations, general-path A/B)
+    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | 0xF800)) == 0, "rf_fused_hash_embed_fwd: unknown flags");  // 0xF800: reserved diagnostic bits (ablations, A/B switches)
     RF_REQUIRE(table_rows >= 1 && table_rows <= (int64_t)0xffffffff, "rf_fused_hash_embed_fwd: table_rows must be in [1, 2^32) (32-bit row ids in LDS)");
     const int64_t n_units = (int64_t)batch * n_slots;
     if (n_units == 0) return RF_OK;

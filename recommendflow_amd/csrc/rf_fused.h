@@ -165,7 +165,18 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         cidx[cc] = FULL ? c : min(c, nchunks - 1);  // a lane past the row re-reads the last chunk, stores nothing
     }
 
-    for (int64_t item = (int64_t)blockIdx.x * kWaves + wave; item < n_items; item += (int64_t)gridDim.x * kWaves) {
+    // slot-interleaved XCD order (diagnostic, opt-in via flag bit 11; a bijection on the items): work
+    // index v is dealt to XCD v % 8 (round-robin dispatch), and XCD x walks ALL b-blocks of slots x,
+    // x + 8, x + 16, ... so a slot's Zipf-hot rows stay in one XCD's L2. Measured SLOWER than the plain
+    // order on MI355X (cfg3 encoder 0.0676 vs 0.0615 ms, cfg2 0.2626 vs 0.2603 ms), so it is off by default.
+    const int64_t s8_items = (int64_t)(n_slots & ~7) * nbb;
+    const bool xcd_order = (flags & (1 << 11)) != 0;
+    for (int64_t v = (int64_t)blockIdx.x * kWaves + wave; v < n_items; v += (int64_t)gridDim.x * kWaves) {
+        int64_t item = v;
+        if (xcd_order && v < s8_items) {
+            const int64_t x = v & 7, p = v >> 3, jj = p / nbb, bb = p - jj * nbb;
+            item = (x + 8 * jj) * nbb + bb;
+        }
         // ---- slot descriptor: wave-uniform ----
         const int s = (int)(item / nbb);
         const int b0 = (int)(item - (int64_t)s * nbb) * kUnits;

@@ -21,7 +21,8 @@ def main():
     hb = synthetic_batch(B, [False] * Ls, seed=77, slot_ids=range(Ls)).to("cuda")
     out = torch.empty((B, enc.out_width), dtype=torch.bfloat16, device="cuda")
     res = {}
-    for name, fl in (("full", 0), ("general_phase2", 1 << 15), ("no_hash", 1 << 12), ("hash_only", 1 << 13)):
+    for name, fl in (("full", 0), ("general_phase2", 1 << 15), ("xcd_order", 1 << 11), ("no_hash", 1 << 12),
+                     ("hash_only", 1 << 13)):
         enc.extra_flags = fl
 
         def run():
@@ -46,7 +47,8 @@ def main():
     enc2 = FusedSparseEncoder([SlotSpec(f.name, nb, tuple(f.hash_seeds), f.pooling.value) for f in feats], 64, seed=2023)
     hb2 = synthetic_batch(4096, [bool(f.multivalued) for f in feats], seed=1234).to("cuda")
     out2 = torch.empty((4096, enc2.out_width), device="cuda")
-    for name, fl in (("cfg2_full", 0), ("cfg2_general_phase2", 1 << 15)):
+    for name, fl in (("cfg2_full", 0), ("cfg2_general_phase2", 1 << 15), ("cfg2_xcd_order", 1 << 11),
+                     ("cfg2_full_again", 0)):
         enc2.extra_flags = fl
         for _ in range(60):
             enc2(hb2, out=out2)
