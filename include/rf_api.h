@@ -54,6 +54,8 @@ extern "C" {
                                     padded positions gather row 0 and count in sum/avg/max/min
                                     (dataloader.py:32-33 pads with b"" which Hashing maps to bin 0) */
 #define RF_FLAG_EMIT_IDX 0x2     /* also write the two bucket ids of every token to idx_out[2*t + k] */
+/* Bits 0xF800 are reserved diagnostic switches (ablations and A/B orders used by tools/); they never change
+   results. Any other bit returns RF_EINVAL. */
 
 /*
  * One hashed feature ("slot") of a fused multi-slot table.
