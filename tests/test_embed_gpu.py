@@ -124,6 +124,22 @@ def test_fused_embed_single_token_items(O, cuda, tdt, odt, dim, mask_padding):
         np.testing.assert_array_equal(bits(got), bits(gen), err_msg=comb)
 
 
+@pytest.mark.parametrize("extra", [1 << 11, (1 << 11) | (1 << 15)])
+def test_fused_embed_diagnostic_item_order_is_exact(O, cuda, extra):
+    """Diagnostic flag bit 11 (slot-interleaved XCD item order, rf_fused.h) only permutes the items: 19
+    slots (two full groups of 8 plus a plain-order tail), mixed single/multi-valued, B spanning several
+    items — bit-exact vs the oracle and vs the default order."""
+    multi = [s % 3 == 0 for s in range(19)]
+    hb = synthetic_batch(300, multi, seed=11)
+    specs = [SlotSpec(f"f{s}", 50 + 17 * s, (s, 3 + s), COMBS[s % len(COMBS)]) for s in range(19)]
+    enc = FusedSparseEncoder(specs, 32, seed=5)
+    got, ref, _, _ = run_both(O, enc, hb, emit=False)
+    np.testing.assert_array_equal(bits(got), bits(ref))
+    enc.extra_flags = extra
+    alt, _, _, _ = run_both(O, enc, hb, emit=False)
+    np.testing.assert_array_equal(bits(alt), bits(got))
+
+
 def test_double_hashing_embedding_api(O, cuda):
     with pytest.raises(ValueError):
         DoubleHashingEmbedding(0, 8, [1, 2], "sum")
