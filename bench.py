@@ -7,9 +7,13 @@ table (458 segments x 21,834 rows), B = 4096 examples per GPU, synthetic Zipf(1.
 f"s{slot:03d}:{id}" (runtime/batch.synthetic_batch). A step = one rf_fused_hash_embed_fwd over one
 resident CSR batch (inputs in HBM when the timed region starts).
 
-Multi-GPU: one process per GPU (torchrun); each rank holds a replica of the 2.56 GB table and its own
-batches (the reference mirrors tables per GPU, gpu_utils.py:13-14): no data-path collective, weak
-scaling; value = examples of all ranks / max-over-ranks time.
+Multi-GPU: one process per GPU; each rank holds a replica of the 2.56 GB table and its own batches (the
+reference mirrors tables per GPU, gpu_utils.py:13-14): no data-path collective, weak scaling; value =
+examples of all ranks / max-over-ranks time. `--gpus N` without a torchrun environment starts the N
+ranks itself (a torch.distributed.run child, launched before this process touches the GPU), like
+MirroredStrategy using every visible GPU without a launcher (gpu_utils.py:13-14). Under torchrun the
+world size must equal --gpus. `--device cpu --backend gloo` is a dry run of that launcher and of the
+barrier / max-over-ranks timing with a no-op step (no GPU, no kernels; the line says "dry_run").
 
 Also reported: roofline of the fused kernel (algorithmic bytes / HIP-event kernel time vs 8 TB/s),
 PMC-measured HBM traffic when profiles/ holds it for this workload, and the CPU baseline (the C
@@ -31,7 +35,9 @@ TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_cfg2.json")
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); started here unless torchrun set WORLD_SIZE")
+    p.add_argument("--device", choices=("cuda", "cpu"), default="cuda", help="cpu = launcher dry run (no kernels)")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default=None, help="process-group backend (default: nccl on cuda)")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=50, help="untimed launches: the clocks and the hot-row cache settle over ~50")
     p.add_argument("--batch", type=int, default=4096)
@@ -55,18 +61,75 @@ def parse():
     return p.parse_args()
 
 
+def launch(args) -> int:
+    """Start args.gpus ranks as a torch.distributed.run CHILD (never exec: this process has not touched
+    the GPU, and it only relays the child's exit code). Rank 0 of the child prints the JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """--device cpu: the launcher and timing protocol with a no-op step (gloo). Proves every rank ran
+    (all_gather of the ranks) and that value / n_gpus aggregate over the world."""
+    import torch
+    import torch.distributed as dist
+
+    for _ in range(args.warmup):
+        pass
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    ranks = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_gather(ranks, torch.tensor([rank], dtype=torch.int64))
+    elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(args.batch * world * args.steps / elapsed, 1),
+                          "unit": "examples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "dry_run": True,
+                          "ranks_reported": [int(r.item()) for r in ranks] if world > 1 else [0],
+                          "dist_world_size": dist.get_world_size() if world > 1 else 1}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+                         f"{world}-rank number as an {args.gpus}-GPU point")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = args.backend or ("nccl" if args.device == "cuda" else "gloo")
+    if args.device == "cpu":
+        if world > 1:
+            dist.init_process_group(backend)
+        return dry_run(args, world, rank)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == world == args.gpus
 
     from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
     from recommendflow_amd.config_parser.configuration import Configuration
@@ -172,6 +235,7 @@ def main():
         "value": round(value, 1),
         "unit": "examples/s",
         "n_gpus": world,
+        "dist_world_size": dist.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -54,8 +54,11 @@ extern "C" {
                                     padded positions gather row 0 and count in sum/avg/max/min
                                     (dataloader.py:32-33 pads with b"" which Hashing maps to bin 0) */
 #define RF_FLAG_EMIT_IDX 0x2     /* also write the two bucket ids of every token to idx_out[2*t + k] */
-/* Bits 0xF800 are reserved diagnostic switches (ablations and A/B orders used by tools/); they never change
-   results. Any other bit returns RF_EINVAL. */
+#define RF_FLAG_DIAG_XCD_ORDER 0x0800      /* A/B switch: slot-interleaved XCD item order (measured slower); results identical */
+#define RF_FLAG_DIAG_GENERAL_PHASE2 0x8000 /* A/B switch: force the general pooling path for Lmax = 1 slots; results identical */
+/* Only these two result-preserving switches are accepted here; any other bit returns RF_EINVAL. Bits 12-14
+   are ablations that CHANGE results (synthetic rows instead of the hash, no pooling, no padding) and are
+   accepted only by rf_diag_fused_hash_embed_fwd (include/rf_diag.h, tools only, not part of this ABI). */
 
 /*
  * One hashed feature ("slot") of a fused multi-slot table.

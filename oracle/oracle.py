@@ -408,6 +408,55 @@ def sdpa(q, k, v, mask=None):
     return (e / e.sum(axis=-1, keepdims=True)) @ v
 
 
+def positional_encoding(length: int, dim: int) -> np.ndarray:
+    """SelfAttention.get_angles / positional_encoding (attention_layers.py:126-134): angle = pos /
+    10000^(2*(i//2) / float32(dim)) in float64, sin on even columns, cos on odd, cast to float32."""
+    pos = np.arange(length)[:, None]
+    i = np.arange(dim)[None, :]
+    ang = pos * (1 / np.power(10000, (2 * (i // 2)) / np.float32(dim)))
+    ang[:, 0::2] = np.sin(ang[:, 0::2])
+    ang[:, 1::2] = np.cos(ang[:, 1::2])
+    return ang.astype(np.float32)
+
+
+def self_attention(q, k, v, mask, W, add_pos=True):
+    """SelfAttention.call (attention_layers.py:98-124): q,k += PE (float32, :101-103); q' = relu(q W),
+    k' = relu(k W) with the ONE shared W (:105-106); logits = q' k'^T / sqrt(dim) (:107-110); mask [B, L, 1]
+    tiled over the keys (:112), rows with mask == 0 become -2^32 + 1 (:113-114); softmax over keys (:116),
+    @ v (:118, v untouched by PE and W), mean over the sequence axis (:119) -> [B, dim]."""
+    q = np.asarray(q, np.float32)
+    k = np.asarray(k, np.float32)
+    dim = q.shape[-1]
+    if add_pos:
+        k = k + positional_encoding(k.shape[1], dim)
+        q = q + positional_encoding(q.shape[1], dim)
+    W = np.asarray(W, np.float64)
+    qn = np.maximum(q.astype(np.float64) @ W, 0.0)
+    kn = np.maximum(k.astype(np.float64) @ W, 0.0)
+    logits = qn @ np.swapaxes(kn, -1, -2) / math.sqrt(float(np.float32(dim)))
+    if mask is not None:
+        m = np.asarray(mask).reshape(q.shape[0], q.shape[1])[:, :, None]
+        logits = np.where(m == 0, -4294967295.0, logits)
+    e = np.exp(logits - logits.max(axis=-1, keepdims=True))
+    out = (e / e.sum(axis=-1, keepdims=True)) @ np.asarray(v, np.float64)
+    return out.mean(axis=1)
+
+
+def multi_head_attention(q, k, v, mask, Wq, bq, Wk, bk, Wv, bv, heads: int):
+    """MultiHeadAttention.call (attention_layers.py:153-168): Dense q/k/v with bias, W as [in, d_model] (:148-150,
+    :154-156); split_heads (layer_utils.py:27-38) -> [B, h, L, depth]; mask [B, L, 1] tiled over heads (:161);
+    scaled_dot_product_attention (layer_utils.py:4-24, row-mask); merge heads (:166-167); NO output projection."""
+    f = lambda x, W, b: np.asarray(x, np.float64) @ np.asarray(W, np.float64) + np.asarray(b, np.float64)
+    qp, kp, vp = f(q, Wq, bq), f(k, Wk, bk), f(v, Wv, bv)
+    B, Lq, dm = qp.shape
+    Lk = kp.shape[1]
+    depth = dm // heads
+    split = lambda x, Ln: x.reshape(B, Ln, heads, depth).transpose(0, 2, 1, 3)
+    m = None if mask is None else np.broadcast_to(np.asarray(mask).reshape(B, 1, Lq), (B, heads, Lq))
+    o = sdpa(split(qp, Lq), split(kp, Lk), split(vp, Lk), m)
+    return o.transpose(0, 2, 1, 3).reshape(B, Lq, dm)
+
+
 def l2_normalize(x, eps=1e-12):
     """K.l2_normalize (dssm.py:35-36): x / sqrt(max(sum x^2, eps))."""
     x = np.asarray(x, np.float64)

@@ -109,7 +109,7 @@ class FusedSparseEncoder(torch.nn.Module):
         self.out_dtype = out_dtype or table_dtype
         self.mask_padding = bool(mask_padding)
         self.seed = int(seed)
-        self.extra_flags = 0  # reserved tuning bits of rf_fused_hash_embed_fwd (diagnostics)
+        self.extra_flags = 0  # diagnostic bits (rf_api.h RF_FLAG_DIAG_*; ablations 12-14 go to rf_diag_fused_hash_embed_fwd)
         desc = np.zeros(len(self.slots), SLOT_DTYPE)
         base = int(row_base0)
         for i, sp in enumerate(self.slots):
@@ -158,7 +158,8 @@ class FusedSparseEncoder(torch.nn.Module):
             raise ValueError("out_col is reserved; pass a column slice through the descriptors instead")
         flags = (L.FLAG_MASK_PADDING if self.mask_padding else 0) | (L.FLAG_EMIT_IDX if emit_idx else 0) | self.extra_flags
         idx = torch.empty((max(batch.n_tokens, 1), 2), dtype=torch.int64, device=self.table.device) if emit_idx else None
-        L.call("rf_fused_hash_embed_fwd", L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes),
+        entry = "rf_diag_fused_hash_embed_fwd" if self.extra_flags & L.DIAG_ABLATIONS else "rf_fused_hash_embed_fwd"
+        L.call(entry, L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes),
                L.ptr(batch.tok_off), L.ptr(batch.bag_off), L.ptr(batch.lmax), B, L.ptr(self.table),
                L.torch_dtype_code(self.table.dtype), self.table.shape[0], self.dim, L.ptr(out),
                L.torch_dtype_code(out.dtype), out.stride(0), flags, L.ptr(idx), L.stream_ptr(stream))

@@ -4,9 +4,14 @@
   (attention_layers.py:15-74 + models/ranking/esim.py:79-84) -> [B, 6d] fp32, in one launch.
 * ``SoftAttention()([a, b]) -> (align_a, align_b)`` — the reference callable (:10-80); same kernel with the
   aligned sequences written out.
-* ``MultiHeadAttention(d_model, num_heads).call(q, k, v, mask)`` (:137-168): Dense q/k/v (rf_linear_fwd),
-  then rf_sdpa_fwd with split_heads/merge folded into addressing; no output projection (as the reference).
-* ``SelfAttention(add_pos)([q, k, v, mask])`` (:83-134): sinusoid PE, shared relu(xW), masked SDPA, mean.
+* ``MultiHeadAttention(d_model, num_heads).call(q, k, v, mask)`` (:137-168): Dense q/k/v with bias in fp32
+  (the reference's Dense dtype; exact-fp32 MFMA, rf_linear_fwd), then rf_sdpa_fwd with split_heads/merge
+  folded into addressing; no output projection (as the reference).
+* ``SelfAttention(add_pos)([q, k, v, mask])`` (:83-134): sinusoid PE, shared relu(xW) in fp32, masked SDPA,
+  mean over the sequence.
+Both run the attention core (QK^T, softmax, PV) with `dtype` (fp16 by default, cfg5's "fp16 MFMA
+attention") operands and fp32 logits/softmax/accumulation; tests/test_attention_gpu.py states the
+tolerance against the float64 oracle.
 """
 from __future__ import annotations
 
@@ -60,15 +65,17 @@ class SoftAttention:
 
 
 class MultiHeadAttention(torch.nn.Module):
-    def __init__(self, d_model: int, num_heads: int, dtype=torch.float16, seed: int = 0, device="cuda"):
+    def __init__(self, d_model: int, num_heads: int, dtype=torch.float16, seed: int = 0, device="cuda",
+                 proj_dtype=torch.float32, in_features: Optional[int] = None):
         super().__init__()
         if d_model % num_heads:
             raise ValueError("d_model must be divisible by num_heads")
         self.d_model, self.num_heads = d_model, num_heads
         self.dtype = dtype
-        self.wq = Dense(d_model, d_model, activation=None, seed=seed + 1, device=device)
-        self.wk = Dense(d_model, d_model, activation=None, seed=seed + 2, device=device)
-        self.wv = Dense(d_model, d_model, activation=None, seed=seed + 3, device=device)
+        k_in = in_features or d_model
+        self.wq = Dense(k_in, d_model, activation=None, dtype=proj_dtype, seed=seed + 1, device=device)
+        self.wk = Dense(k_in, d_model, activation=None, dtype=proj_dtype, seed=seed + 2, device=device)
+        self.wv = Dense(k_in, d_model, activation=None, dtype=proj_dtype, seed=seed + 3, device=device)
 
     def call(self, q, k, v, mask=None):
         B, Lq, _ = q.shape
@@ -96,7 +103,8 @@ class SelfAttention(torch.nn.Module):
         self.dim = dim
         g = torch.Generator().manual_seed(self.seed)
         w = torch.randn((dim, dim), generator=g) * 0.05  # keras 'random_normal' (stddev 0.05)
-        self.W = Dense(dim, dim, activation="relu", use_bias=False, device=self.device, weight=w.T.contiguous())
+        self.W = Dense(dim, dim, activation="relu", use_bias=False, dtype=torch.float32, device=self.device,
+                       weight=w.T.contiguous())
 
     @staticmethod
     def positional_encoding(length: int, dim: int) -> np.ndarray:

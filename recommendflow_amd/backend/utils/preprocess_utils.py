@@ -6,7 +6,8 @@ LookupEmbedding, discrete -> DiscreteEmbedding, bert_encode -> BertEncode, other
 
 MI355X addition: the hashing features of each tower share ONE fused table and ONE fused encoder
 (``layers.encoders[tower]``) so a model runs a whole tower in one kernel launch; the per-feature
-DoubleHashingEmbedding entries are views into that table (same rows, same results).
+DoubleHashingEmbedding entries are views into that table (same rows, same results). A tower whose
+hashing features mix embedding dims gets one fused encoder per dim, keyed ``"tower:dim"``.
 """
 from __future__ import annotations
 
@@ -20,7 +21,8 @@ from ..layers.preprocess_layers import BertEncode, DiscreteEmbedding, DoubleHash
 
 
 class PreprocessLayers(dict):
-    """dict name -> operator, plus ``encoders`` (tower -> FusedSparseEncoder) and ``slots`` (tower -> names)."""
+    """dict name -> operator, plus ``encoders`` (tower, or "tower:dim" for a mixed-dim tower -> FusedSparseEncoder)
+    and ``slots`` (same key -> feature names in the tower's column order)."""
 
     def __init__(self):
         super().__init__()
@@ -38,23 +40,27 @@ def get_preprocess_layers(conf: Configuration, table_dtype=torch.float32, out_dt
     for f in hashing:
         if fused and f.pooling.value != "null":
             groups.setdefault(f.tower.value, []).append(f)
-    for ti, (tower, feats) in enumerate(groups.items()):
-        dims = {dim_override or f.embedding_dim for f in feats}
-        if len(dims) != 1:  # one launch per dim; split the tower by dim
-            raise NotImplementedError("a tower's hashing features must share one embedding_dim for the fused encoder")
-        dim = dims.pop()
-        specs = [SlotSpec(f.name, num_bins_override or f.vocab_size, normalize_seeds(f.hash_seeds), f.pooling.value, True)
-                 for f in feats]
-        enc = FusedSparseEncoder(specs, dim, table_dtype=table_dtype, out_dtype=out_dtype, seed=seed + 7919 * ti,
-                                 mask_padding=mask_padding, device=device)
-        layers.encoders[tower] = enc
-        layers.slots[tower] = [f.name for f in feats]
-        for i, f in enumerate(feats):
-            built[f.name] = DoubleHashingEmbedding(
-                num_bins=specs[i].num_bins, output_dim=dim, seeds=f.hash_seeds, mask_value="", mask_zero=True,
-                combiner=f.pooling.value, name=f"hashing_{f.name}", dtype=table_dtype, out_dtype=out_dtype,
-                mask_padding=mask_padding, device=device, table=enc.table,
-                row_base=int(enc.host_desc[i]["row_base"][0]))
+    ti = 0
+    for tower, tfeats in groups.items():
+        # one fused launch per (tower, embedding_dim): a tower whose features mix dims gets one encoder per
+        # dim, keyed "tower:dim" (a single-dim tower keeps the key "tower")
+        dims = sorted({dim_override or f.embedding_dim for f in tfeats})
+        for dim in dims:
+            feats = [f for f in tfeats if (dim_override or f.embedding_dim) == dim]
+            key = tower if len(dims) == 1 else f"{tower}:{dim}"
+            specs = [SlotSpec(f.name, num_bins_override or f.vocab_size, normalize_seeds(f.hash_seeds), f.pooling.value,
+                              True) for f in feats]
+            enc = FusedSparseEncoder(specs, dim, table_dtype=table_dtype, out_dtype=out_dtype, seed=seed + 7919 * ti,
+                                     mask_padding=mask_padding, device=device)
+            ti += 1
+            layers.encoders[key] = enc
+            layers.slots[key] = [f.name for f in feats]
+            for i, f in enumerate(feats):
+                built[f.name] = DoubleHashingEmbedding(
+                    num_bins=specs[i].num_bins, output_dim=dim, seeds=f.hash_seeds, mask_value="", mask_zero=True,
+                    combiner=f.pooling.value, name=f"hashing_{f.name}", dtype=table_dtype, out_dtype=out_dtype,
+                    mask_padding=mask_padding, device=device, table=enc.table,
+                    row_base=int(enc.host_desc[i]["row_base"][0]))
     for f in conf.train_features:  # reference order (preprocess_utils.py:9)
         if f.name in built:
             layers[f.name] = built[f.name]

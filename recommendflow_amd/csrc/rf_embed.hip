@@ -221,7 +221,7 @@ extern "C" int rf_siphash_bucket(const uint8_t* tok_bytes, const int32_t* tok_of
     return rf_check_launch("siphash_bucket_kernel");
 }
 
-extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+static int fused_hash_embed_fwd_impl(uint32_t allowed_diag, const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
                                        const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
                                        int32_t batch, const void* table, int32_t table_dtype, int64_t table_rows,
                                        int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
@@ -233,7 +233,9 @@ extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_sl
     RF_REQUIRE(dim > 0 && dim % epv == 0, "rf_fused_hash_embed_fwd: dim (%d) must be a positive multiple of %d (16-byte rows chunks)", dim, epv);
     RF_REQUIRE(out_stride % epv == 0, "rf_fused_hash_embed_fwd: out_stride must be a multiple of %d", epv);
     RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)out & 15) == 0, "rf_fused_hash_embed_fwd: table/out must be 16-byte aligned");
-    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | 0xF800)) == 0, "rf_fused_hash_embed_fwd: unknown flags");  // 0xF800: reserved diagnostic bits (ablations, A/B switches)
+    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | (int32_t)allowed_diag)) == 0,
+               "rf_fused_hash_embed_fwd: unknown flags (result-changing ablation bits 12-14 are only accepted by "
+               "rf_diag_fused_hash_embed_fwd)");
     RF_REQUIRE(table_rows >= 1 && table_rows <= (int64_t)0xffffffff, "rf_fused_hash_embed_fwd: table_rows must be in [1, 2^32) (32-bit row ids in LDS)");
     const int64_t n_units = (int64_t)batch * n_slots;
     if (n_units == 0) return RF_OK;
@@ -243,6 +245,27 @@ extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_sl
     hipStream_t st = rf_stream(stream);
     return launch_fused_any(false, table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,
                             table, table_rows, dim, out, out_stride, flags, idx_out, grid, st);
+}
+
+extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                       const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                                       int32_t batch, const void* table, int32_t table_dtype, int64_t table_rows,
+                                       int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
+                                       int64_t* idx_out, void* stream) {
+    // public ABI: only the result-preserving switches (bit 11 XCD item order, bit 15 general phase 2)
+    return fused_hash_embed_fwd_impl(RF_FLAG_DIAG_XCD_ORDER | RF_FLAG_DIAG_GENERAL_PHASE2, d_slots, n_slots, tok_bytes,
+                                     tok_off, bag_off, lmax, batch, table, table_dtype, table_rows, dim, out, out_dtype,
+                                     out_stride, flags, idx_out, stream);
+}
+
+extern "C" int rf_diag_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                            const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                                            int32_t batch, const void* table, int32_t table_dtype, int64_t table_rows,
+                                            int32_t dim, void* out, int32_t out_dtype, int64_t out_stride,
+                                            int32_t flags, int64_t* idx_out, void* stream) {
+    // tools only (include/rf_diag.h): additionally accepts the ablation bits 12-14, which CHANGE results
+    return fused_hash_embed_fwd_impl(0xF800u, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, batch, table,
+                                     table_dtype, table_rows, dim, out, out_dtype, out_stride, flags, idx_out, stream);
 }
 
 extern "C" int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,

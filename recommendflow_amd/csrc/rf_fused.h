@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
     const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
     const bool emit = (flags & RF_FLAG_EMIT_IDX) != 0 && idx_out != nullptr;
     const bool abl_nohash = (flags & (1 << 12)) != 0, abl_nopool = (flags & (1 << 13)) != 0,
-               abl_nopad = (flags & (1 << 14)) != 0;  // diagnostic ablations (tools/kbench.py)
+               abl_nopad = (flags & (1 << 14)) != 0;  // result-changing ablations: rf_diag_fused_hash_embed_fwd only (include/rf_diag.h)
     const bool no_lean = (flags & (1 << 15)) != 0;  // A/B: force the general phase 2 on single-token items
     // rf_pool_rows_fwd: `table` holds pre-gathered rows (token t, table k -> row 2t + k; pad rows after)
     constexpr bool pregathered = PRE;

@@ -8,9 +8,9 @@
 // registers (IPT per thread, columns t + 1024 j: coalesced loads); a radix select (8 bits a pass, per-wave
 // LDS histograms, early exit once the boundary bin holds exactly the missing count) finds the k-th
 // largest key, the selected keys and the previous top-k are written to LDS and bitonic-sorted, and the
-// best k are the new running top-k. NaN scores are never selected. With a full running top-k, keys at or
-// below its k-th entry are dropped on load (they cannot enter), which skips the radix passes for most
-// rows of a long scan.
+// best k are the new running top-k. NaN scores are never selected. With a full running top-k that is
+// sorted (as this kernel writes it), keys at or below its k-th entry are dropped on load (they cannot
+// enter), which skips the radix passes for most rows of a long scan; an unsorted running set gets no floor.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,14 +48,22 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     const int64_t row = blockIdx.x;
     const float* srow = scores + row * ld;
 
-    // a full running top-k bounds the block: only keys above its k-th entry can enter (keys are unique),
-    // so after the first blocks of a scan most rows select a handful of keys and skip the radix passes
-    uint64_t floor_key = 0ull;
-    if (k_prev >= k) {
-        const int64_t pidx = prev_idx[row * prev_ld + k - 1];
-        const float pv = prev_val[row * prev_ld + k - 1];
-        if (pidx >= 0 && !isnan(pv)) floor_key = ((uint64_t)f2key(pv) << 32) | (uint64_t)(~(uint32_t)pidx);
+    // previous running top-k as keys (entries with index -1 are empty), and whether it is sorted
+    if (t == 0) s_unsorted = 0;
+    for (int i = t; i < k_prev; i += kThreads) {
+        const int64_t pidx = prev_idx[row * prev_ld + i];
+        const float pv = prev_val[row * prev_ld + i];
+        const bool ok = pidx >= 0 && !isnan(pv);
+        pk[i] = ok ? ((uint64_t)f2key(pv) << 32) | (uint64_t)(~(uint32_t)pidx) : 0ull;
     }
+    __syncthreads();
+    for (int i = t; i + 1 < k_prev; i += kThreads)
+        if (pk[i] < pk[i + 1]) s_unsorted = 1;
+    __syncthreads();
+    // a full, SORTED running top-k bounds the block: only keys above its k-th entry can enter (keys are
+    // unique), so after the first blocks of a scan most rows select a handful of keys and skip the radix
+    // passes. An unsorted `prev` (any set, per rf_api.h) has no cheap k-th entry: no floor then.
+    const uint64_t floor_key = (k_prev >= k && !s_unsorted) ? pk[k - 1] : 0ull;
     uint64_t key[IPT];
     int nvalid = 0;
 #pragma unroll
@@ -143,20 +151,9 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     }
     __syncthreads();
     const int nsel = s_cnt;
-    // previous running top-k (entries with index -1 are empty)
-    for (int i = t; i < k_prev; i += kThreads) {
-        const int64_t pidx = prev_idx[row * prev_ld + i];
-        const float pv = prev_val[row * prev_ld + i];
-        const bool ok = pidx >= 0 && !isnan(pv);
-        pk[i] = ok ? ((uint64_t)f2key(pv) << 32) | (uint64_t)(~(uint32_t)pidx) : 0ull;
-    }
-    if (t == 0) s_unsorted = 0;
     int p2n = 1;
     while (p2n < nsel) p2n <<= 1;
     for (int i = nsel + t; i < p2n; i += kThreads) cand[i] = 0ull;
-    __syncthreads();
-    for (int i = t; i + 1 < k_prev; i += kThreads)
-        if (pk[i] < pk[i + 1]) s_unsorted = 1;
     __syncthreads();
     auto emit = [&](int r, uint64_t kv) {
         float v = -INFINITY;

@@ -100,7 +100,8 @@ class TrainableDssm(torch.nn.Module):
     def step(self, batch: SparseBatch, labels: torch.Tensor, dp=None) -> torch.Tensor:
         """One training step; `dp` (runtime.dist.DataParallel) = MirroredStrategy-style replicas: the
         loss is scaled by 1/P, dense gradients are SUM-all-reduced in buckets and the table's sparse
-        gradients all-gathered and summed in rank order before the (identical) optimizer steps."""
+        gradients all-gathered and summed in rank order before the (identical) optimizer steps; the
+        BatchNorm moving statistics are then averaged over the replicas (DataParallel.sync_buffers)."""
         self.train()
         self.dense_opt.zero_grad(set_to_none=True)
         u, v = self(batch)
@@ -112,4 +113,6 @@ class TrainableDssm(torch.nn.Module):
             sg = dp.allgather_sparse(sg, self.enc.table_rows)
         self.sparse_opt.apply(sg)
         self.dense_opt.step()
+        if dp is not None:  # BN moving statistics: ON_READ / MEAN across replicas (MirroredStrategy)
+            dp.sync_buffers([self.user_tower, self.ad_tower])
         return loss.detach()

@@ -12,7 +12,10 @@ one process per GPU over torch.distributed (RCCL over xGMI on the GPU box, gloo 
   (counts first, then rows and gradients padded to the largest count) and summed per row in rank order
   0..P-1 with rf_segment_sum_rows — the IndexedSlices all-gather + sum of MirroredStrategy with a
   defined order (deviation D-sharded-grad-order). Every rank then applies the same Adam
-  step to its replica, so the replicas stay bit-identical.
+  step to its replica, so the replicas' PARAMETERS stay bit-identical;
+* non-trainable state (BatchNorm moving mean / variance): MirroredStrategy keeps these as ON_READ
+  variables with MEAN aggregation, so `sync_buffers` all-reduces every floating buffer and divides by
+  P after each step. Without it each replica's moving statistics would follow its own local batches.
 
 `loss_scale()` = 1 / P turns the per-replica mean loss into the reference's per-replica
 sum / global_batch (equal per-replica batches).
@@ -73,6 +76,23 @@ class DataParallel:
                 g.copy_(flat[off: off + n].view_as(g))
                 off += n
         return len(buckets)
+
+    def sync_buffers(self, modules: Iterable[torch.nn.Module]) -> int:
+        """MEAN-all-reduce every floating-point buffer (BatchNorm running_mean / running_var) so rank-local
+        eval and checkpoints agree; integer buffers (num_batches_tracked) advance identically on every rank
+        and are left alone. Returns the number of buffers synced."""
+        bufs = [b for m in modules for b in m.buffers() if b.is_floating_point()]
+        if not bufs or self.world == 1:
+            return len(bufs)
+        flat = torch.cat([b.reshape(-1).float() for b in bufs])
+        self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
+        flat /= self.world
+        off = 0
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off: off + n].view_as(b))
+            off += n
+        return len(bufs)
 
     # -- sparse -----------------------------------------------------------------------------------
     def allgather_sparse(self, sg: SparseGrad, table_rows: int) -> SparseGrad:

@@ -62,6 +62,10 @@ _SIGS = {
     "rf_topk_merge": (ctypes.c_int, [_vp, _i64, _i32, _i32, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _i64, _vp]),
 }
 EXPORTED = tuple(_SIGS)
+# include/rf_diag.h: tools-only entry points (not the production ABI)
+_DIAG_SIGS = {"rf_diag_fused_hash_embed_fwd": _SIGS["rf_fused_hash_embed_fwd"]}
+DIAG_EXPORTED = tuple(_DIAG_SIGS)
+DIAG_ABLATIONS = 0x7000  # bits 12-14: accepted only by rf_diag_fused_hash_embed_fwd
 
 
 class RFError(RuntimeError):
@@ -77,7 +81,7 @@ def load(path: str = LIB_PATH):
         if not os.path.exists(path):
             raise RFError(f"librf.so not found at {path}: build it first (make -C recommendflow_amd/csrc)")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
-        for name, (res, args) in _SIGS.items():
+        for name, (res, args) in list(_SIGS.items()) + list(_DIAG_SIGS.items()):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -63,3 +63,40 @@ def test_gloo_world2_dense_and_sparse(O, tmp_path):
         assert float(z["scale"]) == 0.5
         np.testing.assert_array_equal(z["rows"], want_rows)
         np.testing.assert_array_equal(z["grad"].view(np.uint32), want_grad.view(np.uint32))
+
+
+def buffer_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    from recommendflow_amd.runtime.dist import DataParallel
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        dp = DataParallel(ops=OracleShardOps())
+        bn = torch.nn.BatchNorm1d(6, eps=1e-6, momentum=0.01).train()
+        x = torch.randn(32, 6, generator=torch.Generator().manual_seed(7 + rank)) * (1 + rank)
+        bn(x)  # rank-local moving statistics
+        local = [bn.running_mean.clone(), bn.running_var.clone()]
+        n = dp.sync_buffers([bn])
+        np.savez(os.path.join(out_dir, f"b{rank}.npz"), lm=local[0].numpy(), lv=local[1].numpy(),
+                 m=bn.running_mean.numpy(), v=bn.running_var.numpy(), n=np.array(n),
+                 t=np.array(int(bn.num_batches_tracked)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bn_buffers_mean(tmp_path):
+    """BatchNorm moving statistics are MEAN-aggregated over replicas (MirroredStrategy ON_READ/MEAN):
+    after sync every rank holds the same buffers, equal to the mean of the rank-local ones."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(buffer_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    z = [np.load(tmp_path / f"b{r}.npz") for r in range(2)]
+    assert not np.array_equal(z[0]["lm"], z[1]["lm"])  # the ranks really diverged before the sync
+    for r in range(2):
+        assert int(z[r]["n"]) == 2 and int(z[r]["t"]) == 1
+        np.testing.assert_allclose(z[r]["m"], (z[0]["lm"] + z[1]["lm"]) / 2, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(z[r]["v"], (z[0]["lv"] + z[1]["lv"]) / 2, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(z[0]["m"], z[1]["m"])
+    np.testing.assert_array_equal(z[0]["v"], z[1]["v"])

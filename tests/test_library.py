@@ -8,8 +8,8 @@ from recommendflow_amd.runtime import lib as L
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "rf_api.h")).read()
+def declared_symbols(header="rf_api.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(rf_[a-z0-9_]+)\s*\(", src)))
 
@@ -25,6 +25,22 @@ def test_library_exports_every_declared_symbol():
     for s in declared_symbols():
         assert hasattr(lib, s), s
     assert lib.rf_abi_version() == 1
+
+
+def test_diag_header_exports():
+    lib = L.load()
+    syms = declared_symbols("rf_diag.h")
+    assert set(syms) == set(L.DIAG_EXPORTED)
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_public_entry_rejects_ablation_bits():
+    """Bits 12-14 change results: the production entry refuses them (validation precedes any HIP call)."""
+    lib = L.load()
+    for bit in (1 << 12, 1 << 13, 1 << 14, 1 << 10):
+        rc = lib.rf_fused_hash_embed_fwd(None, 1, None, None, None, None, 4, None, 0, 10, 16, None, 0, 16, bit, None, None)
+        assert rc == L.RF_EINVAL and b"flags" in lib.rf_last_error(), bit
 
 
 def test_argument_errors_without_gpu():

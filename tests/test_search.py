@@ -29,6 +29,41 @@ def test_recall_metrics_formula():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cols,k,k_prev", [(1, 2, 2), (100, 10, 10), (3000, 64, 200), (40, 8, 8)])
+def test_topk_merge_unsorted_prev(cuda, cols, k, k_prev):
+    """`prev` is any set (rf_api.h): an UNSORTED running list with k_prev >= k must not floor out new keys
+    that belong in the top-k (k=2, prev={1,5}, new 3 -> {5,3})."""
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    rng = np.random.default_rng(cols * 7 + k)
+    B = 9
+    s = rng.standard_normal((B, cols)).astype(np.float32)
+    prev_v = rng.standard_normal((B, k_prev)).astype(np.float32)
+    prev_i = (rng.permutation(10 ** 6)[: B * k_prev].reshape(B, k_prev) + 10 ** 7).astype(np.int64)
+    # rows 0/1: ascending (worst case for a floor read from position k-1); others: shuffled
+    prev_v[0] = np.sort(prev_v[0])
+    prev_v[1] = np.sort(prev_v[1])
+    if cols == 1:  # the advisor's case: prev {1, 5}, new score 3
+        prev_v[:, :2] = [1.0, 5.0]
+        s[:, 0] = 3.0
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ov = torch.empty((B, k), device="cuda")
+    oi = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    L.call("rf_topk_merge", L.ptr(dev(s)), cols, B, cols, k, 0, L.ptr(dev(prev_v)), L.ptr(dev(prev_i)), k_prev, k_prev,
+           L.ptr(ov), L.ptr(oi), k, L.stream_ptr())
+    gv, gi = ov.cpu().numpy(), oi.cpu().numpy()
+    for b in range(B):
+        cand = [(float(s[b, c]), c) for c in range(cols)] + [(float(prev_v[b, j]), int(prev_i[b, j])) for j in range(k_prev)]
+        cand.sort(key=lambda x: (-x[0], x[1]))
+        assert gi[b].tolist() == [w[1] for w in cand[:k]], b
+        assert gv[b].tolist() == [w[0] for w in cand[:k]], b
+    if cols == 1:
+        assert gv[0].tolist() == [5.0, 3.0]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cols,k", [(1, 1), (100, 10), (5000, 100), (32768, 1024), (700, 1024)])
 def test_topk_merge_exact(cuda, cols, k):
     import torch

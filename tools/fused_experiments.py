@@ -29,7 +29,7 @@ def main():
     out = torch.empty((B, enc.out_width), device="cuda")
 
     def run(desc, o, stride, flags=0):
-        L.call("rf_fused_hash_embed_fwd", L.ptr(desc), S, L.ptr(db.tok_bytes), L.ptr(db.tok_off), L.ptr(db.bag_off),
+        L.call("rf_diag_fused_hash_embed_fwd", L.ptr(desc), S, L.ptr(db.tok_bytes), L.ptr(db.tok_off), L.ptr(db.bag_off),
                L.ptr(db.lmax), B, L.ptr(enc.table), 0, enc.table.shape[0], D, L.ptr(o), 0, stride, flags, None,
                L.stream_ptr())
 
