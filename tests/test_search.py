@@ -51,8 +51,12 @@ def test_topk_merge_unsorted_prev(cuda, cols, k, k_prev):
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     ov = torch.empty((B, k), device="cuda")
     oi = torch.empty((B, k), dtype=torch.int64, device="cuda")
-    L.call("rf_topk_merge", L.ptr(dev(s)), cols, B, cols, k, 0, L.ptr(dev(prev_v)), L.ptr(dev(prev_i)), k_prev, k_prev,
+    # keep the device copies alive until the kernel has run (an inline temporary is freed at once and
+    # its block handed to the next argument by the caching allocator)
+    ds, pv, pi = dev(s), dev(prev_v), dev(prev_i)
+    L.call("rf_topk_merge", L.ptr(ds), cols, B, cols, k, 0, L.ptr(pv), L.ptr(pi), k_prev, k_prev,
            L.ptr(ov), L.ptr(oi), k, L.stream_ptr())
+    torch.cuda.synchronize()
     gv, gi = ov.cpu().numpy(), oi.cpu().numpy()
     for b in range(B):
         cand = [(float(s[b, c]), c) for c in range(cols)] + [(float(prev_v[b, j]), int(prev_i[b, j])) for j in range(k_prev)]
