@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kEsimWaves * 64) void esim_kernel(const uint16_t* _
     constexpr int HALF = NCH / 2;
     constexpr int LOG_CPR = D == 128 ? 4 : 3;
     uint4 pre[NCH];
-    auto prefetch = [&](int64_t e) {
+    auto prefetch = [&](int64_t e) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int cm = tid + (i % HALF) * NTH;
@@ -331,37 +331,68 @@ __device__ __forceinline__ frag v_frag_tr_acc_h(const uint16_t* V, int rs, int k
     return __builtin_bit_cast(frag, x);
 }
 
-// column softmax of one E^T stripe held in accumulators (j on (lane >> 4, register), i on lane & 15),
-// rounded once to the MFMA dtype as the A operand of P @ V (k order of v_frag_tr_acc). VALU-lean: the
-// padding mask touches only the last tile, exp is v_exp_f32 on a pre-scaled argument (one fma + one
-// exp per score), and P is packed with the hardware round-to-nearest-even conversions.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// LDS row stride (elements) of the ESIM v2 images: D + 16 puts the 8 rows of a ds_read_b64_tr_b16 lane
+// group (and the 16 rows of a ds_read_b128 fragment) on disjoint banks; D + 8 (2-way conflicts) only
+// where the wider images would push the workgroup past 80 KB (two per CU)
+__host__ __device__ constexpr size_t esim2_lds_bytes(int D, int ntt, int rs) {
+    return (size_t)2 * ntt * 16 * rs * 2 + (size_t)kEsim2Waves * 3 * 2 * D * 4;
+}
+__host__ __device__ constexpr int esim2_rs(int D, int ntt) {
+    return esim2_lds_bytes(D, ntt, D + 16) <= 80 * 1024 ? D + 16 : D + 8;
+}
+
+// ---------------------------------------------------------------------------------------------
+// ESIM wave body (v3 statistics; v2 masked every padding row and reduced each statistic separately):
+//  * padding rows i >= L of a stripe get P = 0 (inv = 0), so att = 0 there, and x = 0 (zero image rows):
+//    they add 0 to both sums and a 0 to the max, which never changes it, because every row's max of
+//    [x, att, x - att, x * att] is >= 0 (x > 0: x; x < 0 and att >= 0: att; x < 0 and att < 0: x * att > 0;
+//    x = 0: x * att = 0). No per-row validity masks in the statistics.
+//  * the statistics of a side (NT columns tiles x {sum x, sum x*att, max}) leave the wave by reduce-scatter:
+//    two lane swaps + two ops reduce FOUR values over the four 16-lane rows (1.5 instructions per value
+//    instead of 4), and every lane then stores one reduced value.
+//  * the x reads of a side are issued before its P @ V MFMAs.
+// ---------------------------------------------------------------------------------------------
+
+// four values a, b, c, d (one per call site, same op) summed / maxed over the four 16-lane rows of the wave;
+// row 0 of the result holds a, row 1 c, row 2 b, row 3 d (v_permlane32_swap: a' = [a.lo, b.lo],
+// b' = [a.hi, b.hi]; v_permlane16_swap: a' = [a.r0, b.r0, a.r2, b.r2], b' = [a.r1, b.r1, a.r3, b.r3])
+template <bool MAX>
+__device__ __forceinline__ float rs4(float a, float b, float c, float d) {
+    auto op = [](float x, float y) { return MAX ? __builtin_elementwise_maximum(x, y) : x + y; };
+    const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    const float s1 = op(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(d), false, false);
+    const float s2 = op(__uint_as_float(q[0]), __uint_as_float(q[1]));
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s1), __float_as_uint(s2), false, false);
+    return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// column softmax of one E^T stripe (as stripe_softmax) with the stripe's padding rows zeroed: i = lane & 15
 template <typename M, int nt, typename frag>
-__device__ __forceinline__ void stripe_softmax(f4 (&ev)[8], int L, int lg, frag (&pa)[4]) {
+__device__ __forceinline__ void stripe_softmax3(f4 (&ev)[8], int L, int lg, bool row_ok, frag (&pa)[4]) {
     using elem = decltype(frag{}[0]);
     constexpr float kL2E = 1.4426950408889634f;
-    const bool partial = (L & 15) != 0;
+    if (L < nt * 16) {  // only the last tile can hold rows j >= L
 #pragma unroll
-    for (int jt = 0; jt < 8; ++jt)
-        if (partial && jt == nt - 1)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (jt * 16 + lg * 4 + r >= L) ev[jt][r] = -INFINITY;
+        for (int r = 0; r < 4; ++r)
+            if ((nt - 1) * 16 + lg * 4 + r >= L) ev[nt - 1][r] = -INFINITY;
+    }
     float mx = -INFINITY;
 #pragma unroll
-    for (int jt = 0; jt < 8; ++jt)
-        if (jt < nt) mx = fmx3(fmx3(mx, ev[jt][0], ev[jt][1]), ev[jt][2], ev[jt][3]);
+    for (int jt = 0; jt < nt; ++jt) mx = fmx3(fmx3(mx, ev[jt][0], ev[jt][1]), ev[jt][2], ev[jt][3]);
     mx = rows4_maximum(mx);
     const float mo = -mx * kL2E;
-    float sm = 0.f;
+    f2v sm2 = {0.f, 0.f};
 #pragma unroll
-    for (int jt = 0; jt < 8; ++jt)
-        if (jt < nt)
+    for (int jt = 0; jt < nt; ++jt) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                ev[jt][r] = __builtin_amdgcn_exp2f(fmaf(ev[jt][r], kL2E, mo));
-                sm += ev[jt][r];
-            }
-    const float inv = 1.0f / rows4_sum(sm);
+        for (int r = 0; r < 4; ++r) ev[jt][r] = __builtin_amdgcn_exp2f(fmaf(ev[jt][r], kL2E, mo));
+        sm2 += f2v{ev[jt][0], ev[jt][1]} + f2v{ev[jt][2], ev[jt][3]};
+    }
+    float inv = 1.0f / rows4_sum(sm2[0] + sm2[1]);
+    inv = row_ok ? inv : 0.f;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
         frag f;
@@ -374,51 +405,28 @@ __device__ __forceinline__ void stripe_softmax(f4 (&ev)[8], int L, int lg, frag 
     }
 }
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// ESIM combine statistics of 4 rows of one column: sum x, sum x*att, max of [x, att, x - att, x*att].
-// Pairs of rows go through packed f32 math (v_pk_mul/add_f32); CHECK masks rows >= L (last stripe only).
-template <typename M, bool CHECK>
-__device__ __forceinline__ void esim_rows(s4v xv, f4 at, int row0, int L, f2v& sx, f2v& sm, float& m_all) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-        f2v x = {M::to_f((uint16_t)xv[2 * p]), M::to_f((uint16_t)xv[2 * p + 1])};
-        f2v t = {at[2 * p], at[2 * p + 1]};
-        if (CHECK) {
-            const bool v0 = row0 + 2 * p < L, v1 = row0 + 2 * p + 1 < L;
-            x = f2v{v0 ? x[0] : 0.f, v1 ? x[1] : 0.f};
-            t = f2v{v0 ? t[0] : 0.f, v1 ? t[1] : 0.f};
-            const f2v ml = x * t, d = x - t;
-            sx += x;
-            sm += ml;
-            const float r0 = fmx(fmx3(x[0], t[0], d[0]), ml[0]), r1 = fmx(fmx3(x[1], t[1], d[1]), ml[1]);
-            m_all = fmx3(m_all, v0 ? r0 : -INFINITY, v1 ? r1 : -INFINITY);
-        } else {
-            const f2v ml = x * t, d = x - t;
-            sx += x;
-            sm += ml;
-            m_all = fmx3(m_all, x[0], t[0]);
-            m_all = fmx3(m_all, d[0], ml[0]);
-            m_all = fmx3(m_all, x[1], t[1]);
-            m_all = fmx3(m_all, d[1], ml[1]);
-        }
-    }
+// statistics of 4 rows of one column: x (4 MFMA-dtype values), att (accumulator rows)
+template <typename M>
+__device__ __forceinline__ void esim_acc4(s4v xv, f4 at, f2v& sx, f2v& sm, float& mx) {
+    const f2v x01 = {M::to_f((uint16_t)xv[0]), M::to_f((uint16_t)xv[1])};
+    const f2v x23 = {M::to_f((uint16_t)xv[2]), M::to_f((uint16_t)xv[3])};
+    const f2v t01 = {at[0], at[1]}, t23 = {at[2], at[3]};
+    const f2v m01 = x01 * t01, m23 = x23 * t23;
+    const f2v d01 = x01 - t01, d23 = x23 - t23;
+    sx += x01 + x23;
+    sm += m01 + m23;
+    mx = fmx3(mx, x01[0], t01[0]);
+    mx = fmx3(mx, d01[0], m01[0]);
+    mx = fmx3(mx, x01[1], t01[1]);
+    mx = fmx3(mx, d01[1], m01[1]);
+    mx = fmx3(mx, x23[0], t23[0]);
+    mx = fmx3(mx, d23[0], m23[0]);
+    mx = fmx3(mx, x23[1], t23[1]);
+    mx = fmx3(mx, d23[1], m23[1]);
 }
 
-// LDS row stride (elements) of the ESIM v2 images: D + 16 puts the 8 rows of a ds_read_b64_tr_b16 lane
-// group (and the 16 rows of a ds_read_b128 fragment) on disjoint banks; D + 8 (2-way conflicts) only
-// where the wider images would push the workgroup past 80 KB (two per CU)
-__host__ __device__ constexpr size_t esim2_lds_bytes(int D, int ntt, int rs) {
-    return (size_t)2 * ntt * 16 * rs * 2 + (size_t)kEsim2Waves * 3 * 2 * D * 4;
-}
-__host__ __device__ constexpr int esim2_rs(int D, int ntt) {
-    return esim2_lds_bytes(D, ntt, D + 16) <= 80 * 1024 ? D + 16 : D + 8;
-}
-
-// one wave's share of an ESIM example: score stripes sp0 (and sp1 when TWO), softmax, P @ [q | a] and the
-// combine statistics of its rows -> wst[stat][side*D + n]; NTT = 16-row tiles (compile time: no selects on the tile count)
 template <typename M, int D, int NTT, bool TWO>
-__device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
+__device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
                                            int lane) {
     constexpr int nt = NTT;
     using frag = typename M::frag;
@@ -428,7 +436,6 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
     const int lr = lane & 15, lg = lane >> 4;
     frag pa0[4], pa1[4];
     {
-        // E^T stripes (attention_layers.py:44-47); each q fragment feeds both stripes
         frag b0[DK], b1[DK];
 #pragma unroll
         for (int kk = 0; kk < DK; ++kk) {
@@ -443,7 +450,6 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
             e1[jt] = f4{0.f, 0.f, 0.f, 0.f};
         }
         if constexpr (NTT < 8) {
-            // k-step outer, tiles inner: consecutive MFMAs are independent (no accumulator RAW stalls)
 #pragma unroll
             for (int kk = 0; kk < DK; ++kk) {
 #pragma unroll
@@ -454,7 +460,6 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
                 }
             }
         } else {
-            // 8 tiles: tile-outer keeps fewer q fragments live (measured faster at L = 128)
 #pragma unroll
             for (int jt = 0; jt < nt; ++jt) {
 #pragma unroll
@@ -465,8 +470,8 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
                 }
             }
         }
-        stripe_softmax<M, NTT>(e0, L, lg, pa0);
-        if (TWO) stripe_softmax<M, NTT>(e1, L, lg, pa1);
+        stripe_softmax3<M, NTT>(e0, L, lg, sp0 * 16 + lr < L, pa0);
+        if (TWO) stripe_softmax3<M, NTT>(e1, L, lg, sp1 * 16 + lr < L, pa1);
     }
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
@@ -489,32 +494,28 @@ __device__ __forceinline__ void esim2_wave(const uint16_t* qs, const uint16_t* a
                 }
             }
         }
+        float sx[NT], sm[NT], mx[NT];
 #pragma unroll
         for (int nn = 0; nn < NT; ++nn) {
-            // ESIM combine statistics (esim.py:79-82) over this wave's rows of both stripes:
-            // sum x, sum x*att and max of [x, att, x - att, x*att]
-            const int n = nn * 16 + lr;
-            f2v sx = {0.f, 0.f}, sm = {0.f, 0.f};
-            float m_all = -INFINITY;
+            // this lane's x values: rows sp*16 + 4*lg .. +3 of column nn*16 + lr
+            f2v sx2 = {0.f, 0.f}, sm2 = {0.f, 0.f};
+            float m = -INFINITY;
+            esim_acc4<M>(tr_read(V + (sp0 * 16 + lg * 4 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3)), c0[nn], sx2, sm2, m);
+            if (TWO)
+                esim_acc4<M>(tr_read(V + (sp1 * 16 + lg * 4 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3)), c1[nn], sx2, sm2, m);
+            sx[nn] = sx2[0] + sx2[1];
+            sm[nn] = sm2[0] + sm2[1];
+            mx[nn] = m;
+        }
+        // reduce-scatter over the four 16-lane rows: row k of group g holds tile nn = 4g + perm[k]
+        const int pk = (lg == 1) ? 2 : (lg == 2) ? 1 : lg;
+        float* w = wst + side * D + lr;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (h == 1 && !TWO) break;
-                const int sp = h ? sp1 : sp0;
-                const int row0 = sp * 16 + lg * 4;
-                const s4v xv = tr_read(V + (row0 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3));
-                const f4 at = h ? c1[nn] : c0[nn];
-                if ((L & 15) && sp == nt - 1) esim_rows<M, true>(xv, at, row0, L, sx, sm, m_all);
-                else esim_rows<M, false>(xv, at, row0, L, sx, sm, m_all);
-            }
-            const float s_x = rows4_sum(sx[0] + sx[1]);
-            const float s_mul = rows4_sum(sm[0] + sm[1]);
-            m_all = rows4_maximum(m_all);
-            if (lg == 0) {
-                float* w = wst + side * D + n;
-                w[0] = s_x;
-                w[2 * D] = s_mul;
-                w[4 * D] = m_all;
-            }
+        for (int g = 0; g < NT / 4; ++g) {
+            const int n = (4 * g + pk) * 16;
+            w[n] = rs4<false>(sx[4 * g], sx[4 * g + 1], sx[4 * g + 2], sx[4 * g + 3]);
+            w[2 * D + n] = rs4<false>(sm[4 * g], sm[4 * g + 1], sm[4 * g + 2], sm[4 * g + 3]);
+            w[4 * D + n] = rs4<true>(mx[4 * g], mx[4 * g + 1], mx[4 * g + 2], mx[4 * g + 3]);
         }
     }
 }
@@ -539,17 +540,27 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     float* st = reinterpret_cast<float*>(as + L16 * RS);  // [wave][stat 3][side*D + n]
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
+    // staging loads through buffer descriptors over the example's L rows: the chunks of rows >= L fall past
+    // the descriptor's range and read as zeros (the zero padding rows of the images), with no per-chunk
+    // branch, select or zero-fill (a conditional load makes hipcc branch around every load; an
+    // unconditional one with a clamped row demotes pre[] to scratch)
     uint4 pre[NCH];
-    auto prefetch = [&](int64_t e) {
+    const int img_bytes = L * (int)ld * 2;
+    auto prefetch = [&](int64_t e) __attribute__((always_inline)) {
+        const auto rq = __builtin_amdgcn_make_buffer_rsrc((void*)(q + e * ex_stride), 0, img_bytes, 0x00020000);
+        const auto ra = __builtin_amdgcn_make_buffer_rsrc((void*)(a + e * ex_stride), 0, img_bytes, 0x00020000);
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int cm = tid + (i % HALF) * NTH;
             const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
-            pre[i] = make_uint4(0, 0, 0, 0);
-            if (r < L) pre[i] = *reinterpret_cast<const uint4*>((i < HALF ? q : a) + e * ex_stride + (int64_t)r * ld + ch * 8);
+            pre[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(i < HALF ? rq : ra, (r * (int)ld + ch * 8) * 2, 0, 0));
         }
     };
+    // a chunk of a row past the image (only where 16-row tiles end inside a 256-chunk group: d = 64, odd
+    // tile counts) goes to this thread's dummy slot in the statistics area, rewritten after the barrier
+    uint16_t* dummy = reinterpret_cast<uint16_t*>(st) + (tid & 127) * 8;
     int64_t e = blockIdx.x;
+    uint32_t it = 0;
     if (e < batch) prefetch(e);
     for (; e < batch; e += gridDim.x) {
         __syncthreads();
@@ -557,17 +568,23 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         for (int i = 0; i < NCH; ++i) {
             const int cm = tid + (i % HALF) * NTH;
             const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
-            if (r < L16) *reinterpret_cast<uint4*>((i < HALF ? qs : as) + r * RS + ch * 8) = pre[i];
+            if (i % HALF * NTH < L16 * CPR) {  // compile-time: chunk groups wholly past the image never exist
+                uint16_t* dst = (i % HALF + 1) * NTH <= L16 * CPR || r < L16 ? (i < HALF ? qs : as) + r * RS + ch * 8 : dummy;
+                *reinterpret_cast<uint4*>(dst) = pre[i];
+            }
         }
         __syncthreads();
         if (e + gridDim.x < batch) prefetch(e + gridDim.x);
 
-        const int sp0 = wave, sp1 = wave + kEsim2Waves;
+        // v3: the stripe pairs rotate over the waves from one example to the next, so the wave left with one
+        // stripe (7 tiles over 4 waves) is a different SIMD each time; statistics slots follow the stripe
+        const int rot = (int)(it++ & 3);
+        const int sp0 = (wave + rot) & 3, sp1 = sp0 + kEsim2Waves;
         if (sp0 < nt) {
-            float* wst = st + wave * 3 * 2 * D;
+            float* wst = st + sp0 * 3 * 2 * D;
             // both-stripe / one-stripe waves are separate instantiations: no predicated MFMAs
-            if (sp1 < nt) esim2_wave<M, D, NTT, true>(qs, as, wst, sp0, sp1, L, lane);
-            else esim2_wave<M, D, NTT, false>(qs, as, wst, sp0, sp1, L, lane);
+            if (sp1 < nt) esim3_wave<M, D, NTT, true>(qs, as, wst, sp0, sp1, L, lane);
+            else esim3_wave<M, D, NTT, false>(qs, as, wst, sp0, sp1, L, lane);
         }
         __syncthreads();
 
@@ -765,6 +782,7 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     RF_REQUIRE(d == 64 || d == 128, "rf_esim_soft_attention_fwd: d must be 64 or 128 (got %d)", d);
     RF_REQUIRE(batch >= 0, "rf_esim_soft_attention_fwd: batch < 0");
     RF_REQUIRE(ld % 8 == 0 && ex_stride % 8 == 0 && ld >= d, "rf_esim_soft_attention_fwd: ld/ex_stride must be multiples of 8 elements (16-byte rows)");
+    RF_REQUIRE((int64_t)L * ld * 2 < ((int64_t)1 << 31), "rf_esim_soft_attention_fwd: one example's rows must span < 2 GiB");
     RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)a & 15) == 0, "rf_esim_soft_attention_fwd: q/a must be 16-byte aligned");
     if (batch == 0) return RF_OK;
     RF_REQUIRE(q && a && out, "rf_esim_soft_attention_fwd: null pointer");
