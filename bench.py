@@ -333,12 +333,33 @@ def bench_esim(args):
         model.dense_output(model.output_mlp(pooled))
 
     steps = max(10, args.steps // 2)
-    wall, per = _time_stages([("sparse_encoders", enc), ("esim_attention", att), ("mlp_scorer", mlp)], steps, 3)
+    eager_wall, _ = _time_stages([("forward", lambda: (enc(), att(), mlp()))], steps, 3)
+    # hipGraphs (runtime.graphs): one per stage for the stage times, one per whole forward for the wall
+    # number; the two resident input batches alternate, as in the eager loop
+    from recommendflow_amd.runtime.graphs import CapturedGraph
+
+    def enc_p(p):
+        model.enc_q(hu[p], out=q)
+        model.enc_a(ha[p], out=a)
+
+    g_enc = [CapturedGraph(lambda p=p: enc_p(p)) for p in (0, 1)]
+    g_att, g_mlp = CapturedGraph(att), CapturedGraph(mlp)
+    g_full = [CapturedGraph(lambda p=p: (enc_p(p), att(), mlp())) for p in (0, 1)]
+    par = {"s": 0, "f": 0}
+
+    def nxt(k):
+        par[k] ^= 1
+        return par[k]
+
+    _, per = _time_stages([("sparse_encoders", lambda: g_enc[nxt("s")].replay()), ("esim_attention", g_att.replay),
+                           ("mlp_scorer", g_mlp.replay)], steps, 3)
+    wall, _ = _time_stages([("forward", lambda: g_full[nxt("f")].replay())], steps, 3)
     att_flops = 2 * Ls * Ls * 128 * 3 * B
     mlp_flops = (model.flops_per_example() - 2 * Ls * Ls * 128 * 3) * B
     tok_bytes = sum(int(h.tok_bytes.numel()) + 4 * h.n_tokens for h in (hu[0], ha[0]))
     enc_bytes = 2 * (2 * B * Ls * 128 + B * Ls * 2 * 64 * 2) + tok_bytes
-    return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4),
+    return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4), "launch": "hipGraph",
+            "eager_ms_per_step": round(eager_wall, 4),
             "stage_ms": {k: round(v, 4) for k, v in per.items()},
             "encoder_GBs": round(enc_bytes / per["sparse_encoders"] / 1e6, 1),
             "esim_TFLOPs": round(att_flops / per["esim_attention"] / 1e9, 1),
@@ -384,9 +405,15 @@ def bench_dssm(args, enc, host):
         (u * v).sum(-1)
 
     steps = max(5, args.steps // 5)
-    wall, per = _time_stages([("sparse_encoders", sparse), ("fp32_towers", towers)], steps, 2)
+    eager_wall, _ = _time_stages([("forward", lambda: (sparse(), towers()))], steps, 2)
+    from recommendflow_amd.runtime.graphs import CapturedGraph
+
+    g_sp, g_tw, g_full = CapturedGraph(sparse), CapturedGraph(towers), CapturedGraph(lambda: (sparse(), towers()))
+    _, per = _time_stages([("sparse_encoders", g_sp.replay), ("fp32_towers", g_tw.replay)], steps, 2)
+    wall, _ = _time_stages([("forward", g_full.replay)], steps, 2)
     flops = model.flops_per_example() * B
-    return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4),
+    return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4), "launch": "hipGraph",
+            "eager_ms_per_step": round(eager_wall, 4),
             "stage_ms": {k: round(v, 4) for k, v in per.items()},
             "towers_TFLOPs_fp32": round(flops / per["fp32_towers"] / 1e9, 1),
             "towers_frac_of_157TF_fp32": round(flops / per["fp32_towers"] / 1e9 / 157.3, 4),

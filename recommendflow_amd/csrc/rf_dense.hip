@@ -136,6 +136,99 @@ __global__ __launch_bounds__(256) void norm_vec_kernel(const float* __restrict__
     }
 }
 
+// BatchNormalization at inference (mode 1) is a per-column affine map, no row reduction: each thread owns
+// one float4 column chunk, computes its 4 columns' 1/sqrt(var + eps) once, and walks kRowsPerBn rows
+// (coalesced across the workgroup's 256 chunks = 1024 columns of one row). Any width with cols % 4 == 0.
+constexpr int kRowsPerBn = 16;
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void bn_vec_kernel(const float* __restrict__ x, int64_t rows, int cols, int64_t ldx,
+                                                     float eps, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, const float* __restrict__ mean,
+                                                     const float* __restrict__ var, void* __restrict__ y, int64_t ldy) {
+    const int ncb = (cols / 4 + 255) / 256;  // column blocks; blockIdx.x = row group * ncb + column block
+    const int c4 = (int)(blockIdx.x % ncb) * 256 + threadIdx.x;
+    if (4 * c4 >= cols) return;
+    const float4 m = reinterpret_cast<const float4*>(mean)[c4], vr = reinterpret_cast<const float4*>(var)[c4];
+    const float4 g = gamma ? reinterpret_cast<const float4*>(gamma)[c4] : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 bb = beta ? reinterpret_cast<const float4*>(beta)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float mv[4] = {m.x, m.y, m.z, m.w}, gv[4] = {g.x, g.y, g.z, g.w}, bv[4] = {bb.x, bb.y, bb.z, bb.w};
+    const float rs[4] = {1.0f / sqrtf(vr.x + eps), 1.0f / sqrtf(vr.y + eps), 1.0f / sqrtf(vr.z + eps), 1.0f / sqrtf(vr.w + eps)};
+    const int64_t r0 = (int64_t)(blockIdx.x / ncb) * kRowsPerBn;
+    const int64_t r1 = r0 + kRowsPerBn < rows ? r0 + kRowsPerBn : rows;
+    for (int64_t r = r0; r < r1; ++r) {
+        const float4 xv4 = reinterpret_cast<const float4*>(x + r * ldx)[c4];
+        const float xv[4] = {xv4.x, xv4.y, xv4.z, xv4.w};
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (xv[e] - mv[e]) * rs[e] * gv[e] + bv[e];
+        if constexpr (OUT_BF16) {
+            const uint32_t lo = f32_to_bf16_bits(o[0]) | (f32_to_bf16_bits(o[1]) << 16);
+            const uint32_t hi = f32_to_bf16_bits(o[2]) | (f32_to_bf16_bits(o[3]) << 16);
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(y) + r * ldy + 4 * c4) = make_uint2(lo, hi);
+        } else {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + r * ldy + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
+}
+
+// LayerNormalization of rows wider than the one-wave vector path (2048 < cols <= 32768, cols % 4 == 0):
+// one 256-thread workgroup per row, the row held once in registers (NV float4 per thread), mean and
+// variance (two passes over the registers) reduced through LDS.
+template <bool OUT_BF16, int NV>
+__global__ __launch_bounds__(256) void ln_wide_kernel(const float* __restrict__ x, int cols, int64_t ldx, float eps,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      void* __restrict__ y, int64_t ldy) {
+    __shared__ float red[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t row = blockIdx.x;
+    const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
+    float4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int c4 = tid + 256 * k;
+        v[k] = 4 * c4 < cols ? xr[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    auto block_sum = [&](float s) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) red[wave] = s;
+        __syncthreads();
+        const float t = (red[0] + red[1]) + (red[2] + red[3]);
+        __syncthreads();
+        return t;
+    };
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    const float mu = block_sum(s) / (float)cols;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        if (4 * (tid + 256 * k) < cols) {
+            const float a = v[k].x - mu, b = v[k].y - mu, c = v[k].z - mu, d = v[k].w - mu;
+            q += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    const float rstd = 1.0f / sqrtf(block_sum(q) / (float)cols + eps);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int c4 = tid + 256 * k;
+        if (4 * c4 >= cols) continue;
+        const float4 g = gamma ? reinterpret_cast<const float4*>(gamma)[c4] : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float4 bb = beta ? reinterpret_cast<const float4*>(beta)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float o0 = (v[k].x - mu) * rstd * g.x + bb.x, o1 = (v[k].y - mu) * rstd * g.y + bb.y;
+        const float o2 = (v[k].z - mu) * rstd * g.z + bb.z, o3 = (v[k].w - mu) * rstd * g.w + bb.w;
+        if constexpr (OUT_BF16) {
+            const uint32_t lo = f32_to_bf16_bits(o0) | (f32_to_bf16_bits(o1) << 16);
+            const uint32_t hi = f32_to_bf16_bits(o2) | (f32_to_bf16_bits(o3) << 16);
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(y) + row * ldy + 4 * c4) = make_uint2(lo, hi);
+        } else {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + row * ldy + 4 * c4) = make_float4(o0, o1, o2, o3);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // GEMM y[M,N] = act(x[M,K] W[N,K]^T + b)
 // ---------------------------------------------------------------------------------------------
@@ -338,9 +431,34 @@ extern "C" int rf_norm_fwd(const float* x, int64_t rows, int32_t cols, int64_t l
     RF_REQUIRE(x && y, "rf_norm_fwd: null pointer");
     const unsigned grid = (unsigned)((rows + 3) / 4);
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    const bool vec = cols % 4 == 0 && cols <= 2048 && ldx % 4 == 0 && ldy % 4 == 0 && al16(x) &&
-                     ((uintptr_t)y & (y_dtype == RF_DTYPE_BF16 ? 7 : 15)) == 0 && (!gamma || al16(gamma)) &&
-                     (!beta || al16(beta)) && (mode == 0 || (al16(mean) && al16(var)));
+    const bool aligned = cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16(x) &&
+                         ((uintptr_t)y & (y_dtype == RF_DTYPE_BF16 ? 7 : 15)) == 0 && (!gamma || al16(gamma)) &&
+                         (!beta || al16(beta)) && (mode == 0 || (al16(mean) && al16(var)));
+    const bool bf = y_dtype == RF_DTYPE_BF16;
+    if (aligned && mode == 1) {  // BatchNorm: per-column affine, any width
+        const int64_t blocks = (int64_t)((cols / 4 + 255) / 256) * ((rows + kRowsPerBn - 1) / kRowsPerBn);
+        RF_REQUIRE(blocks < ((int64_t)1 << 31), "rf_norm_fwd: too many rows");
+        const dim3 g((unsigned)blocks);
+        if (bf) hipLaunchKernelGGL(bn_vec_kernel<true>, g, dim3(256), 0, rf_stream(stream), x, rows, cols, ldx, eps, gamma, beta, mean, var, y, ldy);
+        else hipLaunchKernelGGL(bn_vec_kernel<false>, g, dim3(256), 0, rf_stream(stream), x, rows, cols, ldx, eps, gamma, beta, mean, var, y, ldy);
+        return rf_check_launch("bn_vec_kernel");
+    }
+    if (aligned && cols > 2048 && cols <= 32768) {  // LayerNorm, wide rows: a workgroup per row
+        const int nv = (cols + 1023) / 1024;
+        hipStream_t st = rf_stream(stream);
+        const dim3 g((unsigned)rows);
+#define RF_LN_WIDE(B, N) hipLaunchKernelGGL((ln_wide_kernel<B, N>), g, dim3(256), 0, st, x, cols, ldx, eps, gamma, beta, y, ldy)
+        if (bf) {
+            if (nv <= 4) RF_LN_WIDE(true, 4); else if (nv <= 8) RF_LN_WIDE(true, 8);
+            else if (nv <= 16) RF_LN_WIDE(true, 16); else RF_LN_WIDE(true, 32);
+        } else {
+            if (nv <= 4) RF_LN_WIDE(false, 4); else if (nv <= 8) RF_LN_WIDE(false, 8);
+            else if (nv <= 16) RF_LN_WIDE(false, 16); else RF_LN_WIDE(false, 32);
+        }
+#undef RF_LN_WIDE
+        return rf_check_launch("ln_wide_kernel");
+    }
+    const bool vec = aligned && cols <= 2048;
     if (vec) {
         const int nv = (cols + 255) / 256;
         hipStream_t st = rf_stream(stream);

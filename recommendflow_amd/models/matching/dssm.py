@@ -39,6 +39,12 @@ class Dssm(torch.nn.Module):
         u, a = self.embed(user, ad)
         return (u * a).sum(dim=-1)
 
+    def graphed(self, user: SparseBatch, ad: SparseBatch, **kw):
+        """forward() as one hipGraph on static copies of (user, ad) (runtime.graphs.GraphedForward)."""
+        from ...runtime.graphs import GraphedForward
+
+        return GraphedForward(self.forward, user, ad, **kw)
+
     def flops_per_example(self) -> float:
         f = 0
         for m in (self.user_dense, self.ad_dense):

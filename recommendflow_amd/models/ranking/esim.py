@@ -58,6 +58,14 @@ class Esim(torch.nn.Module):
         esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
         return self.dense_output(self.output_mlp(pooled))
 
+    def graphed(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor, **kw):
+        """This forward captured as one hipGraph on static copies of (user, ad, dense) (runtime.graphs):
+        the returned callable takes batches of the same B / slot counts and replays the 14 launches without
+        the per-launch host path. Its output buffer is reused by the next call."""
+        from ...runtime.graphs import GraphedForward
+
+        return GraphedForward(self.forward, user, ad, dense, **kw)
+
     def flops_per_example(self) -> float:
         """Dense FLOPs per example: ESIM products (2 L^2 d for E + 2 * 2 L^2 d for the alignments) + MLP GEMMs."""
         att = 2 * self.L * self.L * self.d * 3

@@ -1,0 +1,114 @@
+"""hipGraph capture of whole forwards (torch.cuda.CUDAGraph is a hipGraph on ROCm).
+
+A forward here is a chain of short launches through the C ABI (cfg3: 2 fused encoders, the ESIM
+kernel, 9 norm / GEMM launches). Eager, every launch pays the Python + ctypes path on the host
+(~13-15 us), which is longer than most of the kernels: the chain is host-bound. Captured once and
+replayed, the chain costs one graph launch; the kernels run back to back.
+
+Nothing in librf synchronises with the host or allocates (rf_api.h: caller-owned buffers, stream-ordered
+launches), so every hot-path op is capturable as-is. Inputs live in static device buffers:
+  * tensors: one static copy (or the caller's own tensor when it is passed again);
+  * SparseBatch: the CSR arrays with a CAPACITY (token bytes and token count vary per batch; the kernels
+    find every token through bag_off, and the launch parameters depend only on B and the slot count), so
+    any batch of the same B / slot count that fits is loaded by device-to-device copies, no recapture.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence
+
+import torch
+
+from .batch import SparseBatch
+
+
+class StaticSparseBatch(SparseBatch):
+    """Device CSR buffers with room for `tok_bytes_cap` bytes and `tok_cap` tokens."""
+
+    def __init__(self, like: SparseBatch, tok_bytes_cap: Optional[int] = None, tok_cap: Optional[int] = None,
+                 device="cuda"):
+        nb = int(len(like.tok_bytes))
+        nt = like.n_tokens
+        tok_bytes_cap = max(16, int(tok_bytes_cap if tok_bytes_cap is not None else nb + nb // 4 + 64))
+        tok_cap = int(tok_cap if tok_cap is not None else nt + nt // 4 + 16)
+        super().__init__(torch.zeros(tok_bytes_cap, dtype=torch.uint8, device=device),
+                         torch.zeros(tok_cap + 1, dtype=torch.int32, device=device),
+                         torch.zeros(like.batch * like.n_slots + 1, dtype=torch.int32, device=device),
+                         torch.zeros(like.n_slots, dtype=torch.int32, device=device), like.batch, like.n_slots)
+        self.n_tok_live = 0
+        self.load(like)
+
+    @property
+    def n_tokens(self) -> int:  # the live batch's token count (the buffers hold capacity)
+        return self.n_tok_live
+
+    def load(self, b: SparseBatch) -> "StaticSparseBatch":
+        if b is self:
+            return self
+        if b.batch != self.batch or b.n_slots != self.n_slots:
+            raise ValueError(f"static batch is B={self.batch} x {self.n_slots} slots, got B={b.batch} x {b.n_slots}")
+        nb, nt = int(len(b.tok_bytes)), b.n_tokens
+        if nb > self.tok_bytes.numel() or nt + 1 > self.tok_off.numel():
+            raise ValueError(f"batch needs {nb} token bytes / {nt} tokens; capacity {self.tok_bytes.numel()} / "
+                             f"{self.tok_off.numel() - 1}: capture with a larger capacity")
+        dev = b if b.is_device() else b.to(self.tok_off.device)
+        self.tok_bytes[:nb].copy_(dev.tok_bytes[:nb], non_blocking=True)
+        self.tok_off[: nt + 1].copy_(dev.tok_off, non_blocking=True)
+        self.bag_off.copy_(dev.bag_off, non_blocking=True)
+        self.lmax.copy_(dev.lmax, non_blocking=True)
+        self.host_lmax = b.lmax if not b.is_device() else b.host_lmax  # never a device sync
+        self.n_tok_live = nt
+        return self
+
+
+class CapturedGraph:
+    """`fn()` (reading and writing fixed device buffers) captured once; replay() re-runs its launches."""
+
+    def __init__(self, fn: Callable[[], object], warmup: int = 2):
+        self.fn = fn
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up off the capture: lazy init, LDS attributes, allocator
+            for _ in range(warmup):
+                fn()
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = fn()
+
+    def replay(self):
+        self.graph.replay()
+        return self.out
+
+
+class GraphedForward:
+    """A module forward captured on static inputs; __call__(*inputs) loads the inputs and replays.
+
+    Tensor inputs are copied into the static buffers unless the caller passes the static tensors
+    themselves (`static_inputs`); SparseBatch inputs go through StaticSparseBatch.load. The returned
+    output tensor is the graph's own buffer, overwritten by the next call (clone it to keep it)."""
+
+    def __init__(self, forward: Callable[..., torch.Tensor], *inputs, warmup: int = 2, capacity_slack: float = 0.25):
+        self.static_inputs: List[object] = []
+        for x in inputs:
+            if isinstance(x, SparseBatch):
+                nb, nt = int(len(x.tok_bytes)), x.n_tokens
+                self.static_inputs.append(StaticSparseBatch(x, int(nb * (1 + capacity_slack)) + 64,
+                                                            int(nt * (1 + capacity_slack)) + 16))
+            elif isinstance(x, torch.Tensor):
+                self.static_inputs.append(x.detach().clone())
+            else:
+                self.static_inputs.append(x)
+        self._g = CapturedGraph(lambda: forward(*self.static_inputs), warmup=warmup)
+
+    def __call__(self, *inputs: Sequence[object]) -> torch.Tensor:
+        if len(inputs) != len(self.static_inputs):
+            raise ValueError(f"expected {len(self.static_inputs)} inputs, got {len(inputs)}")
+        for s, x in zip(self.static_inputs, inputs):
+            if isinstance(s, StaticSparseBatch):
+                s.load(x)
+            elif isinstance(s, torch.Tensor):
+                if x is not s:
+                    if x.shape != s.shape:
+                        raise ValueError(f"input shape {tuple(x.shape)} != captured {tuple(s.shape)}")
+                    s.copy_(x, non_blocking=True)
+        return self._g.replay()

@@ -94,12 +94,13 @@ def test_dense_fp32_exact_mfma(O, cuda, M, K, N):
     np.testing.assert_allclose(y, want, rtol=1e-5, atol=1e-6 * np.sqrt(K))
 
 
-@pytest.mark.parametrize("cols", [16, 200, 256, 1024, 1280, 2048, 2050, 3000])
+@pytest.mark.parametrize("cols", [16, 200, 256, 1024, 1280, 2048, 2050, 3000, 4100, 8704, 20480, 32768, 32772])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
 def test_norm_rows(O, cuda, cols, mode, odt):
-    """rf_norm_fwd: the register-resident float4 path (cols % 4 == 0, <= 2048) and the scalar path
-    (2050, 3000, and a misaligned column offset) against float64 LayerNorm / BatchNorm-inference."""
+    """rf_norm_fwd against float64 LayerNorm / BatchNorm-inference: BatchNorm's per-column float4 kernel
+    (any width), LayerNorm's one-wave register rows (<= 2048), workgroup-per-row wide rows (<= 32768:
+    the DSSM tower inputs 8704 / 20480), and the scalar path (2050, 3000, 32772, a misaligned view)."""
     from recommendflow_amd.backend.layers.core import Norm
 
     spec = LayerNormalization(epsilon=1e-6) if mode == 0 else BatchNormalization(epsilon=1e-3)
