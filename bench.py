@@ -221,7 +221,8 @@ def main():
         if args.no_sharded:
             del dev, out
         torch.cuda.empty_cache()
-        extras = {"cfg3_esim_forward": guarded(bench_esim, args), "cfg2_dssm_forward": guarded(bench_dssm, args, enc, host)}
+        extras = {"cfg2_h2d_inclusive": guarded(bench_h2d, args, enc, host),
+                  "cfg3_esim_forward": guarded(bench_esim, args), "cfg2_dssm_forward": guarded(bench_dssm, args, enc, host)}
     if world == 1 and not args.no_cascade:
         extras = dict(extras or {}, cfg5_cascade=guarded(bench_cascade, args, enc))
     if world == 1 and not args.no_train:
@@ -358,8 +359,11 @@ def bench_esim(args):
     mlp_flops = (model.flops_per_example() - 2 * Ls * Ls * 128 * 3) * B
     tok_bytes = sum(int(h.tok_bytes.numel()) + 4 * h.n_tokens for h in (hu[0], ha[0]))
     enc_bytes = 2 * (2 * B * Ls * 128 + B * Ls * 2 * 64 * 2) + tok_bytes
+    cpu = None
+    if args.cpu_seconds > 0:
+        cpu = cpu_baseline_cfg3(model, q.view(B, Ls, 128), a.view(B, Ls, 128), dense, args.cpu_seconds)
     return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4), "launch": "hipGraph",
-            "eager_ms_per_step": round(eager_wall, 4),
+            "eager_ms_per_step": round(eager_wall, 4), "cpu_baseline": cpu,
             "stage_ms": {k: round(v, 4) for k, v in per.items()},
             "encoder_GBs": round(enc_bytes / per["sparse_encoders"] / 1e6, 1),
             "esim_TFLOPs": round(att_flops / per["esim_attention"] / 1e9, 1),
@@ -367,6 +371,27 @@ def bench_esim(args):
             "mlp_TFLOPs": round(mlp_flops / per["mlp_scorer"] / 1e9, 1),
             "config": "200 slots (100 q + 100 a) x 1M bins/hash, D=64 bf16 (tables 51.2 GB), L=100, d=128, "
                       "input_mlp 16->256->512, output_mlp 1280->1024->512, Dense(2, softmax), bf16 MFMA"}
+
+
+def cpu_baseline_cfg3(model, q, a, dense, budget_s, sample=512):
+    """cfg3's dense stages a.5-a.7 in float32 numpy / BLAS on the host (oracle.esim_scorer_f32) over the
+    first `sample` examples of the GPU's own encoder outputs; all host threads (BLAS)."""
+    from oracle import oracle as O
+
+    def params(m):
+        return [{"W": dn.weight.float().cpu().numpy().T.copy(), "b": dn.bias.cpu().numpy(), "gamma": nm.gamma.cpu().numpy(),
+                 "beta": nm.beta.cpu().numpy()} for nm, dn in zip(m.norms, m.denses)]
+
+    qs, as_, ds = (t[:sample].float().cpu().numpy() for t in (q, a, dense))
+    pin, pout = params(model.input_mlp), params(model.output_mlp)
+    Wo = model.dense_output.weight.float().cpu().numpy().T.copy()
+    bo = model.dense_output.bias.cpu().numpy()
+    cpu_model, ncpu = host_cpu()
+    r = timed_runs(lambda: O.esim_scorer_f32(qs, as_, ds, pin, pout, Wo, bo), sample, budget_s / 2, warmup=2)
+    return dict(r, unit="examples/s", cores=int(os.environ.get("OMP_NUM_THREADS", ncpu)), kind="port", cpu=cpu_model,
+                host_cpus=ncpu, sample=f"{r['runs']} x {sample} cfg3 examples through oracle.esim_scorer_f32 (SoftAttention, "
+                                       f"ESIM combine/pool, input/output MLPs, Dense(2, softmax); float32 numpy/BLAS) "
+                                       f"in {r['seconds']} s; the sparse encoders are not included")
 
 
 def bench_dssm(args, enc, host):
@@ -751,26 +776,101 @@ def bench_pipe(args, enc, specs, multi):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def cpu_baseline(enc, hb, budget_s):
-    """The C oracle (OpenMP) on the same batch; examples/s over ~budget_s seconds of repeated runs."""
+def host_cpu():
+    """CPU model name and logical CPU count of this host (the 'lscpu' model line, from /proc/cpuinfo)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count() or 1
+
+
+def timed_runs(fn, examples, budget_s, warmup=5, min_runs=5):
+    """SURVEY §8d CPU protocol: `warmup` untimed runs, then runs until budget_s has passed (at least
+    min_runs); examples/s as the total rate, the median and the p90 of the per-run rates."""
     import numpy as np
 
+    for _ in range(warmup):
+        fn()
+    ts = []
+    t0 = time.perf_counter()
+    while len(ts) < min_runs or time.perf_counter() - t0 < budget_s:
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    rates = examples / np.asarray(ts)
+    return {"value": round(examples * len(ts) / sum(ts), 1), "median": round(float(np.median(rates)), 1),
+            "p90": round(float(np.percentile(rates, 90)), 1), "runs": len(ts), "seconds": round(sum(ts), 2)}
+
+
+def cpu_baseline(enc, hb, budget_s):
+    """The C oracle (OpenMP) on the same batch: examples/s, median and p90 per batch."""
     from oracle import oracle as O
 
     threads = min(16, os.cpu_count() or 1)
+    model, ncpu = host_cpu()
     table = enc.table.cpu().numpy()
-    n = 0
+    r = timed_runs(lambda: O.fused_hash_embed(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, hb.batch,
+                                              table, enc.dim, enc.out_width, n_threads=threads), hb.batch, budget_s)
+    return dict(r, unit="examples/s", cores=threads, kind="port", cpu=model, host_cpus=ncpu,
+                sample=f"{r['runs']} x one {hb.batch}-example cfg2 batch through oracle/rf_oracle.c "
+                       f"(orf_fused_hash_embed_fwd, OpenMP {threads} threads, gcc -O3) after 5 warm-up runs, "
+                       f"{r['seconds']} s; median / p90 are per-batch rates")
+
+
+def bench_h2d(args, enc, host):
+    """cfg2 with the CSR batches starting in PINNED HOST memory (BASELINE.md §2's second number): batch
+    i+1 is copied H2D on a side stream into the other of two static device buffers while the fused kernel
+    runs on batch i (double buffering, stream-ordered by events). Not the headline (inputs resident)."""
+    import torch
+
+    from recommendflow_amd.runtime.graphs import StaticSparseBatch
+
+    pinned = [[torch.from_numpy(a).pin_memory() for a in (h.tok_bytes, h.tok_off, h.bag_off, h.lmax)] for h in host]
+    cap_b = max(len(h.tok_bytes) for h in host)
+    cap_t = max(h.n_tokens for h in host)
+    bufs = [StaticSparseBatch(host[0], cap_b, cap_t) for _ in range(2)]
+    out = torch.empty((args.batch, enc.out_width), dtype=torch.float32, device="cuda")
+    cs, comp = torch.cuda.Stream(), torch.cuda.current_stream()
+    copied = [torch.cuda.Event() for _ in range(2)]
+    consumed = [torch.cuda.Event() for _ in range(2)]
+    nbytes = sum(int(t.numel() * t.element_size()) for t in pinned[0])
+
+    def issue_copy(i):
+        k, (tb, to, bo, lm) = i & 1, pinned[i % len(pinned)]
+        with torch.cuda.stream(cs):
+            cs.wait_event(consumed[k])
+            b = bufs[k]
+            b.tok_bytes[: tb.numel()].copy_(tb, non_blocking=True)
+            b.tok_off[: to.numel()].copy_(to, non_blocking=True)
+            b.bag_off.copy_(bo, non_blocking=True)
+            b.lmax.copy_(lm, non_blocking=True)
+            copied[k].record(cs)
+
+    def run(n):
+        issue_copy(0)
+        for i in range(n):
+            if i + 1 < n:
+                issue_copy(i + 1)
+            comp.wait_event(copied[i & 1])
+            enc(bufs[i & 1], out=out)
+            consumed[i & 1].record(comp)
+
+    run(8)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    while True:
-        O.fused_hash_embed(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, hb.batch, table, enc.dim,
-                           enc.out_width, n_threads=threads)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round(n * hb.batch / el, 1), "unit": "examples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x one {hb.batch}-example cfg2 batch through oracle/rf_oracle.c "
-                      f"(orf_fused_hash_embed_fwd, OpenMP {threads} threads, gcc -O3) in {el:.1f} s"}
+    run(args.steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"examples_per_s": round(args.batch * args.steps / el, 1), "ms_per_step": round(el / args.steps * 1e3, 4),
+            "h2d_bytes_per_batch": nbytes, "h2d_GBs": round(nbytes * args.steps / el / 1e9, 2),
+            "config": "cfg2 encoder, CSR batches in pinned host memory, H2D on a side stream double-buffered "
+                      "against the fused kernel (PCIe-inclusive; the headline value keeps inputs in HBM)"}
 
 
 if __name__ == "__main__":

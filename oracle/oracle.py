@@ -396,6 +396,42 @@ def mlp(x, layers, act: str, norm: str = "ln", eps: float = 1e-6):
     return x
 
 
+def esim_scorer_f32(q, a, dense, input_layers, output_layers, W_out, b_out, eps=1e-6):
+    """The CPU baseline of cfg3's dense stages (bench.py cpu_baseline): a.5-a.7 in float32
+    numpy / BLAS, operation for operation as the reference graph runs them on a CPU (esim.py:69-89):
+    SoftAttention (attention_layers.py:44-74, batched matmuls, max-subtracted softmax), the [B, 4L, d]
+    concatenations and their mean / max (esim.py:79-84), create_mlp LayerNorm -> Dense(gelu) stacks
+    (mlp.py:4-15), Dense(2, softmax) (esim.py:53,88). Not a checker: the float64 functions above are."""
+    from scipy.special import erf
+
+    f = np.float32
+    q, a, dense = np.asarray(q, f), np.asarray(a, f), np.asarray(dense, f)
+
+    def ln(x, p):
+        mu = x.mean(-1, keepdims=True, dtype=f)
+        d = x - mu
+        var = (d * d).mean(-1, keepdims=True, dtype=f)
+        return d / np.sqrt(var + f(eps)) * p["gamma"].astype(f) + p["beta"].astype(f)
+
+    def stack(x, layers):
+        for p in layers:
+            x = ln(x, p) @ p["W"].astype(f) + p["b"].astype(f)
+            x = f(0.5) * x * (f(1.0) + erf(x / f(math.sqrt(2.0))).astype(f))
+        return x
+
+    E = np.matmul(a, q.transpose(0, 2, 1))
+    E = np.exp(E - E.max(-1, keepdims=True))
+    S = E / E.sum(-1, keepdims=True)
+    att_q, att_a = np.matmul(S, q), np.matmul(S, a)
+    m_q = np.concatenate([q, att_q, q - att_q, q * att_q], axis=1)
+    m_a = np.concatenate([a, att_a, a - att_a, a * att_a], axis=1)
+    avg_q, max_q, avg_a, max_a = m_q.mean(1, dtype=f), m_q.max(1), m_a.mean(1, dtype=f), m_a.max(1)
+    pooled = np.concatenate([stack(dense, input_layers), avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a], axis=1)
+    z = stack(pooled, output_layers) @ np.asarray(W_out, f) + np.asarray(b_out, f)
+    z = np.exp(z - z.max(-1, keepdims=True))
+    return z / z.sum(-1, keepdims=True)
+
+
 def sdpa(q, k, v, mask=None):
     """scaled_dot_product_attention (layer_utils.py:4-24): mask [.., Lq] zero => whole QUERY row filled
     with -4294967295 (the [..., Lq, 1] mask broadcasts over keys), softmax over keys, @ v."""

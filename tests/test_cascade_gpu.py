@@ -1,5 +1,5 @@
-"""GPU: the recall -> prerank -> rank cascade (cfg5 wiring, models/cascade.py) against a float64 / explicit
-recomposition of each stage."""
+"""GPU: the recall -> prerank -> rank cascade (cfg5 wiring, models/cascade.py), every stage against the
+float64 oracle."""
 import numpy as np
 import pytest
 import torch
@@ -11,6 +11,8 @@ from recommendflow_amd.models.matching.dssm import Dssm
 from recommendflow_amd.models.ranking.esim import Esim
 from recommendflow_amd.runtime.batch import synthetic_batch
 
+from model_helpers import enc_ref, mlp_params
+
 pytestmark = pytest.mark.gpu
 
 
@@ -21,8 +23,8 @@ def _build(N=3000, B=16, Ls=8):
     esim = Esim([SlotSpec(f"q{i}", 1000, (7, 8)) for i in range(Ls)], [SlotSpec(f"k{i}", 1000, (7, 8)) for i in range(Ls)],
                 n_dense=16, dim=64, seed=4)
     cas = Cascade(dssm, esim, k_recall=100, k_prerank=20, k_final=5, seed=5)
-    cat_r = [synthetic_batch(1000, [False] * 5, seed=50 + i, slot_ids=range(100, 105)).to("cuda") for i in range(N // 1000)]
-    cat_k = [synthetic_batch(1000, [False] * Ls, seed=80 + i, slot_ids=range(200, 200 + Ls)).to("cuda") for i in range(N // 1000)]
+    cat_r = [c.to("cuda") for c in _catalog_recall_batches(N)]
+    cat_k = [c.to("cuda") for c in _catalog_rank_batches(Ls, N)]
     cas.index_catalog(cat_r, cat_k)
     ur = synthetic_batch(B, [i % 2 == 0 for i in range(6)], seed=7).to("cuda")
     uk = synthetic_batch(B, [False] * Ls, seed=9, slot_ids=range(300, 300 + Ls)).to("cuda")
@@ -39,29 +41,60 @@ def test_topk_rows_and_gather(cuda):
 
 
 def test_cascade_stages(cuda):
+    """Every stage against the float64 oracle composed from the ORACLE's encodings (not the model's own
+    modules): recall towers + exact inner-product top-100, prerank Dense(64, relu) -> Dense(1) scores and
+    their top-20, rank ESIM p(click) (fp16 attention) of the prerank candidates and the best 5 (§8d bar:
+    |dp| <= 1e-2; selections equal up to near-ties)."""
     cas, ur, uk, dense = _build()
     res = cas(ur, uk, dense)
     B = ur.batch
-    items = cas.searcher.index.cpu().numpy()
+    urh, ukh = ur.numpy(), uk.numpy()
+    # recall: oracle user tower, exact search over the catalog vectors
+    un = O.l2_normalize(O.mlp(enc_ref(O, cas.recall.enc_u, urh), mlp_params(cas.recall.user_dense), "selu", "bn"), eps=1e-6)
     with torch.no_grad():
-        u = torch.nn.functional.normalize(cas.recall.user_dense(cas.recall.enc_u(ur)), dim=-1, eps=1e-6)
-    un = u.cpu().numpy()
-    # recall = exact top-100 inner products (ties / fp32-GEMM near-ties excepted)
-    want_s, want_i = O.flat_search(un, items, 100)
-    got = res.recall_items.cpu().numpy()
-    sc = (un.astype(np.float64)[:, None, :] * items[got].astype(np.float64)).sum(-1)
-    np.testing.assert_allclose(sc, want_s, rtol=1e-4, atol=1e-5)
-    # prerank = top-20 of the light model on exactly those candidates
-    with torch.no_grad():
-        x = (u[:, None, :] * cas.searcher.index[res.recall_items]).reshape(B * 100, -1)
-        s2 = cas.pre2(cas.pre1(x)).view(B, 100).cpu().numpy()
+        ug = torch.nn.functional.normalize(cas.recall.user_dense(cas.recall.enc_u(ur)), dim=-1, eps=1e-6).cpu().numpy()
+    np.testing.assert_allclose(ug, un, rtol=1e-4, atol=1e-5)
+    items = np.concatenate([O.l2_normalize(O.mlp(enc_ref(O, cas.recall.enc_a, c), mlp_params(cas.recall.ad_dense), "selu",
+                                                 "bn"), eps=1e-6) for c in _catalog_recall_batches()])
+    np.testing.assert_allclose(cas.searcher.index.cpu().numpy(), items, rtol=1e-4, atol=1e-5)
+    want_s, _ = O.flat_search(un, items, 100)
+    got1 = res.recall_items.cpu().numpy()
+    np.testing.assert_allclose((un[:, None, :] * items[got1]).sum(-1), want_s, rtol=1e-4, atol=1e-5)
+    # prerank: float64 scores of the recall candidates, top-20 (ties within the fp32 error excepted)
+    p1, p2 = cas.pre1, cas.pre2
+    W1, b1 = p1.weight.cpu().numpy().T.astype(np.float64), p1.bias.cpu().numpy()
+    W2, b2 = p2.weight.cpu().numpy().T.astype(np.float64), p2.bias.cpu().numpy()
+    s2 = (np.maximum((un[:, None, :] * items[got1]) @ W1 + b1, 0.0) @ W2 + b2)[..., 0]  # [B, 100]
+    got2 = res.prerank_items.cpu().numpy()
+    pos = {b: {int(i): k for k, i in enumerate(got1[b])} for b in range(B)}
     for b in range(B):
-        order = np.argsort(-s2[b], kind="stable")[:20]
-        assert set(got[b][order].tolist()) == set(res.prerank_items[b].cpu().tolist()) or \
-            np.sort(s2[b])[::-1][19] - np.sort(s2[b])[::-1][20] < 1e-5
-    # rank = ESIM p(click) of the (user, candidate) pairs, best 5
-    assert res.items.shape == (B, 5) and res.scores.shape == (B, 5)
+        srt = np.sort(s2[b])[::-1]
+        kth = srt[19]
+        sel = np.array([s2[b, pos[b][int(i)]] for i in got2[b]])
+        assert np.all(sel >= kth - 1e-5), b  # every selected candidate is within tolerance of the top 20
+        assert np.all(np.diff(sel) <= 1e-5), b  # in descending order
+    # rank: oracle encodings of the user / item sequences (bf16 tables -> fp16 operands, exact), ESIM + MLPs
+    rk = cas.ranker
+    q = enc_ref(O, rk.enc_q, ukh).reshape(B, rk.L, rk.d)
+    cat = np.concatenate([enc_ref(O, rk.enc_a, c.numpy()) for c in _catalog_rank_batches(rk.L)]).reshape(-1, rk.L, rk.d)
+    np.testing.assert_array_equal(cat.astype(np.float16), cas.a_item.cpu().numpy().reshape(cat.shape))
+    d_emb = O.mlp(dense.cpu().numpy(), mlp_params(rk.input_mlp), "gelu", "ln")
+    Wo = rk.dense_output.weight.float().cpu().numpy().T.astype(np.float64)
+    bo = rk.dense_output.bias.cpu().numpy()
+    got3, s3 = res.items.cpu().numpy(), res.scores.cpu().numpy()
+    for b in range(B):
+        qa = np.repeat(q[b:b + 1], 20, axis=0)
+        pooled = np.concatenate([np.repeat(d_emb[b:b + 1], 20, axis=0), O.esim_pool(qa, cat[got2[b]])], axis=1)
+        p = O.activation(O.mlp(pooled, mlp_params(rk.output_mlp), "gelu", "ln") @ Wo + bo, "softmax")[:, 1]
+        pmap = {int(i): p[k] for k, i in enumerate(got2[b])}
+        np.testing.assert_allclose(s3[b], [pmap[int(i)] for i in got3[b]], atol=1e-2, rtol=0)
+        assert min(pmap[int(i)] for i in got3[b]) >= np.sort(p)[::-1][4] - 2e-2, b
     assert torch.all(res.scores[:, :-1] >= res.scores[:, 1:])
-    for b in range(B):
-        assert set(res.items[b].cpu().tolist()) <= set(res.prerank_items[b].cpu().tolist())
-    assert torch.all((res.scores >= 0) & (res.scores <= 1))
+
+
+def _catalog_recall_batches(N=3000):
+    return [synthetic_batch(1000, [False] * 5, seed=50 + i, slot_ids=range(100, 105)) for i in range(N // 1000)]
+
+
+def _catalog_rank_batches(Ls, N=3000):
+    return [synthetic_batch(1000, [False] * Ls, seed=80 + i, slot_ids=range(200, 200 + Ls)) for i in range(N // 1000)]
