@@ -328,9 +328,7 @@ def bench_esim(args):
         esim_soft_attention_pool(q.view(B, Ls, 128), a.view(B, Ls, 128), out=pooled, out_col=model.d_emb)
 
     def mlp():
-        x = dense
-        for k, (norm, dl) in enumerate(zip(model.input_mlp.norms, model.input_mlp.denses)):
-            x = dl(norm(x, out_dtype=torch.bfloat16), out=pooled[:, : model.d_emb] if k == len(model.input_mlp.denses) - 1 else None)
+        model.input_mlp(dense, out=pooled[:, : model.d_emb])
         model.dense_output(model.output_mlp(pooled))
 
     steps = max(10, args.steps // 2)

@@ -187,6 +187,31 @@ int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t 
                   int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream);
 
 /*
+ * A two-layer create_mlp on a narrow input in ONE launch (the ESIM input_mlp [256, 512] over the dense
+ * features, esim.py:45-48; mlp.py:4-15 with LayerNormalization):
+ *   out = act(LN1(act(LN0(x) W0^T + b0)) W1^T + b1)
+ * x: F32 [M][K0] (K0 <= 32), row stride ldx. LN0/LN1: gamma/beta F32 [K0] / [H], epsilon eps.
+ * W0: BF16 [H][K0], W1: BF16 [O][H] (16-byte aligned), b0 [H] / b1 [O] F32 (may be NULL). H = 128 or 256.
+ * LN outputs are rounded once to bf16 (the MFMA operands), as the rf_norm_fwd -> rf_linear_fwd chain.
+ * out: F32 [M][O], row stride ldo (e.g. the first O columns of the pooled [B, 512 + 6d] tensor).
+ * act: an elementwise RF_ACT_* (not SOFTMAX).
+ */
+int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float eps, const float* ln0_gamma,
+                      const float* ln0_beta, const void* W0, const float* b0, int32_t H, const float* ln1_gamma,
+                      const float* ln1_beta, const void* W1, const float* b1, int32_t O, int32_t act, float* out,
+                      int64_t ldo, void* stream);
+
+/*
+ * Small Dense head on fp32 activations  y = act(x @ W + b),  N <= 64 outputs (the ESIM scorer's
+ * Dense(2, 'softmax'), esim.py:53,88): replaces rf_linear_fwd's small-N path when the activations are the
+ * fp32 output of the previous layer (no bf16 round trip of x). x: F32 [M][K], row stride ldx, 16-byte
+ * aligned rows, K % 4 == 0. W: [N][K] in w_dtype (BF16 widened to fp32, or F32). b: F32 [N] or NULL.
+ * y: F32 [M][N], row stride ldy. One wave per row, fp32 products and sums.
+ */
+int rf_dense_head_fwd(const float* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t w_dtype,
+                      int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream);
+
+/*
  * Masked scaled-dot-product attention over heads (backend/layers/layer_utils.py:4-24, with the
  * split_heads / merge transposes of MultiHeadAttention.call, attention_layers.py:159-167, folded
  * into the addressing):

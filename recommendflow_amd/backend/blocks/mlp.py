@@ -9,6 +9,7 @@ from typing import List, Optional, Sequence
 
 import torch
 
+from ...runtime import lib as L
 from ..layers.core import Dense, Norm, act_name
 
 
@@ -40,13 +41,36 @@ class MLP(torch.nn.Module):
         self.out_features = width
         return self
 
-    def forward(self, x: torch.Tensor, stream=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """x [M, in] -> [M, hidden_units[-1]] fp32; `out` (optional) receives the last layer (any row stride).
+        A two-layer LayerNorm MLP on a narrow input runs as ONE launch (rf_mlp2_small_fwd); otherwise
+        each layer is rf_norm_fwd -> rf_linear_fwd."""
         if not self.denses:
             self.build(x.shape[-1])
-        for norm, dense in zip(self.norms, self.denses):
+        if self._fusable(x):
+            return self._forward_fused(x, out, stream)
+        last = len(self.denses) - 1
+        for i, (norm, dense) in enumerate(zip(self.norms, self.denses)):
             h = norm(x, out_dtype=self.dtype, stream=stream) if norm is not None else x
-            x = dense(h, stream=stream)
+            x = dense(h, out=out if i == last else None, stream=stream)
         return x
+
+    def _fusable(self, x: torch.Tensor) -> bool:
+        return (len(self.denses) == 2 and self.dtype == torch.bfloat16 and x.dtype == torch.float32
+                and all(n is not None and n.mode == 0 for n in self.norms) and self.activation != "softmax"
+                and self.denses[0].in_features <= 32 and self.denses[0].units in (128, 256)
+                and x.dim() == 2 and x.stride(-1) == 1)
+
+    def _forward_fused(self, x, out, stream):
+        n0, n1 = self.norms
+        d0, d1 = self.denses
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty((M, d1.units), dtype=torch.float32, device=x.device)
+        L.call("rf_mlp2_small_fwd", L.ptr(x), M, d0.in_features, x.stride(0), n0.eps, L.ptr(n0.gamma), L.ptr(n0.beta),
+               L.ptr(d0.weight), L.ptr(d0.bias), d0.units, L.ptr(n1.gamma), L.ptr(n1.beta), L.ptr(d1.weight),
+               L.ptr(d1.bias), d1.units, L.ACT[self.activation], L.ptr(out), out.stride(0), L.stream_ptr(stream))
+        return out
 
 
 def create_mlp(hidden_units, dropout_rate, activation, normalization_layer, name=None, **kw) -> MLP:

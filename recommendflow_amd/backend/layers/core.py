@@ -47,11 +47,20 @@ class Dense(torch.nn.Module):
         self.bias = None if bias is None else bias.to(device=device, dtype=torch.float32).contiguous()
 
     def forward(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        M = x.shape[0]
+        if (self.units <= 16 or self.activation == "softmax") and x.dtype == torch.float32 and self.units <= 64 \
+                and self.in_features % 4 == 0 and x.stride(-1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0:
+            # small head on fp32 activations: no bf16 round trip of x (rf_dense_head_fwd)
+            if out is None:
+                out = torch.empty((M, self.units), dtype=torch.float32, device=self.weight.device)
+            L.call("rf_dense_head_fwd", L.ptr(x), M, self.in_features, x.stride(0), L.ptr(self.weight),
+                   L.torch_dtype_code(self.dtype), self.units, L.ptr(self.bias), L.ACT[self.activation], L.ptr(out),
+                   out.stride(0), L.stream_ptr(stream))
+            return out
         if x.dtype != self.dtype:
             x = x.to(self.dtype)
         if x.stride(-1) != 1:
             x = x.contiguous()
-        M = x.shape[0]
         if out is None:
             out = torch.empty((M, self.units), dtype=torch.float32, device=self.weight.device)
         L.call("rf_linear_fwd", L.ptr(x), L.torch_dtype_code(self.dtype), M, self.in_features, x.stride(0),

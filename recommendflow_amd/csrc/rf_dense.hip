@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "rf_common.h"
 
@@ -377,6 +378,134 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 GEMM on an LDS-DMA ring (K % 64 == 0): y[M,N] = act(x[M,K] W[N,K]^T + b), fp32 out.
+//   * block tile BM x 128 x 64 (BM = 128: 4 waves 2 x 2 of 64 x 64; BM = 64: 4 waves 1 x 4 of 64 x 32),
+//     v_mfma_f32_16x16x32_bf16 with fp32 accumulators;
+//   * A and B tiles land in LDS by global_load_lds_dwordx4 (no VGPR staging, no ds_write) in a ring of
+//     3 buffers: the loads of step k+2 are issued right after the barrier that opens step k, so two
+//     steps are in flight behind the MFMAs; each wave waits with a COUNTED vmcnt (never 0 inside the
+//     loop) and the buffer is read only after the raw s_barrier that follows the wait;
+//   * 128-byte tile rows, 16-byte chunk c of row r stored at chunk c ^ (r & 7): the ds_read_b128 lane
+//     groups of a 16 x 32 fragment touch 16 distinct (row parity, chunk) bank quads = conflict-free.
+//     LDS-DMA writes lane-linear, so the swizzle is applied on the SOURCE address (lane -> chunk);
+//   * XCD-aware tile order: the workgroups of one XCD (block ids congruent mod 8) take consecutive tiles,
+//     so the N-tiles sharing an A row panel share that XCD's L2.
+// ---------------------------------------------------------------------------------------------
+constexpr int kLdsK = 64, kLdsBN = 128, kLdsStages = 3;
+
+template <int BM>
+__device__ __forceinline__ void glds_stage(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int64_t M, int N,
+                                           int64_t ldx, int K, int64_t m0, int n0, int k0, uint16_t* As, uint16_t* Bs,
+                                           int tid) {
+    // one wave-instruction = 8 tile rows x 8 chunks (1 KiB, lane-linear in LDS); 4 waves
+    const int wave = tid >> 6, lane = tid & 63, rr = lane >> 3, pos = lane & 7;
+#pragma unroll
+    for (int it = 0; it < BM / 32; ++it) {
+        const int g = wave + 4 * it, r = g * 8 + rr;
+        const int64_t row = m0 + r < M ? m0 + r : M - 1;  // rows past M: any valid row (never stored)
+        const uint16_t* src = x + row * ldx + k0 + ((pos ^ rr) << 3);
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + g * 512), 16, 0, 0);
+    }
+#pragma unroll
+    for (int it = 0; it < kLdsBN / 32; ++it) {
+        const int g = wave + 4 * it, r = g * 8 + rr;
+        const int64_t col = n0 + r < N ? n0 + r : N - 1;
+        const uint16_t* src = w + col * (int64_t)K + k0 + ((pos ^ rr) << 3);
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + g * 512), 16, 0, 0);
+    }
+}
+
+template <int BM>
+__global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ y, int64_t M,
+                                                       int N, int K, int64_t ldx, int64_t ldy, int act) {
+    constexpr int WM = BM == 128 ? 2 : 1, WN = 4 / WM;            // wave grid
+    constexpr int TM = BM / WM, TN = kLdsBN / WN;                  // wave tile
+    constexpr int FM = TM / 16, FN = TN / 16;                      // fragments per wave
+    constexpr int A_EL = BM * kLdsK, B_EL = kLdsBN * kLdsK;        // elements per stage
+    constexpr int LOADS = (BM / 8 + kLdsBN / 8) / 4;               // glds per thread per stage
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    uint16_t* lds = reinterpret_cast<uint16_t*>(smem_raw);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int wm = wave / WN, wn = wave % WN;
+    // XCD-aware tile order (bijective): block b runs on XCD b % 8; give each XCD a contiguous tile range
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
+    const int tiles_n = (N + kLdsBN - 1) / kLdsBN;
+    const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
+    const int n0 = (tile % tiles_n) * kLdsBN;
+    const int nk = K / kLdsK;
+
+    f4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+    auto As = [&](int s) { return lds + s * (A_EL + B_EL); };
+    auto Bs = [&](int s) { return lds + s * (A_EL + B_EL) + A_EL; };
+    glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, 0, As(0), Bs(0), tid);
+    if (nk > 1) glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, kLdsK, As(1), Bs(1), tid);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int s = kt % kLdsStages;
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage kt landed for every wave; every wave is done reading stage kt - 1
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 2 < nk) {
+            const int s2 = (kt + 2) % kLdsStages;
+            glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, (kt + 2) * kLdsK, As(s2), Bs(s2), tid);
+        }
+        const uint16_t* A = As(s);
+        const uint16_t* B = Bs(s);
+        // both 32-deep halves' fragments are read up front: the second half's reads run under the first
+        // half's MFMAs
+        bf16x8 af[2][FM], bfr[2][FN];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ch = 4 * h + lg;  // 16-byte chunk of this lane's 8 k values
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int r = wm * TM + i * 16 + lr;
+                af[h][i] = *reinterpret_cast<const bf16x8*>(A + r * kLdsK + ((ch ^ (r & 7)) << 3));
+            }
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int r = wn * TN + j * 16 + lr;
+                bfr[h][j] = *reinterpret_cast<const bf16x8*>(B + r * kLdsK + ((ch ^ (r & 7)) << 3));
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMAs (hipcc would re-serialise them)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[h][i], bfr[h][j], acc[i][j], 0, 0, 0);
+    }
+    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int col = n0 + wn * TN + j * 16 + lr;
+        if (col >= N) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                if (row < M) y[row * ldy + col] = act_apply(act, acc[i][j][r] + bv);
+            }
+    }
+}
+
+template <int BM>
+constexpr size_t gemm_lds_bytes() {
+    return (size_t)kLdsStages * (BM + kLdsBN) * kLdsK * 2;
+}
+
 // small-N head: one wave per row, fp32 dot products, optional row softmax (N <= 64)
 template <bool BF16>
 __global__ __launch_bounds__(256) void small_n_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
@@ -418,7 +547,294 @@ __global__ __launch_bounds__(256) void small_n_kernel(const void* __restrict__ x
         for (int n = 0; n < N; ++n) y[row * ldy + n] = outv[n];
 }
 
+// small Dense head on fp32 activations (rf_dense_head_fwd): one wave per row, float4 loads of x and the
+// weights' 4 matching k values per output, NMAX fp32 partial dots per lane, shuffle-reduced
+template <bool WBF16, int NMAX>
+__global__ __launch_bounds__(256) void dense_head_kernel(const float* __restrict__ x, int64_t M, int K, int64_t ldx,
+                                                         const void* __restrict__ wv, int N, const float* __restrict__ bias,
+                                                         int act, float* __restrict__ y, int64_t ldy) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
+    float acc[NMAX];
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) acc[n] = 0.f;
+    for (int k4 = lane; 4 * k4 < K; k4 += 64) {
+        const float4 xv = xr[k4];
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) {
+            if (n < N) {
+                float4 w;
+                if constexpr (WBF16) {
+                    const uint2 u = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(wv) + (int64_t)n * K)[k4];
+                    w = make_float4(bf16_bits_to_f32(u.x & 0xffffu), bf16_bits_to_f32(u.x >> 16),
+                                    bf16_bits_to_f32(u.y & 0xffffu), bf16_bits_to_f32(u.y >> 16));
+                } else {
+                    w = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(wv) + (int64_t)n * K)[k4];
+                }
+                acc[n] = fmaf(xv.x, w.x, acc[n]);
+                acc[n] = fmaf(xv.y, w.y, acc[n]);
+                acc[n] = fmaf(xv.z, w.z, acc[n]);
+                acc[n] = fmaf(xv.w, w.w, acc[n]);
+            }
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+        if (n < N) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) acc[n] += __shfl_xor(acc[n], o, 64);
+            acc[n] += bias ? bias[n] : 0.f;
+            if (act != RF_ACT_SOFTMAX) acc[n] = act_apply(act, acc[n]);
+            mx = fmaxf(mx, acc[n]);
+        }
+    }
+    if (act == RF_ACT_SOFTMAX) {
+        float sum = 0.f;
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n)
+            if (n < N) {
+                acc[n] = expf(acc[n] - mx);
+                sum += acc[n];
+            }
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n) acc[n] /= sum;
+    }
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n)
+        if (n < N && lane == (n & 63)) y[row * ldy + n] = acc[n];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two-layer create_mlp on a narrow input, one launch (the ESIM input_mlp: 16 -> 256 -> 512, LayerNorm,
+// gelu; esim.py:45-48, mlp.py:4-15): per workgroup 16 rows,
+//   LN0 (K0 <= 32 columns, one 4-lane group per row) -> bf16 A tile in LDS (k padded to 32 with zeros)
+//   H = gelu(A W0^T + b0): one 16x16x32 MFMA per 16-column tile (W0 staged in LDS, k padded)
+//   LN1 over H's columns (row partials reduced in lanes, then across the 4 waves through LDS)
+//   -> bf16 tile in LDS; O = gelu(LN1(H) W1^T + b1): W1 fragments straight from global (L2) with the
+//   next k-step's fragments in flight; fp32 stores into the caller's strided output.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMlp2Rows = 16;
+
+template <int H>
+__global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict__ x, int64_t M, int K0, int64_t ldx, float eps,
+                                                         const float* __restrict__ g0, const float* __restrict__ be0,
+                                                         const uint16_t* __restrict__ W0, const float* __restrict__ b0,
+                                                         const float* __restrict__ g1, const float* __restrict__ be1,
+                                                         const uint16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                         int O, int act, float* __restrict__ out, int64_t ldo) {
+    constexpr int RS0 = 32 + 8, RSH = H + 8;  // LDS row strides (elements): 16-byte row pad
+    constexpr int T0 = H / 64;                // layer-0 column tiles per wave
+    __shared__ __attribute__((aligned(16))) uint16_t xs[kMlp2Rows * RS0];
+    __shared__ __attribute__((aligned(16))) uint16_t w0s[H * RS0];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[kMlp2Rows * RSH];
+    __shared__ float red[4][kMlp2Rows];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int64_t r0 = (int64_t)blockIdx.x * kMlp2Rows;
+    // ---- every small load issued up front (one round trip, not one per element) ----
+    // W0 -> LDS as 16-byte chunks (k zero-padded to 32): H rows x 4 chunks, 256 threads
+    uint4 w0c[H / 64];
+    const bool vec0 = (K0 & 7) == 0;
+#pragma unroll
+    for (int i = 0; i < H / 64; ++i) {
+        const int c = tid + 256 * i, n = c >> 2, ch = c & 3;
+        w0c[i] = make_uint4(0, 0, 0, 0);
+        if (vec0 && 8 * ch < K0) w0c[i] = *reinterpret_cast<const uint4*>(W0 + (int64_t)n * K0 + 8 * ch);
+    }
+    float hb0[T0], hg1[T0], hbe1[T0];
+#pragma unroll
+    for (int t = 0; t < T0; ++t) {
+        const int n = (wave * T0 + t) * 16 + lr;
+        hb0[t] = b0 ? b0[n] : 0.f;
+        hg1[t] = g1 ? g1[n] : 1.f;
+        hbe1[t] = be1 ? be1[n] : 0.f;
+    }
+    // LN0 operands: wave 0, row = lane >> 2, 4 lanes per row, columns k = 4 j + (lane & 3)
+    float xv[8], gv[8], bv[8];
+    const int xr = lane >> 2, sub = lane & 3;
+    if (wave == 0) {
+        const int64_t row = r0 + xr < M ? r0 + xr : M - 1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 4 * j + sub < K0 ? 4 * j + sub : K0 - 1;  // clamped: no per-element branch
+            xv[j] = x[row * ldx + k];
+            gv[j] = g0[k];
+            bv[j] = be0[k];
+        }
+    }
+    // ---- W0 tile ----
+    if (vec0) {
+#pragma unroll
+        for (int i = 0; i < H / 64; ++i) {
+            const int c = tid + 256 * i, n = c >> 2, ch = c & 3;
+            *reinterpret_cast<uint4*>(w0s + n * RS0 + 8 * ch) = w0c[i];
+        }
+    } else {
+        for (int i = tid; i < H * 32; i += 256) {
+            const int n = i >> 5, k = i & 31;
+            w0s[n * RS0 + k] = k < K0 ? W0[(int64_t)n * K0 + k] : (uint16_t)0;
+        }
+    }
+    // ---- LN0 ----
+    if (wave == 0) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            xv[j] = 4 * j + sub < K0 ? xv[j] : 0.f;
+            s += xv[j];
+        }
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        const float mu = s / (float)K0;
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (4 * j + sub < K0) q += (xv[j] - mu) * (xv[j] - mu);
+        q += __shfl_xor(q, 1, 64);
+        q += __shfl_xor(q, 2, 64);
+        const float rstd = 1.0f / sqrtf(q / (float)K0 + eps);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 4 * j + sub;
+            xs[xr * RS0 + k] = k < K0 ? (uint16_t)f32_to_bf16_bits((xv[j] - mu) * rstd * gv[j] + bv[j]) : (uint16_t)0;
+        }
+    }
+    __syncthreads();
+    // ---- layer 0: wave w owns column tiles w * T0 ..; one MFMA each (k = 32) ----
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xs + lr * RS0 + lg * 8);
+    float hv[T0][4];
+    float psum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < T0; ++t) {
+        const int n = (wave * T0 + t) * 16 + lr;
+        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(w0s + n * RS0 + lg * 8);
+        const f4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            hv[t][r] = act_apply(act, c[r] + hb0[t]);
+            psum[r] += hv[t][r];
+        }
+    }
+    // ---- LN1 statistics: rows 4 lg + r of this lane; sum over lanes lr, then over the 4 waves ----
+    auto row_total = [&](float (&p)[4], float (&tot)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) p[r] += __shfl_xor(p[r], o, 64);
+            if (lr == 0) red[wave][4 * lg + r] = p[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * lg + r;
+            tot[r] = (red[0][row] + red[1][row]) + (red[2][row] + red[3][row]);
+        }
+        __syncthreads();
+    };
+    float mu[4], var[4];
+    row_total(psum, mu);
+    float pq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        mu[r] /= (float)H;
+#pragma unroll
+        for (int t = 0; t < T0; ++t) pq[r] += (hv[t][r] - mu[r]) * (hv[t][r] - mu[r]);
+    }
+    row_total(pq, var);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float rstd = 1.0f / sqrtf(var[r] / (float)H + eps);
+#pragma unroll
+        for (int t = 0; t < T0; ++t) {
+            const int n = (wave * T0 + t) * 16 + lr;
+            hs[(4 * lg + r) * RSH + n] = (uint16_t)f32_to_bf16_bits((hv[t][r] - mu[r]) * rstd * hg1[t] + hbe1[t]);
+        }
+    }
+    __syncthreads();
+    // ---- layer 1: O columns in 16-wide tiles, wave w takes tiles w, w + 4, ...; the next tile's W1
+    // fragments (from L2) are in flight while this tile's MFMAs run ----
+    constexpr int KS = H / 32;
+    bf16x8 ha[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) ha[kk] = *reinterpret_cast<const bf16x8*>(hs + lr * RSH + kk * 32 + lg * 8);
+    auto tile = [&](int nt, bf16x8 (&bw)[KS], float& bias1) {  // W1 fragments of column tile nt
+        const int n = nt * 16 + lr < O ? nt * 16 + lr : O - 1;
+        const uint16_t* wrow = W1 + (int64_t)n * H + lg * 8;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) bw[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 32);
+        bias1 = b1 ? b1[n] : 0.f;
+    };
+    auto finish = [&](int nt, const bf16x8 (&bw)[KS], float bias1) {
+        f4 c = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[kk], bw[kk], c, 0, 0, 0);
+        const int n = nt * 16 + lr;
+        if (n < O) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = r0 + 4 * lg + r;
+                if (row < M) out[row * ldo + n] = act_apply(act, c[r] + bias1);
+            }
+        }
+    };
+    // two tiles per step (nt, nt + 4): both tiles' fragments are in flight together
+    for (int nt = wave; nt * 16 < O; nt += 8) {
+        bf16x8 bwa[KS], bwb[KS];
+        float ba = 0.f, bb = 0.f;
+        const bool second = (nt + 4) * 16 < O;
+        tile(nt, bwa, ba);
+        if (second) tile(nt + 4, bwb, bb);
+        finish(nt, bwa, ba);
+        if (second) finish(nt + 4, bwb, bb);
+    }
+}
+
 }  // namespace
+
+extern "C" int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float eps, const float* ln0_gamma,
+                                 const float* ln0_beta, const void* W0, const float* b0, int32_t H, const float* ln1_gamma,
+                                 const float* ln1_beta, const void* W1, const float* b1, int32_t O, int32_t act, float* out,
+                                 int64_t ldo, void* stream) {
+    RF_REQUIRE(K0 >= 1 && K0 <= 32, "rf_mlp2_small_fwd: input width must be 1..32 (got %d)", K0);
+    RF_REQUIRE(H == 128 || H == 256, "rf_mlp2_small_fwd: hidden width must be 128 or 256 (got %d)", H);
+    RF_REQUIRE(O >= 1 && M >= 0 && ldx >= K0 && ldo >= O, "rf_mlp2_small_fwd: bad shape");
+    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_mlp2_small_fwd: activation must be elementwise");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && W0 && W1 && out && ln0_gamma && ln0_beta, "rf_mlp2_small_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)W1 & 15) == 0 && ((uintptr_t)W0 & 15) == 0, "rf_mlp2_small_fwd: W0 / W1 must be 16-byte aligned");
+    const unsigned grid = (unsigned)((M + kMlp2Rows - 1) / kMlp2Rows);
+    hipStream_t st = rf_stream(stream);
+    if (H == 256)
+        hipLaunchKernelGGL(mlp2_small_kernel<256>, dim3(grid), dim3(256), 0, st, x, M, K0, ldx, eps, ln0_gamma, ln0_beta,
+                           (const uint16_t*)W0, b0, ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, out, ldo);
+    else
+        hipLaunchKernelGGL(mlp2_small_kernel<128>, dim3(grid), dim3(256), 0, st, x, M, K0, ldx, eps, ln0_gamma, ln0_beta,
+                           (const uint16_t*)W0, b0, ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, out, ldo);
+    return rf_check_launch("mlp2_small_kernel");
+}
+
+extern "C" int rf_dense_head_fwd(const float* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t w_dtype,
+                                 int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream) {
+    RF_REQUIRE(w_dtype == RF_DTYPE_BF16 || w_dtype == RF_DTYPE_F32, "rf_dense_head_fwd: W dtype must be BF16 or F32");
+    RF_REQUIRE(act >= RF_ACT_NONE && act <= RF_ACT_SOFTMAX, "rf_dense_head_fwd: unknown activation %d", act);
+    RF_REQUIRE(M >= 0 && K > 0 && K % 4 == 0 && N >= 1 && N <= 64 && ldx >= K && ldx % 4 == 0 && ldy >= N,
+               "rf_dense_head_fwd: need K %% 4 == 0, 1 <= N <= 64, ldx %% 4 == 0");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && W && y, "rf_dense_head_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & (w_dtype == RF_DTYPE_BF16 ? 7 : 15)) == 0,
+               "rf_dense_head_fwd: x must be 16-byte and W 8/16-byte aligned");
+    const unsigned grid = (unsigned)((M + 3) / 4);
+    hipStream_t st = rf_stream(stream);
+#define RF_HEAD(WB, NM) hipLaunchKernelGGL((dense_head_kernel<WB, NM>), dim3(grid), dim3(256), 0, st, x, M, K, ldx, W, N, b, act, y, ldy)
+    const bool wb = w_dtype == RF_DTYPE_BF16;
+    if (N <= 2) { if (wb) RF_HEAD(true, 2); else RF_HEAD(false, 2); }
+    else if (N <= 16) { if (wb) RF_HEAD(true, 16); else RF_HEAD(false, 16); }
+    else { if (wb) RF_HEAD(true, 64); else RF_HEAD(false, 64); }
+#undef RF_HEAD
+    return rf_check_launch("dense_head_kernel");
+}
 
 extern "C" int rf_norm_fwd(const float* x, int64_t rows, int32_t cols, int64_t ldx, int32_t mode, float eps,
                            const float* gamma, const float* beta, const float* mean, const float* var, void* y,
@@ -507,8 +923,43 @@ extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t 
     RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0, "rf_linear_fwd: x/W must be 16-byte aligned");
     // 128-tiles unless that grid would give fewer than 2 workgroups per CU (256 CUs): then 64-tiles
     // (4x the workgroups; same per-element accumulation order, so identical results)
+    static const bool lds_off = [] {  // A/B against the register-staged kernel (measurement only)
+        const char* e = getenv("RF_GEMM_LDS");
+        return e && e[0] == '0';
+    }();
+    // the LDS-DMA kernel where it measured faster (profiles/r02/gemm_ab.txt): deep K, at most ~4 tiles of
+    // 64 x 128 per CU (its per-CU load path is the limit on long grids; short K is all pipeline fill)
+    const int64_t t64 = ((M + 63) / 64) * ((N + kLdsBN - 1) / kLdsBN);
+    if (bf && !lds_off && K % kLdsK == 0 && K >= 512 && t64 <= 1024) {
+        const int64_t t128 = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
+        static const int force_bm = [] {  // A/B of the row tile (measurement only): RF_GEMM_BM=64|128
+            const char* e = getenv("RF_GEMM_BM");
+            return e ? atoi(e) : 0;
+        }();
+        // 128-row tiles when they give two per CU (one 98 KiB workgroup per CU), else 64-row tiles: two
+        // 74 KiB workgroups share a CU
+        const bool big = force_bm ? force_bm == 128 : t128 >= 512;
+        const int64_t tiles = big ? t128 : ((M + 63) / 64) * ((N + kLdsBN - 1) / kLdsBN);
+        RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_linear_fwd: too many tiles");
+        if (big) {
+            auto kern = gemm_lds_kernel<128>;
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<128>());
+            if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel: %s", hipGetErrorString(e));
+            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act);
+        } else {
+            auto kern = gemm_lds_kernel<64>;
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64>());
+            if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel: %s", hipGetErrorString(e));
+            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act);
+        }
+        return rf_check_launch("gemm_lds_kernel");
+    }
     const int64_t tiles128 = ((M + 127) / 128) * ((N + 127) / 128);
-    const bool small = tiles128 < 512;
+    static const int force_bt = [] {  // A/B of the tile choice (measurement only): RF_GEMM_BT=64|128
+        const char* e = getenv("RF_GEMM_BT");
+        return e ? atoi(e) : 0;
+    }();
+    const bool small = force_bt ? force_bt == 64 : tiles128 < 512;
     const int bt = small ? 64 : 128;
     const int64_t tiles = ((M + bt - 1) / bt) * ((N + bt - 1) / bt);
     RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_linear_fwd: too many tiles");

@@ -111,10 +111,7 @@ class Cascade(torch.nn.Module):
         a = gather_rows(self.a_item, cand2).view(B * self.k2, Lq, d)
         pooled = torch.empty((B * self.k2, self.ranker.pooled_width), dtype=torch.float32, device=u.device)
         xd = dense.repeat_interleave(self.k2, dim=0) if dense.shape[0] == B else dense
-        for i, (norm, dl) in enumerate(zip(self.ranker.input_mlp.norms, self.ranker.input_mlp.denses)):
-            h = norm(xd, out_dtype=self.ranker.input_mlp.dtype)
-            last = i == len(self.ranker.input_mlp.denses) - 1
-            xd = dl(h, out=pooled[:, : self.ranker.d_emb] if last else None)
+        self.ranker.input_mlp(xd, out=pooled[:, : self.ranker.d_emb])
         esim_soft_attention_pool(q, a, out=pooled, out_col=self.ranker.d_emb)
         p = self.ranker.dense_output(self.ranker.output_mlp(pooled))[:, 1].view(B, self.k2)
         s3, pos3 = topk_rows(p, self.k3)

@@ -50,17 +50,13 @@ class Esim(torch.nn.Module):
         q = self.enc_q(user).view(B, self.L, self.d)
         a = self.enc_a(ad).view(B, self.L, self.d)
         pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=q.device)
-        x = dense
-        for i, (norm, dense_l) in enumerate(zip(self.input_mlp.norms, self.input_mlp.denses)):
-            h = norm(x, out_dtype=self.input_mlp.dtype)
-            last = i == len(self.input_mlp.denses) - 1
-            x = dense_l(h, out=pooled[:, : self.d_emb] if last else None)
+        self.input_mlp(dense, out=pooled[:, : self.d_emb])
         esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
         return self.dense_output(self.output_mlp(pooled))
 
     def graphed(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor, **kw):
         """This forward captured as one hipGraph on static copies of (user, ad, dense) (runtime.graphs):
-        the returned callable takes batches of the same B / slot counts and replays the 14 launches without
+        the returned callable takes batches of the same B / slot counts and replays the launches without
         the per-launch host path. Its output buffer is reused by the next call."""
         from ...runtime.graphs import GraphedForward
 

@@ -68,7 +68,8 @@ def test_soft_attention_api(O, cuda):
     np.testing.assert_allclose(aa.cpu().numpy(), wa, atol=4e-3)
 
 
-@pytest.mark.parametrize("M,K,N", [(1, 16, 256), (129, 64, 130), (256, 1280, 1024), (300, 512, 2), (64, 8704, 48)])
+@pytest.mark.parametrize("M,K,N", [(1, 16, 256), (129, 64, 130), (256, 1280, 1024), (300, 512, 2), (64, 8704, 48),
+                                   (1000, 1024, 512), (4100, 256, 300), (4096, 1280, 1024)])
 @pytest.mark.parametrize("act", [None, "gelu", "relu", "selu", "softmax"])
 def test_dense_bf16(O, cuda, M, K, N, act):
     if act == "softmax" and N > 64:
@@ -81,6 +82,22 @@ def test_dense_bf16(O, cuda, M, K, N, act):
     # operands are exact in bf16; only fp32 accumulation error remains: ~K * 2^-24 * sum|xw|
     bound = 1e-5 * np.abs(x.float().numpy()) @ np.abs(W.T) + 1e-6
     np.testing.assert_array_less(np.abs(y - want), bound * 4 + 1e-5)
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 4, 1), (300, 512, 2), (4097, 1000, 16), (77, 64, 48)])
+@pytest.mark.parametrize("act", [None, "gelu", "softmax"])
+@pytest.mark.parametrize("wdt", [torch.bfloat16, torch.float32])
+def test_dense_head_fp32_activations(O, cuda, M, K, N, act, wdt):
+    """rf_dense_head_fwd (Dense with N <= 16 or a softmax head on fp32 x, e.g. esim.py:53's Dense(2,
+    'softmax') after the output MLP): fp32 products of x and the (bf16-stored) weights, fp32 sums."""
+    if not (N <= 16 or act == "softmax"):
+        pytest.skip("wider non-softmax layers take the MFMA GEMM (bf16 operands)")
+    x = (torch.rand((M, K), generator=torch.Generator().manual_seed(M + K)) * 2 - 1).float()
+    dense = Dense(K, N, activation=act, dtype=wdt, seed=N + 7, bias=torch.linspace(-0.5, 0.5, N))
+    y = dense(x.cuda()).cpu().numpy()
+    W = dense.weight.float().cpu().numpy().astype(np.float64)
+    want = O.activation(x.numpy().astype(np.float64) @ W.T + dense.bias.cpu().numpy(), act)
+    np.testing.assert_allclose(y, want, rtol=1e-5, atol=2e-6 * np.sqrt(K))
 
 
 @pytest.mark.parametrize("M,K,N", [(100, 32, 64), (257, 8704, 1024), (64, 20480, 256)])
@@ -122,6 +139,35 @@ def test_norm_rows(O, cuda, cols, mode, odt):
                                       nm.var.cpu().numpy(), 1e-3)
         tol = 1e-4 if odt == torch.float32 else 2e-2
         np.testing.assert_allclose(y, want, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("M,K0,H,O_", [(4100, 16, 256, 512), (1, 5, 128, 200), (37, 32, 256, 64), (300, 16, 128, 1024)])
+def test_mlp2_small_fused(O, cuda, M, K0, H, O_):
+    """rf_mlp2_small_fwd (the ESIM input_mlp in one launch) against the float64 create_mlp oracle, and
+    against the layer-by-layer rf_norm_fwd -> rf_linear_fwd chain; written into a strided column slice."""
+    from recommendflow_amd.backend.blocks.mlp import create_mlp as cm
+
+    mlp = cm([H, O_], 0.3, "gelu", LayerNormalization(epsilon=1e-6), in_features=K0, dtype=torch.bfloat16, seed=K0 + H)
+    g = torch.Generator().manual_seed(M)
+    for nm in mlp.norms:
+        nm.gamma.copy_(torch.rand(nm.width, generator=g) + 0.5)
+        nm.beta.copy_(torch.randn(nm.width, generator=g) * 0.1)
+    for dn in mlp.denses:
+        dn.bias.copy_(torch.randn(dn.units, generator=g) * 0.1)
+    x = (torch.randn(M, K0, generator=g) * 2 + 0.5).cuda()
+    assert mlp._fusable(x)
+    big = torch.full((M, O_ + 40), float("nan"), device="cuda")
+    y = mlp(x, out=big[:, 20: 20 + O_]).cpu().numpy()
+    assert torch.isnan(big[:, :20]).all() and torch.isnan(big[:, 20 + O_:]).all()
+    h = x if K0 % 8 == 0 else None  # the unfused chain (its bf16 GEMM needs 16-byte rows)
+    for nm, dn in zip(mlp.norms, mlp.denses):
+        h = dn(nm(h, out_dtype=torch.bfloat16)) if h is not None else None
+    params = [{"W": dn.weight.float().cpu().numpy().T, "b": dn.bias.cpu().numpy(), "gamma": nm.gamma.cpu().numpy(),
+               "beta": nm.beta.cpu().numpy()} for nm, dn in zip(mlp.norms, mlp.denses)]
+    want = O.mlp(x.cpu().numpy(), params, "gelu", "ln")
+    np.testing.assert_allclose(y, want, rtol=2e-2, atol=2e-2)
+    if h is not None:
+        np.testing.assert_allclose(y, h.cpu().numpy(), rtol=1e-2, atol=1e-2)
 
 
 @pytest.mark.parametrize("norm", ["ln", "bn"])

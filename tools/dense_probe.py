@@ -73,6 +73,7 @@ def main():
     in_mlp = create_mlp([256, 512], 0.3, "gelu", ln, in_features=16, dtype=torch.bfloat16, seed=3)
     xd = torch.randn((B, 16), generator=g, device="cuda")
     mlp_stages("cfg3.input_mlp", in_mlp, xd, res)
+    res["cfg3.input_mlp.fused_ms"] = round(timeit(lambda: in_mlp(xd)), 4)
     # cfg2 DSSM towers
     bn = BatchNormalization(epsilon=1e-6)
     for name, width in (("user", 8704), ("ad", 20480)):
