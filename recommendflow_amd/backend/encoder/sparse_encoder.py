@@ -109,6 +109,7 @@ class FusedSparseEncoder(torch.nn.Module):
         self.out_dtype = out_dtype or table_dtype
         self.mask_padding = bool(mask_padding)
         self.seed = int(seed)
+        self.single_token = True  # RF_FLAG_SINGLE_TOKEN when a batch's host-side Lmax allows it (A/B: False)
         self.extra_flags = 0  # diagnostic bits (rf_api.h RF_FLAG_DIAG_*; ablations 12-14 go to rf_diag_fused_hash_embed_fwd)
         desc = np.zeros(len(self.slots), SLOT_DTYPE)
         base = int(row_base0)
@@ -141,6 +142,15 @@ class FusedSparseEncoder(torch.nn.Module):
             raise ValueError(f"shared table {tuple(table.shape)} too small for {self.table_rows} x {self.dim}")
         self.table = table
 
+    def _single_token_batch(self, batch: SparseBatch) -> bool:
+        """True when the batch's per-slot Lmax is known on the host without a device sync and is <= 1, and the
+        row width suits the single-token kernel (4, 8 or 16 chunks of 16 bytes)."""
+        lm = batch.lmax if not batch.is_device() else batch.host_lmax
+        if lm is None:
+            return False
+        chunks = self.dim * self.table.element_size() // 16
+        return chunks in (4, 8, 16) and int(np.max(lm, initial=0)) <= 1
+
     def slot_offsets(self) -> List[Tuple[str, int, int]]:
         return [(sp.name, i * 2 * self.dim, (i + 1) * 2 * self.dim) for i, sp in enumerate(self.slots)]
 
@@ -157,6 +167,8 @@ class FusedSparseEncoder(torch.nn.Module):
         if out_col:
             raise ValueError("out_col is reserved; pass a column slice through the descriptors instead")
         flags = (L.FLAG_MASK_PADDING if self.mask_padding else 0) | (L.FLAG_EMIT_IDX if emit_idx else 0) | self.extra_flags
+        if not emit_idx and not self.extra_flags and self.single_token and self._single_token_batch(batch):
+            flags |= L.FLAG_SINGLE_TOKEN  # every slot's batch Lmax <= 1: the low-register single-token kernel
         idx = torch.empty((max(batch.n_tokens, 1), 2), dtype=torch.int64, device=self.table.device) if emit_idx else None
         entry = "rf_diag_fused_hash_embed_fwd" if self.extra_flags & L.DIAG_ABLATIONS else "rf_fused_hash_embed_fwd"
         L.call(entry, L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes),

@@ -233,7 +233,7 @@ static int fused_hash_embed_fwd_impl(uint32_t allowed_diag, const rf_slot_desc* 
     RF_REQUIRE(dim > 0 && dim % epv == 0, "rf_fused_hash_embed_fwd: dim (%d) must be a positive multiple of %d (16-byte rows chunks)", dim, epv);
     RF_REQUIRE(out_stride % epv == 0, "rf_fused_hash_embed_fwd: out_stride must be a multiple of %d", epv);
     RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)out & 15) == 0, "rf_fused_hash_embed_fwd: table/out must be 16-byte aligned");
-    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | (int32_t)allowed_diag)) == 0,
+    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_EMIT_IDX | RF_FLAG_SINGLE_TOKEN | (int32_t)allowed_diag)) == 0,
                "rf_fused_hash_embed_fwd: unknown flags (result-changing ablation bits 12-14 are only accepted by "
                "rf_diag_fused_hash_embed_fwd)");
     RF_REQUIRE(table_rows >= 1 && table_rows <= (int64_t)0xffffffff, "rf_fused_hash_embed_fwd: table_rows must be in [1, 2^32) (32-bit row ids in LDS)");
@@ -241,8 +241,14 @@ static int fused_hash_embed_fwd_impl(uint32_t allowed_diag, const rf_slot_desc* 
     if (n_units == 0) return RF_OK;
     RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && lmax && table && out, "rf_fused_hash_embed_fwd: null pointer");
     const int64_t items = (int64_t)n_slots * ((batch + kUnits - 1) / kUnits);  // slot-major items
-    const int grid = grid_for(items, kWaves, 256 * 32 * 2);
     hipStream_t st = rf_stream(stream);
+    if (flags & RF_FLAG_SINGLE_TOKEN) {
+        RF_REQUIRE(!(flags & RF_FLAG_EMIT_IDX), "rf_fused_hash_embed_fwd: RF_FLAG_SINGLE_TOKEN does not emit ids");
+        RF_REQUIRE(!(flags & 0xF800), "rf_fused_hash_embed_fwd: RF_FLAG_SINGLE_TOKEN takes no diagnostic bits");
+        return launch_single_token_any(table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,
+                                       table, table_rows, dim, out, out_stride, flags, grid_for(items, 1, 256 * 32 * 2), st);
+    }
+    const int grid = grid_for(items, kWaves, 256 * 32 * 2);
     return launch_fused_any(false, table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,
                             table, table_rows, dim, out, out_stride, flags, idx_out, grid, st);
 }

@@ -74,6 +74,10 @@ __device__ __forceinline__ uint4 load_chunk(const TT* __restrict__ table, int64_
     return *reinterpret_cast<const uint4*>(table + row * (int64_t)dim + (int64_t)c * EPV);
 }
 
+// the mean of zero positions (a slot with Lmax = 0 unmasked): 0/0 with the x86 default-NaN bits (sign set),
+// what the reference's CPU reduce_mean and the oracle produce; GPU division would give the positive NaN
+#define kMeanOfNothing __uint_as_float(0xffc00000u)
+
 __device__ __forceinline__ float comb_init(int comb) {
     return comb == RF_COMB_MAX ? -INFINITY : comb == RF_COMB_MIN ? INFINITY : 0.0f;
 }
@@ -436,7 +440,7 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     if (comb == RF_COMB_AVG) {
                         const float fl = (float)Lu;
 #pragma unroll
-                        for (int e = 0; e < EPV; ++e) a[e] = __fdiv_rn(a[e], fl);
+                        for (int e = 0; e < EPV; ++e) a[e] = Lu == 0 ? kMeanOfNothing : __fdiv_rn(a[e], fl);
                     }
                     if (Lu == 0 && (mask_pad || comb == RF_COMB_FIRST || comb == RF_COMB_LAST)) {
 #pragma unroll
@@ -562,6 +566,127 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// single-token slots (RF_FLAG_SINGLE_TOKEN: the caller knows every slot's batch Lmax is <= 1, e.g. cfg3's
+// 200 single-valued slots). The general kernel's pooling pipeline sets its register allocation (~195
+// VGPRs: two waves per SIMD), so its lean path cannot overlap one item's hashing with another's
+// gather. This kernel keeps only what an Lmax = 1 item needs (~100 VGPRs): lane j hashes bag j's token
+// (both keys, one read), the rows move to the gathering teams by lane shuffles (no LDS, no barrier),
+// and every team issues all of its bags' row loads at once (the whole row: one 16-byte chunk per lane).
+// Values are the general kernel's for Lmax = 1 (its lean phase 2): sum/avg 0 + x, max/min
+// comb_step(init, x), first/last/null x, an empty bag reads the pad rows (zeros when masked), NaN for a
+// slot that does not fit the table; a slot with Lmax = 0 gets the empty-reduction values (sum/first/
+// last 0, avg 0/0, max -inf, min +inf; zeros when masked; null: nothing) and one with Lmax > 1 (a
+// broken promise) NaN.
+template <int LPR, typename TT, typename OT>
+__global__ __launch_bounds__(64) void single_token_embed_kernel(
+    const rf_slot_desc* __restrict__ slots, int n_slots, const uint8_t* __restrict__ tok_bytes,
+    const int32_t* __restrict__ tok_off, const int32_t* __restrict__ bag_off, const int32_t* __restrict__ lmax,
+    int64_t n_units, const TT* __restrict__ table, int64_t table_rows, int dim, OT* __restrict__ out,
+    int64_t out_stride, int flags) {
+    constexpr int EPV = Elem<TT>::EPV;
+    constexpr int TEAMS = 64 / LPR;   // one team per bag at a time, one 16-byte chunk per lane
+    constexpr int G = kUnits / TEAMS;  // bags per team per item
+    constexpr int GH = G > 8 ? 8 : G;  // bags per load batch (16 row chunks per lane in flight)
+    const int lane = threadIdx.x, team = lane / LPR, tl = lane % LPR;
+    const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
+    const int batch = (int)(n_units / n_slots);
+    const int nbb = (batch + kUnits - 1) / kUnits;
+    const int64_t n_items = (int64_t)n_slots * nbb;
+    for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+        const int s = (int)(item / nbb);
+        const int b0 = (int)(item - (int64_t)s * nbb) * kUnits;
+        const int nu = min(kUnits, batch - b0);
+        const rf_slot_desc* sd = slots + s;
+        const int comb = sd->combiner;
+        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
+        const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
+        const int mask_empty = sd->mask_empty;
+        const int64_t out_off = sd->out_off;
+        const int lm = lmax[s];
+        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
+        int64_t pb0 = 0, pb1 = 0;
+        if (!mask_empty) {
+            pb0 = (int64_t)(siphash24_dev(salt0, salt0, tok_bytes, 0) % (uint64_t)nbins);
+            pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
+        }
+        // lane j: bag b0 + j -> its two rows (the pad rows when empty)
+        uint32_t r0 = ok ? (uint32_t)(rb0 + pb0) : 0u, r1 = ok ? (uint32_t)(rb1 + pb1) : 0u;
+        int has = 0;
+        if (lane < nu) {
+            const int64_t u = (int64_t)(b0 + lane) * n_slots + s;
+            const int t = bag_off[u];
+            if (bag_off[u + 1] > t) {
+                const int tb = tok_off[t], n = tok_off[t + 1] - tb;
+                uint64_t h0, h1;
+                siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
+                if (ok) {
+                    r0 = (uint32_t)(rb0 + bucket_from_hash(h0, n, nbins, mask_empty));
+                    r1 = (uint32_t)(rb1 + bucket_from_hash(h1, n, nbins, mask_empty));
+                }
+                has = 1;
+            }
+        }
+        if (lm == 0 && comb == RF_COMB_NULL) continue;  // no positions: nothing to write
+        const float initv = comb_init(comb);
+        float special = 0.0f;  // the value of every element when the slot's Lmax is not 1
+        if (lm == 0 && !mask_pad)
+            special = comb == RF_COMB_AVG ? kMeanOfNothing : (comb == RF_COMB_MAX || comb == RF_COMB_MIN) ? initv : 0.0f;
+        if (lm > 1 || !ok) special = __builtin_nanf("");
+        const bool use_special = lm != 1 || !ok;
+#pragma unroll
+        for (int g0 = 0; g0 < G; g0 += GH) {
+            uint4 v[GH][2];
+#pragma unroll
+            for (int g = 0; g < GH; ++g) {
+                const int j = team + TEAMS * (g0 + g);
+                const uint32_t q0 = (uint32_t)__shfl((int)r0, j, 64), q1 = (uint32_t)__shfl((int)r1, j, 64);
+                v[g][0] = row_chunk(table, q0, dim, tl);
+                v[g][1] = row_chunk(table, q1, dim, tl);
+            }
+#pragma unroll
+            for (int g = 0; g < GH; ++g) {
+                const int j = team + TEAMS * (g0 + g);
+                const int hj = __shfl(has, j, 64);
+                if (j >= nu) continue;
+                const bool zero = mask_pad && !hj;
+                const int64_t ob = (int64_t)(b0 + j) * out_stride + out_off;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    float f[EPV], a[EPV];
+                    unpack16<TT>(v[g][k], f);
+#pragma unroll
+                    for (int e = 0; e < EPV; ++e) {
+                        if (use_special) a[e] = special;
+                        else if (zero) a[e] = 0.0f;
+                        else if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) a[e] = __fadd_rn(0.0f, f[e]);
+                        else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) a[e] = comb_step(comb, initv, f[e]);
+                        else a[e] = f[e];
+                    }
+                    store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + tl * EPV, a);
+                }
+            }
+        }
+    }
+}
+
+template <typename TT, typename OT>
+int launch_single_token(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                        const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table,
+                        int64_t table_rows, int32_t dim, void* out, int64_t out_stride, int32_t flags, int grid,
+                        hipStream_t st) {
+    const int nchunks = dim / Elem<TT>::EPV;
+#define RF_ST(L)                                                                                                      \
+    hipLaunchKernelGGL((single_token_embed_kernel<L, TT, OT>), dim3(grid), dim3(64), 0, st, d_slots, n_slots, tok_bytes, \
+                       tok_off, bag_off, lmax, n_units, (const TT*)table, table_rows, dim, (OT*)out, out_stride, flags)
+    if (nchunks == 4) RF_ST(4);
+    else if (nchunks == 8) RF_ST(8);
+    else if (nchunks == 16) RF_ST(16);
+    else return rf_set_error(RF_EINVAL, "single-token kernel: rows of %d 16-byte chunks (4, 8 or 16 supported)", nchunks);
+#undef RF_ST
+    return rf_check_launch("single_token_embed_kernel");
+}
+
 // lanes per row / 16-byte chunks per lane for `nchunks` 16-byte chunks per row: teams of up to
 // kDefaultMaxLpr = 16 lanes (tuned on MI355X: 16 > 8 >> 4, 2), at most 4 chunks per lane.
 template <typename F>
@@ -616,6 +741,12 @@ RF_FUSED_LAUNCH_DECL(launch_pool_f32_of32);
 RF_FUSED_LAUNCH_DECL(launch_pool_f32_obf16);
 RF_FUSED_LAUNCH_DECL(launch_pool_bf16_of32);
 RF_FUSED_LAUNCH_DECL(launch_pool_bf16_obf16);
+
+// rf_single.hip: the single-token kernel for (table dtype, output dtype)
+int launch_single_token_any(int32_t table_dtype, int32_t out_dtype, const rf_slot_desc* d_slots, int32_t n_slots,
+                            const uint8_t* tok_bytes, const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                            int64_t n_units, const void* table, int64_t table_rows, int32_t dim, void* out,
+                            int64_t out_stride, int32_t flags, int grid, hipStream_t st);
 
 // picks the launcher for (table dtype, output dtype)
 inline int launch_fused_any(bool pre, int32_t table_dtype, int32_t out_dtype, const rf_slot_desc* d_slots,

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("RF_LIB") or os.path.normpath(os.path.join(_HERE, ".."
 RF_OK, RF_EINVAL, RF_EHIP, RF_EOOB = 0, -1, -2, -3
 DT_F32, DT_BF16, DT_F16 = 0, 1, 2
 COMB = {"sum": 0, "avg": 1, "max": 2, "min": 3, "first": 4, "last": 5, "null": 6, "cls": 4}
-FLAG_MASK_PADDING, FLAG_EMIT_IDX = 0x1, 0x2
+FLAG_MASK_PADDING, FLAG_EMIT_IDX, FLAG_SINGLE_TOKEN = 0x1, 0x2, 0x4
 ACT = {None: 0, "none": 0, "linear": 0, "gelu": 1, "relu": 2, "selu": 3, "softmax": 4}
 
 _lock = threading.Lock()

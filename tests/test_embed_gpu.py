@@ -124,6 +124,42 @@ def test_fused_embed_single_token_items(O, cuda, tdt, odt, dim, mask_padding):
         np.testing.assert_array_equal(bits(got), bits(gen), err_msg=comb)
 
 
+@pytest.mark.parametrize("tdt,odt,dim", [(torch.bfloat16, torch.bfloat16, 64), (torch.bfloat16, torch.bfloat16, 32),
+                                         (torch.bfloat16, torch.float32, 128), (torch.float32, torch.float32, 16),
+                                         (torch.float32, torch.bfloat16, 64)])
+@pytest.mark.parametrize("mask_padding", [False, True])
+def test_single_token_kernel(O, cuda, tdt, odt, dim, mask_padding):
+    """RF_FLAG_SINGLE_TOKEN (set by the encoder when the batch's host-side Lmax is <= 1): the low-register
+    single-token kernel is bit-exact vs the oracle and vs the general kernel, for every combiner, empty
+    bags (pad rows / zeros when masked), b"" tokens, unmasked-empty salts, and a slot whose Lmax is 0
+    (empty-reduction values). A batch that breaks the promise (a 2-token bag) gets NaN in that slot only."""
+    rng = np.random.default_rng(dim)
+    S, B = 6, 200
+    rows = [[([b"" if rng.random() < 0.05 else b"t%d" % rng.integers(0, 900)] if (s != 5 and rng.random() < 0.85) else [])
+             for s in range(S)] for _ in range(B)]
+    hb = from_lists(rows)
+    assert list(hb.lmax) == [1, 1, 1, 1, 1, 0]
+    for comb in COMBS:
+        specs = [SlotSpec(f"f{s}", 40 + 13 * s, (s, 7 + s), comb, mask_empty=s != 3) for s in range(S)]
+        enc = FusedSparseEncoder(specs, dim, table_dtype=tdt, out_dtype=odt, seed=dim + 1, mask_padding=mask_padding)
+        assert enc._single_token_batch(hb)
+        got, ref, _, _ = run_both(O, enc, hb, emit=False)
+        np.testing.assert_array_equal(bits(got), bits(ref), err_msg=comb)
+        enc.single_token = False
+        gen, _, _, _ = run_both(O, enc, hb, emit=False)
+        np.testing.assert_array_equal(bits(got), bits(gen), err_msg=comb)
+    rows[17][2] = [b"a", b"b"]
+    bad = from_lists(rows).to("cuda")
+    out = torch.empty((B, enc.out_width), dtype=odt, device="cuda")
+    L.call("rf_fused_hash_embed_fwd", L.ptr(enc.desc), S, L.ptr(bad.tok_bytes), L.ptr(bad.tok_off), L.ptr(bad.bag_off),
+           L.ptr(bad.lmax), B, L.ptr(enc.table), L.torch_dtype_code(tdt), enc.table.shape[0], dim, L.ptr(out),
+           L.torch_dtype_code(odt), out.stride(0), L.FLAG_SINGLE_TOKEN | (L.FLAG_MASK_PADDING if mask_padding else 0),
+           None, L.stream_ptr())
+    o = out.float().cpu().numpy()
+    assert np.isnan(o[:, 2 * 2 * dim: 3 * 2 * dim]).all()
+    assert not np.isnan(o[:, : 2 * 2 * dim]).any()
+
+
 @pytest.mark.parametrize("extra", [1 << 11, (1 << 11) | (1 << 15)])
 def test_fused_embed_diagnostic_item_order_is_exact(O, cuda, extra):
     """Diagnostic flag bit 11 (slot-interleaved XCD item order, rf_fused.h) only permutes the items: 19

@@ -21,9 +21,10 @@ def main():
     hb = synthetic_batch(B, [False] * Ls, seed=77, slot_ids=range(Ls)).to("cuda")
     out = torch.empty((B, enc.out_width), dtype=torch.bfloat16, device="cuda")
     res = {}
-    for name, fl in (("full", 0), ("general_phase2", 1 << 15), ("xcd_order", 1 << 11), ("no_hash", 1 << 12),
-                     ("hash_only", 1 << 13)):
+    for name, fl, st in (("single_token_kernel", 0, True), ("general_kernel_lean", 0, False),
+                         ("general_phase2", 1 << 15, False), ("no_hash", 1 << 12, False), ("hash_only", 1 << 13, False)):
         enc.extra_flags = fl
+        enc.single_token = st
 
         def run():
             enc(hb, out=out)
@@ -60,6 +61,9 @@ def main():
             e[i].record()
         torch.cuda.synchronize()
         res[name] = round(sorted(a.elapsed_time(b) for a, b in zip(s, e))[25], 4)
+    by = 2 * B * Ls * 128 + B * Ls * 256 + int(hb.tok_bytes.numel()) + 4 * hb.n_tokens
+    res["single_token_GBs"] = round(by / res["single_token_kernel"] / 1e6, 1)
+    res["general_lean_GBs"] = round(by / res["general_kernel_lean"] / 1e6, 1)
     print(json.dumps(res))
 
 
