@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--no-shard-train", action="store_true", help="skip the cfg4 sharded training-step extra")
     p.add_argument("--no-cascade", action="store_true", help="skip the cfg5 recall->prerank->rank extra")
     p.add_argument("--catalog", type=int, default=1_000_000, help="cfg5: items in the catalog")
+    p.add_argument("--cascade-sharded", action="store_true", help="cfg5 sharded-recall leg at N=1 too (always at N>1)")
     p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
     p.add_argument("--pipe-examples", type=int, default=65536, help="feature pipe: examples written and read back")
     p.add_argument("--pipe-threads", type=int, default=16, help="feature pipe: reader threads (the box's CPU share)")
@@ -192,6 +193,17 @@ def main():
         else:
             sharded = bench_sharded(args, specs, multi, rank, world)
 
+    cascade_sh = None
+    if not args.no_cascade and (world > 1 or args.cascade_sharded):
+        torch.cuda.empty_cache()
+        try:
+            cascade_sh = bench_cascade_sharded(args, specs, rank, world)
+        except Exception as e:  # noqa: BLE001 — reported in place of the numbers; the headline line still prints
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            cascade_sh = {"error": f"{type(e).__name__}: {e}"[:300]}
+            if world > 1:
+                raise
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -269,6 +281,7 @@ def main():
         "cpu_baseline": cpu,
         "extras": extras,
         "cfg4_sharded": sharded,
+        "cfg5_cascade_sharded": cascade_sh,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
@@ -632,6 +645,81 @@ def bench_cascade(args, enc):
            "config": f"1024 users/step; recall: cfg2 towers, Flat IP top-200 over {N} items (fp32 MFMA + rf_topk_merge); "
                      "prerank: u*v -> Dense(64, relu) -> Dense(1), top-50; rank: cfg3 ESIM (fp16 attention) top-10"}
     del cas, esim, dssm, rb, kb, ur, uk
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_cascade_sharded(args, specs, rank, world):
+    """cfg5 as configured (BASELINE.json configs[4]): recall -> prerank -> rank with DATA-PARALLEL request
+    batches (1024 users per rank per step) and the recall towers' sparse lookups on ROW-SHARDED tables (the
+    cfg2 user / ad slot layouts, 10M x 64 fp32 rows in all, owner = row mod P, one RCCL all-to-all pair per
+    lookup); the catalog index is encoded collectively (rank r: its 1/P slice) and all-gathered; prerank and
+    the cfg3 ESIM ranker (fp16 attention, replicated tables) run on each rank's own candidates. Timed: a
+    barrier, K steps, a barrier; users/s = users of all ranks / the max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+
+    from recommendflow_amd.backend.encoder.sharded_encoder import LocalComm, ShardedFusedEncoder, TorchDistComm
+    from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
+    from recommendflow_amd.config_parser.configuration import Configuration
+    from recommendflow_amd.models.cascade import ShardedCascade
+    from recommendflow_amd.models.matching.dssm import Dssm
+    from recommendflow_amd.models.ranking.esim import Esim
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "base_recall_sdpa.yaml"))
+    feats = conf.features.hashing_features
+    users = [i for i, f in enumerate(feats) if f.tower.value == "user"]
+    ads = [i for i, f in enumerate(feats) if f.tower.value == "ad"]
+    mv = [bool(f.multivalued) for f in feats]
+    comm = TorchDistComm() if world > 1 else LocalComm()
+    eu = ShardedFusedEncoder([specs[i] for i in users], args.dim, rank, world, comm=comm, seed=31)
+    ea = ShardedFusedEncoder([specs[i] for i in ads], args.dim, rank, world, comm=comm, seed=32)
+    # the towers' weights: a Dssm over two tiny stand-in encoders of the same output widths (never called)
+    tiny = lambda sl: FusedSparseEncoder([SlotSpec(s.name, 2, (1, 2)) for s in sl], args.dim)
+    dssm = Dssm(tiny([specs[i] for i in users]), tiny([specs[i] for i in ads]), seed=5)
+    Ls = 100
+    esim = Esim([SlotSpec(f"u{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)],
+                [SlotSpec(f"a{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)], n_dense=16, dim=64,
+                table_dtype=torch.bfloat16, seed=3)
+    cas = ShardedCascade(dssm, esim, eu, ea, comm, k_recall=200, k_prerank=50, k_final=10, seed=9)
+    N, CB = args.catalog, 8192
+    nb = max(1, (N + CB - 1) // CB)
+    per = (nb + world - 1) // world  # catalog batches per rank (every rank encodes the same count)
+    t0 = time.perf_counter()
+    rb = [synthetic_batch(CB, [mv[i] for i in ads], seed=600 + j, slot_ids=ads).to("cuda") for j in range(2)]
+    kb = [synthetic_batch(CB, [False] * Ls, seed=700 + j, slot_ids=range(Ls, 2 * Ls)).to("cuda") for j in range(2)]
+    cas.index_catalog([rb[(rank * per + j) % 2] for j in range(per)], [kb[j % 2] for j in range(per * world)])
+    torch.cuda.synchronize()
+    index_s = time.perf_counter() - t0
+    B = 1024
+    ur = [synthetic_batch(B, [mv[i] for i in users], seed=800 + 10 * rank + j, slot_ids=users).to("cuda") for j in range(2)]
+    uk = [synthetic_batch(B, [False] * Ls, seed=900 + 10 * rank + j, slot_ids=range(Ls)).to("cuda") for j in range(2)]
+    dense = torch.randn(B, 16, device="cuda")
+    for j in range(2):
+        cas(ur[j % 2], uk[j % 2], dense)
+    steps = max(3, args.steps // 10)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(steps):
+        cas(ur[j % 2], uk[j % 2], dense)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item()) / steps * 1e3
+    out = {"users_per_s": round(B * world / ms * 1e3, 1), "ms_per_step": round(ms, 3), "ranks": world,
+           "users_per_rank_per_step": B, "catalog_items": int(cas.searcher.index.shape[0]),
+           "catalog_index_s": round(index_s, 2), "recall_table_rows": eu.table_rows + ea.table_rows,
+           "recall_shard_rows_rank0": eu.local_rows + ea.local_rows,
+           "config": f"DP {B} users/rank/step; recall towers over row-sharded cfg2 user/ad tables (P={world}, "
+                     "RCCL all-to-all per lookup), catalog encoded per rank + all-gathered, Flat IP top-200; prerank "
+                     "top-50; rank cfg3 ESIM (fp16 attention, replicated 1M-bin tables) top-10"}
+    del cas, esim, dssm, eu, ea, rb, kb, ur, uk
     torch.cuda.empty_cache()
     return out
 

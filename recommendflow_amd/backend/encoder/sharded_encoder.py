@@ -193,6 +193,27 @@ class TorchDistComm:
                                     group=self.group)
         return out
 
+    def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """Every rank's rows concatenated in rank order (row counts may differ: padded to the largest)."""
+        n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(ns, n, group=self.group)
+        ns = [int(v.item()) for v in ns]
+        m = max(ns)
+        xp = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        xp[: x.shape[0]] = x
+        bufs = [torch.empty_like(xp) for _ in range(self.world)]
+        self.dist.all_gather(bufs, xp, group=self.group)
+        return torch.cat([b[:k] for b, k in zip(bufs, ns)])
+
+    def all_gather_ints(self, v: int) -> List[int]:
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        if self.dist.get_backend(self.group) != "gloo":
+            t = t.cuda()
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return [int(o.item()) for o in out]
+
 
 class LocalComm:
     """P = 1: the exchange is the identity (the sharded pipeline on one GPU, for weak-scaling baselines)."""
@@ -204,6 +225,12 @@ class LocalComm:
 
     def exchange(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]) -> torch.Tensor:
         return x
+
+    def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
+        return x
+
+    def all_gather_ints(self, v: int) -> List[int]:
+        return [int(v)]
 
 
 @dataclass

@@ -94,10 +94,12 @@ class Cascade(torch.nn.Module):
 
     @torch.no_grad()
     def forward(self, recall_user: SparseBatch, rank_user: SparseBatch, dense: torch.Tensor) -> CascadeResult:
-        B = recall_user.batch
         u = torch.nn.functional.normalize(self.recall.user_dense(self.recall.enc_u(recall_user)), dim=-1, eps=1e-6)
-        # recall
         _, cand1 = self.searcher.search_index(u, self.k1)                                   # [B, K1] item ids
+        return self._prerank_rank(u, cand1, rank_user, dense)
+
+    def _prerank_rank(self, u: torch.Tensor, cand1: torch.Tensor, rank_user: SparseBatch, dense: torch.Tensor):
+        B = u.shape[0]
         v = gather_rows(self.searcher.index, cand1)                                         # [B*K1, E]
         x = (u[:, None, :] * v.view(B, self.k1, -1)).reshape(B * self.k1, -1).contiguous()
         # prerank
@@ -116,3 +118,82 @@ class Cascade(torch.nn.Module):
         p = self.ranker.dense_output(self.ranker.output_mlp(pooled))[:, 1].view(B, self.k2)
         s3, pos3 = topk_rows(p, self.k3)
         return CascadeResult(torch.gather(cand2, 1, pos3), s3, cand1, cand2)
+
+
+# ------------------------------------------------------------------------------------------------
+# cfg5 over P ranks (BASELINE.json configs[4]: "8-GPU data-parallel + sharded tables")
+# ------------------------------------------------------------------------------------------------
+class ShardedRecall:
+    """The recall stage over P ranks, the only stage of the cascade with collectives:
+
+      * request batches are data-parallel (each rank its own users);
+      * both towers' sparse lookups read row-sharded fused tables (ShardedFusedEncoder: one all-to-all
+        pair per lookup, bit-identical to the single-table kernel for any P);
+      * the catalog index is built collectively: rank r encodes its contiguous slice of the catalog, then an
+        all-gather assembles the full [N, E] index on every rank (rank order = catalog order);
+      * the search is local (exact inner-product top-k over the replicated index).
+
+    The dense parts are callables so the orchestration runs on CPU ranks in the tests with oracle ops:
+    user_tower / ad_tower: pooled [B, W] -> l2-normalised [B, E]; search(u, index, k) -> (scores, ids).
+    """
+
+    def __init__(self, enc_u, enc_a, user_tower, ad_tower, search, comm, k: int):
+        self.enc_u, self.enc_a = enc_u, enc_a
+        self.user_tower, self.ad_tower, self.search = user_tower, ad_tower, search
+        self.comm, self.k = comm, int(k)
+        self.index: Optional[torch.Tensor] = None
+        self.offsets = None  # catalog id of each rank's first item
+
+    @torch.no_grad()
+    def index_catalog(self, local_batches: Sequence[SparseBatch]) -> torch.Tensor:
+        """Collective: every rank passes ITS slice of the catalog (the same number of batches on every rank:
+        each batch is one sharded lookup, a collective)."""
+        counts = self.comm.all_gather_ints(len(local_batches))
+        if len(set(counts)) != 1:
+            raise ValueError(f"every rank must encode the same number of catalog batches, got {counts}")
+        vs = [self.ad_tower(self.enc_a(b)) for b in local_batches]
+        local = torch.cat(vs) if vs else torch.zeros((0, 1))
+        sizes = self.comm.all_gather_ints(local.shape[0])
+        self.offsets = [sum(sizes[:r]) for r in range(len(sizes))]
+        self.index = self.comm.all_gather_rows(local.contiguous())
+        return self.index
+
+    @torch.no_grad()
+    def forward(self, user_batch: SparseBatch):
+        """Collective (the sharded user lookup): (u [B, E], scores [B, k], catalog ids [B, k])."""
+        u = self.user_tower(self.enc_u(user_batch))
+        scores, ids = self.search(u, self.index, self.k)
+        return u, scores, ids
+
+
+class ShardedCascade(Cascade):
+    """Cascade with a ShardedRecall (recall towers on row-sharded tables, collective catalog index) and the
+    prerank / rank stages of Cascade, data-parallel (each rank ranks its own users' candidates against the
+    replicated ESIM catalog)."""
+
+    def __init__(self, recall: Dssm, ranker: Esim, enc_u, enc_a, comm, **kw):
+        super().__init__(recall, ranker, **kw)
+        self.srecall = ShardedRecall(enc_u, enc_a, self._tower(recall.user_dense), self._tower(recall.ad_dense),
+                                     self._search, comm, self.k1)
+
+    @staticmethod
+    def _tower(mlp):
+        return lambda x: torch.nn.functional.normalize(mlp(x), dim=-1, eps=1e-6)
+
+    def _search(self, u, index, k):
+        d, i = self.searcher.search_index(u, k)
+        return d, i
+
+    @torch.no_grad()
+    def index_catalog(self, recall_ad_local: Sequence[SparseBatch], rank_ad: Sequence[SparseBatch]):
+        """Collective. recall_ad_local: this rank's slice of the catalog (ad slots of the recall tables);
+        rank_ad: the whole catalog's ESIM ad sequences (replicated ranker tables: every rank encodes all)."""
+        items = self.srecall.index_catalog(recall_ad_local)
+        self.searcher = FaissSearcher(items=items, index_param="Flat", measurement="ip").train()
+        self.a_item = torch.cat([self.ranker.enc_a(kb).to(self.rank_dtype) for kb in rank_ad]).contiguous()
+        return self
+
+    @torch.no_grad()
+    def forward(self, recall_user: SparseBatch, rank_user: SparseBatch, dense: torch.Tensor) -> CascadeResult:
+        u, _, cand1 = self.srecall.forward(recall_user)
+        return self._prerank_rank(u, cand1, rank_user, dense)

@@ -98,3 +98,25 @@ def _catalog_recall_batches(N=3000):
 
 def _catalog_rank_batches(Ls, N=3000):
     return [synthetic_batch(1000, [False] * Ls, seed=80 + i, slot_ids=range(200, 200 + Ls)) for i in range(N // 1000)]
+
+
+def test_sharded_cascade_p1_equals_cascade(cuda):
+    """ShardedCascade (recall towers on row-sharded tables, collective catalog index; LocalComm at P = 1)
+    gives exactly the single-table Cascade's candidates and scores."""
+    from recommendflow_amd.backend.encoder.sharded_encoder import LocalComm, ShardedFusedEncoder
+    from recommendflow_amd.models.cascade import ShardedCascade
+
+    cas, ur, uk, dense = _build()
+    want = cas(ur, uk, dense)
+    user = [SlotSpec(f"u{i}", 5000, (2022, 2023)) for i in range(6)]
+    ad = [SlotSpec(f"a{i}", 5000, (2022, 2023)) for i in range(5)]
+    comm = LocalComm()
+    scas = ShardedCascade(cas.recall, cas.ranker, ShardedFusedEncoder(user, 16, 0, 1, comm=comm, seed=1),
+                          ShardedFusedEncoder(ad, 16, 0, 1, comm=comm, seed=2), comm, k_recall=100, k_prerank=20,
+                          k_final=5, seed=5)
+    scas.index_catalog([c.to("cuda") for c in _catalog_recall_batches()],
+                       [c.to("cuda") for c in _catalog_rank_batches(cas.ranker.L)])
+    assert torch.equal(scas.searcher.index, cas.searcher.index)
+    got = scas(ur, uk, dense)
+    for f in ("recall_items", "prerank_items", "items", "scores"):
+        assert torch.equal(getattr(got, f), getattr(want, f)), f
