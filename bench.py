@@ -797,11 +797,15 @@ def bench_train(args, specs, multi):
 
 
 def bench_pipe(args, enc, specs, multi):
-    """cfg2 examples as GZIP TFRecord files (the reference's on-disk format,
-    make_tfrecord.py:142) -> C++ decode (inflate + framing CRC + tf.train.Example parse) into pinned
-    buffers -> side-stream H2D -> the fused encoder. Reports the host decode rate alone and the
-    end-to-end rate with the encoder consuming every batch (the pipe overlaps decode, copy and
-    kernel). Files are written first with zlib level 1 (not timed)."""
+    """cfg2 examples as TFRecord files (the reference's on-disk format, make_tfrecord.py:142,
+    read by TFRecordDataset(compression_type), dataloader.py:567) -> the fused encoder, three ways:
+      gzip_host    GZIP files, C++ inflate + framing + tf.train.Example parse into pinned buffers,
+                   side-stream H2D (the host decode rate alone is reported too);
+      gzip_device  GZIP files, C++ inflate + framing on the host, Example parse on the GPU;
+      none_device  uncompressed files (compression_type=""), host framing + CRC only, records streamed
+                   to HBM as they are and parsed there (rf_tfr_parse_device).
+    Each end-to-end rate has the encoder consuming every batch (decode, copy and kernels overlap).
+    Files are written first (zlib level 1 for GZIP; not timed) and read from the page cache."""
     import shutil
     import tempfile
     from concurrent.futures import ThreadPoolExecutor
@@ -812,27 +816,42 @@ def bench_pipe(args, enc, specs, multi):
     from recommendflow_amd.runtime import tfrecord as T
     from recommendflow_amd.runtime.batch import synthetic_batch
 
-    n_files = max(1, min(16, args.pipe_threads))  # one GZIP part file per reader thread (tf.data interleave)
+    n_files = max(1, min(16, args.pipe_threads))  # one part file per reader thread (tf.data interleave)
     per = max(1, args.pipe_examples // n_files)
     fspecs = [T.FeatureSpec(s.name, T.BYTES, T.SEQ, "") for s in specs] + [T.FeatureSpec("label", T.FLOAT, T.SCALAR, 0.0)]
     tmp = tempfile.mkdtemp(prefix="rf_pipe_", dir="/tmp")
-    paths = [os.path.join(tmp, f"part-{f:02d}.tfrecord.gz") for f in range(n_files)]
+    paths = {c: [os.path.join(tmp, f"part-{f:02d}.tfrecord{'.gz' if c == 'GZIP' else ''}") for f in range(n_files)]
+             for c in ("GZIP", None)}
 
     def write(f):
         hb = synthetic_batch(per, multi, seed=777 + f)
         fb = T.FeatureBatch(per, hb, [s.name for s in specs], None, None, np.zeros((per, 0), np.int64), [],
                             np.ones((per, 1), np.float32), ["label"])
         data, off = T.encode_examples(fspecs, fb)
-        with T.TFRecordWriter(paths[f], "GZIP", level=1) as w:
-            w.write_many(data, off)
+        for c in ("GZIP", None):
+            with T.TFRecordWriter(paths[c][f], c, level=1) as w:
+                w.write_many(data, off)
         return int(off[-1])
+
+    def e2e(comp, parse):
+        out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
+        pipe = T.FeaturePipe(paths[comp] * 2, fspecs, B, thread_num=thr, prefetch=3, compression_type=comp, parse=parse)
+        torch.cuda.synchronize()
+        t0, m = time.perf_counter(), 0
+        for fb in pipe:
+            enc(fb.sparse, out=out[: fb.batch])
+            m += fb.batch
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        pipe.close()
+        return round(m / dt, 1)
 
     try:
         with ThreadPoolExecutor(n_files) as ex:
             raw = sum(ex.map(write, range(n_files)))
-        gz = sum(os.path.getsize(p) for p in paths)
+        gz = sum(os.path.getsize(p) for p in paths["GZIP"])
         B, thr = args.batch, args.pipe_threads
-        rd = T.TFRecordReader(paths, fspecs, B, thread_num=thr, pinned=True)
+        rd = T.TFRecordReader(paths["GZIP"], fspecs, B, thread_num=thr, pinned=True)
         cols, n = rd.new_columns(), 0
         t0 = time.perf_counter()
         while True:
@@ -843,21 +862,19 @@ def bench_pipe(args, enc, specs, multi):
             n += c.batch
         dec = time.perf_counter() - t0
         rd.close()
-        out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
-        pipe = T.FeaturePipe(paths, fspecs, B, thread_num=thr, prefetch=3)
-        torch.cuda.synchronize()
-        t0, m = time.perf_counter(), 0
-        for fb in pipe:
-            enc(fb.sparse, out=out[: fb.batch])
-            m += fb.batch
-        torch.cuda.synchronize()
-        e2e = time.perf_counter() - t0
-        pipe.close()
-        return {"decode_examples_per_s": round(n / dec, 1), "decode_raw_GBs": round(raw / dec / 1e9, 3),
-                "pipe_to_encoder_examples_per_s": round(m / e2e, 1), "examples": n, "threads": thr,
+        e2e("GZIP", "host")  # warm the pinned pools and the allocator
+        legs = {"gzip_host": e2e("GZIP", "host"), "gzip_device": e2e("GZIP", "device")}
+        e2e(None, "device")
+        legs["none_device"] = e2e(None, "device")
+        return {"pipe_to_encoder_examples_per_s": max(legs.values()), "legs_examples_per_s": legs,
+                "decode_examples_per_s": round(n / dec, 1), "decode_raw_GBs": round(raw / dec / 1e9, 3),
+                "none_device_raw_GBs": round(legs["none_device"] * raw / n / 1e9, 3),
+                "examples": n, "examples_e2e": 2 * n, "threads": thr,
                 "bytes_per_example_raw": round(raw / n, 1), "bytes_per_example_gzip": round(gz / n, 1),
-                "config": f"{n_files} GZIP TFRecord files x {per} cfg2 examples (229 bytes features + label), "
-                          f"batch {B}, {thr} reader threads, pinned ring of 3, side-stream H2D, fused encoder consumes"}
+                "config": f"{n_files} TFRecord files x {per} cfg2 examples (229 bytes features + label), batch {B}, "
+                          f"{thr} reader threads, pinned ring of 3, side-stream H2D, fused encoder consumes; end-to-end legs read "
+                          f"the file list twice; "
+                          f"decode_* = host C++ parse alone on the GZIP files"}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -134,6 +134,65 @@ int rf_tfr_next_batch(void* reader, const rf_tfr_feature* feats, int32_t n_feats
 int64_t rf_tfr_records_read(void* reader);
 int rf_tfr_close(void* reader);
 
+/* ---- device parse: the same batch, parsed on the GPU ------------------------------------------ */
+/*
+ * Host half. Frames (and CRC-checks) the next `batch` records in the same interleave order as
+ * rf_tfr_next_batch and packs their serialized tf.train.Example payloads back to back into `out`
+ * (a pinned host buffer, so it can be streamed to HBM): record i = out[rec_off[i], rec_off[i+1]),
+ * rec_off has batch+1 entries. *n_records = records packed (0 at end of data), *n_bytes =
+ * rec_off[*n_records]. RF_ENOSPC if out_cap < the payload bytes (*n_bytes = bytes needed; the
+ * records stay pending, so a retry with a larger buffer returns them).
+ */
+int rf_tfr_next_records(void* reader, int32_t batch, uint8_t* out, int64_t out_cap, int64_t* rec_off,
+                        int32_t* n_records, int64_t* n_bytes);
+
+/*
+ * Device schema: the feature description compiled into one flat blob (names, kinds, group
+ * positions, defaults and an open-addressing hash of the keys) that the parse kernels read from
+ * HBM. rf_tfr_schema_blob writes it to a host buffer (the caller copies it to device memory once);
+ * *needed = its size. RF_EINVAL for a schema the CPU reader also rejects (bad kind/shape,
+ * duplicate name).
+ */
+int rf_tfr_schema_blob(const rf_tfr_feature* feats, int32_t n_feats, void* out, int64_t out_cap, int64_t* needed);
+
+/* Written by rf_tfr_parse_device (device memory), read back by the host (rf_tfr_device_check). */
+typedef struct rf_tfr_dev_stats {
+    int64_t n_tok_bytes, n_tok, n_ival, n_fval; /* as rf_tfr_columns.n_* */
+    int32_t err_b;    /* first failing batch position, or INT32_MAX when the batch parsed */
+    int32_t err_type; /* 1 malformed Example, 2 kind mismatch, 3 malformed list, 4 SCALAR value count */
+    int32_t err_feat; /* schema index of the failing key (types 2-4) */
+    int32_t err_kind; /* type 2: the kind found */
+    int64_t err_count; /* type 4: the value count found */
+    int64_t reserved;
+} rf_tfr_dev_stats; /* 64 bytes */
+
+/* Device scratch rf_tfr_parse_device needs for a batch of B examples (bytes). */
+int64_t rf_tfr_device_workspace_bytes(const void* schema_blob_host, int32_t batch);
+
+/*
+ * Device half: parses B packed records (`rec`, `rec_off[B+1]`, both DEVICE memory; `rec` readable
+ * up to rec_off[B] + 16 bytes) into `cols`, whose pointers are DEVICE buffers with the layout of
+ * rf_tfr_columns — the same values, offsets and lmax as rf_tfr_next_batch on the same records.
+ * n_rec_bytes = rec_off[B] and max_rec_bytes = the longest record (host copies; the latter sizes the
+ * per-record LDS staging, records that do not fit are parsed straight from HBM). Capacities must cover the worst case those bytes allow:
+ * tok_bytes_cap >= n_rec_bytes, tok_cap >= n_rec_bytes / 2 + B * Sb, ival_cap >= n_rec_bytes,
+ * fval_cap >= n_rec_bytes / 4 (RF_ENOSPC otherwise); tok_off needs tok_cap + 1 entries.
+ * Stream-ordered and asynchronous: totals, lmax and the first parse error land in `stats` and
+ * `cols->lmax/ilmax/flmax` (device); nothing else is written when the batch has an error. cols->n_*
+ * and cols->batch are not written (read them from stats after the stream reaches this point).
+ */
+int rf_tfr_parse_device(const void* schema_blob_dev, const void* schema_blob_host, const uint8_t* rec,
+                        const int64_t* rec_off, int32_t batch, int64_t n_rec_bytes, int64_t max_rec_bytes,
+                        const rf_tfr_columns* cols,
+                        rf_tfr_dev_stats* stats, void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
+ * RF_OK when the stats (copied to the host) report no error; otherwise RF_EDATA with the message
+ * rf_tfr_next_batch gives for the same record (first_record = records handed out before this batch).
+ */
+int rf_tfr_device_check(const rf_tfr_dev_stats* stats, const rf_tfr_feature* feats, int32_t n_feats,
+                        int64_t first_record);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -29,6 +30,7 @@
 #include <vector>
 
 #include "../../include/rf_io.h"
+#include "rf_tfr_blob.h"
 
 #if defined(__x86_64__)
 #include <nmmintrin.h>
@@ -123,7 +125,8 @@ struct Status {
 Status fail(int code, std::string msg) { return Status{code, std::move(msg)}; }
 
 // ------------------------------------------------------------------------------------------------
-// Byte stream over a file, plain or gzip (concatenated members allowed).
+// Byte stream over a file, plain or gzip (concatenated members allowed), read straight into the
+// caller's buffer (fread, or inflate with the buffer as its output window).
 // ------------------------------------------------------------------------------------------------
 class InStream {
   public:
@@ -135,63 +138,47 @@ class InStream {
     Status open() {
         f_ = std::fopen(path_.c_str(), "rb");
         if (!f_) return fail(RF_EIO, "cannot open " + path_ + ": " + std::strerror(errno));
-        out_.resize(1 << 20);
         if (gz_) {
             in_.resize(1 << 20);
             std::memset(&zs_, 0, sizeof(zs_));
             if (inflateInit2(&zs_, 16 + MAX_WBITS) != Z_OK) return fail(RF_EIO, "inflateInit2 failed");
             z_init_ = true;
+        } else {
+            std::setvbuf(f_, nullptr, _IONBF, 0);  // large reads go straight into the chunk
         }
         return {};
     }
-    // Reads exactly n bytes unless the stream ends first; *got = bytes delivered.
+    // Fills dst[0, n) as far as the stream allows; *got < n only at the end of the stream.
     Status read(uint8_t* dst, size_t n, size_t* got) {
         *got = 0;
-        while (*got < n) {
-            if (pos_ == len_) {
-                bool eof = false;
-                Status s = refill(&eof);
-                if (!s.ok()) return s;
-                if (eof) return {};
-            }
-            const size_t k = std::min(n - *got, len_ - pos_);
-            std::memcpy(dst + *got, out_.data() + pos_, k);
-            pos_ += k;
-            *got += k;
-        }
-        return {};
-    }
-
-  private:
-    Status refill(bool* eof) {
-        pos_ = len_ = 0;
         if (!gz_) {
-            len_ = std::fread(out_.data(), 1, out_.size(), f_);
-            if (len_ == 0) {
-                if (std::ferror(f_)) return fail(RF_EIO, "read error in " + path_);
-                *eof = true;
+            while (*got < n) {
+                const size_t k = std::fread(dst + *got, 1, n - *got, f_);
+                if (k == 0) {
+                    if (std::ferror(f_)) return fail(RF_EIO, "read error in " + path_);
+                    break;
+                }
+                *got += k;
             }
             return {};
         }
-        while (len_ == 0) {
+        while (*got < n) {
             if (zs_.avail_in == 0) {
                 const size_t k = std::fread(in_.data(), 1, in_.size(), f_);
                 if (k == 0) {
                     if (std::ferror(f_)) return fail(RF_EIO, "read error in " + path_);
-                    if (!member_open_) { *eof = true; return {}; }
+                    if (!member_open_) return {};
                     return fail(RF_EDATA, "truncated gzip stream in " + path_);
                 }
                 zs_.next_in = in_.data();
                 zs_.avail_in = static_cast<uInt>(k);
             }
-            if (!member_open_) {
-                // a new gzip member begins (the first, or one concatenated after a finished one)
-                member_open_ = true;
-            }
-            zs_.next_out = out_.data();
-            zs_.avail_out = static_cast<uInt>(out_.size());
+            member_open_ = true;  // a gzip member begins (the first, or one concatenated after a finished one)
+            const size_t want = std::min<size_t>(n - *got, 1u << 30);
+            zs_.next_out = dst + *got;
+            zs_.avail_out = static_cast<uInt>(want);
             const int rc = inflate(&zs_, Z_NO_FLUSH);
-            len_ = out_.size() - zs_.avail_out;
+            *got += want - zs_.avail_out;
             if (rc == Z_STREAM_END) {
                 member_open_ = false;
                 if (inflateReset(&zs_) != Z_OK) return fail(RF_EIO, "inflateReset failed");
@@ -203,23 +190,27 @@ class InStream {
         return {};
     }
 
+  private:
     std::string path_;
     bool gz_;
     FILE* f_ = nullptr;
     z_stream zs_;
     bool z_init_ = false, member_open_ = false;
-    std::vector<uint8_t> in_, out_;
-    size_t pos_ = 0, len_ = 0;
+    std::vector<uint8_t> in_;
 };
 
-// Records of one file in decode order, packed into chunks.
+// A block of one file's decoded bytes and the records framed inside it (payloads in place).
 struct Chunk {
-    std::vector<uint8_t> data;
-    std::vector<uint64_t> off{0};  // record i = data[off[i], off[i+1])
-    size_t size() const { return off.size() - 1; }
+    std::unique_ptr<uint8_t[]> buf;  // not zero-initialised
+    size_t cap = 0;
+    std::vector<uint64_t> start;  // record i = buf[start[i], start[i] + len[i])
+    std::vector<uint32_t> len;
+    explicit Chunk(size_t c) : buf(new uint8_t[c]), cap(c) {}
+    size_t size() const { return start.size(); }
 };
 
-// One open file: a thread decompresses and de-frames records into a bounded chunk queue.
+// One open file: a thread reads (or inflates) blocks and frames the records inside them into a
+// bounded chunk queue.
 class FileProducer {
   public:
     FileProducer(std::string path, bool gz) : path_(std::move(path)), gz_(gz) {
@@ -245,8 +236,8 @@ class FileProducer {
             g.unlock();
             cv_.notify_all();
         }
-        *p = cur_->data.data() + cur_->off[idx_];
-        *n = static_cast<uint32_t>(cur_->off[idx_ + 1] - cur_->off[idx_]);
+        *p = cur_->buf.get() + cur_->start[idx_];
+        *n = cur_->len[idx_];
         *hold = cur_;
         ++idx_;
         return 1;
@@ -254,7 +245,7 @@ class FileProducer {
     const Status& status() const { return st_; }
 
   private:
-    static constexpr size_t kChunkRecords = 1024, kChunkBytes = 4u << 20, kQueueChunks = 6;
+    static constexpr size_t kBlockBytes = 4u << 20, kQueueChunks = 6;
 
     void run() {
         Status s = produce();
@@ -263,41 +254,53 @@ class FileProducer {
         done_ = true;
         cv_.notify_all();
     }
+    // Blocks of kBlockBytes; a record cut by the block end moves (with its header) to the front of
+    // the next block, which grows when one record needs more than a block.
     Status produce() {
         InStream in(path_, gz_);
         Status s = in.open();
         if (!s.ok()) return s;
-        auto chunk = std::make_shared<Chunk>();
         uint64_t rec_no = 0;
+        auto chunk = std::make_shared<Chunk>(kBlockBytes);
+        size_t have = 0;  // bytes in chunk->buf
         for (;;) {
-            uint8_t hdr[12];
             size_t got = 0;
-            s = in.read(hdr, 12, &got);
+            s = in.read(chunk->buf.get() + have, chunk->cap - have, &got);
             if (!s.ok()) return s;
-            if (got == 0) break;
-            if (got < 12) return fail(RF_EDATA, "truncated record header at record " + std::to_string(rec_no) + " of " + path_);
-            const uint64_t len = load_u64(hdr);
-            if (mask_crc(crc32c(0, hdr, 8)) != load_u32(hdr + 8))
-                return fail(RF_EDATA, "corrupted record length crc at record " + std::to_string(rec_no) + " of " + path_);
-            if (len > (1ull << 31)) return fail(RF_EDATA, "record too large at record " + std::to_string(rec_no) + " of " + path_);
-            const size_t base = chunk->data.size();
-            chunk->data.resize(base + len + 4);
-            s = in.read(chunk->data.data() + base, len + 4, &got);
-            if (!s.ok()) return s;
-            if (got < len + 4) return fail(RF_EDATA, "truncated record at record " + std::to_string(rec_no) + " of " + path_);
-            const uint32_t want = load_u32(chunk->data.data() + base + len);
-            if (mask_crc(crc32c(0, chunk->data.data() + base, len)) != want)
-                return fail(RF_EDATA, "corrupted record data crc at record " + std::to_string(rec_no) + " of " + path_);
-            chunk->data.resize(base + len);
-            chunk->off.push_back(base + len);
-            ++rec_no;
-            if (chunk->size() >= kChunkRecords || chunk->data.size() >= kChunkBytes) {
-                if (!push(std::move(chunk))) return {};
-                chunk = std::make_shared<Chunk>();
+            const bool eof = have + got < chunk->cap;
+            have += got;
+            const uint8_t* base = chunk->buf.get();
+            size_t pos = 0, need = 0;
+            while (have - pos >= 12) {
+                const uint8_t* h = base + pos;
+                const uint64_t len = load_u64(h);
+                if (mask_crc(crc32c(0, h, 8)) != load_u32(h + 8))
+                    return fail(RF_EDATA, "corrupted record length crc at record " + std::to_string(rec_no) + " of " + path_);
+                if (len > (1ull << 31)) return fail(RF_EDATA, "record too large at record " + std::to_string(rec_no) + " of " + path_);
+                need = 12 + static_cast<size_t>(len) + 4;
+                if (have - pos < need) break;
+                if (mask_crc(crc32c(0, h + 12, len)) != load_u32(h + 12 + len))
+                    return fail(RF_EDATA, "corrupted record data crc at record " + std::to_string(rec_no) + " of " + path_);
+                chunk->start.push_back(pos + 12);
+                chunk->len.push_back(static_cast<uint32_t>(len));
+                pos += need;
+                need = 0;
+                ++rec_no;
             }
+            const size_t tail = have - pos;
+            if (eof) {
+                if (tail && tail < 12)
+                    return fail(RF_EDATA, "truncated record header at record " + std::to_string(rec_no) + " of " + path_);
+                if (tail) return fail(RF_EDATA, "truncated record at record " + std::to_string(rec_no) + " of " + path_);
+                if (chunk->size()) push(std::move(chunk));
+                return {};
+            }
+            auto next = std::make_shared<Chunk>(std::max(kBlockBytes, need + (need >> 2)));
+            std::memcpy(next->buf.get(), base + pos, tail);
+            have = tail;
+            if (chunk->size() && !push(std::move(chunk))) return {};
+            chunk = std::move(next);
         }
-        if (chunk->size()) push(std::move(chunk));
-        return {};
     }
     bool push(std::shared_ptr<Chunk> c) {
         std::unique_lock<std::mutex> g(mu_);
@@ -699,6 +702,39 @@ class Reader {
         return {};
     }
     int64_t handed() const { return handed_; }
+
+    // The device-parse host half: the next `batch` records' payloads, packed back to back (rf_io.h).
+    Status next_records(int32_t batch, uint8_t* out, int64_t cap, int64_t* rec_off, int32_t* n_out, int64_t* bytes) {
+        *n_out = 0;
+        *bytes = 0;
+        Status s = fill(batch);
+        if (!s.ok()) return s;
+        const int32_t B = static_cast<int32_t>(std::min<size_t>(batch, pend_.size()));
+        int64_t total = 0;
+        rec_off[0] = 0;
+        for (int32_t b = 0; b < B; ++b) {
+            total += pend_[b].n;
+            rec_off[b + 1] = total;
+        }
+        *bytes = total;
+        if (total > cap || (total && !out))
+            return fail(RF_ENOSPC, "record buffer too small: need " + std::to_string(total) + " bytes, have " +
+                                       std::to_string(cap));
+        if (B) {
+            // ~1 MiB of copying per task
+            const int T = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(B, std::min<int64_t>(pool_.size() * 4, total >> 20))));
+            pool_.run(T, [&](int t) {
+                const int32_t b0 = static_cast<int32_t>(static_cast<int64_t>(B) * t / T);
+                const int32_t b1 = static_cast<int32_t>(static_cast<int64_t>(B) * (t + 1) / T);
+                for (int32_t b = b0; b < b1; ++b) std::memcpy(out + rec_off[b], pend_[b].p, pend_[b].n);
+            });
+        }
+        pend_.erase(pend_.begin(), pend_.begin() + B);
+        hold_.erase(hold_.begin(), hold_.begin() + B);
+        handed_ += B;
+        *n_out = B;
+        return {};
+    }
 
   private:
     // Interleave (tf.data InterleaveDataset order, block_length 1) until `batch` records are pending.
@@ -1250,6 +1286,98 @@ extern "C" int rf_tfr_next_batch(void* reader, const rf_tfr_feature* feats, int3
     if (s.ok()) s = static_cast<Reader*>(reader)->next_batch(sc, batch, cols);
     if (!s.ok()) return rf_set_error(s.code, "rf_tfr_next_batch: %s", s.msg.c_str());
     return RF_OK;
+}
+
+extern "C" int rf_tfr_next_records(void* reader, int32_t batch, uint8_t* out, int64_t out_cap, int64_t* rec_off,
+                                   int32_t* n_records, int64_t* n_bytes) {
+    if (!reader || batch <= 0 || !rec_off || !n_records || !n_bytes || out_cap < 0)
+        return rf_set_error(RF_EINVAL, "rf_tfr_next_records: bad argument");
+    Status s = static_cast<Reader*>(reader)->next_records(batch, out, out_cap, rec_off, n_records, n_bytes);
+    if (!s.ok()) return rf_set_error(s.code, "rf_tfr_next_records: %s", s.msg.c_str());
+    return RF_OK;
+}
+
+extern "C" int rf_tfr_schema_blob(const rf_tfr_feature* feats, int32_t n_feats, void* out, int64_t out_cap,
+                                  int64_t* needed) {
+    if (!feats || n_feats <= 0 || !needed) return rf_set_error(RF_EINVAL, "rf_tfr_schema_blob: bad argument");
+    Schema sc;
+    Status s = sc.build(feats, n_feats);
+    if (!s.ok()) return rf_set_error(s.code, "rf_tfr_schema_blob: %s", s.msg.c_str());
+    int32_t hsize = 1;
+    while (hsize < 2 * n_feats) hsize <<= 1;
+    int64_t names = 0;
+    for (auto& nm : sc.names) names += static_cast<int64_t>(nm.size());
+    const int64_t names_off = static_cast<int64_t>(sizeof(TfrBlobHdr)) + static_cast<int64_t>(sizeof(TfrBlobFeat)) * n_feats +
+                              4 * static_cast<int64_t>(hsize);
+    const int64_t total = (names_off + names + 15) & ~int64_t{15};
+    *needed = total;
+    if (names_off + names > INT32_MAX) return rf_set_error(RF_EINVAL, "rf_tfr_schema_blob: schema too large");
+    if (!out || out_cap < total)
+        return rf_set_error(RF_ENOSPC, "rf_tfr_schema_blob: need %lld bytes", static_cast<long long>(total));
+    auto* base = static_cast<uint8_t*>(out);
+    std::memset(base, 0, static_cast<size_t>(total));
+    TfrBlobHdr h{};
+    h.F = n_feats;
+    h.Sb = sc.n_bytes;
+    h.Si = sc.n_iseq;
+    h.Sf = sc.n_fseq;
+    h.Ni = sc.n_iscalar;
+    h.Nf = sc.n_fscalar;
+    h.hmask = hsize - 1;
+    h.names_off = static_cast<int32_t>(names_off);
+    h.total_bytes = total;
+    std::memcpy(base, &h, sizeof(h));
+    auto* fe = reinterpret_cast<TfrBlobFeat*>(base + sizeof(TfrBlobHdr));
+    auto* ht = reinterpret_cast<int32_t*>(base + sizeof(TfrBlobHdr) + sizeof(TfrBlobFeat) * n_feats);
+    for (int32_t i = 0; i < hsize; ++i) ht[i] = -1;
+    int64_t no = 0;
+    for (int32_t j = 0; j < n_feats; ++j) {
+        TfrBlobFeat f{};
+        f.kind = sc.kind[j];
+        f.shape = sc.shape[j];
+        f.gpos = sc.group_pos[j];
+        f.name_off = static_cast<int32_t>(no);
+        f.name_len = static_cast<int32_t>(sc.names[j].size());
+        f.def_i = sc.def_i[j];
+        f.def_f = sc.def_f[j];
+        fe[j] = f;
+        std::memcpy(base + names_off + no, sc.names[j].data(), sc.names[j].size());
+        no += f.name_len;
+        uint32_t slot = tfr_key_hash_host(reinterpret_cast<const uint8_t*>(sc.names[j].data()),
+                                          static_cast<uint32_t>(sc.names[j].size())) & static_cast<uint32_t>(hsize - 1);
+        while (ht[slot] >= 0) slot = (slot + 1) & static_cast<uint32_t>(hsize - 1);
+        ht[slot] = j;
+    }
+    return RF_OK;
+}
+
+extern "C" int rf_tfr_device_check(const rf_tfr_dev_stats* st, const rf_tfr_feature* feats, int32_t n_feats,
+                                   int64_t first_record) {
+    if (!st || !feats || n_feats <= 0) return rf_set_error(RF_EINVAL, "rf_tfr_device_check: bad argument");
+    if (st->err_b == INT32_MAX) return RF_OK;
+    const int64_t rec = first_record + st->err_b;
+    const int32_t j = st->err_feat;
+    if (st->err_type != 1 && (j < 0 || j >= n_feats || !feats[j].name))
+        return rf_set_error(RF_EDATA, "rf_tfr_next_batch: parse error %d at record %lld", st->err_type, (long long)rec);
+    std::string m;
+    switch (st->err_type) {  // the texts of Reader::parse
+        case 1:
+            m = "malformed tf.train.Example at batch position " + std::to_string(st->err_b) + " (record " +
+                std::to_string(rec) + ")";
+            break;
+        case 2:
+            m = std::string("Key: ") + feats[j].name + ". Data types don't match. Expected " + kind_name(feats[j].kind) +
+                ", got " + kind_name(st->err_kind) + " (record " + std::to_string(rec) + ")";
+            break;
+        case 3:
+            m = std::string("Key: ") + feats[j].name + ". malformed " + kind_name(feats[j].kind) + " list (record " +
+                std::to_string(rec) + ")";
+            break;
+        default:
+            m = std::string("Key: ") + feats[j].name + ". Number of values != expected. Values size: " +
+                std::to_string(st->err_count) + " but output shape: [] (record " + std::to_string(rec) + ")";
+    }
+    return rf_set_error(RF_EDATA, "rf_tfr_next_batch: %s", m.c_str());
 }
 
 extern "C" int64_t rf_tfr_records_read(void* reader) {

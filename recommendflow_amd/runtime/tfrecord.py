@@ -78,6 +78,13 @@ class _Cols(ctypes.Structure):
                [("batch", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class _DevStats(ctypes.Structure):
+    _fields_ = [("n_tok_bytes", ctypes.c_int64), ("n_tok", ctypes.c_int64), ("n_ival", ctypes.c_int64),
+                ("n_fval", ctypes.c_int64), ("err_b", ctypes.c_int32), ("err_type", ctypes.c_int32),
+                ("err_feat", ctypes.c_int32), ("err_kind", ctypes.c_int32), ("err_count", ctypes.c_int64),
+                ("reserved", ctypes.c_int64)]
+
+
 _vp, _i32, _i64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
 IO_SIGS = {
     "rf_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, _vp, _sz]),
@@ -91,6 +98,12 @@ IO_SIGS = {
     "rf_tfr_next_batch": (ctypes.c_int, [_vp, ctypes.POINTER(_Feat), _i32, _i32, ctypes.POINTER(_Cols)]),
     "rf_tfr_records_read": (_i64, [_vp]),
     "rf_tfr_close": (ctypes.c_int, [_vp]),
+    "rf_tfr_next_records": (ctypes.c_int, [_vp, _i32, _vp, _i64, _vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64)]),
+    "rf_tfr_schema_blob": (ctypes.c_int, [ctypes.POINTER(_Feat), _i32, _vp, _i64, ctypes.POINTER(_i64)]),
+    "rf_tfr_device_workspace_bytes": (_i64, [_vp, _i32]),
+    "rf_tfr_parse_device": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i64, _i64, ctypes.POINTER(_Cols), _vp, _vp, _i64,
+                                           _vp]),
+    "rf_tfr_device_check": (ctypes.c_int, [_vp, ctypes.POINTER(_Feat), _i32, _i64]),
 }
 _io_lock = threading.Lock()
 _io_bound = False
@@ -415,6 +428,19 @@ def columns_from_rows(specs: Sequence[FeatureSpec], rows: Sequence[Dict[str, obj
                         dense(g["iscalar"], np.int64), g["iscalar"], dense(g["fscalar"], np.float32), g["fscalar"])
 
 
+def _nbytes(x) -> int:
+    return int(x.numel()) if hasattr(x, "numel") else int(x.size)
+
+
+def _like(x, n: int):
+    """A new uint8 host buffer of n bytes, pinned if x is a pinned torch tensor."""
+    if hasattr(x, "numel"):
+        import torch
+
+        return torch.empty(n, dtype=torch.uint8, pin_memory=x.is_pinned())
+    return np.empty(n, np.uint8)
+
+
 # ---- reader -------------------------------------------------------------------------------------
 class TFRecordReader:
     """TFRecordDataset(paths, compression_type, num_parallel_reads=thread_num).batch(B).map(parse_example)
@@ -461,6 +487,22 @@ class TFRecordReader:
                 return None
             return cols, c
 
+    def read_records(self, buf, rec_off):
+        """Device-parse host half (rf_tfr_next_records): packs the next batch's serialized records into
+        `buf` (uint8, pinned torch or numpy; replaced by a larger one when too small) with offsets in
+        rec_off[:n+1]. Returns (buf, n, n_bytes); n = 0 at end of data (or a dropped remainder)."""
+        n, nb = ctypes.c_int32(0), ctypes.c_int64(0)
+        while True:
+            rc = _lib().rf_tfr_next_records(self._h, self.B, _HostColumns._addr(buf), _nbytes(buf), _HostColumns._addr(rec_off),
+                                            ctypes.byref(n), ctypes.byref(nb))
+            if rc == RF_ENOSPC:
+                buf = _like(buf, int(nb.value * 1.25) + 4096)
+                continue
+            _check(rc, "rf_tfr_next_records")
+            if n.value == 0 or (self.drop_remainder and n.value < self.B):
+                return buf, 0, 0
+            return buf, int(n.value), int(nb.value)
+
     def __iter__(self):
         cols = self.new_columns()
         while True:
@@ -487,6 +529,90 @@ class TFRecordReader:
             pass
 
 
+class DeviceParser:
+    """parse_example on the GPU (rf_tfr_parse_device): serialized records in HBM -> the same columns
+    TFRecordReader's C++ parse produces, as device tensors. The schema is compiled once into a device
+    blob (rf_tfr_schema_blob)."""
+
+    def __init__(self, specs: Sequence[FeatureSpec], device):
+        import torch
+
+        self.specs, self.device = list(specs), torch.device(device)
+        self.groups = _groups(self.specs)
+        self._feats, self._names = _feats_array(self.specs)
+        need = ctypes.c_int64(0)
+        rc = _lib().rf_tfr_schema_blob(self._feats, len(self.specs), None, 0, ctypes.byref(need))
+        if rc not in (L.RF_OK, RF_ENOSPC):
+            _check(rc, "rf_tfr_schema_blob")
+        self.blob_host = np.zeros(int(need.value), np.uint8)
+        _check(_lib().rf_tfr_schema_blob(self._feats, len(self.specs), self.blob_host.ctypes.data, self.blob_host.size,
+                                         ctypes.byref(need)), "rf_tfr_schema_blob")
+        self.blob_dev = torch.from_numpy(self.blob_host).to(self.device)
+        self.Sb, self.Si, self.Sf = len(self.groups["bytes"]), len(self.groups["iseq"]), len(self.groups["fseq"])
+        self.Ni, self.Nf = len(self.groups["iscalar"]), len(self.groups["fscalar"])
+        # one small block read back per batch: stats (64 B = 16 int32) | lmax | ilmax | flmax
+        self.small_len = 16 + self.Sb + self.Si + self.Sf
+
+    def parse(self, rec, rec_off, B: int, n_bytes: int, max_rec: int, stream):
+        """Enqueues the parse of B records (rec: device uint8 with >= 16 bytes of slack past n_bytes;
+        rec_off: device int64 [B+1]) on `stream`. Returns (device column buffers, small), `small` the
+        device int32 block holding the stats and lmax arrays."""
+        import torch
+
+        dev = self.device
+        Sb, Si, Sf = self.Sb, self.Si, self.Sf
+        small = torch.empty(self.small_len, dtype=torch.int32, device=dev)
+        lm = small[16:]
+
+        def buf(n, dt, need):
+            return torch.empty(max(int(n), 1), dtype=dt, device=dev) if need else None
+
+        tok_cap = n_bytes // 2 + B * Sb
+        b = {"tok_bytes": buf(n_bytes + 16, torch.uint8, Sb), "tok_off": buf(tok_cap + 1, torch.int32, Sb),
+             "bag_off": buf(B * Sb + 1, torch.int32, Sb), "lmax": lm[:Sb] if Sb else None,
+             "ival": buf(n_bytes, torch.int64, Si), "ibag_off": buf(B * Si + 1, torch.int32, Si),
+             "ilmax": lm[Sb:Sb + Si] if Si else None,
+             "fval": buf(n_bytes // 4 + 1, torch.float32, Sf), "fbag_off": buf(B * Sf + 1, torch.int32, Sf),
+             "flmax": lm[Sb + Si:] if Sf else None,
+             "iscalar": buf(B * self.Ni, torch.int64, self.Ni), "fscalar": buf(B * self.Nf, torch.float32, self.Nf)}
+        c = _Cols()
+        for k, v in b.items():
+            setattr(c, k, int(v.data_ptr()) if v is not None else None)
+        c.tok_bytes_cap, c.tok_cap = n_bytes + 16, tok_cap
+        c.ival_cap, c.fval_cap = n_bytes, n_bytes // 4 + 1
+        ws_n = int(_lib().rf_tfr_device_workspace_bytes(self.blob_host.ctypes.data, B))
+        ws = torch.empty(max(ws_n, 1), dtype=torch.uint8, device=dev)
+        _check(_lib().rf_tfr_parse_device(self.blob_dev.data_ptr(), self.blob_host.ctypes.data, rec.data_ptr(),
+                                          rec_off.data_ptr(), B, n_bytes, max_rec, ctypes.byref(c), small.data_ptr(),
+                                          ws.data_ptr(), ws_n, stream.cuda_stream), "rf_tfr_parse_device")
+        b["_ws"] = ws
+        return b, small
+
+    def check(self, small_host, first_record: int) -> _DevStats:
+        """Raises DataLossError with the host reader's message if the batch failed; else the stats."""
+        st = _DevStats.from_buffer_copy(np.ascontiguousarray(small_host[:16]).tobytes())
+        _check(_lib().rf_tfr_device_check(ctypes.addressof(st), self._feats, len(self.specs), int(first_record)),
+               "rf_tfr_next_batch")
+        return st
+
+    def views(self, b, st: _DevStats, B: int):
+        """Columns trimmed to the batch's counts (the rf_tfr_columns views TFRecordReader hands out)."""
+        Sb, Si, Sf, Ni, Nf = self.Sb, self.Si, self.Sf, self.Ni, self.Nf
+        v = {}
+        if Sb:
+            v["tok_bytes"] = b["tok_bytes"][: st.n_tok_bytes] if st.n_tok_bytes else b["tok_bytes"][:16]
+            v["tok_off"], v["bag_off"], v["lmax"] = b["tok_off"][: st.n_tok + 1], b["bag_off"][: B * Sb + 1], b["lmax"]
+        if Si:
+            v["ival"], v["ibag_off"], v["ilmax"] = b["ival"][: st.n_ival], b["ibag_off"][: B * Si + 1], b["ilmax"]
+        if Sf:
+            v["fval"], v["fbag_off"], v["flmax"] = b["fval"][: st.n_fval], b["fbag_off"][: B * Sf + 1], b["flmax"]
+        import torch
+
+        v["iscalar"] = b["iscalar"][: B * Ni] if Ni else torch.empty(0, dtype=torch.int64, device=self.device)
+        v["fscalar"] = b["fscalar"][: B * Nf] if Nf else torch.empty(0, dtype=torch.float32, device=self.device)
+        return v
+
+
 class FeaturePipe:
     """Batches from TFRecord files, decoded in C++ into pinned host buffers and streamed to HBM on a
     side HIP stream. Iterating yields device FeatureBatches whose tensors are safe to
@@ -494,18 +620,26 @@ class FeaturePipe:
 
     `prefetch` pinned buffer sets rotate: the decoder thread fills set i+1 while the H2D copy of set
     i runs and the model consumes batch i-1.
+
+    parse="device": the host only frames and packs the serialized records (rf_tfr_next_records); they
+    are streamed to HBM as they are and parsed there (DeviceParser), so the host's per-example
+    protobuf work leaves the critical path. Same batches, same bytes, same errors.
     """
 
     _END = object()
 
     def __init__(self, paths, specs, batch_size: int, thread_num: int = 8, compression_type="GZIP",
-                 drop_remainder: bool = False, prefetch: int = 3, device=None):
+                 drop_remainder: bool = False, prefetch: int = 3, device=None, parse: str = "host"):
         import torch
 
         L.require_gpu()
+        if parse not in ("host", "device"):
+            raise ValueError(f"parse must be 'host' or 'device', got {parse!r}")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.reader = TFRecordReader(paths, specs, batch_size, thread_num, compression_type, drop_remainder, pinned=True)
         self.groups = self.reader.groups
+        self.parse = parse
+        self.parser = DeviceParser(specs, self.device) if parse == "device" else None
         self.stream = torch.cuda.Stream(device=self.device)
         self._free: "queue.Queue" = queue.Queue()
         for _ in range(max(1, prefetch)):
@@ -513,7 +647,7 @@ class FeaturePipe:
         self._ready: "queue.Queue" = queue.Queue(maxsize=max(1, prefetch))
         self._stop = False
         self._err: Optional[BaseException] = None
-        self._th = threading.Thread(target=self._produce, daemon=True)
+        self._th = threading.Thread(target=self._produce_device if parse == "device" else self._produce, daemon=True)
         self._th.start()
 
     def _produce(self):
@@ -540,7 +674,43 @@ class FeaturePipe:
                     ev = torch.cuda.Event()
                     ev.record(self.stream)
                 dev["_host_lmax"] = np.array(host["lmax"].numpy(), np.int32)
-                self._ready.put((dev, c.batch, ev, cols))
+                self._ready.put(("host", dev, c.batch, ev, cols))
+        except BaseException as e:  # surfaced to the consumer
+            self._err = e
+        self._ready.put(self._END)
+
+    def _produce_device(self):
+        """Frames + packs records into a pinned set, streams them to HBM and enqueues the device parse
+        and the read-back of its stats, all on the side stream; the consumer waits on the event."""
+        import torch
+
+        P, B = self.parser, self.reader.B
+        try:
+            torch.cuda.set_device(self.device)
+            while not self._stop:
+                slot = self._free.get()
+                if slot is not None:
+                    slot["ev"].synchronize()  # the H2D copies out of (and stats into) this set are done
+                else:
+                    slot = {"rec": torch.empty(B * 4096, dtype=torch.uint8, pin_memory=True),
+                            "off": torch.empty(B + 1, dtype=torch.int64, pin_memory=True),
+                            "small": torch.empty(P.small_len, dtype=torch.int32, pin_memory=True)}
+                slot["rec"], n, nb = self.reader.read_records(slot["rec"], slot["off"])
+                if n == 0:
+                    break
+                first = self.reader.records_read - n
+                off = slot["off"][: n + 1]
+                max_rec = int(np.diff(off.numpy()).max())
+                with torch.cuda.stream(self.stream):
+                    rec = torch.empty(nb + 64, dtype=torch.uint8, device=self.device)
+                    rec[:nb].copy_(slot["rec"][:nb], non_blocking=True)
+                    off_d = off.to(self.device, non_blocking=True)
+                    bufs, small = P.parse(rec, off_d, n, nb, max_rec, self.stream)
+                    slot["small"].copy_(small, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                slot["ev"] = ev
+                self._ready.put(("device", bufs, n, ev, slot, first))
         except BaseException as e:  # surfaced to the consumer
             self._err = e
         self._ready.put(self._END)
@@ -554,13 +724,24 @@ class FeaturePipe:
                 if self._err is not None:
                     raise self._err
                 return
-            dev, B, ev, cols = item
-            host_lmax = dev.pop("_host_lmax")
             cur = torch.cuda.current_stream(self.device)
-            cur.wait_event(ev)
-            for t in dev.values():
-                t.record_stream(cur)
-            self._free.put((cols, ev))
+            if item[0] == "host":
+                _, dev, B, ev, cols = item
+                host_lmax = dev.pop("_host_lmax")
+                cur.wait_event(ev)
+                for t in dev.values():
+                    t.record_stream(cur)
+                self._free.put((cols, ev))
+            else:
+                _, bufs, B, ev, slot, first = item
+                ev.synchronize()  # parse done, stats and lmax are on the host
+                small = slot["small"].numpy().copy()
+                self._free.put(slot)
+                st = self.parser.check(small, first)
+                dev = self.parser.views(bufs, st, B)
+                host_lmax = small[16:16 + self.parser.Sb].astype(np.int32)
+                for t in dev.values():
+                    t.record_stream(cur)
             fb = _make_batch(self.groups, B, dev)
             if fb.sparse is not None:
                 fb.sparse.host_lmax = host_lmax

@@ -309,3 +309,67 @@ def test_library_exports_io_symbols():
     for s in syms:
         assert hasattr(lib, s), s
     assert struct.calcsize("<qiiqd") == 32
+
+
+@pytest.mark.parametrize("compression", ["GZIP", None])
+def test_next_records_packs_the_interleaved_records(tmp_path, compression):
+    """The device-parse host half (rf_tfr_next_records): same records, same order as the host parse."""
+    counts = [7, 0, 12, 5]
+    paths, recs = [], []
+    for f, n in enumerate(counts):
+        r = [pb_record(x) for x in random_rows(n, 30 + f)]
+        p = str(tmp_path / f"n{f}")
+        TO.write_file(p, r, compression or "NONE")
+        paths.append(p)
+        recs.append(r)
+    want = [recs[f][i] for f, i in TO.interleave_order(counts, 3)]
+    rd = T.TFRecordReader(paths, SPECS, 5, thread_num=3, compression_type=compression)
+    buf, off, got = np.empty(8, np.uint8), np.empty(6, np.int64), []  # 8 bytes: forces the ENOSPC -> grow path
+    while True:
+        buf, n, nb = rd.read_records(buf, off)
+        if n == 0:
+            break
+        assert off[0] == 0 and off[n] == nb
+        got += [bytes(buf[off[i]:off[i + 1]]) for i in range(n)]
+    assert got == want and rd.records_read == len(want)
+
+
+def test_schema_blob_and_device_check_messages():
+    """The device schema blob (rf_tfr_blob.h) and the host-side error text for device parse errors."""
+    import ctypes
+
+    L = T._lib()
+    feats, _keep = T._feats_array(SPECS)
+    need = ctypes.c_int64(0)
+    assert L.rf_tfr_schema_blob(feats, len(SPECS), None, 0, ctypes.byref(need)) == T.RF_ENOSPC
+    blob = np.zeros(int(need.value), np.uint8)
+    assert L.rf_tfr_schema_blob(feats, len(SPECS), blob.ctypes.data, blob.size, ctypes.byref(need)) == 0
+    F, Sb, Si, Sf, Ni, Nf, hmask, names_off = (int(x) for x in np.frombuffer(blob[:32].tobytes(), np.int32))
+    assert (F, Sb, Si, Sf, Ni, Nf) == (7, 3, 1, 1, 1, 1) and hmask + 1 >= 2 * F and (hmask + 1) & hmask == 0
+    fe = blob[40:40 + 40 * F].reshape(F, 40)
+    ht = np.frombuffer(blob[40 + 40 * F:40 + 40 * F + 4 * (hmask + 1)].tobytes(), np.int32)
+    for j, s in enumerate(SPECS):
+        kind, shape, gpos, no, nl = np.frombuffer(fe[j, :20].tobytes(), np.int32)
+        assert (kind, shape) == (s.kind, s.shape)
+        assert bytes(blob[names_off + no:names_off + no + nl]) == s.name.encode()
+        h = 2166136261
+        for ch in s.name.encode():
+            h = ((h ^ ch) * 16777619) & 0xFFFFFFFF
+        slot = h & hmask
+        while ht[slot] != j:  # linear probing reaches the key before an empty slot
+            assert ht[slot] >= 0
+            slot = (slot + 1) & hmask
+    assert int(L.rf_tfr_device_workspace_bytes(blob.ctypes.data, 100)) > 16 * 100 * F
+
+    def msg(**kw):
+        st = T._DevStats(err_b=kw.pop("b", 2147483647), **kw)
+        rc = L.rf_tfr_device_check(ctypes.addressof(st), feats, len(SPECS), 40)
+        return rc, L.rf_last_error().decode()
+
+    assert msg()[0] == 0
+    assert msg(b=3, err_type=1) == (T.RF_EDATA, "rf_tfr_next_batch: malformed tf.train.Example at batch position 3 (record 43)")
+    assert msg(b=0, err_type=2, err_feat=5, err_kind=T.FLOAT)[1] == \
+        "rf_tfr_next_batch: Key: cnt. Data types don't match. Expected int64, got float (record 40)"
+    assert msg(b=1, err_type=3, err_feat=3)[1] == "rf_tfr_next_batch: Key: disc. malformed float list (record 41)"
+    assert msg(b=1, err_type=4, err_feat=4, err_count=2)[1] == \
+        "rf_tfr_next_batch: Key: label. Number of values != expected. Values size: 2 but output shape: [] (record 41)"
