@@ -17,14 +17,52 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// GELU, exact form 0.5 x (1 + erf(x / sqrt 2)) (Keras 'gelu', approximate=False), without branches:
+// erfc(|z|) = t exp(-z^2 + P(t)), t = 1 / (1 + |z| / 2), P the Chebyshev fit of Numerical Recipes' erfcc
+// (fractional error < 1.2e-7 everywhere); for z < 0 the result is x erfc(|z|) / 2 directly (no 1 - (1 - e)
+// cancellation). Straight-line code, so an epilogue's elements interleave instead of each taking a branch.
+__device__ __forceinline__ float gelu_erf(float x) {
+    const float z = x * 0.70710678118654752440f, a = fabsf(z);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, a, 1.0f));
+    float p = fmaf(t, 0.17087277f, -0.82215223f);
+    p = fmaf(t, p, 1.48851587f);
+    p = fmaf(t, p, -1.13520398f);
+    p = fmaf(t, p, 0.27886807f);
+    p = fmaf(t, p, -0.18628806f);
+    p = fmaf(t, p, 0.09678418f);
+    p = fmaf(t, p, 0.37409196f);
+    p = fmaf(t, p, 1.00002368f);
+    p = fmaf(t, p, -1.26551223f);
+    const float e = t * __expf(fmaf(-a, a, p));  // erfc(|z|)
+    return z >= 0.f ? x * fmaf(-0.5f, e, 1.0f) : 0.5f * x * e;
+}
+
+struct ActNone { __device__ __forceinline__ float operator()(float x) const { return x; } };
+struct ActGelu { __device__ __forceinline__ float operator()(float x) const { return gelu_erf(x); } };
+struct ActRelu { __device__ __forceinline__ float operator()(float x) const { return x > 0.f ? x : 0.f; } };
+struct ActSelu {
+    __device__ __forceinline__ float operator()(float x) const {
+        const float alpha = 1.6732632423543772848170429916717f, scale = 1.0507009873554804934193349852946f;
+        return x > 0.f ? scale * x : scale * alpha * (__expf(x) - 1.0f);
+    }
+};
+
+// Runs f(Act{}) with the activation resolved once, outside the element loops f contains.
+template <class F>
+__device__ __forceinline__ void with_act(int act, F&& f) {
+    switch (act) {
+        case RF_ACT_GELU: f(ActGelu{}); break;
+        case RF_ACT_RELU: f(ActRelu{}); break;
+        case RF_ACT_SELU: f(ActSelu{}); break;
+        default: f(ActNone{}); break;
+    }
+}
+
 __device__ __forceinline__ float act_apply(int act, float x) {
     switch (act) {
-        case RF_ACT_GELU: return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
-        case RF_ACT_RELU: return x > 0.f ? x : 0.f;
-        case RF_ACT_SELU: {
-            const float alpha = 1.6732632423543772848170429916717f, scale = 1.0507009873554804934193349852946f;
-            return x > 0.f ? scale * x : scale * alpha * (expf(x) - 1.0f);
-        }
+        case RF_ACT_GELU: return gelu_erf(x);
+        case RF_ACT_RELU: return ActRelu{}(x);
+        case RF_ACT_SELU: return ActSelu{}(x);
         default: return x;
     }
 }
@@ -363,19 +401,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
         __syncthreads();
     }
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+    with_act(act, [&](auto A) {
 #pragma unroll
-    for (int j = 0; j < FR; ++j) {
-        const int col = n0 + wn * WT + j * 16 + lr;
-        if (col >= N) continue;
-        const float bv = bias ? bias[col] : 0.f;
+        for (int j = 0; j < FR; ++j) {
+            const int col = n0 + wn * WT + j * 16 + lr;
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
-        for (int i = 0; i < FR; ++i)
+            for (int i = 0; i < FR; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = m0 + wm * WT + i * 16 + lg * 4 + r;
-                if (row < M) y[row * ldy + col] = act_apply(act, acc[i][j][r] + bv);
-            }
-    }
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t row = m0 + wm * WT + i * 16 + lg * 4 + r;
+                    if (row < M) y[row * ldy + col] = A(acc[i][j][r] + bv);
+                }
+        }
+    });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -486,19 +526,21 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[h][i], bfr[h][j], acc[i][j], 0, 0, 0);
     }
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+    with_act(act, [&](auto A) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-        const int col = n0 + wn * TN + j * 16 + lr;
-        if (col >= N) continue;
-        const float bv = bias ? bias[col] : 0.f;
+        for (int j = 0; j < FN; ++j) {
+            const int col = n0 + wn * TN + j * 16 + lr;
+            if (col >= N) continue;
+            const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+            for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                if (row < M) y[row * ldy + col] = act_apply(act, acc[i][j][r] + bv);
-            }
-    }
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                    if (row < M) y[row * ldy + col] = A(acc[i][j][r] + bv);
+                }
+        }
+    });
 }
 
 template <int BM>
@@ -609,52 +651,82 @@ __global__ __launch_bounds__(256) void dense_head_kernel(const float* __restrict
 
 // ---------------------------------------------------------------------------------------------
 // Two-layer create_mlp on a narrow input, one launch (the ESIM input_mlp: 16 -> 256 -> 512, LayerNorm,
-// gelu; esim.py:45-48, mlp.py:4-15): per workgroup 16 rows,
-//   LN0 (K0 <= 32 columns, one 4-lane group per row) -> bf16 A tile in LDS (k padded to 32 with zeros)
-//   H = gelu(A W0^T + b0): one 16x16x32 MFMA per 16-column tile (W0 staged in LDS, k padded)
-//   LN1 over H's columns (row partials reduced in lanes, then across the 4 waves through LDS)
-//   -> bf16 tile in LDS; O = gelu(LN1(H) W1^T + b1): W1 fragments straight from global (L2) with the
-//   next k-step's fragments in flight; fp32 stores into the caller's strided output.
+// gelu; esim.py:45-48, mlp.py:4-15). A workgroup owns 64 rows x 128 output columns (grid: row blocks x
+// column blocks, 256 workgroups at cfg3), so W1 is read once per workgroup into LDS instead of once per
+// 16 rows from L2:
+//   W1[c0 .. c0+127][:] loads are issued first (registers), then LN0 (K0 <= 32 columns, a 4-lane group
+//   per row, each wave its 16 rows) -> bf16 A tile in LDS (k zero-padded to 32), W0 and the W1 slice
+//   -> LDS;
+//   H = act(A W0^T + b0): wave w computes its 16 rows x all H columns (one 16x16x32 MFMA per column
+//   tile), LN1 over the row entirely inside the wave (16-lane shuffles) -> bf16 rows in LDS
+//   (the layer-0 work is repeated by the O/128 column blocks of a row block: 16 x 256 x 32 per row);
+//   O = act(LN1(H) W1^T + b1) for the wave's 16 rows x the block's 128 columns, fp32 stores into the
+//   caller's strided output.
 // ---------------------------------------------------------------------------------------------
-constexpr int kMlp2Rows = 16;
+constexpr int kMlp2Rows = 64, kMlp2Cols = 128;
 
 template <int H>
+constexpr size_t mlp2_lds_bytes() {
+    return 2 * ((size_t)kMlp2Rows * 40 + (size_t)H * 32 + (size_t)kMlp2Rows * (H + 8) + (size_t)kMlp2Cols * H) +
+           4 * (3 * (size_t)H + kMlp2Cols);
+}
+
+// VEC0: K0 % 8 == 0 and H * K0 * 2 a multiple of 1 KiB, so W0 moves by LDS-DMA as it lies in memory.
+template <int H, bool VEC0>
 __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict__ x, int64_t M, int K0, int64_t ldx, float eps,
                                                          const float* __restrict__ g0, const float* __restrict__ be0,
                                                          const uint16_t* __restrict__ W0, const float* __restrict__ b0,
                                                          const float* __restrict__ g1, const float* __restrict__ be1,
                                                          const uint16_t* __restrict__ W1, const float* __restrict__ b1,
                                                          int O, int act, float* __restrict__ out, int64_t ldo) {
-    constexpr int RS0 = 32 + 8, RSH = H + 8;  // LDS row strides (elements): 16-byte row pad
-    constexpr int T0 = H / 64;                // layer-0 column tiles per wave
-    __shared__ __attribute__((aligned(16))) uint16_t xs[kMlp2Rows * RS0];
-    __shared__ __attribute__((aligned(16))) uint16_t w0s[H * RS0];
-    __shared__ __attribute__((aligned(16))) uint16_t hs[kMlp2Rows * RSH];
-    __shared__ float red[4][kMlp2Rows];
+    constexpr int RS0 = 32 + 8, RSH = H + 8;  // LDS row strides (elements) of the A tiles: 16-byte row pad
+    constexpr int T0 = H / 16;                // layer-0 column tiles (all of them, per wave)
+    constexpr int KS = H / 32;                // layer-1 k steps
+    constexpr int CPR = H / 8;                // 16-byte chunks per W1 row
+    constexpr int NI1 = kMlp2Cols * H * 2 / 1024;  // W1-slice LDS-DMA wave-instructions (1 KiB each)
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    uint16_t* xs = reinterpret_cast<uint16_t*>(smem_raw);
+    uint16_t* w0s = xs + kMlp2Rows * RS0;
+    uint16_t* hs = w0s + H * 32;
+    uint16_t* w1s = hs + kMlp2Rows * RSH;  // [128][H], chunk c of row r at chunk c ^ (r & 7)
+    float* pb0 = reinterpret_cast<float*>(w1s + kMlp2Cols * H);
+    float* pg1 = pb0 + H;
+    float* pbe1 = pg1 + H;
+    float* pb1 = pbe1 + H;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int64_t r0 = (int64_t)blockIdx.x * kMlp2Rows;
-    // ---- every small load issued up front (one round trip, not one per element) ----
-    // W0 -> LDS as 16-byte chunks (k zero-padded to 32): H rows x 4 chunks, 256 threads
-    uint4 w0c[H / 64];
-    const bool vec0 = (K0 & 7) == 0;
+    const int c0 = blockIdx.y * kMlp2Cols;
+    // ---- W1 slice and W0 straight into LDS (no registers, nothing for the compiler to sink) ----
 #pragma unroll
-    for (int i = 0; i < H / 64; ++i) {
-        const int c = tid + 256 * i, n = c >> 2, ch = c & 3;
-        w0c[i] = make_uint4(0, 0, 0, 0);
-        if (vec0 && 8 * ch < K0) w0c[i] = *reinterpret_cast<const uint4*>(W0 + (int64_t)n * K0 + 8 * ch);
+    for (int i = 0; i < NI1 / 4; ++i) {
+        const int g = wave + 4 * i, e = g * 64 + lane;  // chunk index in the LDS image
+        const int row = e / CPR, cp = e % CPR;
+        const int col = c0 + row < O ? c0 + row : O - 1;  // columns past O: any valid row (never stored)
+        const uint16_t* src = W1 + (int64_t)col * H + 8 * (cp ^ (row & 7));
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(w1s + g * 512), 16, 0, 0);
     }
-    float hb0[T0], hg1[T0], hbe1[T0];
-#pragma unroll
-    for (int t = 0; t < T0; ++t) {
-        const int n = (wave * T0 + t) * 16 + lr;
-        hb0[t] = b0 ? b0[n] : 0.f;
-        hg1[t] = g1 ? g1[n] : 1.f;
-        hbe1[t] = be1 ? be1[n] : 0.f;
+    if (VEC0) {
+        const int ni0 = H * K0 * 2 / 1024;
+        for (int g = wave; g < ni0; g += 4)
+            __builtin_amdgcn_global_load_lds(W0 + g * 512 + lane * 8, (__attribute__((address_space(3))) void*)(w0s + g * 512), 16, 0, 0);
     }
-    // LN0 operands: wave 0, row = lane >> 2, 4 lanes per row, columns k = 4 j + (lane & 3)
+    // ---- per-column parameters -> LDS (NULL bias / affine: 0 / 1); a dummy valid address, then a select ----
+    {
+        const int n = tid < H ? tid : H - 1;
+        const float vb0 = (b0 ? b0 : g0)[b0 ? n : 0], vg1 = (g1 ? g1 : g0)[g1 ? n : 0], vbe1 = (be1 ? be1 : g0)[be1 ? n : 0];
+        const int n1 = tid & (kMlp2Cols - 1), col = c0 + n1 < O ? c0 + n1 : O - 1;
+        const float vb1 = (b1 ? b1 : g0)[b1 ? col : 0];
+        if (tid < H) {
+            pb0[tid] = b0 ? vb0 : 0.f;
+            pg1[tid] = g1 ? vg1 : 1.f;
+            pbe1[tid] = be1 ? vbe1 : 0.f;
+        }
+        if (tid < kMlp2Cols) pb1[tid] = b1 ? vb1 : 0.f;
+    }
+    // ---- LN0: each wave its 16 rows, 4 lanes per row ----
     float xv[8], gv[8], bv[8];
-    const int xr = lane >> 2, sub = lane & 3;
-    if (wave == 0) {
+    const int xr = 16 * wave + (lane >> 2), sub = lane & 3;
+    {
         const int64_t row = r0 + xr < M ? r0 + xr : M - 1;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -664,21 +736,7 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             bv[j] = be0[k];
         }
     }
-    // ---- W0 tile ----
-    if (vec0) {
-#pragma unroll
-        for (int i = 0; i < H / 64; ++i) {
-            const int c = tid + 256 * i, n = c >> 2, ch = c & 3;
-            *reinterpret_cast<uint4*>(w0s + n * RS0 + 8 * ch) = w0c[i];
-        }
-    } else {
-        for (int i = tid; i < H * 32; i += 256) {
-            const int n = i >> 5, k = i & 31;
-            w0s[n * RS0 + k] = k < K0 ? W0[(int64_t)n * K0 + k] : (uint16_t)0;
-        }
-    }
-    // ---- LN0 ----
-    if (wave == 0) {
+    {
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -690,8 +748,10 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
         const float mu = s / (float)K0;
         float q = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (4 * j + sub < K0) q += (xv[j] - mu) * (xv[j] - mu);
+        for (int j = 0; j < 8; ++j) {
+            const float d = 4 * j + sub < K0 ? xv[j] - mu : 0.f;
+            q += d * d;
+        }
         q += __shfl_xor(q, 1, 64);
         q += __shfl_xor(q, 2, 64);
         const float rstd = 1.0f / sqrtf(q / (float)K0 + eps);
@@ -701,94 +761,91 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             xs[xr * RS0 + k] = k < K0 ? (uint16_t)f32_to_bf16_bits((xv[j] - mu) * rstd * gv[j] + bv[j]) : (uint16_t)0;
         }
     }
+    if (!VEC0) {  // W0 [H][K0] -> LDS [H][32], k zero-padded
+        for (int i = tid; i < H * 32; i += 256) {
+            const int n = i >> 5, k = i & 31;
+            w0s[n * 32 + k] = k < K0 ? W0[(int64_t)n * K0 + k] : (uint16_t)0;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
     __syncthreads();
-    // ---- layer 0: wave w owns column tiles w * T0 ..; one MFMA each (k = 32) ----
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xs + lr * RS0 + lg * 8);
+    // ---- layer 0 + LN1: this wave's 16 rows x all H columns ----
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xs + (16 * wave + lr) * RS0 + lg * 8);
     float hv[T0][4];
     float psum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < T0; ++t) {
-        const int n = (wave * T0 + t) * 16 + lr;
-        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(w0s + n * RS0 + lg * 8);
+        const int n = t * 16 + lr;
+        bf16x8 bw;
+        if (VEC0) {
+            const bool live = lg * 8 < K0;  // k chunk lg exists; else its A lanes are zero and B must be too
+            bw = *reinterpret_cast<const bf16x8*>(w0s + n * K0 + (live ? lg * 8 : 0));
+            if (!live) bw = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        } else {
+            bw = *reinterpret_cast<const bf16x8*>(w0s + n * 32 + lg * 8);
+        }
         const f4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const float bb = pb0[n];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            hv[t][r] = act_apply(act, c[r] + hb0[t]);
-            psum[r] += hv[t][r];
-        }
+        for (int r = 0; r < 4; ++r) hv[t][r] = c[r] + bb;
     }
-    // ---- LN1 statistics: rows 4 lg + r of this lane; sum over lanes lr, then over the 4 waves ----
-    auto row_total = [&](float (&p)[4], float (&tot)[4]) {
+    with_act(act, [&](auto A) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int t = 0; t < T0; ++t)
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) p[r] += __shfl_xor(p[r], o, 64);
-            if (lr == 0) red[wave][4 * lg + r] = p[r];
-        }
-        __syncthreads();
+            for (int r = 0; r < 4; ++r) hv[t][r] = A(hv[t][r]);
+    });
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 4 * lg + r;
-            tot[r] = (red[0][row] + red[1][row]) + (red[2][row] + red[3][row]);
-        }
-        __syncthreads();
-    };
-    float mu[4], var[4];
-    row_total(psum, mu);
-    float pq[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < T0; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) psum[r] += hv[t][r];
+    float mu[4], rstd[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        mu[r] /= (float)H;
 #pragma unroll
-        for (int t = 0; t < T0; ++t) pq[r] += (hv[t][r] - mu[r]) * (hv[t][r] - mu[r]);
+        for (int o = 1; o < 16; o <<= 1) psum[r] += __shfl_xor(psum[r], o, 64);
+        mu[r] = psum[r] / (float)H;
+        float q = 0.f;
+#pragma unroll
+        for (int t = 0; t < T0; ++t) q += (hv[t][r] - mu[r]) * (hv[t][r] - mu[r]);
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+        rstd[r] = 1.0f / sqrtf(q / (float)H + eps);
     }
-    row_total(pq, var);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float rstd = 1.0f / sqrtf(var[r] / (float)H + eps);
+    for (int t = 0; t < T0; ++t) {
+        const int n = t * 16 + lr;
+        const float gg = pg1[n], bb = pbe1[n];
 #pragma unroll
-        for (int t = 0; t < T0; ++t) {
-            const int n = (wave * T0 + t) * 16 + lr;
-            hs[(4 * lg + r) * RSH + n] = (uint16_t)f32_to_bf16_bits((hv[t][r] - mu[r]) * rstd * hg1[t] + hbe1[t]);
-        }
+        for (int r = 0; r < 4; ++r)
+            hs[(16 * wave + 4 * lg + r) * RSH + n] = (uint16_t)f32_to_bf16_bits((hv[t][r] - mu[r]) * rstd[r] * gg + bb);
     }
     __syncthreads();
-    // ---- layer 1: O columns in 16-wide tiles, wave w takes tiles w, w + 4, ...; the next tile's W1
-    // fragments (from L2) are in flight while this tile's MFMAs run ----
-    constexpr int KS = H / 32;
+    // ---- layer 1: this wave's 16 rows x the block's 128 columns ----
     bf16x8 ha[KS];
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) ha[kk] = *reinterpret_cast<const bf16x8*>(hs + lr * RSH + kk * 32 + lg * 8);
-    auto tile = [&](int nt, bf16x8 (&bw)[KS], float& bias1) {  // W1 fragments of column tile nt
-        const int n = nt * 16 + lr < O ? nt * 16 + lr : O - 1;
-        const uint16_t* wrow = W1 + (int64_t)n * H + lg * 8;
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) bw[kk] = *reinterpret_cast<const bf16x8*>(wrow + kk * 32);
-        bias1 = b1 ? b1[n] : 0.f;
-    };
-    auto finish = [&](int nt, const bf16x8 (&bw)[KS], float bias1) {
-        f4 c = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[kk], bw[kk], c, 0, 0, 0);
-        const int n = nt * 16 + lr;
-        if (n < O) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = r0 + 4 * lg + r;
-                if (row < M) out[row * ldo + n] = act_apply(act, c[r] + bias1);
+    for (int kk = 0; kk < KS; ++kk) ha[kk] = *reinterpret_cast<const bf16x8*>(hs + (16 * wave + lr) * RSH + kk * 32 + lg * 8);
+    with_act(act, [&](auto A) {
+    #pragma unroll
+        for (int nt = 0; nt < kMlp2Cols / 16; ++nt) {
+            const int rr = nt * 16 + lr;
+            f4 c = f4{0.f, 0.f, 0.f, 0.f};
+    #pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                const bf16x8 bw = *reinterpret_cast<const bf16x8*>(w1s + rr * H + 8 * ((kk * 4 + lg) ^ (rr & 7)));
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[kk], bw, c, 0, 0, 0);
+            }
+            const int n = c0 + rr;
+            const float bb = pb1[rr];
+            if (n < O) {
+    #pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t row = r0 + 16 * wave + 4 * lg + r;
+                    if (row < M) out[row * ldo + n] = A(c[r] + bb);
+                }
             }
         }
-    };
-    // two tiles per step (nt, nt + 4): both tiles' fragments are in flight together
-    for (int nt = wave; nt * 16 < O; nt += 8) {
-        bf16x8 bwa[KS], bwb[KS];
-        float ba = 0.f, bb = 0.f;
-        const bool second = (nt + 4) * 16 < O;
-        tile(nt, bwa, ba);
-        if (second) tile(nt + 4, bwb, bb);
-        finish(nt, bwa, ba);
-        if (second) finish(nt + 4, bwb, bb);
-    }
+    });
 }
 
 }  // namespace
@@ -804,14 +861,16 @@ extern "C" int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t 
     if (M == 0) return RF_OK;
     RF_REQUIRE(x && W0 && W1 && out && ln0_gamma && ln0_beta, "rf_mlp2_small_fwd: null pointer");
     RF_REQUIRE(((uintptr_t)W1 & 15) == 0 && ((uintptr_t)W0 & 15) == 0, "rf_mlp2_small_fwd: W0 / W1 must be 16-byte aligned");
-    const unsigned grid = (unsigned)((M + kMlp2Rows - 1) / kMlp2Rows);
+    const dim3 grid((unsigned)((M + kMlp2Rows - 1) / kMlp2Rows), (unsigned)((O + kMlp2Cols - 1) / kMlp2Cols));
     hipStream_t st = rf_stream(stream);
-    if (H == 256)
-        hipLaunchKernelGGL(mlp2_small_kernel<256>, dim3(grid), dim3(256), 0, st, x, M, K0, ldx, eps, ln0_gamma, ln0_beta,
-                           (const uint16_t*)W0, b0, ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, out, ldo);
-    else
-        hipLaunchKernelGGL(mlp2_small_kernel<128>, dim3(grid), dim3(256), 0, st, x, M, K0, ldx, eps, ln0_gamma, ln0_beta,
-                           (const uint16_t*)W0, b0, ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, out, ldo);
+    const bool vec0 = (K0 & 7) == 0 && (H * K0 * 2) % 1024 == 0;
+    auto kern = H == 256 ? (vec0 ? mlp2_small_kernel<256, true> : mlp2_small_kernel<256, false>)
+                         : (vec0 ? mlp2_small_kernel<128, true> : mlp2_small_kernel<128, false>);
+    const size_t lds = H == 256 ? mlp2_lds_bytes<256>() : mlp2_lds_bytes<128>();
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return rf_set_error(RF_EHIP, "mlp2_small_kernel: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, x, M, K0, ldx, eps, ln0_gamma, ln0_beta, (const uint16_t*)W0, b0,
+                       ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, out, ldo);
     return rf_check_launch("mlp2_small_kernel");
 }
 

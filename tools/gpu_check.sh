@@ -21,7 +21,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 if [ "${SKIP_PROF:-0}" != 1 ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- \
-      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --cpu-seconds 0 > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1
+      python3 "$GRAFT_REPO_ROOT/bench.py" ${PROF_ARGS:---cpu-seconds 0} > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$GRAFT_REPO_ROOT/$OUT/prof.log"
   find "$GRAFT_REPO_ROOT/$OUT/prof" -name "*stats*" | head
 fi
