@@ -292,38 +292,71 @@ struct GemmCfg {
     static constexpr int FR = BT / 32;                    // 16x16 fragments per wave and dimension
 };
 
-template <bool BF16, int BT>
-__device__ __forceinline__ void load_tile(uint4 (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], const char* __restrict__ x,
-                                          const char* __restrict__ w, int64_t M, int N, int K, int64_t ldx, int64_t m0,
-                                          int n0, int k0, int tid) {
+// The next k-step's tile loads are issued as inline asm: the compiler keeps volatile asm in program order,
+// so they go out before the MFMAs of the current step (as plain loads of read-only memory the DAG
+// scheduler places them right before their use, at the end of the step, and the latency is exposed every
+// step). The compiler does not track these loads: wait_tile waits for them (vmcnt) through the registers
+// themselves, so the LDS stores that consume them cannot move above the wait.
+using v4u = unsigned int __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4u gload_asm(const char* p) {
+    v4u r;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p));
+    return r;
+}
+
+// Rows past M / N read a valid row (M-1 / N-1) instead of branching: they only feed outputs that are never
+// stored. Only a K tail (KTAIL: K % BK != 0) needs zeros: the chunk's mask, applied after the wait.
+template <bool BF16, int BT, bool KTAIL>
+__device__ __forceinline__ void load_tile(v4u (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], uint32_t (&msk)[(GemmCfg<BF16, BT>::PER_THREAD)],
+                                          const char* __restrict__ x, const char* __restrict__ w, int64_t M, int N, int K,
+                                          int64_t ldx, int64_t m0, int n0, int k0, int tid) {
     using C = GemmCfg<BF16, BT>;
 #pragma unroll
     for (int i = 0; i < C::PER_THREAD; ++i) {
         const int c = tid + i * 256;
         const int r = c / C::CPR, ch = c - r * C::CPR;
         const int kk = k0 + ch * C::EPC;
-        uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-        if (m0 + r < M && kk < K) va = *reinterpret_cast<const uint4*>(x + ((m0 + r) * ldx + kk) * C::ESZ);
-        if (n0 + r < N && kk < K) vb = *reinterpret_cast<const uint4*>(w + ((int64_t)(n0 + r) * K + kk) * C::ESZ);
-        rg[0][i] = va;
-        rg[1][i] = vb;
+        const int64_t row = m0 + r < M ? m0 + r : M - 1;
+        const int64_t col = n0 + r < N ? n0 + r : N - 1;
+        int kc = kk;
+        if constexpr (KTAIL) {
+            msk[i] = kk < K ? 0xffffffffu : 0u;
+            kc = kk < K ? kk : K - C::EPC;
+        }
+        rg[0][i] = gload_asm(x + (row * ldx + kc) * C::ESZ);
+        rg[1][i] = gload_asm(w + (col * K + kc) * C::ESZ);
+    }
+}
+
+template <bool BF16, int BT, bool KTAIL>
+__device__ __forceinline__ void wait_tile(v4u (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], const uint32_t (&msk)[(GemmCfg<BF16, BT>::PER_THREAD)]) {
+    using C = GemmCfg<BF16, BT>;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < C::PER_THREAD; ++i) {
+        asm volatile("" : "+v"(rg[0][i]), "+v"(rg[1][i]));  // the registers are defined here, after the wait
+        if constexpr (KTAIL) {
+            rg[0][i] &= msk[i];
+            rg[1][i] &= msk[i];
+        }
     }
 }
 
 template <bool BF16, int BT>
 __device__ __forceinline__ void store_tile(char* __restrict__ As, char* __restrict__ Bs,
-                                           const uint4 (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], int tid) {
+                                           const v4u (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], int tid) {
     using C = GemmCfg<BF16, BT>;
 #pragma unroll
     for (int i = 0; i < C::PER_THREAD; ++i) {
         const int c = tid + i * 256;
         const int r = c / C::CPR, ch = c - r * C::CPR;
-        *reinterpret_cast<uint4*>(As + (r * C::RS + ch * C::EPC) * C::ESZ) = rg[0][i];
-        *reinterpret_cast<uint4*>(Bs + (r * C::RS + ch * C::EPC) * C::ESZ) = rg[1][i];
+        *reinterpret_cast<v4u*>(As + (r * C::RS + ch * C::EPC) * C::ESZ) = rg[0][i];
+        *reinterpret_cast<v4u*>(Bs + (r * C::RS + ch * C::EPC) * C::ESZ) = rg[1][i];
     }
 }
 
-template <bool BF16, int BT>
+template <bool BF16, int BT, bool KTAIL>
 __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
                                                    const float* __restrict__ bias, float* __restrict__ y, int64_t M,
                                                    int N, int K, int64_t ldx, int64_t ldy, int act) {
@@ -344,14 +377,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
     for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int j = 0; j < FR; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    uint4 rg[2][C::PER_THREAD];
+    v4u rg[2][C::PER_THREAD];
+    uint32_t msk[C::PER_THREAD];
     const int nk = (K + C::BK - 1) / C::BK;
-    load_tile<BF16, BT>(rg, x, w, M, N, K, ldx, m0, n0, 0, tid);
+    load_tile<BF16, BT, KTAIL>(rg, msk, x, w, M, N, K, ldx, m0, n0, 0, tid);
+    wait_tile<BF16, BT, KTAIL>(rg, msk);
     store_tile<BF16, BT>(smem[0][0], smem[0][1], rg, tid);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) load_tile<BF16, BT>(rg, x, w, M, N, K, ldx, m0, n0, (kt + 1) * C::BK, tid);
+        // the last step re-loads its own stage into the idle buffer: no branch around the loads
+        load_tile<BF16, BT, KTAIL>(rg, msk, x, w, M, N, K, ldx, m0, n0, (kt + 1 < nk ? kt + 1 : kt) * C::BK, tid);
         const char* As = smem[cur][0];
         const char* Bs = smem[cur][1];
         if constexpr (BF16) {
@@ -397,9 +433,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
                     }
         }
-        if (kt + 1 < nk) store_tile<BF16, BT>(smem[cur ^ 1][0], smem[cur ^ 1][1], rg, tid);
+        if (kt + 1 < nk) {  // its own block: the MFMAs above stay ahead of the wait
+            wait_tile<BF16, BT, KTAIL>(rg, msk);
+            store_tile<BF16, BT>(smem[cur ^ 1][0], smem[cur ^ 1][1], rg, tid);
+        }
         __syncthreads();
     }
+    wait_tile<BF16, BT, KTAIL>(rg, msk);  // the last step's spare loads land before their registers are reused
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
     with_act(act, [&](auto A) {
 #pragma unroll
@@ -1023,9 +1063,16 @@ extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t 
     const int64_t tiles = ((M + bt - 1) / bt) * ((N + bt - 1) / bt);
     RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_linear_fwd: too many tiles");
     const dim3 g((unsigned)tiles);
-    if (bf && small) hipLaunchKernelGGL((gemm_kernel<true, 64>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
-    else if (bf) hipLaunchKernelGGL((gemm_kernel<true, 128>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
-    else if (small) hipLaunchKernelGGL((gemm_kernel<false, 64>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
-    else hipLaunchKernelGGL((gemm_kernel<false, 128>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act);
+    const bool ktail = K % (bf ? BKH : BKF) != 0;
+#define RF_GEMM(BF, BT_)                                                                                              \
+    do {                                                                                                             \
+        if (ktail) hipLaunchKernelGGL((gemm_kernel<BF, BT_, true>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act); \
+        else hipLaunchKernelGGL((gemm_kernel<BF, BT_, false>), g, dim3(256), 0, st, x, W, b, y, M, N, K, ldx, ldy, act); \
+    } while (0)
+    if (bf && small) RF_GEMM(true, 64);
+    else if (bf) RF_GEMM(true, 128);
+    else if (small) RF_GEMM(false, 64);
+    else RF_GEMM(false, 128);
+#undef RF_GEMM
     return rf_check_launch("gemm_kernel");
 }
