@@ -1058,7 +1058,9 @@ extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t 
         const char* e = getenv("RF_GEMM_BT");
         return e ? atoi(e) : 0;
     }();
-    const bool small = force_bt ? force_bt == 64 : tiles128 < 512;
+    // bf16: 64-tiles below two 128-tiles per CU; fp32 (4x the MFMA cycles per byte staged): 128-tiles from one
+    // per CU (profiles/r02/gemm_ab2.txt: 8704 -> 1024 at M = 4096, 108 -> 116 TFLOP/s)
+    const bool small = force_bt ? force_bt == 64 : tiles128 < (bf ? 512 : 256);
     const int bt = small ? 64 : 128;
     const int64_t tiles = ((M + bt - 1) / bt) * ((N + bt - 1) / bt);
     RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_linear_fwd: too many tiles");

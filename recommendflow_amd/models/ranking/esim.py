@@ -46,13 +46,30 @@ class Esim(torch.nn.Module):
                                   seed=seed + 30, device=device)
 
     def forward(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor) -> torch.Tensor:
+        """The input MLP (dense features only) runs on a side stream, concurrently with the two encoders and
+        the attention: it is a latency-bound launch of 256 workgroups that the encoders' tails leave room
+        for. It writes pooled[:, :d_emb], the attention pooled[:, d_emb:]; the output MLP waits for both
+        (also inside a hipGraph capture: the fork/join become graph edges)."""
         B = user.batch
+        cur = torch.cuda.current_stream(dense.device)
+        pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=dense.device)
+        side = self._side_stream(dense.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self.input_mlp(dense, out=pooled[:, : self.d_emb])
+        pooled.record_stream(side)
+        dense.record_stream(side)
         q = self.enc_q(user).view(B, self.L, self.d)
         a = self.enc_a(ad).view(B, self.L, self.d)
-        pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=q.device)
-        self.input_mlp(dense, out=pooled[:, : self.d_emb])
         esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
+        cur.wait_stream(side)
         return self.dense_output(self.output_mlp(pooled))
+
+    def _side_stream(self, device):
+        s = getattr(self, "_side", None)
+        if s is None or s.device != device:
+            s = self._side = torch.cuda.Stream(device=device)
+        return s
 
     def graphed(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor, **kw):
         """This forward captured as one hipGraph on static copies of (user, ad, dense) (runtime.graphs):
