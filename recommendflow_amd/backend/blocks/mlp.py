@@ -1,7 +1,8 @@
 """create_mlp (reference: backend/blocks/mlp.py:4-15): per hidden size  Norm -> Dense(act) -> Dropout.
 
 Dropout is the identity at inference. Each layer runs rf_norm_fwd (fp32 -> MFMA operand dtype) then
-rf_linear_fwd (MFMA GEMM with bias + activation fused in the epilogue).
+rf_linear_fwd (MFMA GEMM with bias + activation fused in the epilogue); an fp32 layer behind a
+BatchNormalization runs as ONE GEMM with the normalisation folded into its weights (MLP._bn_folded).
 """
 from __future__ import annotations
 
@@ -51,9 +52,37 @@ class MLP(torch.nn.Module):
             return self._forward_fused(x, out, stream)
         last = len(self.denses) - 1
         for i, (norm, dense) in enumerate(zip(self.norms, self.denses)):
+            o = out if i == last else None
+            if norm is not None and norm.mode == 1 and self.dtype == torch.float32 and x.dtype == torch.float32:
+                w, b = self._bn_folded(i)  # no normalisation pass: BatchNorm lives in the weights
+                x = dense.forward_with(x, w, b, out=o, stream=stream)
+                continue
             h = norm(x, out_dtype=self.dtype, stream=stream) if norm is not None else x
-            x = dense(h, out=out if i == last else None, stream=stream)
+            x = dense(h, out=o, stream=stream)
         return x
+
+    def _bn_folded(self, i: int):
+        """denses[i] with norms[i] folded in, for fp32 layers. BatchNormalization at inference is a per-column
+        affine x a + c (a = gamma / sqrt(var + eps), c = beta - mean a), so
+            BN(x) W^T + b = x (W diag(a))^T + (W c + b)
+        and the GEMM reads the raw activations: the [M, K] normalisation pass (and its HBM round trip)
+        disappears. Cached until a parameter changes (tensor identity or in-place version)."""
+        n, d = self.norms[i], self.denses[i]
+        ts = (d.weight, d.bias, n.gamma, n.beta, n.mean, n.var)
+        key = tuple((id(t), t._version) if t is not None else None for t in ts) + (n.eps,)
+        cache = getattr(self, "_fold_cache", None)
+        if cache is None:
+            cache = self._fold_cache = {}
+        hit = cache.get(i)
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
+        a = n.gamma.double() / torch.sqrt(n.var.double() + n.eps)
+        c = n.beta.double() - n.mean.double() * a
+        w64 = d.weight.double()
+        w = (w64 * a[None, :]).to(d.dtype).contiguous()
+        b = (w64 @ c + (d.bias.double() if d.bias is not None else 0.0)).float().contiguous()
+        cache[i] = (key, w, b)
+        return w, b
 
     def _fusable(self, x: torch.Tensor) -> bool:
         return (len(self.denses) == 2 and self.dtype == torch.bfloat16 and x.dtype == torch.float32

@@ -69,6 +69,23 @@ class Dense(torch.nn.Module):
         return out
 
 
+    def forward_with(self, x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                     out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """This layer's GEMM + activation with substitute parameters ([N][K] weight of this layer's dtype,
+        fp32 bias): the path MLP takes with a normalisation folded into the weights."""
+        if x.dtype != self.dtype:
+            x = x.to(self.dtype)
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty((M, self.units), dtype=torch.float32, device=self.weight.device)
+        L.call("rf_linear_fwd", L.ptr(x), L.torch_dtype_code(self.dtype), M, self.in_features, x.stride(0),
+               L.ptr(weight), self.units, L.ptr(bias), L.ACT[self.activation], L.ptr(out), out.stride(0),
+               L.stream_ptr(stream))
+        return out
+
+
 class LayerNormalization:
     mode = 0
 

@@ -186,6 +186,32 @@ def test_create_mlp(O, cuda, norm):
     np.testing.assert_allclose(y, want, rtol=1e-4, atol=1e-5)
 
 
+def test_mlp_batchnorm_folded_into_fp32_dense(O, cuda):
+    """fp32 layers behind a BatchNormalization run as one GEMM with the normalisation folded into the weights
+    (MLP._bn_folded): against float64 BN -> Dense with non-trivial statistics, and again after the BN
+    parameters change in place (the fold cache must notice)."""
+    mlp = create_mlp([96, 40], 0.3, "selu", BatchNormalization(epsilon=1e-3), in_features=200, dtype=torch.float32, seed=5)
+    g = torch.Generator().manual_seed(11)
+    x = rnd((70, 200), 12, 2.0, torch.float32)
+
+    def randomise():
+        for nm in mlp.norms:
+            nm.gamma.copy_(torch.rand(nm.width, generator=g) + 0.5)
+            nm.beta.copy_(torch.randn(nm.width, generator=g) * 0.3)
+            nm.mean.copy_(torch.randn(nm.width, generator=g) * 0.5)
+            nm.var.copy_(torch.rand(nm.width, generator=g) * 2 + 0.1)
+        for dn in mlp.denses:
+            dn.bias.copy_(torch.randn(dn.units, generator=g) * 0.1)
+
+    for _ in range(2):
+        randomise()
+        y = mlp(x.cuda()).cpu().numpy()
+        layers = [{"W": dn.weight.cpu().numpy().T, "b": dn.bias.cpu().numpy(), "gamma": nm.gamma.cpu().numpy(),
+                   "beta": nm.beta.cpu().numpy(), "mean": nm.mean.cpu().numpy(), "var": nm.var.cpu().numpy()}
+                  for nm, dn in zip(mlp.norms, mlp.denses)]
+        np.testing.assert_allclose(y, O.mlp(x.numpy(), layers, "selu", "bn", eps=1e-3), rtol=1e-4, atol=1e-5)
+
+
 @pytest.mark.parametrize("Lq,Lk,depth,heads", [(10, 10, 64, 2), (100, 100, 32, 4), (37, 200, 128, 1), (1, 5, 64, 3)])
 def test_sdpa_masked_rows(O, cuda, Lq, Lk, depth, heads):
     B = 3
