@@ -205,6 +205,28 @@ int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float 
                       int64_t ldo, void* stream);
 
 /*
+ * A create_mlp layer pair with the second layer's LayerNormalization folded across the GEMMs (mlp.py:10-13:
+ * Norm -> Dense(act) per hidden size; the reference normalises between the two Dense layers):
+ *   rf_linear_stats_fwd   y = act(x W^T + b) stored as BF16 [M][N] (row stride ldy), and row_stats
+ *                         [M][P][2], P = 4 * ceil(N / 128): partial (sum, sum of squares) of each row's fp32
+ *                         values per column slice, written by the GEMM's epilogue (no pass over y, no
+ *                         atomics: the fold sums the P partials in a fixed order, so results are
+ *                         deterministic).
+ *   rf_linear_lnfold_fwd  y = act(rstd_r (x Wg^T - mu_r s) + t) = act(LN(x) W^T + b) for the raw BF16 x of
+ *                         the previous call, with Wg = W diag(gamma) (BF16 [N][K]), s[c] = sum_k Wg[c][k],
+ *                         t[c] = sum_k W[c][k] beta[k] + b[c] (F32 [N]), mu_r = sum_r / K and
+ *                         rstd_r = 1 / sqrt(max(sumsq_r / K - mu_r^2, 0) + eps) from row_stats (the stats
+ *                         call's N is this call's K).
+ * Both: x BF16 [M][K] (16-byte aligned, ldx % 8 == 0), K >= 512 and K % 64 == 0 (the LDS-DMA GEMM),
+ * elementwise activations only. The pair replaces rf_norm_fwd -> rf_linear_fwd for the second layer.
+ */
+int rf_linear_stats_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t N, const float* b,
+                        int32_t act, void* y_bf16, int64_t ldy, float* row_stats, void* stream);
+int rf_linear_lnfold_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N, const float* s,
+                         const float* t, const float* row_stats, float eps, int32_t act, float* y, int64_t ldy,
+                         void* stream);
+
+/*
  * Small Dense head on fp32 activations  y = act(x @ W + b),  N <= 64 outputs (the ESIM scorer's
  * Dense(2, 'softmax'), esim.py:53,88): replaces rf_linear_fwd's small-N path when the activations are the
  * fp32 output of the previous layer (no bf16 round trip of x). x: F32 [M][K], row stride ldx, 16-byte

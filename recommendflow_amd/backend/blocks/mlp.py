@@ -51,15 +51,72 @@ class MLP(torch.nn.Module):
         if self._fusable(x):
             return self._forward_fused(x, out, stream)
         last = len(self.denses) - 1
-        for i, (norm, dense) in enumerate(zip(self.norms, self.denses)):
+        i = 0
+        while i <= last:
+            norm, dense = self.norms[i], self.denses[i]
             o = out if i == last else None
             if norm is not None and norm.mode == 1 and self.dtype == torch.float32 and x.dtype == torch.float32:
                 w, b = self._bn_folded(i)  # no normalisation pass: BatchNorm lives in the weights
                 x = dense.forward_with(x, w, b, out=o, stream=stream)
+                i += 1
                 continue
             h = norm(x, out_dtype=self.dtype, stream=stream) if norm is not None else x
+            if self._ln_pair_ok(i, h):
+                x = self._ln_pair(i, h, out if i + 1 == last else None, stream)
+                i += 2
+                continue
             x = dense(h, out=o, stream=stream)
+            i += 1
         return x
+
+    fold_ln = True  # set False to run every LayerNorm as its own pass (A/B and tests)
+
+    def _ln_pair_ok(self, i: int, h: torch.Tensor) -> bool:
+        """Layers i, i+1 as rf_linear_stats_fwd -> rf_linear_lnfold_fwd: bf16 GEMMs on the LDS-DMA path
+        (K >= 512, K % 64 == 0 for both), a LayerNorm in front of layer i+1, an elementwise activation."""
+        if not self.fold_ln or i + 1 >= len(self.denses) or self.dtype != torch.bfloat16 or self.activation == "softmax":
+            return False
+        n1 = self.norms[i + 1]
+        k0, k1 = self.denses[i].in_features, self.denses[i + 1].in_features
+        return (n1 is not None and n1.mode == 0 and k0 >= 512 and k0 % 64 == 0 and k1 >= 512 and k1 % 64 == 0
+                and h.dtype == torch.bfloat16 and h.dim() == 2 and h.stride(-1) == 1 and h.stride(0) % 8 == 0
+                and h.data_ptr() % 16 == 0)
+
+    def _ln_pair(self, i, h, out, stream):
+        """act(LN(act(h W0^T + b0)) W1^T + b1) without the LayerNorm pass: the first GEMM writes its output
+        as bf16 plus per-row (sum, sum of squares) from its epilogue, the second applies the normalisation
+        after the product (W1 diag(gamma) and the per-column terms from _ln_folded)."""
+        d0, d1, n1 = self.denses[i], self.denses[i + 1], self.norms[i + 1]
+        M = h.shape[0]
+        yb = torch.empty((M, d0.units), dtype=torch.bfloat16, device=h.device)
+        st = torch.empty((M, 4 * ((d0.units + 127) // 128), 2), dtype=torch.float32, device=h.device)
+        L.call("rf_linear_stats_fwd", L.ptr(h), M, d0.in_features, h.stride(0), L.ptr(d0.weight), d0.units,
+               L.ptr(d0.bias), L.ACT[self.activation], L.ptr(yb), yb.stride(0), L.ptr(st), L.stream_ptr(stream))
+        wg, sv, tv = self._ln_folded(i + 1)
+        if out is None:
+            out = torch.empty((M, d1.units), dtype=torch.float32, device=h.device)
+        L.call("rf_linear_lnfold_fwd", L.ptr(yb), M, d1.in_features, yb.stride(0), L.ptr(wg), d1.units, L.ptr(sv),
+               L.ptr(tv), L.ptr(st), n1.eps, L.ACT[self.activation], L.ptr(out), out.stride(0), L.stream_ptr(stream))
+        return out
+
+    def _ln_folded(self, i: int):
+        """(W diag(gamma) in bf16, s = its row sums, t = W beta + b) of denses[i] behind LayerNorm norms[i];
+        cached until a parameter changes (tensor identity or in-place version)."""
+        n, d = self.norms[i], self.denses[i]
+        ts = (d.weight, d.bias, n.gamma, n.beta)
+        key = ("ln",) + tuple((id(t), t._version) if t is not None else None for t in ts)
+        cache = getattr(self, "_fold_cache", None)
+        if cache is None:
+            cache = self._fold_cache = {}
+        hit = cache.get(("ln", i))
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        w64 = d.weight.double()
+        wg = (w64 * n.gamma.double()[None, :]).to(torch.bfloat16).contiguous()
+        sv = wg.double().sum(dim=1).float().contiguous()
+        tv = (w64 @ n.beta.double() + (d.bias.double() if d.bias is not None else 0.0)).float().contiguous()
+        cache[("ln", i)] = (key, (wg, sv, tv))
+        return wg, sv, tv
 
     def _bn_folded(self, i: int):
         """denses[i] with norms[i] folded in, for fp32 layers. BatchNormalization at inference is a per-column

@@ -496,10 +496,30 @@ __device__ __forceinline__ void glds_stage(const uint16_t* __restrict__ x, const
     }
 }
 
-template <int BM>
+// Epilogue variants of gemm_lds_kernel (the LayerNorm of the next layer folded across the pair):
+//   kEpiPlain  y = act(acc + b), fp32
+//   kEpiStats  y = act(acc + b) stored as bf16, and every row's (sum, sum of squares) of the fp32 values
+//              over the wave's columns written to stats[row][p] (p = column tile * 4 + wave column; 16-lane
+//              shuffle reduce); no atomics, so the reduction order (and the result) is fixed
+//   kEpiLnFold y = act(rstd_r (acc - mu_r s_c) + t_c): acc = x W'^T with x the previous layer's raw bf16
+//              output and W' = W diag(gamma); mu_r, rstd_r from stats over the K columns; s_c = sum_k W'[c][k],
+//              t_c = W beta + b. That is LN(x) W^T + b with the normalisation applied after the product.
+//              The workgroup first reduces its rows' P partials in a fixed order into LDS.
+enum { kEpiPlain = 0, kEpiStats = 1, kEpiLnFold = 2 };
+
+struct EpiArgs {
+    uint16_t* yb;        // kEpiStats output
+    float* stats;        // kEpiStats: accumulated; kEpiLnFold: read
+    const float* fs;     // kEpiLnFold s_c
+    const float* ft;     // kEpiLnFold t_c
+    float eps;
+    int P;               // partials per row (4 per 128-column tile of the stats GEMM)
+};
+
+template <int BM, int EPI = kEpiPlain>
 __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                        const float* __restrict__ bias, float* __restrict__ y, int64_t M,
-                                                       int N, int K, int64_t ldx, int64_t ldy, int act) {
+                                                       int N, int K, int64_t ldx, int64_t ldy, int act, EpiArgs ea) {
     constexpr int WM = BM == 128 ? 2 : 1, WN = 4 / WM;            // wave grid
     constexpr int TM = BM / WM, TN = kLdsBN / WN;                  // wave tile
     constexpr int FM = TM / 16, FN = TN / 16;                      // fragments per wave
@@ -566,21 +586,113 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[h][i], bfr[h][j], acc[i][j], 0, 0, 0);
     }
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
-    with_act(act, [&](auto A) {
+    if constexpr (EPI == kEpiPlain) {
+        with_act(act, [&](auto A) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            const int col = n0 + wn * TN + j * 16 + lr;
-            if (col >= N) continue;
-            const float bv = bias ? bias[col] : 0.f;
+            for (int j = 0; j < FN; ++j) {
+                const int col = n0 + wn * TN + j * 16 + lr;
+                if (col >= N) continue;
+                const float bv = bias ? bias[col] : 0.f;
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
+                for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                    if (row < M) y[row * ldy + col] = A(acc[i][j][r] + bv);
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                        if (row < M) y[row * ldy + col] = A(acc[i][j][r] + bv);
+                    }
+            }
+        });
+    } else if constexpr (EPI == kEpiStats) {
+        float rs[FM][4], rq[FM][4];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rs[i][r] = rq[i][r] = 0.f;
+        with_act(act, [&](auto A) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int col = n0 + wn * TN + j * 16 + lr;
+                const bool cok = col < N;
+                const float bv = bias && cok ? bias[col] : 0.f;
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                        const float v = A(acc[i][j][r] + bv);
+                        if (cok) {
+                            rs[i][r] += v;
+                            rq[i][r] += v * v;
+                            if (row < M) ea.yb[row * ldy + col] = (uint16_t)f32_to_bf16_bits(v);
+                        }
+                    }
+            }
+        });
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    rs[i][r] += __shfl_xor(rs[i][r], o, 64);
+                    rq[i][r] += __shfl_xor(rq[i][r], o, 64);
                 }
+                const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                if (lr == 0 && row < M)
+                    *reinterpret_cast<float2*>(ea.stats + 2 * (row * ea.P + (n0 / kLdsBN) * 4 + wn)) = make_float2(rs[i][r], rq[i][r]);
+            }
+    } else {  // kEpiLnFold
+        // the tile's rows: P partials each, summed in a fixed order (TPR threads per row, each a strided
+        // subset, then a commutative shuffle combine that gives every lane the same bits) -> LDS
+        constexpr int TPR = 256 / BM;
+        float* srow = reinterpret_cast<float*>(smem_raw);
+        __syncthreads();  // every wave is done with the LDS ring
+        {
+            const int rl = tid / TPR, part = tid % TPR;
+            const int64_t row = m0 + rl < M ? m0 + rl : M - 1;
+            float s1 = 0.f, s2 = 0.f;
+            for (int p = part; p < ea.P; p += TPR) {
+                const float2 v = *reinterpret_cast<const float2*>(ea.stats + 2 * (row * ea.P + p));
+                s1 += v.x;
+                s2 += v.y;
+            }
+#pragma unroll
+            for (int o = 1; o < TPR; o <<= 1) {
+                s1 += __shfl_xor(s1, o, 64);
+                s2 += __shfl_xor(s2, o, 64);
+            }
+            if (part == 0) {
+                const float m = s1 / (float)K;
+                srow[2 * rl] = m;
+                srow[2 * rl + 1] = 1.0f / sqrtf(fmaxf(s2 / (float)K - m * m, 0.f) + ea.eps);
+            }
         }
-    });
+        __syncthreads();
+        float mu[FM][4], rstd[FM][4];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rl = wm * TM + i * 16 + lg * 4 + r;
+                mu[i][r] = srow[2 * rl];
+                rstd[i][r] = srow[2 * rl + 1];
+            }
+        with_act(act, [&](auto A) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int col = n0 + wn * TN + j * 16 + lr;
+                if (col >= N) continue;
+                const float sc = ea.fs[col], tc = ea.ft[col];
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                        if (row < M) y[row * ldy + col] = A(rstd[i][r] * (acc[i][j][r] - mu[i][r] * sc) + tc);
+                    }
+            }
+        });
+    }
 }
 
 template <int BM>
@@ -999,6 +1111,67 @@ extern "C" int rf_norm_fwd(const float* x, int64_t rows, int32_t cols, int64_t l
     return rf_check_launch("norm_kernel");
 }
 
+namespace {
+// Launches gemm_lds_kernel<BM, EPI> with the tile choice of rf_linear_fwd's LDS path.
+template <int EPI>
+int launch_lds_epi(const void* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t N, const float* b, int32_t act,
+                   float* y, int64_t ldy, const EpiArgs& ea, hipStream_t st, const char* who) {
+    const int64_t t128 = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
+    const bool big = t128 >= 512;
+    const int64_t tiles = big ? t128 : ((M + 63) / 64) * ((N + kLdsBN - 1) / kLdsBN);
+    RF_REQUIRE(tiles < (int64_t)1 << 31, "%s: too many tiles", who);
+    if (big) {
+        auto kern = gemm_lds_kernel<128, EPI>;
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<128>());
+        if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea);
+    } else {
+        auto kern = gemm_lds_kernel<64, EPI>;
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64>());
+        if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea);
+    }
+    return rf_check_launch(who);
+}
+}  // namespace
+
+extern "C" int rf_linear_stats_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t N, const float* b,
+                                   int32_t act, void* y_bf16, int64_t ldy, float* row_stats, void* stream) {
+    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_linear_stats_fwd: activation must be elementwise");
+    RF_REQUIRE(M >= 0 && N > 0 && K >= 512 && K % 64 == 0 && ldx >= K && ldx % 8 == 0 && ldy >= N,
+               "rf_linear_stats_fwd: needs K >= 512, K %% 64 == 0, ldx %% 8 == 0");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && W && y_bf16 && row_stats, "rf_linear_stats_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0, "rf_linear_stats_fwd: x/W must be 16-byte aligned");
+    hipStream_t st = rf_stream(stream);
+    const int P = 4 * ((N + kLdsBN - 1) / kLdsBN);
+    const hipError_t e = hipMemsetAsync(row_stats, 0, (size_t)M * P * 2 * sizeof(float), st);  // slots a tile shape leaves unused
+    if (e != hipSuccess) return rf_set_error(RF_EHIP, "rf_linear_stats_fwd: %s", hipGetErrorString(e));
+    EpiArgs ea{};
+    ea.yb = static_cast<uint16_t*>(y_bf16);
+    ea.stats = row_stats;
+    ea.P = P;
+    return launch_lds_epi<kEpiStats>(x, M, K, ldx, W, N, b, act, nullptr, ldy, ea, st, "rf_linear_stats_fwd");
+}
+
+extern "C" int rf_linear_lnfold_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
+                                    const float* s, const float* t, const float* row_stats, float eps, int32_t act,
+                                    float* y, int64_t ldy, void* stream) {
+    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_linear_lnfold_fwd: activation must be elementwise");
+    RF_REQUIRE(M >= 0 && N > 0 && K >= 512 && K % 64 == 0 && ldx >= K && ldx % 8 == 0 && ldy >= N,
+               "rf_linear_lnfold_fwd: needs K >= 512, K %% 64 == 0, ldx %% 8 == 0");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && Wg && s && t && row_stats && y, "rf_linear_lnfold_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)Wg & 15) == 0, "rf_linear_lnfold_fwd: x/W must be 16-byte aligned");
+    EpiArgs ea{};
+    ea.stats = const_cast<float*>(row_stats);
+    ea.fs = s;
+    ea.ft = t;
+    ea.eps = eps;
+    ea.P = 4 * ((K + kLdsBN - 1) / kLdsBN);  // the stats call's N is this call's K
+    return launch_lds_epi<kEpiLnFold>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, rf_stream(stream), "rf_linear_lnfold_fwd");
+}
+
 extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,
                              int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream) {
     RF_REQUIRE(x_dtype == RF_DTYPE_BF16 || x_dtype == RF_DTYPE_F32, "rf_linear_fwd: x dtype must be BF16 or F32");
@@ -1044,12 +1217,12 @@ extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t 
             auto kern = gemm_lds_kernel<128>;
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<128>());
             if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel: %s", hipGetErrorString(e));
-            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act);
+            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, EpiArgs{});
         } else {
             auto kern = gemm_lds_kernel<64>;
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64>());
             if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel: %s", hipGetErrorString(e));
-            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act);
+            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, EpiArgs{});
         }
         return rf_check_launch("gemm_lds_kernel");
     }

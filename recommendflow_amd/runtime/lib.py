@@ -34,6 +34,9 @@ _SIGS = {
     "rf_norm_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _vp]),
     "rf_linear_fwd": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
     "rf_dense_head_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i32, _vp, _i32, _vp, _i64, _vp]),
+    "rf_linear_stats_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _i64, _vp, _vp]),
+    "rf_linear_lnfold_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _f32, _i32, _vp, _i64,
+                                            _vp]),
     "rf_mlp2_small_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32,
                                          _i32, _vp, _i64, _vp]),
     "rf_sdpa_fwd": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),

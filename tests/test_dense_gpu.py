@@ -234,3 +234,31 @@ def test_multi_head_attention_api(O, cuda):
     x = rnd((2, 20, 128), 8, 1.0, torch.float32).cuda()
     out = mha.call(x, x, x, None)
     assert tuple(out.shape) == (2, 20, 128) and torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("M", [300, 4096])
+def test_mlp_layernorm_folded_across_gemms(O, cuda, M):
+    """A bf16 LayerNorm MLP whose second LayerNorm is folded across the GEMM pair (rf_linear_stats_fwd ->
+    rf_linear_lnfold_fwd: row sums from the first GEMM's epilogue, the normalisation applied after the
+    second product): against float64 create_mlp at the unfused path's tolerance, and against the unfused
+    chain (LN -> bf16 -> GEMM) of the same module; cfg3's output-MLP shapes."""
+    mlp = create_mlp([1024, 512], 0.3, "gelu", LayerNormalization(epsilon=1e-6), in_features=1280, dtype=torch.bfloat16,
+                     seed=7)
+    g = torch.Generator().manual_seed(M)
+    for nm in mlp.norms:
+        nm.gamma.copy_(torch.rand(nm.width, generator=g) + 0.5)
+        nm.beta.copy_(torch.randn(nm.width, generator=g) * 0.2)
+    for dn in mlp.denses:
+        dn.bias.copy_(torch.randn(dn.units, generator=g) * 0.1)
+    x = (torch.randn(M, 1280, generator=g) * 1.5 + 0.3).cuda()
+    assert mlp._ln_pair_ok(0, mlp.norms[0](x))
+    y = mlp(x).cpu().numpy()
+    mlp.fold_ln = False
+    y_unfused = mlp(x).cpu().numpy()
+    params = [{"W": dn.weight.float().cpu().numpy().T, "b": dn.bias.cpu().numpy(), "gamma": nm.gamma.cpu().numpy(),
+               "beta": nm.beta.cpu().numpy()} for nm, dn in zip(mlp.norms, mlp.denses)]
+    want = O.mlp(x.cpu().numpy(), params, "gelu", "ln")
+    err_fold, err_unfused = np.abs(y - want).max(), np.abs(y_unfused - want).max()
+    np.testing.assert_allclose(y, want, rtol=2e-2, atol=2e-2)
+    np.testing.assert_allclose(y, y_unfused, rtol=2e-2, atol=2e-2)
+    assert err_fold <= 2 * err_unfused + 1e-3, (err_fold, err_unfused)
