@@ -277,8 +277,9 @@ __global__ __launch_bounds__(256) void ln_wide_kernel(const float* __restrict__ 
 // bf16: BK = 64 (128-byte rows), LDS rows padded to 72 elements (144 B): conflict-free ds_read_b128
 // for the 16 rows a 16-lane group reads.
 constexpr int BKH = 64, RSH = BKH + 8;
-// f32: BK = 32 (128-byte rows), rows padded to 36 floats (144 B).
-constexpr int BKF = 32, RSF = BKF + 4;
+// f32: BK = 64 (256-byte rows: half the k-steps, barriers and LDS round trips of BK = 32; 139 KiB of LDS
+// at BT = 128, one workgroup per CU), rows padded to 68 floats (272 B).
+constexpr int BKF = 64, RSF = BKF + 4;
 
 template <bool BF16, int BT>
 struct GemmCfg {
@@ -407,31 +408,34 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
         } else {
-            // 16x16x4 f32: lane (lr, lg) supplies A[lr][k], B[k][lr] for k = lg*8 + s at step s (the k order is
-            // permuted consistently for A and B, so the dot product is over all 32 k of the tile)
-            f4 a0[FR], a1[FR], b0[FR], b1[FR];
+            // 16x16x4 f32: lane (lr, lg) supplies A[lr][k], B[k][lr] for k = kh + lg*8 + s at step s (the k order
+            // is permuted consistently for A and B, so the dot product is over all 32 k of each half)
 #pragma unroll
-            for (int i = 0; i < FR; ++i) {
-                const float* p = reinterpret_cast<const float*>(As) + (wm * WT + i * 16 + lr) * C::RS + lg * 8;
-                a0[i] = *reinterpret_cast<const f4*>(p);
-                a1[i] = *reinterpret_cast<const f4*>(p + 4);
+            for (int kh = 0; kh < C::BK; kh += 32) {
+                f4 a0[FR], a1[FR], b0[FR], b1[FR];
+#pragma unroll
+                for (int i = 0; i < FR; ++i) {
+                    const float* p = reinterpret_cast<const float*>(As) + (wm * WT + i * 16 + lr) * C::RS + kh + lg * 8;
+                    a0[i] = *reinterpret_cast<const f4*>(p);
+                    a1[i] = *reinterpret_cast<const f4*>(p + 4);
+                }
+#pragma unroll
+                for (int j = 0; j < FR; ++j) {
+                    const float* p = reinterpret_cast<const float*>(Bs) + (wn * WT + j * 16 + lr) * C::RS + kh + lg * 8;
+                    b0[j] = *reinterpret_cast<const f4*>(p);
+                    b1[j] = *reinterpret_cast<const f4*>(p + 4);
+                }
+#pragma unroll
+                for (int s = 0; s < 8; ++s)
+#pragma unroll
+                    for (int i = 0; i < FR; ++i)
+#pragma unroll
+                        for (int j = 0; j < FR; ++j) {
+                            const float av = s < 4 ? a0[i][s] : a1[i][s - 4];
+                            const float bv = s < 4 ? b0[j][s] : b1[j][s - 4];
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
+                        }
             }
-#pragma unroll
-            for (int j = 0; j < FR; ++j) {
-                const float* p = reinterpret_cast<const float*>(Bs) + (wn * WT + j * 16 + lr) * C::RS + lg * 8;
-                b0[j] = *reinterpret_cast<const f4*>(p);
-                b1[j] = *reinterpret_cast<const f4*>(p + 4);
-            }
-#pragma unroll
-            for (int s = 0; s < 8; ++s)
-#pragma unroll
-                for (int i = 0; i < FR; ++i)
-#pragma unroll
-                    for (int j = 0; j < FR; ++j) {
-                        const float av = s < 4 ? a0[i][s] : a1[i][s - 4];
-                        const float bv = s < 4 ? b0[j][s] : b1[j][s - 4];
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i][j], 0, 0, 0);
-                    }
         }
         if (kt + 1 < nk) {  // its own block: the MFMAs above stay ahead of the wait
             wait_tile<BF16, BT, KTAIL>(rg, msk);
