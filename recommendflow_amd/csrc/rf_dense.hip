@@ -277,9 +277,10 @@ __global__ __launch_bounds__(256) void ln_wide_kernel(const float* __restrict__ 
 // bf16: BK = 64 (128-byte rows), LDS rows padded to 72 elements (144 B): conflict-free ds_read_b128
 // for the 16 rows a 16-lane group reads.
 constexpr int BKH = 64, RSH = BKH + 8;
-// f32: BK = 64 (256-byte rows: half the k-steps, barriers and LDS round trips of BK = 32; 139 KiB of LDS
-// at BT = 128, one workgroup per CU), rows padded to 68 floats (272 B).
-constexpr int BKF = 64, RSF = BKF + 4;
+// f32: BK = 32 (128-byte rows), rows padded to 36 floats (144 B). BK = 64 measured +3 % on the K = 8704
+// tower GEMM but -7 % on the cascade's K = 256 catalog scoring (139 KiB of LDS: one workgroup per CU, so
+// no tile's epilogue overlaps another's main loop), so 32 it stays (profiles/r02/gemm_probe_r02f.json).
+constexpr int BKF = 32, RSF = BKF + 4;
 
 template <bool BF16, int BT>
 struct GemmCfg {
