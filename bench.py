@@ -59,6 +59,7 @@ def parse():
     p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
     p.add_argument("--pipe-examples", type=int, default=65536, help="feature pipe: examples written and read back")
     p.add_argument("--pipe-threads", type=int, default=16, help="feature pipe: reader threads (the box's CPU share)")
+    p.add_argument("--dist-timeout", type=int, default=300, help="seconds before a stuck collective raises (N > 1)")
     return p.parse_args()
 
 
@@ -129,7 +130,13 @@ def main():
         return dry_run(args, world, rank)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        # a collective that never completes (an extra leg failing on one rank only) raises after the
+        # timeout instead of hanging the run, so the headline line still prints
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        import datetime
+
+        dist.init_process_group(backend, device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=args.dist_timeout))
         assert dist.get_world_size() == world == args.gpus
 
     from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
@@ -183,18 +190,16 @@ def main():
     if not args.no_sharded:
         del dev, out
         torch.cuda.empty_cache()
-        if world == 1:
-            try:
-                sharded = bench_sharded(args, specs, multi, rank, world)
-            except Exception as e:  # noqa: BLE001 — the headline line must still print
-                torch.cuda.synchronize()
-                torch.cuda.empty_cache()
-                sharded = {"error": f"{type(e).__name__}: {e}"[:300]}
-        else:
+        try:
             sharded = bench_sharded(args, specs, multi, rank, world)
+        except Exception as e:  # noqa: BLE001 — the headline line must still print
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            sharded = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     cascade_sh = None
-    if not args.no_cascade and (world > 1 or args.cascade_sharded):
+    if not args.no_cascade and (world > 1 or args.cascade_sharded) and not (isinstance(sharded, dict) and "error" in sharded
+                                                                           and world > 1):
         torch.cuda.empty_cache()
         try:
             cascade_sh = bench_cascade_sharded(args, specs, rank, world)
@@ -202,11 +207,12 @@ def main():
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             cascade_sh = {"error": f"{type(e).__name__}: {e}"[:300]}
-            if world > 1:
-                raise
     if rank != 0:
         if world > 1:
-            dist.destroy_process_group()
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001 — a communicator aborted by a failed leg
+                pass
         return
 
     traffic = None
@@ -285,7 +291,10 @@ def main():
     }
     print(json.dumps(line), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 — a communicator aborted by a failed leg
+            pass
 
 
 def _time_stages(stages, steps, warmup):
