@@ -425,7 +425,38 @@ __device__ __forceinline__ void esim_acc4(s4v xv, f4 at, f2v& sx, f2v& sm, float
     mx = fmx3(mx, d23[1], m23[1]);
 }
 
-template <typename M, int D, int NTT, bool TWO>
+// statistics of 4 rows of one column with x in fp32 (from the selector MFMA, v5): scalar ops only — packed
+// f32 VALU beside MFMAs costs more than the two scalar ops it replaces (MI355X_MICROARCH constants table;
+// rf_attn.hip is built with -fno-slp-vectorize so the compiler does not re-pack them)
+__device__ __forceinline__ void esim_acc4x(f4 x, f4 at, float& sx, float& sm, float& mx) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float m = x[r] * at[r];
+        const float d = x[r] - at[r];
+        sx += x[r];
+        sm += m;
+        mx = fmx3(mx, x[r], at[r]);
+        mx = fmx3(mx, d, m);
+    }
+}
+
+// A operand selecting the 16 rows of stripe sp out of its 32-row P @ V k-step, in the k order of
+// stripe_softmax3's accumulator-sourced fragments (element j of lane (lr, g): k = 4g + j for j < 4,
+// 16 + 4g + j - 4 for j >= 4): row lr picks k = 16 (sp & 1) + lr, so sel @ V_kstep = x of the stripe,
+// exactly, in the accumulator layout of att (one 1.0 per row, fp32 accumulation of one product)
+template <typename M>
+__device__ __forceinline__ typename M::frag stripe_selector(int sp, int lr, int lg) {
+    using frag = typename M::frag;
+    using elem = decltype(frag{}[0]);
+    frag f;
+    const int jh = 4 * (sp & 1) + (lr & 3);
+    const bool mine = lg == (lr >> 2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (elem)((mine && j == jh) ? 1.0f : 0.0f);
+    return f;
+}
+
+template <typename M, int D, int NTT, bool TWO, bool XM = false>
 __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
                                            int lane) {
     constexpr int nt = NTT;
@@ -482,30 +513,93 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
             c0[nn] = f4{0.f, 0.f, 0.f, 0.f};
             c1[nn] = f4{0.f, 0.f, 0.f, 0.f};
         }
+        float sx[NT], sm[NT], mx[NT];
+        if constexpr (!XM) {
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-            if (2 * kt < nt) {
-                const bool hi_ok = 2 * kt + 1 < nt;
+            for (int kt = 0; kt < 4; ++kt) {
+                if (2 * kt < nt) {
+                    const bool hi_ok = 2 * kt + 1 < nt;
 #pragma unroll
-                for (int nn = 0; nn < NT; ++nn) {
-                    const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, nn * 16, lane, hi_ok);
-                    c0[nn] = M::mma(pa0[kt], vf, c0[nn]);
-                    if (TWO) c1[nn] = M::mma(pa1[kt], vf, c1[nn]);
+                    for (int nn = 0; nn < NT; ++nn) {
+                        const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, nn * 16, lane, hi_ok);
+                        c0[nn] = M::mma(pa0[kt], vf, c0[nn]);
+                        if (TWO) c1[nn] = M::mma(pa1[kt], vf, c1[nn]);
+                    }
                 }
             }
-        }
-        float sx[NT], sm[NT], mx[NT];
 #pragma unroll
-        for (int nn = 0; nn < NT; ++nn) {
-            // this lane's x values: rows sp*16 + 4*lg .. +3 of column nn*16 + lr
-            f2v sx2 = {0.f, 0.f}, sm2 = {0.f, 0.f};
-            float m = -INFINITY;
-            esim_acc4<M>(tr_read(V + (sp0 * 16 + lg * 4 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3)), c0[nn], sx2, sm2, m);
-            if (TWO)
-                esim_acc4<M>(tr_read(V + (sp1 * 16 + lg * 4 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3)), c1[nn], sx2, sm2, m);
-            sx[nn] = sx2[0] + sx2[1];
-            sm[nn] = sm2[0] + sm2[1];
-            mx[nn] = m;
+            for (int nn = 0; nn < NT; ++nn) {
+                // this lane's x values: rows sp*16 + 4*lg .. +3 of column nn*16 + lr
+                f2v sx2 = {0.f, 0.f}, sm2 = {0.f, 0.f};
+                float m = -INFINITY;
+                esim_acc4<M>(tr_read(V + (sp0 * 16 + lg * 4 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3)), c0[nn], sx2, sm2, m);
+                if (TWO)
+                    esim_acc4<M>(tr_read(V + (sp1 * 16 + lg * 4 + (lr >> 2)) * RS + nn * 16 + 4 * (lr & 3)), c1[nn], sx2, sm2, m);
+                sx[nn] = sx2[0] + sx2[1];
+                sm[nn] = sm2[0] + sm2[1];
+                mx[nn] = m;
+            }
+        } else {
+            // v5: x of the wave's stripes comes out of the MFMA pipe in fp32 (selector @ the k-step's V
+            // fragments, already loaded for P @ V): no x reads, no bf16 -> f32 conversions. The columns run
+            // in halves at d = 128 (att and x of both stripes for 4 column tiles at a time: 64 accumulator
+            // registers instead of 128, no spills next to the 64 prefetch registers)
+            constexpr int NH = NT >= 8 ? 2 : 1, NC = NT / NH;
+            const frag sel = stripe_selector<M>(sp0, lr, lg);  // sp1 = sp0 + 4: the same row half
+            const int kt0 = sp0 >> 1, kt1 = sp1 >> 1;  // kt0 in {0, 1}, kt1 in {2, 3}
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                f4 a0[NC], a1[NC], x0[NC], x1[NC];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    a0[c] = f4{0.f, 0.f, 0.f, 0.f};
+                    a1[c] = f4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt) {
+                    if (2 * kt < nt) {
+                        const bool hi_ok = 2 * kt + 1 < nt;
+                        // wave-uniform: this k-step holds the rows of stripe sp0 (kt < 2) or sp1 (kt >= 2)
+                        if (kt < 2 ? kt == kt0 : (TWO && kt == kt1)) {
+#pragma unroll
+                            for (int c = 0; c < NC; ++c) {
+                                const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, (h * NC + c) * 16, lane, hi_ok);
+                                a0[c] = M::mma(pa0[kt], vf, a0[c]);
+                                if (TWO) a1[c] = M::mma(pa1[kt], vf, a1[c]);
+                                if (kt < 2) x0[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
+                                else x1[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
+                            }
+                        } else {
+#pragma unroll
+                            for (int c = 0; c < NC; ++c) {
+                                const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, (h * NC + c) * 16, lane, hi_ok);
+                                a0[c] = M::mma(pa0[kt], vf, a0[c]);
+                                if (TWO) a1[c] = M::mma(pa1[kt], vf, a1[c]);
+                            }
+                        }
+                    }
+                }
+                float hx[NC], hm[NC], hmx[NC];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    hx[c] = 0.f;
+                    hm[c] = 0.f;
+                    hmx[c] = -INFINITY;
+                    esim_acc4x(x0[c], a0[c], hx[c], hm[c], hmx[c]);
+                    if (TWO) esim_acc4x(x1[c], a1[c], hx[c], hm[c], hmx[c]);
+                }
+                // this half's reduce-scatter and stores now (nothing carried into the next half)
+                const int pk = (lg == 1) ? 2 : (lg == 2) ? 1 : lg;
+                float* w = wst + side * D + lr;
+#pragma unroll
+                for (int g = 0; g < NC / 4; ++g) {
+                    const int n = (h * NC + 4 * g + pk) * 16;
+                    w[n] = rs4<false>(hx[4 * g], hx[4 * g + 1], hx[4 * g + 2], hx[4 * g + 3]);
+                    w[2 * D + n] = rs4<false>(hm[4 * g], hm[4 * g + 1], hm[4 * g + 2], hm[4 * g + 3]);
+                    w[4 * D + n] = rs4<true>(hmx[4 * g], hmx[4 * g + 1], hmx[4 * g + 2], hmx[4 * g + 3]);
+                }
+            }
+            continue;  // statistics stored
         }
         // reduce-scatter over the four 16-lane rows: row k of group g holds tile nn = 4g + perm[k]
         const int pk = (lg == 1) ? 2 : (lg == 2) ? 1 : lg;
@@ -520,7 +614,7 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
     }
 }
 
-template <bool F16, int D, int NTT>
+template <bool F16, int D, int NTT, bool XM>
 __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
                                                                      const uint16_t* __restrict__ a, int batch, int L,
                                                                      int64_t ex_stride, int64_t ld, float* __restrict__ out,
@@ -583,8 +677,8 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         if (sp0 < nt) {
             float* wst = st + sp0 * 3 * 2 * D;
             // both-stripe / one-stripe waves are separate instantiations: no predicated MFMAs
-            if (sp1 < nt) esim3_wave<M, D, NTT, true>(qs, as, wst, sp0, sp1, L, lane);
-            else esim3_wave<M, D, NTT, false>(qs, as, wst, sp0, sp1, L, lane);
+            if (sp1 < nt) esim3_wave<M, D, NTT, true, XM>(qs, as, wst, sp0, sp1, L, lane);
+            else esim3_wave<M, D, NTT, false, XM>(qs, as, wst, sp0, sp1, L, lane);
         }
         __syncthreads();
 
@@ -751,7 +845,12 @@ int launch_big_lds(K kernel, int grid, size_t lds, hipStream_t st, const char* n
 template <bool F16, int D, int NTT>
 int launch_esim2_nt(int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L, int64_t ex_stride,
                     int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
-    auto kern = esim2_kernel<F16, D, NTT>;
+    // RF_ESIM_XM=0 keeps the v3 statistics (x read from LDS and converted on the VALU) for A/B runs
+    static const bool xm = [] {
+        const char* e = getenv("RF_ESIM_XM");
+        return !(e && e[0] == '0');
+    }();
+    auto kern = xm ? esim2_kernel<F16, D, NTT, true> : esim2_kernel<F16, D, NTT, false>;
     const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, (const uint16_t*)q, (const uint16_t*)a, batch, L,
