@@ -363,15 +363,9 @@ def bench_esim(args):
     # number; the two resident input batches alternate, as in the eager loop
     from recommendflow_amd.runtime.graphs import CapturedGraph
 
-    side_a = torch.cuda.Stream()
-
-    def enc_p(p):  # as the model's forward: the ad tower on a side stream, concurrently with the user tower
-        cur = torch.cuda.current_stream()
-        side_a.wait_stream(cur)
-        with torch.cuda.stream(side_a):
-            model.enc_a(ha[p], out=a)
+    def enc_p(p):
         model.enc_q(hu[p], out=q)
-        cur.wait_stream(side_a)
+        model.enc_a(ha[p], out=a)
 
     g_enc = [CapturedGraph(lambda p=p: enc_p(p)) for p in (0, 1)]
     g_att, g_mlp = CapturedGraph(att), CapturedGraph(mlp)

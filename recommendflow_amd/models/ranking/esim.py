@@ -47,7 +47,7 @@ class Esim(torch.nn.Module):
 
     def forward(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor) -> torch.Tensor:
         """The input MLP (dense features only) runs on a side stream, concurrently with the two encoders and
-        the attention (the ad tower's encoder on a second side stream, concurrently with the user tower's): it is a latency-bound launch of 256 workgroups that the encoders' tails leave room
+        the attention: it is a latency-bound launch of 256 workgroups that the encoders' tails leave room
         for. It writes pooled[:, :d_emb], the attention pooled[:, d_emb:]; the output MLP waits for both
         (also inside a hipGraph capture: the fork/join become graph edges)."""
         B = user.batch
@@ -59,24 +59,16 @@ class Esim(torch.nn.Module):
             self.input_mlp(dense, out=pooled[:, : self.d_emb])
         pooled.record_stream(side)
         dense.record_stream(side)
-        # the two towers' encoder launches run on two streams: each is a grid of 1-wave workgroups, and the
-        # second fills the first one's tail instead of waiting for it (graph edges under capture)
-        side_a = self._side_stream(dense.device, "_side_a")
-        side_a.wait_stream(cur)
-        with torch.cuda.stream(side_a):
-            a = self.enc_a(ad).view(B, self.L, self.d)
         q = self.enc_q(user).view(B, self.L, self.d)
-        cur.wait_stream(side_a)
-        a.record_stream(cur)
+        a = self.enc_a(ad).view(B, self.L, self.d)
         esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
         cur.wait_stream(side)
         return self.dense_output(self.output_mlp(pooled))
 
-    def _side_stream(self, device, name: str = "_side"):
-        s = getattr(self, name, None)
+    def _side_stream(self, device):
+        s = getattr(self, "_side", None)
         if s is None or s.device != device:
-            s = torch.cuda.Stream(device=device)
-            setattr(self, name, s)
+            s = self._side = torch.cuda.Stream(device=device)
         return s
 
     def graphed(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor, **kw):
