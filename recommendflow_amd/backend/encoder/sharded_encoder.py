@@ -276,17 +276,33 @@ class ShardedFusedEncoder(torch.nn.Module):
         self.pad_rows = self.ops.hash_rows(self.desc, S, empty)
 
     # -- the three local stages -------------------------------------------------------------------
-    def route(self, batch: SparseBatch) -> RouteState:
+    def _route_device(self, batch: SparseBatch):
         rows = self.ops.hash_rows(self.desc, len(self.slots), batch)
         req = torch.cat([rows, self.pad_rows])
         if self.dedup:
             counts, local, row_map = self.ops.route(req, self.nranks, self.table_rows)
-            counts = [int(c) for c in counts.cpu().tolist()]
-            local = local[: sum(counts)]
         else:
             counts, _, local, row_map = self.ops.bucketize(req, self.nranks)
-            counts = [int(c) for c in counts.cpu().tolist()]
-        return RouteState(counts, local, row_map, int(local.numel()), req.numel())
+        return counts.to(torch.int64), local, row_map, req.numel()
+
+    def _route_state(self, counts: List[int], local, row_map, n_logical: int) -> RouteState:
+        if self.dedup:
+            local = local[: sum(counts)]  # rf_route_rows sizes the id buffer for the undeduplicated worst case
+        return RouteState(counts, local, row_map, int(local.numel()), n_logical)
+
+    def route(self, batch: SparseBatch) -> RouteState:
+        counts, local, row_map, n = self._route_device(batch)
+        return self._route_state([int(c) for c in counts.cpu().tolist()], local, row_map, n)
+
+    def route_exchange(self, batch: SparseBatch):
+        """route() plus the all-to-all of the per-owner counts with ONE host synchronisation: the counts
+        stay on the device for the exchange, and the send and receive counts come back together (the
+        split sizes of the id and row all-to-alls are host lists). -> (RouteState, recv_counts)."""
+        counts, local, row_map, n = self._route_device(batch)
+        recv = self.comm.exchange_counts(counts)
+        both = [int(c) for c in torch.cat([counts, recv.to(counts.device)]).cpu().tolist()]
+        P = counts.numel()
+        return self._route_state(both[:P], local, row_map, n), both[P:]
 
     def serve(self, local_rows: torch.Tensor) -> torch.Tensor:
         # rows beyond the shard come back NaN (rf_gather_rows), poisoning the pooled output loudly
@@ -305,9 +321,7 @@ class ShardedFusedEncoder(torch.nn.Module):
         if batch.n_slots != len(self.slots):
             raise ValueError(f"batch has {batch.n_slots} slots, encoder {len(self.slots)}")
         batch = self.ops.prepare_batch(batch)
-        st = self.route(batch)
-        counts_t = torch.tensor(st.counts, dtype=torch.int64, device=st.local.device)
-        recv_counts = [int(c) for c in self.comm.exchange_counts(counts_t).cpu().tolist()]
+        st, recv_counts = self.route_exchange(batch)
         wanted = self.comm.exchange(st.local, st.counts, recv_counts)        # ids other ranks want from me
         vec = self.serve(wanted)
         back = self.comm.exchange(vec, recv_counts, st.counts)               # my rows, owner-major
@@ -335,9 +349,7 @@ def _shard_training_methods():
     def forward_train(self, batch: SparseBatch, out: Optional[torch.Tensor] = None) -> TrainCtx:
         """forward() that keeps what the backward needs (route state, received rows, served ids)."""
         batch = self.ops.prepare_batch(batch)
-        st = self.route(batch)
-        counts_t = torch.tensor(st.counts, dtype=torch.int64, device=st.local.device)
-        recv_counts = [int(c) for c in self.comm.exchange_counts(counts_t).cpu().tolist()]
+        st, recv_counts = self.route_exchange(batch)
         wanted = self.comm.exchange(st.local, st.counts, recv_counts)
         back = self.comm.exchange(self.serve(wanted), recv_counts, st.counts)
         out = self.combine(batch, st, back, out)
