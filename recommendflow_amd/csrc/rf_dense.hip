@@ -643,8 +643,13 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
                     rq[i][r] += __shfl_xor(rq[i][r], o, 64);
                 }
                 const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                if (lr == 0 && row < M)
-                    *reinterpret_cast<float2*>(ea.stats + 2 * (row * ea.P + (n0 / kLdsBN) * 4 + wn)) = make_float2(rs[i][r], rq[i][r]);
+                if (lr == 0 && row < M) {
+                    float* sp = ea.stats + 2 * (row * ea.P + (n0 / kLdsBN) * 4 + wn);
+                    *reinterpret_cast<float2*>(sp) = make_float2(rs[i][r], rq[i][r]);
+                    // two wave columns per tile (128-row tiles): the tile's other two slots hold zeros, so
+                    // every slot of a row is written and the stats buffer needs no clearing launch
+                    if constexpr (WN == 2) *reinterpret_cast<float2*>(sp + 4) = make_float2(0.f, 0.f);
+                }
             }
     } else {  // kEpiLnFold
         // the tile's rows: P partials each, summed in a fixed order (TPR threads per row, each a strided
@@ -1149,9 +1154,7 @@ extern "C" int rf_linear_stats_fwd(const void* x, int64_t M, int32_t K, int64_t 
     RF_REQUIRE(x && W && y_bf16 && row_stats, "rf_linear_stats_fwd: null pointer");
     RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0, "rf_linear_stats_fwd: x/W must be 16-byte aligned");
     hipStream_t st = rf_stream(stream);
-    const int P = 4 * ((N + kLdsBN - 1) / kLdsBN);
-    const hipError_t e = hipMemsetAsync(row_stats, 0, (size_t)M * P * 2 * sizeof(float), st);  // slots a tile shape leaves unused
-    if (e != hipSuccess) return rf_set_error(RF_EHIP, "rf_linear_stats_fwd: %s", hipGetErrorString(e));
+    const int P = 4 * ((N + kLdsBN - 1) / kLdsBN);  // every slot of rows < M is written by the epilogue
     EpiArgs ea{};
     ea.yb = static_cast<uint16_t*>(y_bf16);
     ea.stats = row_stats;
