@@ -161,6 +161,21 @@ int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int3
                                int32_t d, int64_t ex_stride, int64_t ld, float* out, int64_t out_stride,
                                int64_t out_off, float* att_out, void* stream);
 
+/*
+ * rf_esim_soft_attention_fwd (without att_out) followed, in the same launch, by the LayerNormalization that
+ * create_mlp puts in front of the output MLP's first Dense (backend/blocks/mlp.py:10-13 over the concat of
+ * models/ranking/esim.py:84-85). Each out row is [head | pooled]: columns [0, out_off) are written
+ * BEFORE this call by another producer (ESIM: the input MLP's d_emb columns, esim.py:75), the kernel writes
+ * the 6d pooled features at out_off (F32, as above) and then normalises the whole row of out_off + 6d
+ * values: y = (x - mean) / sqrt(var + eps) * gamma + beta (two-pass mean / variance, as rf_norm_fwd mode 0),
+ * stored as BF16 into y_bf16 [batch][ldy] - the A operand of the next GEMM. gamma / beta may be NULL
+ * (ones / zeros). Constraints as above plus 0 <= out_off <= 512.
+ */
+int rf_esim_pool_ln_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                        int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
+                        const float* ln_gamma, const float* ln_beta, float eps, void* y_bf16, int64_t ldy,
+                        void* stream);
+
 /* activations for rf_linear_fwd */
 #define RF_ACT_NONE 0
 #define RF_ACT_GELU 1 /* exact erf gelu (tf.keras.activations.gelu, approximate=False) */

@@ -456,7 +456,7 @@ __device__ __forceinline__ typename M::frag stripe_selector(int sp, int lr, int 
     return f;
 }
 
-template <typename M, int D, int NTT, bool TWO, bool XM = false>
+template <typename M, int D, int NTT, bool TWO, int XM = 0>
 __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
                                            int lane) {
     constexpr int nt = NTT;
@@ -514,7 +514,7 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
             c1[nn] = f4{0.f, 0.f, 0.f, 0.f};
         }
         float sx[NT], sm[NT], mx[NT];
-        if constexpr (!XM) {
+        if constexpr (XM == 0) {
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) {
                 if (2 * kt < nt) {
@@ -614,11 +614,31 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
     }
 }
 
-template <bool F16, int D, int NTT, bool XM>
+// LayerNorm epilogue (rf_esim_pool_ln_fwd): the row of `out` is [head columns 0..out_off) | the 6d pooled
+// features], the head written beforehand by another producer (cfg3: the input MLP); the kernel normalises the
+// whole row (two-pass mean / variance, as rf_norm_fwd) and writes it as bf16 -> the output MLP's first GEMM
+struct EsimLn {
+    const float* gamma;  // [out_off + 6d] or null (ones)
+    const float* beta;   // [out_off + 6d] or null (zeros)
+    float eps;
+    uint16_t* y;         // [batch][ldy] bf16
+    int64_t ldy;
+};
+
+constexpr int kEsimLnHead = 2;  // head columns per thread: out_off <= 512
+
+// sum over the 64 lanes of a wave, every lane gets the total (same bits everywhere)
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <bool F16, int D, int NTT, int XM, bool LNE = false>
 __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
                                                                      const uint16_t* __restrict__ a, int batch, int L,
                                                                      int64_t ex_stride, int64_t ld, float* __restrict__ out,
-                                                                     int64_t out_stride, int64_t out_off) {
+                                                                     int64_t out_stride, int64_t out_off, EsimLn ln) {
     using M = Mfma<F16>;
     constexpr int NTH = kEsim2Waves * 64;
     constexpr int RS = esim2_rs(D, NTT);
@@ -669,6 +689,16 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         }
         __syncthreads();
         if (e + gridDim.x < batch) prefetch(e + gridDim.x);
+        // LN epilogue: this example's head columns (written by the other producer before the launch) are
+        // fetched now, in flight under the compute phase (2 registers)
+        float hv[LNE ? kEsimLnHead : 1];
+        if constexpr (LNE) {
+            int64_t hc = out_off;
+            asm volatile("" : "+s"(hc));
+            const float* orow = out + e * out_stride;
+#pragma unroll
+            for (int k = 0; k < kEsimLnHead; ++k) hv[k] = tid + k * NTH < hc ? orow[tid + k * NTH] : 0.f;
+        }
 
         // v3: the stripe pairs rotate over the waves from one example to the next, so the wave left with one
         // stripe (7 tiles over 4 waves) is a different SIMD each time; statistics slots follow the stripe
@@ -709,6 +739,76 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                 if (side == 0) {
                     o[4 * D] = avg - avg_o;
                     o[5 * D] = m3 - mx_o;
+                }
+            }
+            if constexpr (LNE) {
+                static_assert(NTH / 2 >= D, "one column per thread and side");
+                int64_t hc = out_off;  // opaque: no loop-invariant index math hoisted into the compute phase
+                asm volatile("" : "+s"(hc));
+                // this thread's features (side 0: 4, side 1: 2; none past d) and up to 4 head columns
+                const bool own = n < D;
+                const float v[4] = {avg, m3, avg - avg_o, m3 - mx_o};
+                const int nv = own ? (side == 0 ? 4 : 2) : 0;
+                // the LN parameters of this thread's columns, all loads issued before the two reductions (their
+                // latency hides under the barriers); opaque pointer copies keep these loop-invariant loads out
+                // of the compute phase (hoisted, they hold 12 registers there and spill)
+                const float* lgam = ln.gamma;
+                const float* lbet = ln.beta;
+                asm volatile("" : "+s"(lgam), "+s"(lbet));
+                float gh[kEsimLnHead], bh[kEsimLnHead], gvv[4], bvv[4];
+#pragma unroll
+                for (int k = 0; k < kEsimLnHead; ++k) {
+                    const int c = tid + k * NTH < hc ? tid + k * NTH : 0;
+                    gh[k] = lgam ? lgam[c] : 1.f;
+                    bh[k] = lbet ? lbet[c] : 0.f;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int c = (int)hc + (k < 2 ? (2 * side + k) * D : (2 + k) * D) + (own ? n : 0);
+                    gvv[k] = lgam ? lgam[c] : 1.f;
+                    bvv[k] = lbet ? lbet[c] : 0.f;
+                }
+                // 2 x 4 wave partials in the q image: no wave reads the images between the post-compute barrier
+                // and the next example's staging (which follows the loop-top barrier)
+                float* red = reinterpret_cast<float*>(qs);
+                const float cols = (float)(hc + 6 * D);
+                float s1 = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) s1 += k < nv ? v[k] : 0.f;
+#pragma unroll
+                for (int k = 0; k < kEsimLnHead; ++k) s1 += hv[k];
+                s1 = wave_sum64(s1);
+                if (lane == 0) red[wave] = s1;
+                __syncthreads();
+                const float mu = ((red[0] + red[1]) + (red[2] + red[3])) / cols;
+                float s2 = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float dv = k < nv ? v[k] - mu : 0.f;
+                    s2 += dv * dv;
+                }
+#pragma unroll
+                for (int k = 0; k < kEsimLnHead; ++k) {
+                    const float dh = tid + k * NTH < hc ? hv[k] - mu : 0.f;
+                    s2 += dh * dh;
+                }
+                s2 = wave_sum64(s2);
+                if (lane == 0) red[4 + wave] = s2;
+                __syncthreads();
+                const float rstd = 1.0f / sqrtf(((red[4] + red[5]) + (red[6] + red[7])) / cols + ln.eps);
+                uint16_t* yr = ln.y + e * ln.ldy;
+#pragma unroll
+                for (int k = 0; k < kEsimLnHead; ++k) {
+                    const int c = tid + k * NTH;
+                    if (c < hc) yr[c] = (uint16_t)f32_to_bf16_bits((hv[k] - mu) * rstd * gh[k] + bh[k]);
+                }
+                // the pooled columns: side 0 avg, max, avg_q - avg_a, max_q - max_a; side 1 avg, max
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k < nv) {
+                        const int c = (int)hc + (k < 2 ? (2 * side + k) * D : (2 + k) * D) + n;
+                        yr[c] = (uint16_t)f32_to_bf16_bits((v[k] - mu) * rstd * gvv[k] + bvv[k]);
+                    }
                 }
             }
         }
@@ -844,30 +944,46 @@ int launch_big_lds(K kernel, int grid, size_t lds, hipStream_t st, const char* n
 
 template <bool F16, int D, int NTT>
 int launch_esim2_nt(int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L, int64_t ex_stride,
-                    int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
-    // RF_ESIM_XM=0 keeps the v3 statistics (x read from LDS and converted on the VALU) for A/B runs
-    static const bool xm = [] {
+                    int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimLn* ln) {
+    // RF_ESIM_XM=0 keeps the v3 statistics (x read from LDS and converted on the VALU); A/B runs only
+    static const int xm = [] {
         const char* e = getenv("RF_ESIM_XM");
-        return !(e && e[0] == '0');
+        return e && e[0] == '0' ? 0 : 1;
     }();
-    auto kern = xm ? esim2_kernel<F16, D, NTT, true> : esim2_kernel<F16, D, NTT, false>;
+    auto kern = ln ? esim2_kernel<F16, D, NTT, 1, true> : xm == 0 ? esim2_kernel<F16, D, NTT, 0> : esim2_kernel<F16, D, NTT, 1>;
     const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, (const uint16_t*)q, (const uint16_t*)a, batch, L,
-                       ex_stride, ld, out, out_stride, out_off);
+                       ex_stride, ld, out, out_stride, out_off, ln ? *ln : EsimLn{});
     return RF_OK;
 }
 
 template <bool F16, int D>
 int launch_esim2(int nt, int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L,
-                 int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
+                 int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimLn* ln) {
     switch (nt) {
 #define RF_NT(N) \
-    case N: return launch_esim2_nt<F16, D, N>(grid, lds, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
+    case N: return launch_esim2_nt<F16, D, N>(grid, lds, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln);
         RF_NT(1) RF_NT(2) RF_NT(3) RF_NT(4) RF_NT(5) RF_NT(6) RF_NT(7) RF_NT(8)
 #undef RF_NT
         default: return rf_set_error(RF_EINVAL, "esim2: bad tile count %d", nt);
     }
+}
+
+// the 4-wave persistent kernel (two workgroups per CU when the images fit 80 KB)
+int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d, int64_t ex_stride,
+                   int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimLn* ln, hipStream_t st) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int nt = (L + 15) >> 4;
+    const size_t lds2 = esim2_lds_bytes(d, nt, esim2_rs(d, nt));
+    const int per_cu = lds2 <= 80 * 1024 ? 2 : 1;
+    const int grid2 = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
+    if (dtype == RF_DTYPE_BF16)
+        return d == 64 ? launch_esim2<false, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln)
+                       : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln);
+    return d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln)
+                   : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln);
 }
 
 }  // namespace
@@ -894,18 +1010,7 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
         return e && e[0] == '1';
     }();
     if (!v1 && !att_out) {
-        const int nt = (L + 15) >> 4;
-        const size_t lds2 = esim2_lds_bytes(d, nt, esim2_rs(d, nt));
-        const int per_cu = lds2 <= 80 * 1024 ? 2 : 1;
-        const int grid2 = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
-        int rc = RF_OK;
-        if (dtype == RF_DTYPE_BF16) {
-            rc = d == 64 ? launch_esim2<false, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
-                         : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
-        } else {
-            rc = d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
-                         : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
-        }
+        const int rc = esim2_dispatch(q, a, dtype, batch, L, d, ex_stride, ld, out, out_stride, out_off, nullptr, st);
         if (rc) return rc;
         return rf_check_launch("rf_esim_soft_attention_fwd");
     }
@@ -928,6 +1033,28 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     }
 #undef RF_ESIM_LAUNCH
     return rf_check_launch("esim_kernel");
+}
+
+extern "C" int rf_esim_pool_ln_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                                   int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
+                                   const float* ln_gamma, const float* ln_beta, float eps, void* y_bf16, int64_t ldy,
+                                   void* stream) {
+    RF_REQUIRE(dtype == RF_DTYPE_BF16 || dtype == RF_DTYPE_F16, "rf_esim_pool_ln_fwd: dtype must be BF16 or F16");
+    RF_REQUIRE(L >= 1 && L <= 128, "rf_esim_pool_ln_fwd: need 1 <= L <= 128 (got %d)", L);
+    RF_REQUIRE(d == 64 || d == 128, "rf_esim_pool_ln_fwd: d must be 64 or 128 (got %d)", d);
+    RF_REQUIRE(batch >= 0, "rf_esim_pool_ln_fwd: batch < 0");
+    RF_REQUIRE(ld % 8 == 0 && ex_stride % 8 == 0 && ld >= d, "rf_esim_pool_ln_fwd: ld/ex_stride must be multiples of 8 elements (16-byte rows)");
+    RF_REQUIRE((int64_t)L * ld * 2 < ((int64_t)1 << 31), "rf_esim_pool_ln_fwd: one example's rows must span < 2 GiB");
+    RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)a & 15) == 0, "rf_esim_pool_ln_fwd: q/a must be 16-byte aligned");
+    RF_REQUIRE(out_off >= 0 && out_off <= kEsimLnHead * kEsim2Waves * 64, "rf_esim_pool_ln_fwd: need 0 <= out_off <= 512 head columns (got %lld)", (long long)out_off);
+    RF_REQUIRE(out_stride >= out_off + 6 * d && ldy >= out_off + 6 * d, "rf_esim_pool_ln_fwd: rows narrower than out_off + 6d");
+    RF_REQUIRE(eps >= 0.f, "rf_esim_pool_ln_fwd: eps < 0");
+    if (batch == 0) return RF_OK;
+    RF_REQUIRE(q && a && out && y_bf16, "rf_esim_pool_ln_fwd: null pointer");
+    const EsimLn ln{ln_gamma, ln_beta, eps, static_cast<uint16_t*>(y_bf16), ldy};
+    const int rc = esim2_dispatch(q, a, dtype, batch, L, d, ex_stride, ld, out, out_stride, out_off, &ln, rf_stream(stream));
+    if (rc) return rc;
+    return rf_check_launch("rf_esim_pool_ln_fwd");
 }
 
 extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int32_t batch, int32_t heads,

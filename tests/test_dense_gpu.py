@@ -6,7 +6,8 @@ import pytest
 import torch
 
 from recommendflow_amd.backend.blocks.mlp import create_mlp
-from recommendflow_amd.backend.layers.attention_layers import MultiHeadAttention, SoftAttention, esim_soft_attention_pool
+from recommendflow_amd.backend.layers.attention_layers import (MultiHeadAttention, SoftAttention, esim_soft_attention_pool,
+                                                               esim_soft_attention_pool_ln)
 from recommendflow_amd.backend.layers.core import BatchNormalization, Dense, LayerNormalization
 from recommendflow_amd.backend.layers.layer_utils import scaled_dot_product_attention
 
@@ -49,6 +50,39 @@ def test_esim_pool_fast_path(O, cuda, L, d, dt):
         want = O.esim_pool(q.float().numpy(), a.float().numpy())
         tol = (2 ** -7 if dt == torch.bfloat16 else 2 ** -10) * scale
         np.testing.assert_allclose(got, want, atol=tol * (scale + 1), rtol=0)
+
+
+@pytest.mark.parametrize("L,d", [(1, 64), (33, 128), (100, 128), (100, 64), (128, 128)])
+@pytest.mark.parametrize("head", [0, 130, 512])
+def test_esim_pool_ln_epilogue(O, cuda, L, d, head):
+    """rf_esim_pool_ln_fwd: the pooled features are the pooled-only kernel's bit for bit, and the bf16 row
+    LN([head | pooled]) equals a float64 LayerNorm of the kernel's own fp32 row within the bf16 rounding of
+    the output (|rel| <= 2^-8); against the oracle pooling at the ESIM bar of test_esim_pool_fast_path."""
+    B, scale, eps = 300, 0.5, 1e-6
+    q, a = rnd((B, L, d), L + d, scale), rnd((B, L, d), L + d + 9, scale)
+    W = head + 6 * d
+    out = torch.empty((B, W + 8), device="cuda")
+    hv = (torch.randn((B, max(head, 1)), generator=torch.Generator().manual_seed(head + 1)) * 0.7 + 0.2)[:, :head]
+    out[:, :head] = hv.cuda()
+    g = torch.Generator().manual_seed(L * 3 + d)
+    gamma = (torch.rand(W, generator=g) + 0.5).cuda()
+    beta = (torch.rand(W, generator=g) - 0.5).cuda()
+    y = esim_soft_attention_pool_ln(q.cuda(), a.cuda(), out, head, gamma, beta, eps)
+    plain = esim_soft_attention_pool(q.cuda(), a.cuda()).cpu().numpy()
+    row = out[:, :W].cpu().numpy()
+    assert np.array_equal(row[:, head:].view(np.uint32), plain.view(np.uint32))
+    np.testing.assert_array_equal(row[:, :head], hv.numpy())
+    want = O.layer_norm(row.astype(np.float64), gamma.double().cpu().numpy(), beta.double().cpu().numpy(), eps)
+    np.testing.assert_allclose(y.float().cpu().numpy(), want, rtol=2 ** -8, atol=1e-5)
+    want_p = O.esim_pool(q.float().numpy(), a.float().numpy())
+    np.testing.assert_allclose(row[:, head:], want_p, atol=2 ** -7 * scale * (scale + 1), rtol=0)
+
+
+def test_esim_pool_ln_rejects_wide_head(cuda):
+    q = rnd((2, 4, 64), 1).cuda()
+    out = torch.empty((2, 513 + 384), device="cuda")
+    with pytest.raises(Exception, match="out_off"):
+        esim_soft_attention_pool_ln(q, q, out, 513, None, None, 1e-6)
 
 
 def test_esim_strided_views(O, cuda):
