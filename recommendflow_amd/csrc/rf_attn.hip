@@ -675,6 +675,19 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     uint16_t* dummy = reinterpret_cast<uint16_t*>(st) + (tid & 127) * 8;
     int64_t e = blockIdx.x;
     uint32_t it = 0;
+    // the pooled features of the previous example, stored one example late (right before the next prefetch):
+    // vmcnt counts stores as well as loads, in issue order, so stores issued after a prefetch make the next
+    // staging wait for them (hipcc emits vmcnt(0) for the last chunk); issued before it, they have the whole
+    // compute phase to land. Four buffer stores per thread, unused ones at an offset past the descriptor.
+    constexpr int kOff = 1 << 30;
+    float pv[4] = {0.f, 0.f, 0.f, 0.f};
+    int po[4] = {kOff, kOff, kOff, kOff};
+    int64_t pe = -1;
+    auto flush = [&]() __attribute__((always_inline)) {
+        const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + pe * out_stride + out_off), 0, 6 * D * 4, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pv[k]), ro, po[k], 0, 0);
+    };
     if (e < batch) prefetch(e);
     for (; e < batch; e += gridDim.x) {
         __syncthreads();
@@ -688,6 +701,7 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
             }
         }
         __syncthreads();
+        if (pe >= 0) flush();
         if (e + gridDim.x < batch) prefetch(e + gridDim.x);
         // LN epilogue: this example's head columns (written by the other producer before the launch) are
         // fetched now, in flight under the compute phase (2 registers)
@@ -732,14 +746,18 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
             }
             const float avg = (2.0f * sx + smul) / (float)(4 * L);
             const float avg_o = __shfl_xor(avg, 32, 64), mx_o = __shfl_xor(m3, 32, 64);
-            if (n < D) {
-                float* o = out + e * out_stride + out_off + n;
-                o[2 * side * D] = avg;
-                o[(2 * side + 1) * D] = m3;
-                if (side == 0) {
-                    o[4 * D] = avg - avg_o;
-                    o[5 * D] = m3 - mx_o;
-                }
+            {
+                static_assert(NTH / 2 >= D, "one column per thread and side: four pending values");
+                const bool ok = n < D, ok0 = ok && side == 0;
+                pv[0] = avg;
+                pv[1] = m3;
+                pv[2] = avg - avg_o;
+                pv[3] = m3 - mx_o;
+                po[0] = ok ? (2 * side * D + n) * 4 : kOff;
+                po[1] = ok ? ((2 * side + 1) * D + n) * 4 : kOff;
+                po[2] = ok0 ? (4 * D + n) * 4 : kOff;
+                po[3] = ok0 ? (5 * D + n) * 4 : kOff;
+                pe = e;
             }
             if constexpr (LNE) {
                 static_assert(NTH / 2 >= D, "one column per thread and side");
@@ -813,6 +831,7 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
             }
         }
     }
+    if (pe >= 0) flush();  // the last example's features
 }
 
 // ---------------------------------------------------------------------------------------------
