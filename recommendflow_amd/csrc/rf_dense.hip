@@ -1102,12 +1102,15 @@ extern "C" int rf_norm_fwd(const float* x, int64_t rows, int32_t cols, int64_t l
 #define RF_NORM_VEC(B, N)                                                                                         \
     hipLaunchKernelGGL((norm_vec_kernel<B, N>), dim3(grid), dim3(256), 0, st, x, rows, cols, ldx, mode, eps, gamma, \
                        beta, mean, var, y, ldy)
+        // exact register counts for the common widths (1280 = cfg3's pooled row: 5 float4 per lane)
         if (y_dtype == RF_DTYPE_BF16) {
             if (nv <= 1) RF_NORM_VEC(true, 1); else if (nv <= 2) RF_NORM_VEC(true, 2);
-            else if (nv <= 4) RF_NORM_VEC(true, 4); else RF_NORM_VEC(true, 8);
+            else if (nv <= 4) RF_NORM_VEC(true, 4); else if (nv == 5) RF_NORM_VEC(true, 5);
+            else if (nv == 6) RF_NORM_VEC(true, 6); else RF_NORM_VEC(true, 8);
         } else {
             if (nv <= 1) RF_NORM_VEC(false, 1); else if (nv <= 2) RF_NORM_VEC(false, 2);
-            else if (nv <= 4) RF_NORM_VEC(false, 4); else RF_NORM_VEC(false, 8);
+            else if (nv <= 4) RF_NORM_VEC(false, 4); else if (nv == 5) RF_NORM_VEC(false, 5);
+            else if (nv == 6) RF_NORM_VEC(false, 6); else RF_NORM_VEC(false, 8);
         }
 #undef RF_NORM_VEC
         return rf_check_launch("norm_vec_kernel");

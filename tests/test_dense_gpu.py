@@ -145,7 +145,7 @@ def test_dense_fp32_exact_mfma(O, cuda, M, K, N):
     np.testing.assert_allclose(y, want, rtol=1e-5, atol=1e-6 * np.sqrt(K))
 
 
-@pytest.mark.parametrize("cols", [16, 200, 256, 1024, 1280, 2048, 2050, 3000, 4100, 8704, 20480, 32768, 32772])
+@pytest.mark.parametrize("cols", [16, 200, 256, 1024, 1280, 1400, 1536, 2048, 2050, 3000, 4100, 8704, 20480, 32768, 32772])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
 def test_norm_rows(O, cuda, cols, mode, odt):
