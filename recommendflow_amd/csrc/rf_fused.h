@@ -190,6 +190,7 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
         const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
         const int mask_empty = sd->mask_empty;
+        const BucketMod bmod = bucket_mod_init(nbins, mask_empty);  // once per item (the slot is wave-uniform)
         const int64_t out_off = sd->out_off;
         const int lm = lmax[s];
         const bool ok = pregathered || (rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows);
@@ -267,8 +268,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
             const int tb = tok_off[t], n = tok_off[t + 1] - tb;
             uint64_t h0, h1;
             siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
-            const int64_t i0 = bucket_from_hash(h0, n, nbins, mask_empty);
-            const int64_t i1 = bucket_from_hash(h1, n, nbins, mask_empty);
+            const int64_t i0 = bucket_from_hash(h0, n, bmod);
+            const int64_t i1 = bucket_from_hash(h1, n, bmod);
             if (i < kCap) {
                 s_row[wave][0][i] = ok ? (uint32_t)(rb0 + i0) : 0u;
                 s_row[wave][1][i] = ok ? (uint32_t)(rb1 + i1) : 0u;
@@ -545,8 +546,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     const int tb = tok_off[t], n = tok_off[t + 1] - tb;
                     uint64_t h0, h1;
                     siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
-                    r0 = ok ? (uint32_t)(rb0 + bucket_from_hash(h0, n, nbins, mask_empty)) : 0u;
-                    r1 = ok ? (uint32_t)(rb1 + bucket_from_hash(h1, n, nbins, mask_empty)) : 0u;
+                    r0 = ok ? (uint32_t)(rb0 + bucket_from_hash(h0, n, bmod)) : 0u;
+                    r1 = ok ? (uint32_t)(rb1 + bucket_from_hash(h1, n, bmod)) : 0u;
                 }
                 uint4 v[2][CPL];
 #pragma unroll
@@ -602,6 +603,7 @@ __global__ __launch_bounds__(64) void single_token_embed_kernel(
         const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
         const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
         const int mask_empty = sd->mask_empty;
+        const BucketMod bmod = bucket_mod_init(nbins, mask_empty);  // once per item (the slot is wave-uniform)
         const int64_t out_off = sd->out_off;
         const int lm = lmax[s];
         const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
@@ -621,8 +623,8 @@ __global__ __launch_bounds__(64) void single_token_embed_kernel(
                 uint64_t h0, h1;
                 siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
                 if (ok) {
-                    r0 = (uint32_t)(rb0 + bucket_from_hash(h0, n, nbins, mask_empty));
-                    r1 = (uint32_t)(rb1 + bucket_from_hash(h1, n, nbins, mask_empty));
+                    r0 = (uint32_t)(rb0 + bucket_from_hash(h0, n, bmod));
+                    r1 = (uint32_t)(rb1 + bucket_from_hash(h1, n, bmod));
                 }
                 has = 1;
             }
