@@ -2,8 +2,10 @@
 //   rf_esim_soft_attention_fwd  SoftAttention + ESIM combine/pool  (attention_layers.py:15-74, esim.py:78-84)
 //   rf_sdpa_fwd                 masked multi-head SDPA             (layer_utils.py:4-38, attention_layers.py:153-168)
 //
-// ESIM runs persistent 8-wave workgroups (one per CU, next example prefetched into registers); SDPA one
-// (example, head) per 4-wave workgroup. Shared structure:
+// ESIM (pooled output) runs esim2_kernel: persistent 4-wave workgroups, two per CU, the next example
+// prefetched into registers, x of each stripe taken from a selector MFMA, pooled features stored one example
+// late; with the attention output requested, the 8-wave esim_kernel. SDPA: one (example, head)
+// per 4-wave workgroup. Shared structure:
 //   * the [L, d] operand images sit in LDS with a 16-byte row pad (conflict-free ds_read_b128 for the
 //     16x16x32 A/B fragments, 8-byte aligned rows for ds_read_b64_tr_b16);
 //   * each wave owns 16-row stripes of the score matrix; scores stay in registers (never HBM), the
