@@ -166,20 +166,22 @@ __global__ __launch_bounds__(kHashUnits) void hash_rows_kernel(const rf_slot_des
         for (int j = threadIdx.x; j <= nu; j += kHashUnits) s_off[j] = bag_off[u0 + j];
         __syncthreads();
         const int t0 = s_off[0], t1 = s_off[nu];
+        const uint32_t s_first = (uint32_t)(u0 % n_slots);  // slot of unit u0 (one 64-bit remainder per block step)
         for (int t = t0 + (int)threadIdx.x; t < t1; t += kHashUnits) {
             int lo = 0, hi = nu - 1;  // last unit j with s_off[j] <= t
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 if (s_off[mid] <= t) lo = mid; else hi = mid - 1;
             }
-            const rf_slot_desc* sd = slots + (int)((u0 + lo) % n_slots);
+            const rf_slot_desc* sd = slots + (int)((s_first + (uint32_t)lo) % (uint32_t)n_slots);
             const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
             uint64_t h0, h1;
             siphash24x2_dev(sd->salt[0], sd->salt[1], tok_bytes + b0, n, h0, h1);
-            const int64_t nbins = sd->num_bins;
+            // both keys share the slot's modulus: one reciprocal instead of two 64-bit remainders
+            const BucketMod bm = bucket_mod_init(sd->num_bins, sd->mask_empty);
             longlong2 r;
-            r.x = sd->row_base[0] + bucket_from_hash(h0, n, nbins, sd->mask_empty);
-            r.y = sd->row_base[1] + bucket_from_hash(h1, n, nbins, sd->mask_empty);
+            r.x = sd->row_base[0] + bucket_from_hash(h0, n, bm);
+            r.y = sd->row_base[1] + bucket_from_hash(h1, n, bm);
             reinterpret_cast<longlong2*>(rows_out)[t] = r;
         }
     }
