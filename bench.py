@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--no-pipe", action="store_true", help="skip the TFRecord(GZIP) -> HBM feature-pipe extra")
     p.add_argument("--pipe-examples", type=int, default=65536, help="feature pipe: examples written and read back")
     p.add_argument("--pipe-threads", type=int, default=16, help="feature pipe: reader threads (the box's CPU share)")
+    p.add_argument("--no-probes", action="store_true", help="skip the STREAM-copy peak and random-row gather ceilings")
+    p.add_argument("--probe-table-gb", type=float, default=32.0, help="gather-ceiling table size (>> 256 MiB Infinity Cache)")
+    p.add_argument("--no-uniform-leg", action="store_true", help="skip the uniform-id (no locality) headline leg")
     p.add_argument("--dist-timeout", type=int, default=300, help="seconds before a stuck collective raises (N > 1)")
     return p.parse_args()
 
@@ -138,6 +141,9 @@ def main():
         dist.init_process_group(backend, device_id=torch.device("cuda", local),
                                 timeout=datetime.timedelta(seconds=args.dist_timeout))
         assert dist.get_world_size() == world == args.gpus
+        # host-side group for the legs' failure flags: a leg that failed on one rank may have aborted the RCCL
+        # communicator, so the decision to run the next collective leg goes over gloo
+        args.flag_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
 
     from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
     from recommendflow_amd.config_parser.configuration import Configuration
@@ -186,6 +192,22 @@ def main():
     achieved = bytes_per_launch / avg_kern_s / 1e9
     n_tok = sum(h.n_tokens for h in host) / len(host)
 
+    uniform_leg = None
+    if not args.no_uniform_leg and not args.uniform:
+        try:
+            uniform_leg = bench_uniform(args, enc, multi, rank, out)
+        except Exception as e:  # noqa: BLE001 — the headline line must still print
+            uniform_leg = {"error": f"{type(e).__name__}: {e}"[:300]}
+    probes = None
+    if not args.no_probes:
+        try:
+            probes = bench_probes(args)
+        except Exception as e:  # noqa: BLE001
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            probes = {"error": f"{type(e).__name__}: {e}"[:300]}
+    args.probes = probes
+
     sharded = None
     if not args.no_sharded:
         del dev, out
@@ -198,8 +220,12 @@ def main():
             sharded = {"error": f"{type(e).__name__}: {e}"[:300]}
 
     cascade_sh = None
-    if not args.no_cascade and (world > 1 or args.cascade_sharded) and not (isinstance(sharded, dict) and "error" in sharded
-                                                                           and world > 1):
+    sharded_failed = isinstance(sharded, dict) and "error" in sharded
+    if world > 1:  # every rank skips the next collective leg together if the sharded leg failed on ANY rank
+        flag = torch.tensor([1 if sharded_failed else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=args.flag_group)
+        sharded_failed = bool(flag.item())
+    if not args.no_cascade and (world > 1 or args.cascade_sharded) and not (sharded_failed and world > 1):
         torch.cuda.empty_cache()
         try:
             cascade_sh = bench_cascade_sharded(args, specs, rank, world)
@@ -247,6 +273,8 @@ def main():
         extras = dict(extras or {}, cfg2_dssm_train_step=guarded(bench_train, args, specs, multi))
     if world == 1 and not args.no_pipe:
         extras = dict(extras or {}, feature_pipe=guarded(bench_pipe, args, enc, specs, multi))
+    if world == 1 and not args.no_extras:
+        extras = dict(extras or {}, cfg1_demo_two_tower=guarded(bench_cfg1, args))
 
     value = args.batch * world * args.steps / elapsed
     line = {
@@ -283,7 +311,15 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "kernel_ms": round(avg_kern_s * 1e3, 4),
+            "peak_measured": (probes or {}).get("stream_copy_GBs"),
+            "frac_of_peak_measured": (round(achieved / probes["stream_copy_GBs"], 4)
+                                      if probes and probes.get("stream_copy_GBs") else None),
+            "gather_ceiling_256B_GBs": (probes or {}).get("gather_copy_256B_GBs"),
+            "frac_of_gather_ceiling": (round(achieved / probes["gather_copy_256B_GBs"], 4)
+                                       if probes and probes.get("gather_copy_256B_GBs") else None),
+            "uniform": uniform_leg,
         },
+        "probes": probes,
         "cpu_baseline": cpu,
         "extras": extras,
         "cfg4_sharded": sharded,
@@ -399,6 +435,9 @@ def bench_esim(args):
             "stage_ms": {k: round(v, 4) for k, v in per.items()},
             "first_ln_in_attention_epilogue": fused_ln,
             "encoder_GBs": round(enc_bytes / per["sparse_encoders"] / 1e6, 1),
+            "encoder_frac_of_measured_gather_ceiling": (
+                round(enc_bytes / per["sparse_encoders"] / 1e6 / args.probes["gather_copy_128B_GBs"], 4)
+                if isinstance(getattr(args, "probes", None), dict) and args.probes.get("gather_copy_128B_GBs") else None),
             "esim_TFLOPs": round(att_flops / per["esim_attention"] / 1e9, 1),
             "esim_mfma_frac_of_2500TF": round(att_flops / per["esim_attention"] / 1e9 / 2500, 4),
             "mlp_TFLOPs": round(mlp_flops / per["mlp_scorer"] / 1e9, 1),
@@ -900,6 +939,144 @@ def bench_pipe(args, enc, specs, multi):
                           f"{thr} reader threads, pinned ring of 3, side-stream H2D, fused encoder consumes; end-to-end legs read "
                           f"the file list twice; "
                           f"decode_* = host C++ parse alone on the GZIP files"}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _event_ms(fn, reps, warmup=3):
+    """Mean ms per call of fn(i) over `reps` calls, HIP events on the current stream."""
+    import torch
+
+    for i in range(warmup):
+        fn(i)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for i in range(reps):
+        fn(warmup + i)
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def bench_probes(args):
+    """The ceilings the roofline is stated against, both from librf.so:
+      stream_copy_GBs       rf_stream_copy, float4 STREAM copy of 4 GiB (read + write bytes / time): the box's
+                            achievable streaming HBM rate, reported beside the 8 TB/s spec as roofline.peak_measured;
+      gather_copy_{R}B_GBs  rf_gather_probe: uniformly random R-byte rows of a `--probe-table-gb` table (far past the
+                            256 MiB Infinity Cache; a new row set every call) copied to a contiguous output, as many
+                            rows as one batch of the encoder reads (R = 128: cfg3's bf16 D=64 rows, 2 x 200 x 4096;
+                            R = 256: cfg2's fp32 D=64 rows, 2 x 439 x 4096), best of 4 / 8 / 16 rows in flight per
+                            team; bytes = read + write. gather_read_*: the same reads without the copy."""
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    res = {}
+    n = 4 << 30
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    ms = _event_ms(lambda i: L.call("rf_stream_copy", L.ptr(src), L.ptr(dst), n, L.stream_ptr()), 10)
+    res["stream_copy_GBs"] = round(2 * n / ms / 1e6, 1)
+    res["stream_copy_bytes"] = n
+    del src, dst
+    torch.cuda.empty_cache()
+    tb = int(args.probe_table_gb * (1 << 30)) // 512 * 512
+    table = torch.empty(tb, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(4, dtype=torch.int32, device="cuda")
+    res["table_bytes"] = tb
+    for rb, nread in ((128, 2 * 200 * args.batch), (256, 2 * 439 * args.batch)):
+        out = torch.empty(nread * rb, dtype=torch.uint8, device="cuda")
+        for mode, o in (("copy", out), ("read", None)):
+            best, best_g = 0.0, None
+            for g in (4, 8, 16):
+                ms = _event_ms(lambda i, g=g, o=o: L.call("rf_gather_probe", L.ptr(table), tb // rb, rb, nread, g,
+                                                        0x5eed0000 + 977 * i + g, L.ptr(o), L.ptr(sink), L.stream_ptr()), 10)
+                gbs = nread * rb * (2 if o is not None else 1) / ms / 1e6
+                if gbs > best:
+                    best, best_g = gbs, g
+            res[f"gather_{mode}_{rb}B_GBs"] = round(best, 1)
+            res[f"gather_{mode}_{rb}B_in_flight"] = best_g
+        res[f"gather_{rb}B_rows_per_call"] = nread
+        del out
+    del table, sink
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_uniform(args, enc, multi, rank, out):
+    """The headline kernel on uniformly random ids over [1, 1e6] instead of Zipf(1.1) (the
+    no-locality worst case): same slots, table, batch and timing protocol (50 warm-up launches, HIP events)."""
+    import torch
+
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    host = [synthetic_batch(args.batch, multi, seed=91234 + rank * 1000 + i, uniform=True) for i in range(args.batches)]
+    dev = [h.to("cuda") for h in host]
+    algo = [enc.algorithmic_bytes(h) for h in host]
+    for i in range(args.warmup):
+        enc(dev[i % len(dev)], out=out)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    for i in range(args.steps):
+        ev[i][0].record()
+        enc(dev[i % len(dev)], out=out)
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    k = sum(a.elapsed_time(b) for a, b in ev) / args.steps / 1e3
+    by = sum(algo[i % len(algo)] for i in range(args.steps)) / args.steps
+    ach = by / k / 1e9
+    res = {"ids": "uniform [1, 1e6]", "kernel_ms": round(k * 1e3, 4), "examples_per_s_kernel": round(args.batch / k, 1),
+           "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_launch": int(by)}
+    del dev
+    return res
+
+
+def bench_cfg1(args):
+    """cfg1 (BASELINE.json configs[0]): demo_conf.yaml two-tower matching end to end — 4096 synthetic examples
+    of its working features written as GZIP TFRecord by the build's writer (make_tfrecord.py:142), read back by
+    FeaturePipe (device parse), scored by ConfTwoTower (get_preprocess_layers operators + BN/selu towers).
+    Plumbing: the rate is dominated by the tiny batches and the per-batch host work; parity is tested in
+    tests/test_cfg1_gpu.py."""
+    import shutil
+    import tempfile
+
+    import torch
+
+    from recommendflow_amd.config_parser.configuration import Configuration
+    from recommendflow_amd.models.matching.two_tower import ConfTwoTower
+    from recommendflow_amd.runtime import tfrecord as T
+    from recommendflow_amd.runtime.batch import synthetic_demo_rows
+
+    conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "demo_conf.yaml"))
+    specs = T.build_feature_description(conf)
+    n, B = 4096, 1024
+    tmp = tempfile.mkdtemp(prefix="rf_cfg1_", dir="/tmp")
+    try:
+        path = os.path.join(tmp, "demo-part-0.tfrecord.gz")
+        data, off = T.encode_examples(specs, T.columns_from_rows(specs, synthetic_demo_rows(n, 2024)))
+        with T.TFRecordWriter(path, "GZIP") as w:
+            w.write_many(data, off)
+        model = ConfTwoTower(conf, seed=1)
+
+        def run():
+            pipe = T.FeaturePipe([path], specs, B, thread_num=1, compression_type="GZIP", parse="device")
+            m = 0
+            for fb in pipe:
+                model(fb)
+                m += fb.batch
+            torch.cuda.synchronize()
+            pipe.close()
+            return m
+
+        run()
+        t0 = time.perf_counter()
+        m = run()
+        dt = time.perf_counter() - t0
+        return {"examples_per_s": round(m / dt, 1), "examples": m, "batch": B, "file_bytes": os.path.getsize(path),
+                "config": "demo_conf.yaml working features (2 user + 3 ad incl. app_id hashing 3000x16 sum), GZIP "
+                          "TFRecord -> FeaturePipe(device parse) -> ConfTwoTower towers [64, 32] selu/BN fp32, l2norm, dot"}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

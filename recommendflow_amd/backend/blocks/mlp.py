@@ -14,6 +14,24 @@ from ...runtime import lib as L
 from ..layers.core import Dense, Norm, act_name
 
 
+def _param_key(ts):
+    """Cache key of a folded-weight entry: the source tensors themselves (strong references, so a freed
+    tensor's id can never be reused by a replacement) with their in-place versions."""
+    return tuple((t, t._version) if isinstance(t, torch.Tensor) else t for t in ts)
+
+
+def _same_key(a, b) -> bool:
+    if a is None or b is None or len(a) != len(b):
+        return False
+    for x, y in zip(a, b):
+        if isinstance(x, tuple) and isinstance(y, tuple):
+            if x[0] is not y[0] or x[1] != y[1]:
+                return False
+        elif x != y:
+            return False
+    return True
+
+
 class MLP(torch.nn.Module):
     def __init__(self, hidden_units: Sequence[int], dropout_rate: float, activation, normalization_layer,
                  name: Optional[str] = None, in_features: Optional[int] = None, dtype=torch.bfloat16, seed: int = 0,
@@ -111,15 +129,15 @@ class MLP(torch.nn.Module):
 
     def _ln_folded(self, i: int):
         """(W diag(gamma) in bf16, s = its row sums, t = W beta + b) of denses[i] behind LayerNorm norms[i];
-        cached until a parameter changes (tensor identity or in-place version)."""
+        cached until a parameter changes (replaced tensor or in-place version)."""
         n, d = self.norms[i], self.denses[i]
         ts = (d.weight, d.bias, n.gamma, n.beta)
-        key = ("ln",) + tuple((id(t), t._version) if t is not None else None for t in ts)
+        key = _param_key(ts)
         cache = getattr(self, "_fold_cache", None)
         if cache is None:
             cache = self._fold_cache = {}
         hit = cache.get(("ln", i))
-        if hit is not None and hit[0] == key:
+        if hit is not None and _same_key(hit[0], key):
             return hit[1]
         w64 = d.weight.double()
         wg = (w64 * n.gamma.double()[None, :]).to(torch.bfloat16).contiguous()
@@ -134,12 +152,12 @@ class MLP(torch.nn.Module):
         changes (tensor identity or in-place version)."""
         n, d = self.norms[i], self.denses[i]
         ts = (d.weight, d.bias, n.gamma, n.beta)
-        key = ("aff",) + tuple((id(t), t._version) if t is not None else None for t in ts)
+        key = _param_key(ts)
         cache = getattr(self, "_fold_cache", None)
         if cache is None:
             cache = self._fold_cache = {}
         hit = cache.get(("aff", i))
-        if hit is not None and hit[0] == key:
+        if hit is not None and _same_key(hit[0], key):
             return hit[1]
         w64 = d.weight.double()
         w = (w64 * n.gamma.double()[None, :]).to(d.dtype).contiguous()
@@ -152,15 +170,15 @@ class MLP(torch.nn.Module):
         affine x a + c (a = gamma / sqrt(var + eps), c = beta - mean a), so
             BN(x) W^T + b = x (W diag(a))^T + (W c + b)
         and the GEMM reads the raw activations: the [M, K] normalisation pass (and its HBM round trip)
-        disappears. Cached until a parameter changes (tensor identity or in-place version)."""
+        disappears. Cached until a parameter changes (replaced tensor or in-place version)."""
         n, d = self.norms[i], self.denses[i]
         ts = (d.weight, d.bias, n.gamma, n.beta, n.mean, n.var)
-        key = tuple((id(t), t._version) if t is not None else None for t in ts) + (n.eps,)
+        key = _param_key(ts + (n.eps,))
         cache = getattr(self, "_fold_cache", None)
         if cache is None:
             cache = self._fold_cache = {}
         hit = cache.get(i)
-        if hit is not None and hit[0] == key:
+        if hit is not None and _same_key(hit[0], key):
             return hit[1], hit[2]
         a = n.gamma.double() / torch.sqrt(n.var.double() + n.eps)
         c = n.beta.double() - n.mean.double() * a

@@ -178,3 +178,23 @@ def synthetic_batch(batch: int, multivalued: Sequence[bool], seed: int = 1234, z
     np.cumsum(flat, out=bag_off[1:])
     lmax = lens.max(axis=0).astype(np.int32) if batch else np.zeros(S, np.int32)
     return SparseBatch(tok_bytes, tok_off, bag_off, lmax, batch, S)
+
+
+def synthetic_demo_rows(n: int, seed: int = 1234, missing: float = 0.05):
+    """cfg1 rows (BASELINE.json configs[0]: conf/demo_conf.yaml's working features) as per-example
+    dicts for runtime.tfrecord.columns_from_rows: app_id "app{id}", id ~ Zipf(1.1) over 5,000, a `missing`
+    share written as "-1" -> b"" (utils/make_tfrecord.py:40); query / app_name token ids: 8 ints ~ U[1, 21128),
+    segment ids 8 ints in {0, 1}; label ~ Bernoulli(0.1); down ~ U(0, 1) float32."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for _ in range(n):
+        z = int(rng.zipf(1.1))
+        while z > 5000:
+            z = int(rng.zipf(1.1))
+        app = "" if rng.random() < missing else f"app{z}"
+        rows.append({
+            "query_tok_id": rng.integers(1, 21128, 8).tolist(), "query_seg_id": rng.integers(0, 2, 8).tolist(),
+            "app_name_tok_id": rng.integers(1, 21128, 8).tolist(), "app_name_seg_id": rng.integers(0, 2, 8).tolist(),
+            "app_id": [app], "label": float(rng.random() < 0.1), "down": float(np.float32(rng.random())),
+        })
+    return rows

@@ -35,7 +35,13 @@ class StaticSparseBatch(SparseBatch):
                          torch.zeros(like.batch * like.n_slots + 1, dtype=torch.int32, device=device),
                          torch.zeros(like.n_slots, dtype=torch.int32, device=device), like.batch, like.n_slots)
         self.n_tok_live = 0
+        self.single_token_capture = False
         self.load(like)
+        # FusedSparseEncoder picks the single-token kernel (RF_FLAG_SINGLE_TOKEN) from the host Lmax of the
+        # batch it sees, so a graph captured on this batch bakes that choice in: remember it, and refuse a
+        # later batch the single-token kernel cannot pool (load below)
+        hl = self.host_lmax
+        self.single_token_capture = hl is not None and len(hl) > 0 and int(max(hl)) <= 1
 
     @property
     def n_tokens(self) -> int:  # the live batch's token count (the buffers hold capacity)
@@ -46,6 +52,12 @@ class StaticSparseBatch(SparseBatch):
             return self
         if b.batch != self.batch or b.n_slots != self.n_slots:
             raise ValueError(f"static batch is B={self.batch} x {self.n_slots} slots, got B={b.batch} x {b.n_slots}")
+        if self.single_token_capture:
+            hl = b.lmax if not b.is_device() else b.host_lmax
+            if hl is None or (len(hl) and int(max(hl)) > 1):
+                raise ValueError("this static batch was captured on a batch whose slots hold at most one token "
+                                 "(single-token kernel); a batch with Lmax > 1 (or without a host copy of lmax) "
+                                 "needs a graph captured on a multi-token batch")
         nb, nt = int(len(b.tok_bytes)), b.n_tokens
         if nb > self.tok_bytes.numel() or nt + 1 > self.tok_off.numel():
             raise ValueError(f"batch needs {nb} token bytes / {nt} tokens; capacity {self.tok_bytes.numel()} / "

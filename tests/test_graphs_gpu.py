@@ -61,3 +61,23 @@ def test_static_batch_and_captured_graph(cuda):
     x.add_(1.0)
     cg.replay()
     assert torch.equal(y, (torch.arange(1024, device="cuda") + 1.0) * 2.0)
+
+
+def test_single_token_capture_refuses_multi_token_batch(cuda):
+    """a graph captured on an all-single-valued batch runs the single-token kernel; replaying a
+    batch with Lmax > 1 through it would pool that slot wrongly, so the load raises instead."""
+    B, D = 128, 16
+    us = [SlotSpec(f"u{i}", 3000, (2022, 2023)) for i in range(4)]
+    as_ = [SlotSpec(f"a{i}", 3000, (2022, 2023)) for i in range(5)]
+    m = Dssm(FusedSparseEncoder(us, D, seed=1), FusedSparseEncoder(as_, D, seed=2), units=(64, 32), seed=4)
+    single = (synthetic_batch(B, [False] * 4, seed=3).to("cuda"), synthetic_batch(B, [False] * 5, seed=4).to("cuda"))
+    single2 = (synthetic_batch(B, [False] * 4, seed=5).to("cuda"), synthetic_batch(B, [False] * 5, seed=6).to("cuda"))
+    fwd = m.graphed(*single)
+    assert torch.equal(fwd(*single2), m(*single2))
+    multi = synthetic_batch(B, [True, False, False, False], seed=7).to("cuda")
+    with pytest.raises(ValueError, match="single-token"):
+        fwd(multi, single[1])
+    # captured on a multi-token batch: single-valued batches replay through the general kernel, which
+    # pools them bit-identically to the single-token kernel the eager forward picks
+    fwd2 = m.graphed(multi, single[1])
+    assert torch.equal(fwd2(*single2), m(*single2))

@@ -1,0 +1,72 @@
+"""Timed-window summary of the headline kernel from a rocprofv3 kernel trace.
+
+usage: python tools/headline_summary.py <rocprofv3 output dir> <bench line json> [--warmup 50] [--steps 100]
+
+Picks the launches of the headline kernel (fused_hash_embed_kernel) with the headline grid (the grid of the
+first such launch: the bench's headline leg runs first), takes them in dispatch order, and reports the
+average duration over the bench's timed window (launches warmup .. warmup + steps - 1), over the warm-up,
+and over every launch of that shape; then the roofline fraction recomputed from the bench line's algorithmic
+bytes per launch. Output: plain text on stdout (committed under profiles/rNN/).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("bench_json")
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--kernel", default="fused_hash_embed_kernel")
+    ap.add_argument("--peak", type=float, default=8000.0)
+    a = ap.parse_args()
+    files = sorted(glob.glob(os.path.join(a.prof_dir, "**", "*kernel_trace.csv"), recursive=True))
+    if not files:
+        raise SystemExit(f"no *kernel_trace.csv under {a.prof_dir}")
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if a.kernel in r["Kernel_Name"]:
+                    rows.append(r)
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    if not rows:
+        raise SystemExit(f"no {a.kernel} launches")
+    grid = rows[0]["Grid_Size_X"] if "Grid_Size_X" in rows[0] else rows[0].get("Grid_Size")
+    gkey = "Grid_Size_X" if "Grid_Size_X" in rows[0] else "Grid_Size"
+    head = [r for r in rows if r[gkey] == grid]
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in head]
+    win = dur[a.warmup:a.warmup + a.steps]
+    line = None
+    with open(a.bench_json) as fh:
+        for ln in fh:
+            ln = ln.strip()
+            if ln.startswith("{") and '"metric"' in ln:
+                line = json.loads(ln)
+    print(f"headline kernel {head[0]['Kernel_Name'][:120]}")
+    print(f"grid {grid}; trace files: {len(files)}; launches of this shape: {len(head)}")
+    print(f"timed window (launches {a.warmup}..{a.warmup + len(win) - 1}): average {statistics.mean(win):.2f} us, "
+          f"median {statistics.median(win):.2f} us, min {min(win):.2f}, max {max(win):.2f}")
+    if a.warmup:
+        print(f"warm-up launches 0..{a.warmup - 1}: average {statistics.mean(dur[:a.warmup]):.2f} us")
+    print(f"all {len(dur)} launches of this shape: average {statistics.mean(dur):.2f} us")
+    if line is not None:
+        rl = line.get("roofline", {})
+        by = rl.get("algorithmic_bytes_per_launch")
+        if by:
+            ach = by / (statistics.mean(win) * 1e-6) / 1e9
+            print(f"bench line (same command, un-profiled run): kernel_ms {rl.get('kernel_ms')}, achieved {rl.get('achieved')} "
+                  f"GB/s, frac {rl.get('frac')}")
+            print(f"recomputed from the trace: {by} B / {statistics.mean(win):.2f} us = {ach:.1f} GB/s = "
+                  f"{ach / a.peak:.4f} of {a.peak:.0f} GB/s"
+                  + (f" = {ach / rl['peak_measured']:.4f} of the measured STREAM-copy peak {rl['peak_measured']} GB/s"
+                     if rl.get("peak_measured") else ""))
+
+
+if __name__ == "__main__":
+    main()
