@@ -451,13 +451,15 @@ int rf_attention_fusion_fwd(const float* x, int32_t batch, int32_t channels, int
 
 /*
  * Measurement probes (not a reference operator: the ceilings SURVEY §8d states the hot path against).
- * rf_stream_copy: dst = src, n_bytes % 16 == 0, 16-byte aligned; float4 STREAM copy (2 * n_bytes of HBM traffic).
+ * rf_stream_copy: dst = src, n_bytes % 16 == 0, 16-byte aligned; float4 STREAM copy (2 * n_bytes of HBM traffic);
+ * variant 0: 4 float4 per lane, one pass per block; 1: 8 per lane; 2: as 0 with nontemporal loads/stores;
+ * 3: nontemporal, persistent grid of 2048 blocks.
  * rf_gather_probe: n uniformly random rows (row r_i = mulhi(splitmix64(seed ^ i), rows), no index array) of
  * row_bytes (64/128/256/512) from table [rows][row_bytes], in_flight (4/8/16) rows per team of row_bytes/16
  * lanes; out != NULL: row i is copied to out[i] (the fused encoder's read-random / write-streaming shape),
  * else only read (sink: one device word, written only on an impossible value).
  */
-int rf_stream_copy(const void* src, void* dst, int64_t n_bytes, void* stream);
+int rf_stream_copy(const void* src, void* dst, int64_t n_bytes, int32_t variant, void* stream);
 int rf_gather_probe(const void* table, int64_t rows, int32_t row_bytes, int64_t n, int32_t in_flight, uint64_t seed,
                     void* out, uint32_t* sink, void* stream);
 

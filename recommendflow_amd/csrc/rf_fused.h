@@ -111,6 +111,20 @@ __device__ __forceinline__ uint4 row_chunk(const TT* __restrict__ table, uint32_
     return *reinterpret_cast<const uint4*>(table + (int64_t)r * dim + (int64_t)c * Elem<TT>::EPV);
 }
 
+// PRE (rf_pool_rows_fwd): a row id with bit 31 set is row (r & 0x7fffffff) of the caller's LOCAL table
+// (the rank's own shard: rows it owns are read in place instead of travelling through the receive buffer),
+// any other id a row of the gathered buffer. One select per row load; with local == nullptr no id has bit 31.
+template <bool PRE, typename TT>
+__device__ __forceinline__ uint4 row_chunk_src(const TT* __restrict__ table, const TT* __restrict__ local, uint32_t r,
+                                               int dim, int c) {
+    if constexpr (PRE) {
+        const bool loc = (r & 0x80000000u) != 0u;
+        return row_chunk(loc ? local : table, r & 0x7fffffffu, dim, c);
+    } else {
+        return row_chunk(table, r, dim, c);
+    }
+}
+
 // Slot-major items: item = (slot s, examples b0 .. b0+kUnits-1). Every unit of an item shares the slot's
 // combiner, Lmax, salts, table segments and pad rows — all wave-uniform (scalar loads, one pad-row
 // prefetch per item) — and unit lengths follow one distribution, so the teams stay balanced.
@@ -157,6 +171,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
     // PRE: tok_bytes is unused and tok_off carries the optional row map (logical row j of the pre-gathered
     // buffer lives at row_map[j]; nullptr = identity) — rf_pool_rows_fwd's un-permute, fused into the loads
     const int32_t* row_map = PRE ? tok_off : nullptr;
+    // PRE: tok_bytes carries the rank-local table (row ids with bit 31 set), or nullptr
+    const TT* local_tab = PRE ? reinterpret_cast<const TT*>(tok_bytes) : nullptr;
     const int batch = (int)(n_units / n_slots);
     const int nbb = (batch + kUnits - 1) / kUnits;
     const int64_t n_items = (int64_t)n_slots * nbb;
@@ -302,8 +318,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     const uint32_t r1 = has[g] ? s_row[wave][1][i] : pad1;
 #pragma unroll
                     for (int cc = 0; cc < CPL; ++cc) {
-                        v[g][0][cc] = row_chunk(table, r0, dim, cidx[cc]);
-                        v[g][1][cc] = row_chunk(table, r1, dim, cidx[cc]);
+                        v[g][0][cc] = row_chunk_src<PRE>(table, local_tab, r0, dim, cidx[cc]);
+                        v[g][1][cc] = row_chunk_src<PRE>(table, local_tab, r1, dim, cidx[cc]);
                     }
                 }
 #pragma unroll
@@ -353,8 +369,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         uint4 padv[2][CPL];
 #pragma unroll
         for (int cc = 0; cc < CPL; ++cc) {
-            padv[0][cc] = row_chunk(table, pad0, dim, cidx[cc]);
-            padv[1][cc] = row_chunk(table, pad1, dim, cidx[cc]);
+            padv[0][cc] = row_chunk_src<PRE>(table, local_tab, pad0, dim, cidx[cc]);
+            padv[1][cc] = row_chunk_src<PRE>(table, local_tab, pad1, dim, cidx[cc]);
         }
         const float init = comb_init(comb);
         int j = ja, ubeg = 0, uend = 0, Lu = 0;
@@ -495,8 +511,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                     const uint32_t r0 = s_row[wave][0][i], r1 = s_row[wave][1][i];
 #pragma unroll
                     for (int cc = 0; cc < CPL; ++cc) {
-                        v[q][0][cc] = row_chunk(table, r0, dim, cidx[cc]);
-                        v[q][1][cc] = row_chunk(table, r1, dim, cidx[cc]);
+                        v[q][0][cc] = row_chunk_src<PRE>(table, local_tab, r0, dim, cidx[cc]);
+                        v[q][1][cc] = row_chunk_src<PRE>(table, local_tab, r1, dim, cidx[cc]);
                     }
                 }
             };
@@ -552,8 +568,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                 uint4 v[2][CPL];
 #pragma unroll
                 for (int cc = 0; cc < CPL; ++cc) {
-                    v[0][cc] = row_chunk(table, r0, dim, cidx[cc]);
-                    v[1][cc] = row_chunk(table, r1, dim, cidx[cc]);
+                    v[0][cc] = row_chunk_src<PRE>(table, local_tab, r0, dim, cidx[cc]);
+                    v[1][cc] = row_chunk_src<PRE>(table, local_tab, r1, dim, cidx[cc]);
                 }
                 consume(v, i - ubeg);
             }

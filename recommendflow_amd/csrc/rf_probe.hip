@@ -1,32 +1,44 @@
 // rf_probe.hip — measurement probes that state the ceilings the hot-path kernels are judged against
 // (SURVEY §8d "Peak: the measured STREAM-copy bandwidth on the box"). Not on the
 // hot path; the bench calls them beside the headline.
-//   rf_stream_copy   float4 STREAM copy dst = src: the box's achievable HBM rate for a streaming kernel
+//   rf_stream_copy   float4 STREAM copy dst = src (4 variants: lanes' depth, nontemporal, persistent grid; the bench
+//                    reports the best): the box's achievable HBM rate for a streaming kernel
 //   rf_gather_probe  uniformly random whole-row reads (optionally copied out contiguously): the achievable
 //                    rate of the fused encoder's access pattern (random 128-/256-B rows, streaming output)
 //                    from a table far larger than the 256 MiB Infinity Cache
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rf_common.h"
 
 namespace {
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+
 // Every lane moves U float4 per pass, all loads issued before the first store (U * 16 B in flight per lane).
-template <int U>
-__global__ __launch_bounds__(256) void stream_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
-                                                          int64_t n4) {
-    const int64_t base = (int64_t)blockIdx.x * (256 * U) + threadIdx.x;
-    if (base + (int64_t)(U - 1) * 256 < n4) {
-        float4 v[U];
+// NT: nontemporal loads / stores (streamed once, no reuse). GRID > 0: a persistent grid of GRID blocks strides
+// over the buffer; GRID == 0: one pass per block.
+template <int U, bool NT, int GRID>
+__global__ __launch_bounds__(256) void stream_copy_kernel(const v4f* __restrict__ src, v4f* __restrict__ dst, int64_t n4) {
+    const int64_t step = GRID > 0 ? (int64_t)gridDim.x * 256 * U : 0;
+    for (int64_t base = (int64_t)blockIdx.x * (256 * U) + threadIdx.x; base < n4; base += step) {
+        if (base + (int64_t)(U - 1) * 256 < n4) {
+            v4f v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = src[base + u * 256];
+            for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + base + u * 256) : src[base + u * 256];
 #pragma unroll
-        for (int u = 0; u < U; ++u) dst[base + u * 256] = v[u];
-    } else {
-        for (int u = 0; u < U; ++u) {
-            const int64_t i = base + u * 256;
-            if (i < n4) dst[i] = src[i];
+            for (int u = 0; u < U; ++u) {
+                if (NT) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+                else dst[base + u * 256] = v[u];
+            }
+        } else {
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = base + u * 256;
+                if (i < n4) dst[i] = src[i];
+            }
         }
+        if (GRID == 0) break;
     }
 }
 
@@ -96,17 +108,26 @@ int launch_gather_g(int g, const void* table, int64_t rows, int64_t n, uint64_t 
 
 }  // namespace
 
-extern "C" int rf_stream_copy(const void* src, void* dst, int64_t n_bytes, void* stream) {
+extern "C" int rf_stream_copy(const void* src, void* dst, int64_t n_bytes, int32_t variant, void* stream) {
     RF_REQUIRE(n_bytes >= 0 && n_bytes % 16 == 0, "rf_stream_copy: n_bytes must be a multiple of 16");
+    RF_REQUIRE(variant >= 0 && variant <= 3, "rf_stream_copy: variant must be 0..3");
     if (n_bytes == 0) return RF_OK;
     RF_REQUIRE(src && dst && ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0),
                "rf_stream_copy: 16-byte aligned src and dst required");
-    constexpr int U = 4;
     const int64_t n4 = n_bytes / 16;
-    const int64_t blocks = (n4 + 256 * U - 1) / (256 * U);
-    RF_REQUIRE(blocks < (1ll << 31), "rf_stream_copy: too large");
-    hipLaunchKernelGGL(stream_copy_kernel<U>, dim3((unsigned)blocks), dim3(256), 0, rf_stream(stream),
-                       (const float4*)src, (float4*)dst, n4);
+    const hipStream_t st = rf_stream(stream);
+    const v4f* s4 = (const v4f*)src;
+    v4f* d4 = (v4f*)dst;
+    auto one_pass = [&](int U) {
+        const int64_t b = (n4 + 256 * U - 1) / (256 * U);
+        return (unsigned)std::min<int64_t>(b, (int64_t)1 << 30);
+    };
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((stream_copy_kernel<4, false, 0>), dim3(one_pass(4)), dim3(256), 0, st, s4, d4, n4); break;
+        case 1: hipLaunchKernelGGL((stream_copy_kernel<8, false, 0>), dim3(one_pass(8)), dim3(256), 0, st, s4, d4, n4); break;
+        case 2: hipLaunchKernelGGL((stream_copy_kernel<4, true, 0>), dim3(one_pass(4)), dim3(256), 0, st, s4, d4, n4); break;
+        default: hipLaunchKernelGGL((stream_copy_kernel<4, true, 1>), dim3(256 * 8), dim3(256), 0, st, s4, d4, n4); break;
+    }
     return rf_check_launch("stream_copy_kernel");
 }
 

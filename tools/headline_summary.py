@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--kernel", default="fused_hash_embed_kernel")
     ap.add_argument("--peak", type=float, default=8000.0)
+    ap.add_argument("--write-trace", default=None, help="write the headline-shape launches' trace rows here (CSV)")
     a = ap.parse_args()
     files = sorted(glob.glob(os.path.join(a.prof_dir, "**", "*kernel_trace.csv"), recursive=True))
     if not files:
@@ -41,6 +42,14 @@ def main():
     gkey = "Grid_Size_X" if "Grid_Size_X" in rows[0] else "Grid_Size"
     head = [r for r in rows if r[gkey] == grid]
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in head]
+    if a.write_trace:
+        keep = [k for k in ("Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp", gkey, "Workgroup_Size_X",
+                            "LDS_Block_Size", "VGPR_Count", "SGPR_Count") if k in head[0]]
+        with open(a.write_trace, "w", newline="") as fh:
+            wr = csv.writer(fh)
+            wr.writerow(keep + ["duration_us"])
+            for r, d in zip(head[:a.warmup + a.steps], dur):
+                wr.writerow([r[k] for k in keep] + [f"{d:.3f}"])
     win = dur[a.warmup:a.warmup + a.steps]
     line = None
     with open(a.bench_json) as fh:
