@@ -524,9 +524,11 @@ def bench_dssm(args, enc, host):
 def bench_sharded(args, specs, multi, rank, world):
     """cfg4, weak scaling: the cfg2 slot layout over a row-sharded fused fp32 table of
     shard_rows x P rows x shard_dim (owner = row mod P), shard_batch examples per GPU. One step =
-    route (hash rows + owner bucketize) -> all-to-all ids -> gather local rows -> all-to-all vectors ->
-    un-permute + pool. Bit-identical to the unsharded kernel (tests/test_sharded_gpu.py). All ranks run;
-    value = examples of all ranks / max-over-ranks time."""
+    route (hash rows; hash-table dedup of the rows other ranks own; the counts' all-to-all and ONE host read)
+    -> all-to-all ids -> owners gather -> all-to-all vectors -> pool (this rank's own rows read in place from
+    its shard, the others from the receive buffer through the row map). Bit-identical to the unsharded kernel
+    (tests/test_sharded_gpu.py). All ranks run; value = examples of all ranks / max-over-ranks time. Also
+    the pipelined forward (2 micro-batches, async all-to-alls overlapping the other micro-batch's stages)."""
     import torch
     import torch.distributed as dist
 
@@ -540,24 +542,23 @@ def bench_sharded(args, specs, multi, rank, world):
     sp = [SlotSpec(s.name, n_bins, s.seeds, s.combiner, s.mask_empty) for s in specs]
     comm = TorchDistComm() if world > 1 else LocalComm()
     enc = ShardedFusedEncoder(sp, D, rank, P, comm=comm, seed=2024)
-    batches = [synthetic_batch(B, multi, seed=4321 + 1000 * rank + i).to("cuda") for i in range(2)]
+    host_b = [synthetic_batch(B, multi, seed=4321 + 1000 * rank + i) for i in range(2)]
+    batches = [h.to("cuda") for h in host_b]
     out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
     ev_names = ["route", "a2a_ids", "gather", "a2a_rows", "pool"]
     st = {}
 
     def step(i, ev=None):
         b = batches[i % 2]
-        r = enc.route(b)
+        r, recv = enc.route_exchange(b, local_fast=enc.local_fast)  # hash route + counts exchange, one host sync
         if ev: ev[1].record()
-        counts_t = torch.tensor(r.counts, dtype=torch.int64, device="cuda")
-        recv = [int(c) for c in comm.exchange_counts(counts_t).cpu().tolist()]
         wanted = comm.exchange(r.local, r.counts, recv)
         if ev: ev[2].record()
         vec = enc.serve(wanted)
         if ev: ev[3].record()
         back = comm.exchange(vec, recv, r.counts)
         if ev: ev[4].record()
-        enc.combine(b, r, back, out)
+        enc.combine(b, r, back, out, local_fast=enc.local_fast)
         if ev: ev[5].record()
         st["req"], st["served"], st["logical"] = r.n_requests, int(wanted.shape[0]), r.n_logical
 
@@ -565,35 +566,53 @@ def bench_sharded(args, specs, multi, rank, world):
     for i in range(3):
         step(i)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def staged(i):
         evs[i][0].record()
         step(i, evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+
+    el = timed(staged)
     stage = {n: round(sum(e[k].elapsed_time(e[k + 1]) for e in evs) / steps, 4) for k, n in enumerate(ev_names)}
+    # the pipelined forward: 2 micro-batches, all-to-alls on RCCL's stream beside the other micro-batch's stages
+    from recommendflow_amd.runtime.batch import split_examples
+
+    micro = [[m.to("cuda") for m in split_examples(h, 2)] for h in host_b]
+    mouts = [torch.empty((m.batch, enc.out_width), dtype=torch.float32, device="cuda") for m in micro[0]]
+    for i in range(2):
+        enc.forward_pipelined(micro[i % 2], mouts)
+    el_pipe = timed(lambda i: enc.forward_pipelined(micro[i % 2], mouts))
     row_b = D * 4
     xgmi = (st["req"] * (8 + row_b)) * (P - 1) / P if P > 1 else 0
     res = {"examples_per_s": round(B * P * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
-           "stage_ms_rank0": stage, "gather_GBs": round(st["served"] * (2 * row_b + 8) / stage["gather"] / 1e6, 1),
+           "pipelined_examples_per_s": round(B * P * steps / el_pipe, 1),
+           "pipelined_ms_per_step": round(el_pipe / steps * 1e3, 4),
+           "stage_ms_rank0": stage, "gather_GBs": round(st["served"] * (2 * row_b + 8) / max(stage["gather"], 1e-6) / 1e6, 1),
            "a2a_bytes_per_rank_each_way": int(xgmi),
            "rows_read_by_pool": st["logical"], "rows_requested_after_dedup": st["req"],
-           "dedup_factor": round(st["logical"] / max(st["req"], 1), 3),
+           "rows_pooled_in_place": st["logical"] - st["req"] if P == 1 else None,
+           "route": enc.route_mode + (" + local rows pooled in place" if enc.local_fast else ""),
            "config": f"cfg2 slots ({S}) over a {enc.table_rows}x{D} fp32 fused table row-sharded over {P} GPU(s) "
                      f"({enc.local_rows} rows/GPU), {B} examples/GPU (global {B * P}), owner = row mod P, "
-                     f"per-step row dedup, RCCL all_to_all_single for ids and rows"}
+                     f"hash-table dedup of the remote rows, this rank's rows pooled in place, RCCL all_to_all_single "
+                     f"for ids and rows; pipelined = 2 micro-batches with async all-to-alls"}
     if not args.no_shard_train:
         res["train_step"] = bench_sharded_train(args, enc, batches, out, world)
-    del enc, batches, out
+    del enc, batches, out, micro, mouts
     torch.cuda.empty_cache()
     return res
 

@@ -289,10 +289,13 @@ int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* to
  * (bin 0 of the segment, or the bin of b"" when mask_empty == 0). Descriptors supply combiner, out_off, dim.
  * row_map (int32 [2*n_tok + 2*n_slots], may be NULL = identity): logical row j is read from gathered row
  * row_map[j] — pass rf_bucketize_owner's inv_perm to pool straight from the all-to-all receive buffer.
+ * local_table (may be NULL; same dtype/dim): a row_map entry with bit 31 set reads row (entry & 0x7fffffff) of
+ * local_table instead — the rank's own shard, so rows it owns are pooled in place (rf_route_hash_build).
  */
 int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
-                     int32_t batch, int64_t n_tok, const void* gathered, const int32_t* row_map, int32_t dtype,
-                     int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags, void* stream);
+                     int32_t batch, int64_t n_tok, const void* gathered, const int32_t* row_map,
+                     const void* local_table, int32_t dtype, int32_t dim, void* out, int32_t out_dtype,
+                     int64_t out_stride, int32_t flags, void* stream);
 
 /*
  * Route one step's row requests WITH dedup (the default requester stage of the sharded lookup; SURVEY
@@ -304,6 +307,21 @@ int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t
  * Deterministic (radix sort, no atomics). ws: rf_route_ws_bytes(n, P, table_rows) bytes, 256-B aligned.
  */
 size_t rf_route_ws_bytes(int64_t n, int32_t nranks, int64_t table_rows);
+/*
+ * The same routing by a hash-table dedup, in two calls around the host's read of the counts (the split sizes of
+ * the all-to-alls): rf_route_hash_build inserts every request's owner-major key into an open-addressing table
+ * (one atomicCAS per DISTINCT row; repeats find their key with a plain load) and writes counts[P] (distinct rows
+ * per owner, DEVICE int32). With rank >= 0 the rows that rank owns are NOT routed: row_map[j] = 0x80000000 |
+ * local for them (rf_pool_rows_fwd reads them from its local_table), counts[rank] = 0. rf_route_hash_finish
+ * (n_uniq = the sum of counts, from the host) sorts the distinct keys (radix over the key bits of the distinct
+ * set only) and writes local_out[0 .. n_uniq) in (owner, local) order and the remaining row_map entries, exactly
+ * as rf_route_rows would for the routed rows. Same ws for both calls: rf_route_hash_ws_bytes(n, P, table_rows).
+ */
+size_t rf_route_hash_ws_bytes(int64_t n, int32_t nranks, int64_t table_rows);
+int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nranks, int32_t rank, int64_t table_rows,
+                        int32_t* row_map, int32_t* counts, void* ws, size_t ws_bytes, void* stream);
+int rf_route_hash_finish(int64_t n, int32_t nranks, int64_t table_rows, int64_t n_uniq, int64_t* local_out,
+                         int32_t* row_map, void* ws, size_t ws_bytes, void* stream);
 int rf_route_rows(const int64_t* rows, int64_t n, int32_t nranks, int64_t table_rows, int32_t* counts,
                   int64_t* local_out, int32_t* row_map, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
 

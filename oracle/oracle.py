@@ -298,6 +298,20 @@ def route_rows(rows: np.ndarray, nranks: int, table_rows: int):
     return counts, local, row_map.astype(np.int32).reshape(-1)
 
 
+def route_rows_local(rows: np.ndarray, nranks: int, rank: int, table_rows: int):
+    """rf_route_hash_build + rf_route_hash_finish restated: as route_rows over the rows NOT owned by `rank`
+    (rank = -1: every row routed); a row the rank owns keeps row_map = 0x80000000 | local (int32 bits) and is
+    read in place from the rank's shard by rf_pool_rows_fwd. Returns (counts int32 [P], local int64, row_map)."""
+    rows = np.asarray(rows, np.int64)
+    ok = (rows >= 0) & (rows < table_rows)
+    own = ok & (rows % nranks == rank) if rank >= 0 else np.zeros(len(rows), bool)
+    counts, local, rm = route_rows(rows[~own], nranks, table_rows)
+    row_map = np.empty(len(rows), np.int32)
+    row_map[~own] = rm
+    row_map[own] = (np.uint32(0x80000000) | (rows[own] // nranks).astype(np.uint32)).view(np.int32)
+    return counts, local, row_map
+
+
 def bf16_to_f32(u16: np.ndarray) -> np.ndarray:
     return (np.asarray(u16, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
 

@@ -116,6 +116,26 @@ class GpuShardOps:
                L.ptr(ws), ws_bytes, L.stream_ptr(None))
         return counts, local, row_map[:n]
 
+    def route_hash_build(self, rows: torch.Tensor, nranks: int, rank: int, table_rows: int):
+        """rf_route_hash_build: -> (counts int32 [P] device, state for route_hash_finish). rank >= 0: rows that
+        rank owns are not routed (row_map = 0x80000000 | local, pooled in place from the shard)."""
+        n = rows.numel()
+        counts = torch.empty(nranks, dtype=torch.int32, device=self.device)
+        row_map = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        ws_bytes = int(L.load().rf_route_hash_ws_bytes(n, nranks, table_rows))
+        ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=self.device)
+        L.call("rf_route_hash_build", L.ptr(rows), n, nranks, rank, table_rows, L.ptr(row_map), L.ptr(counts), L.ptr(ws),
+               ws_bytes, L.stream_ptr(None))
+        return counts, (n, nranks, table_rows, row_map, ws, ws_bytes)
+
+    def route_hash_finish(self, state, n_uniq: int):
+        """rf_route_hash_finish -> (local int64 [n_uniq], row_map int32 [n])."""
+        n, nranks, table_rows, row_map, ws, ws_bytes = state
+        local = torch.empty(max(n_uniq, 1), dtype=torch.int64, device=self.device)
+        L.call("rf_route_hash_finish", n, nranks, table_rows, n_uniq, L.ptr(local), L.ptr(row_map), L.ptr(ws), ws_bytes,
+               L.stream_ptr(None))
+        return local[:n_uniq], row_map[:n]
+
     def gather(self, shard: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
         n = local.numel()
         out = torch.empty((max(n, 1), shard.shape[1]), dtype=shard.dtype, device=self.device)
@@ -125,17 +145,21 @@ class GpuShardOps:
         return out[:n]
 
     def pool(self, desc, n_slots: int, batch: SparseBatch, gathered: torch.Tensor, out: torch.Tensor, flags: int,
-             row_map: Optional[torch.Tensor] = None):
+             row_map: Optional[torch.Tensor] = None, local_table: Optional[torch.Tensor] = None):
+        if gathered.numel() == 0:  # every row is rank-local: any aligned buffer (never read)
+            gathered = local_table if local_table is not None and local_table.numel() else \
+                torch.empty((1, out.shape[1] if out.dim() == 2 else 4), dtype=out.dtype, device=self.device)
         L.call("rf_pool_rows_fwd", L.ptr(desc), n_slots, L.ptr(batch.bag_off), L.ptr(batch.lmax), batch.batch,
-               batch.n_tokens, L.ptr(gathered), L.ptr(row_map), L.torch_dtype_code(gathered.dtype), gathered.shape[1], L.ptr(out),
-               L.torch_dtype_code(out.dtype), out.stride(0), flags, L.stream_ptr(None))
+               batch.n_tokens, L.ptr(gathered), L.ptr(row_map), L.ptr(local_table), L.torch_dtype_code(gathered.dtype),
+               gathered.shape[1], L.ptr(out), L.torch_dtype_code(out.dtype), out.stride(0), flags, L.stream_ptr(None))
         return out
 
 
     # -- training -------------------------------------------------------------
     def pool_bwd(self, desc, n_slots: int, batch: SparseBatch, row_map: torch.Tensor, gathered: torch.Tensor,
-                 out: torch.Tensor, dout: torch.Tensor, flags: int, need_minmax: bool):
-        """rf_pool_rows_bwd -> (rows into `gathered` [U] ascending, grads [U, D])."""
+                 out: torch.Tensor, dout: torch.Tensor, flags: int, need_minmax: bool, sync: bool = True):
+        """rf_pool_rows_bwd -> (rows into `gathered` [U] ascending, grads [U, D]); sync=False: the capacity-sized
+        buffers and the DEVICE count (no host read: the caller folds it into its one synchronisation)."""
         lm = batch.lmax_numpy()
         n_pos = batch.batch * int(2 * np.asarray(lm, np.int64).sum())
         R = gathered.shape[0]
@@ -151,6 +175,8 @@ class GpuShardOps:
                batch.n_tokens, n_pos, L.ptr(row_map), L.ptr(gathered), R, D, L.ptr(out) if need_minmax else None,
                L.ptr(dout), dout.stride(0), flags, L.ptr(cnt), L.ptr(rows), L.ptr(grad), cap, L.ptr(n_uniq), L.ptr(ws),
                ws.numel(), L.stream_ptr(None))
+        if not sync:
+            return rows, grad, n_uniq
         n = int(n_uniq.item())
         if n < 0:
             raise ValueError(f"rf_pool_rows_bwd: invalid batch (error bits {-n})")
@@ -193,6 +219,14 @@ class TorchDistComm:
                                     group=self.group)
         return out
 
+    def exchange_async(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]):
+        """exchange() without waiting: (output, work). RCCL runs it on its own stream, ordered after the work
+        already queued on the current stream; work.wait() orders the current stream after it."""
+        out = torch.empty((sum(recv_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        work = self.dist.all_to_all_single(out, x.contiguous(), output_split_sizes=recv_splits,
+                                           input_split_sizes=send_splits, group=self.group, async_op=True)
+        return out, work
+
     def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
         """Every rank's rows concatenated in rank order (row counts may differ: padded to the largest)."""
         n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
@@ -226,6 +260,9 @@ class LocalComm:
     def exchange(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]) -> torch.Tensor:
         return x
 
+    def exchange_async(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]):
+        return x, None
+
     def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
         return x
 
@@ -247,7 +284,7 @@ class ShardedFusedEncoder(torch.nn.Module):
 
     def __init__(self, slots: Sequence[SlotSpec], dim: int, rank: int, nranks: int, comm=None, ops=None,
                  table_dtype=torch.float32, out_dtype=None, seed: int = 0, mask_padding: bool = False,
-                 init_range=(-0.05, 0.05), device="cuda", dedup: bool = True):
+                 init_range=(-0.05, 0.05), device="cuda", dedup: bool = True, route: str = "hash"):
         super().__init__()
         if not slots:
             raise ValueError("ShardedFusedEncoder needs at least one slot")
@@ -261,7 +298,12 @@ class ShardedFusedEncoder(torch.nn.Module):
         self.table_dtype = table_dtype
         self.out_dtype = out_dtype or table_dtype
         self.mask_padding = bool(mask_padding)
-        self.dedup = bool(dedup)  # send each distinct row once per step (rf_route_rows)
+        self.dedup = bool(dedup)  # send each distinct row once per step
+        if route not in ("hash", "radix"):
+            raise ValueError(f"route must be 'hash' or 'radix', got {route!r}")
+        # hash: rf_route_hash_build/finish (one atomic per distinct row, only the distinct set sorted) and the
+        # forward pools the rows this rank owns in place; radix: rf_route_rows (a sort of every request)
+        self.route_mode = route if self.dedup else "radix"
         self.host_desc, self.table_rows = build_slot_desc(self.slots, self.dim)
         self.out_width = 2 * self.dim * len(self.slots)
         self.desc = self.ops.upload_desc(self.host_desc)
@@ -290,14 +332,36 @@ class ShardedFusedEncoder(torch.nn.Module):
             local = local[: sum(counts)]  # rf_route_rows sizes the id buffer for the undeduplicated worst case
         return RouteState(counts, local, row_map, int(local.numel()), n_logical)
 
-    def route(self, batch: SparseBatch) -> RouteState:
+    def route(self, batch: SparseBatch, local_fast: bool = False) -> RouteState:
+        if self.route_mode == "hash":
+            st, _ = self._route_hash(batch, local_fast, exchange=False)
+            return st
         counts, local, row_map, n = self._route_device(batch)
         return self._route_state([int(c) for c in counts.cpu().tolist()], local, row_map, n)
 
-    def route_exchange(self, batch: SparseBatch):
+    def _route_hash(self, batch: SparseBatch, local_fast: bool, exchange: bool):
+        """hash route: build (device counts) -> [counts all-to-all] -> ONE host read of send (+ receive) counts
+        -> finish. local_fast: this rank's own rows stay out of the exchange (row_map bit 31)."""
+        rows = self.ops.hash_rows(self.desc, len(self.slots), batch)
+        req = torch.cat([rows, self.pad_rows])
+        counts, state = self.ops.route_hash_build(req, self.nranks, self.rank if local_fast else -1, self.table_rows)
+        counts = counts.to(torch.int64)
+        P = counts.numel()
+        if exchange:
+            recv = self.comm.exchange_counts(counts)
+            both = [int(c) for c in torch.cat([counts, recv.to(counts.device)]).cpu().tolist()]
+            send, recv_l = both[:P], both[P:]
+        else:
+            send, recv_l = [int(c) for c in counts.cpu().tolist()], None
+        local, row_map = self.ops.route_hash_finish(state, sum(send))
+        return RouteState(send, local, row_map, int(local.numel()), req.numel()), recv_l
+
+    def route_exchange(self, batch: SparseBatch, local_fast: bool = False):
         """route() plus the all-to-all of the per-owner counts with ONE host synchronisation: the counts
         stay on the device for the exchange, and the send and receive counts come back together (the
         split sizes of the id and row all-to-alls are host lists). -> (RouteState, recv_counts)."""
+        if self.route_mode == "hash":
+            return self._route_hash(batch, local_fast, exchange=True)
         counts, local, row_map, n = self._route_device(batch)
         recv = self.comm.exchange_counts(counts)
         both = [int(c) for c in torch.cat([counts, recv.to(counts.device)]).cpu().tolist()]
@@ -308,11 +372,18 @@ class ShardedFusedEncoder(torch.nn.Module):
         # rows beyond the shard come back NaN (rf_gather_rows), poisoning the pooled output loudly
         return self.ops.gather(self.shard, local_rows)
 
-    def combine(self, batch: SparseBatch, st: RouteState, back: torch.Tensor, out: Optional[torch.Tensor] = None):
+    def combine(self, batch: SparseBatch, st: RouteState, back: torch.Tensor, out: Optional[torch.Tensor] = None,
+                local_fast: bool = False):
         if out is None:
             out = torch.empty((batch.batch, self.out_width), dtype=self.out_dtype, device=back.device)
         flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
-        return self.ops.pool(self.desc, len(self.slots), batch, back, out, flags, row_map=st.row_map)
+        return self.ops.pool(self.desc, len(self.slots), batch, back, out, flags, row_map=st.row_map,
+                             local_table=self.shard if local_fast else None)
+
+    @property
+    def local_fast(self) -> bool:
+        """The inference forward pools this rank's own rows in place (hash route only)."""
+        return self.route_mode == "hash"
 
     def forward(self, batch: SparseBatch, out: Optional[torch.Tensor] = None):
         if self.comm is None:
@@ -321,11 +392,39 @@ class ShardedFusedEncoder(torch.nn.Module):
         if batch.n_slots != len(self.slots):
             raise ValueError(f"batch has {batch.n_slots} slots, encoder {len(self.slots)}")
         batch = self.ops.prepare_batch(batch)
-        st, recv_counts = self.route_exchange(batch)
+        lf = self.local_fast
+        st, recv_counts = self.route_exchange(batch, local_fast=lf)
         wanted = self.comm.exchange(st.local, st.counts, recv_counts)        # ids other ranks want from me
         vec = self.serve(wanted)
         back = self.comm.exchange(vec, recv_counts, st.counts)               # my rows, owner-major
-        return self.combine(batch, st, back, out)
+        return self.combine(batch, st, back, out, local_fast=lf)
+
+    def forward_pipelined(self, micro: Sequence[SparseBatch], outs: Optional[Sequence[torch.Tensor]] = None):
+        """forward() over micro-batches (runtime.batch.split_examples: consecutive examples, the whole batch's
+        lmax) with the all-to-alls of one micro-batch overlapping the local stages of the others (SURVEY §5.8
+        "Scheduling"). Enqueue order, R = route, A/B = id/row all-to-all (RCCL's stream), G = gather, P = pool:
+            R0 | A0 | R1 | A1 | G0 | B0 | G1 | B1 | P0 | P1 ...
+        so the compute stream runs R1 and G0 while A0 / A1 are on the wire, and G1 while B0 is. Each micro-batch
+        costs one host read of its counts (the split sizes). Same outputs as forward() on each micro-batch."""
+        m = len(micro)
+        micro = [self.ops.prepare_batch(b) for b in micro]
+        lf = self.local_fast
+        st, recv, ids, vec = [None] * m, [None] * m, [None] * m, [None] * m
+        for i in range(m):
+            st[i], recv[i] = self.route_exchange(micro[i], local_fast=lf)
+            ids[i] = self.comm.exchange_async(st[i].local, st[i].counts, recv[i])
+        for i in range(m):
+            wanted, work = ids[i]
+            if work is not None:
+                work.wait()
+            vec[i] = self.comm.exchange_async(self.serve(wanted), recv[i], st[i].counts)
+        res = []
+        for i in range(m):
+            back, work = vec[i]
+            if work is not None:
+                work.wait()
+            res.append(self.combine(micro[i], st[i], back, None if outs is None else outs[i], local_fast=lf))
+        return res
 
 
 @dataclass
@@ -373,12 +472,32 @@ def _shard_training_methods():
         return SparseGrad(uid, uval, n_uniq, cap)
 
     def backward(self, ctx: TrainCtx, dout: torch.Tensor):
-        """Reverse all-to-all of row gradients; returns the SparseGrad of the local shard (feed SparseAdam(shard))."""
-        ids, grad, send = self.requester_grad(ctx, dout)
-        recv = [int(c) for c in self.comm.exchange_counts(torch.tensor(send, dtype=torch.int64, device=ids.device)).cpu().tolist()]
-        r_ids = self.comm.exchange(ids, send, recv)
-        r_grad = self.comm.exchange(grad, send, recv)
-        return self.owner_grad(r_ids, r_grad)
+        """Reverse all-to-all of row gradients; returns the SparseGrad of the local shard (feed SparseAdam(shard)).
+        ONE host synchronisation: the requester's distinct-row count and its per-owner counts are computed on the
+        device, the counts exchanged there, and all three read back together."""
+        if not isinstance(self.ops, GpuShardOps):
+            ids, grad, send = self.requester_grad(ctx, dout)
+            recv = [int(c) for c in self.comm.exchange_counts(torch.tensor(send, dtype=torch.int64, device=ids.device)).cpu().tolist()]
+            return self.owner_grad(self.comm.exchange(ids, send, recv), self.comm.exchange(grad, send, recv))
+        if self.table_dtype != torch.float32:
+            raise ValueError("sharded training needs an fp32 table")
+        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        mm = any(sp.combiner in ("max", "min") for sp in self.slots)
+        rows, grad, n_dev = self.ops.pool_bwd(self.desc, len(self.slots), ctx.batch, ctx.st.row_map, ctx.back, ctx.out,
+                                             dout.float().contiguous(), flags, mm, sync=False)
+        P = self.nranks
+        dev = rows.device
+        bounds = torch.tensor(np.cumsum(ctx.st.counts), dtype=torch.int64).to(dev, non_blocking=True)
+        owner = torch.bucketize(rows, bounds, right=True).clamp_(max=P - 1)
+        valid = (torch.arange(rows.numel(), device=dev) < n_dev.to(torch.int64)).to(torch.int64)
+        send_dev = torch.zeros(P, dtype=torch.int64, device=dev).scatter_add_(0, owner, valid)
+        recv_dev = self.comm.exchange_counts(send_dev)
+        both = [int(v) for v in torch.cat([n_dev.to(torch.int64), send_dev, recv_dev.to(dev)]).cpu().tolist()]
+        n, send, recv = both[0], both[1:1 + P], both[1 + P:]
+        if n < 0:
+            raise ValueError(f"rf_pool_rows_bwd: invalid batch (error bits {-n})")
+        ids = ctx.st.local[rows[:n]]
+        return self.owner_grad(self.comm.exchange(ids, send, recv), self.comm.exchange(grad[:n], send, recv))
 
     return forward_train, requester_grad, owner_grad, backward
 
@@ -417,11 +536,13 @@ def simulate_sharded_backward(encoders: Sequence[ShardedFusedEncoder], batches: 
     return [c.out for c in ctxs], grads
 
 
-def simulate_sharded_forward(encoders: Sequence[ShardedFusedEncoder], batches: Sequence[SparseBatch]):
-    """All P ranks in one process (no collective): the exchange done by slicing, for parity tests."""
+def simulate_sharded_forward(encoders: Sequence[ShardedFusedEncoder], batches: Sequence[SparseBatch],
+                             local_fast: bool = False):
+    """All P ranks in one process (no collective): the exchange done by slicing, for parity tests.
+    local_fast: each rank pools its own rows in place (hash route), as forward() does."""
     P = len(encoders)
     batches = [enc.ops.prepare_batch(b) for enc, b in zip(encoders, batches)]
-    states = [enc.route(b) for enc, b in zip(encoders, batches)]
+    states = [enc.route(b, local_fast=local_fast) for enc, b in zip(encoders, batches)]
     offs = [np.concatenate([[0], np.cumsum(st.counts)]) for st in states]
     vec = []
     for o in range(P):
@@ -431,5 +552,5 @@ def simulate_sharded_forward(encoders: Sequence[ShardedFusedEncoder], batches: S
     for r in range(P):
         pos = [int(sum(states[q].counts[o] for q in range(r))) for o in range(P)]
         back = torch.cat([vec[o][pos[o]: pos[o] + states[r].counts[o]] for o in range(P)])
-        outs.append(encoders[r].combine(batches[r], states[r], back))
+        outs.append(encoders[r].combine(batches[r], states[r], back, local_fast=local_fast))
     return outs

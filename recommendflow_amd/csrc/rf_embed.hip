@@ -291,8 +291,8 @@ extern "C" int rf_hash_rows(const rf_slot_desc* d_slots, int32_t n_slots, const 
 
 extern "C" int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off,
                                 const int32_t* lmax, int32_t batch, int64_t n_tok, const void* gathered,
-                                const int32_t* row_map, int32_t dtype, int32_t dim, void* out, int32_t out_dtype, int64_t out_stride, int32_t flags,
-                                void* stream) {
+                                const int32_t* row_map, const void* local_table, int32_t dtype, int32_t dim, void* out,
+                                int32_t out_dtype, int64_t out_stride, int32_t flags, void* stream) {
     RF_REQUIRE(n_slots >= 1 && batch >= 0 && n_tok >= 0, "rf_pool_rows_fwd: need n_slots >= 1, batch, n_tok >= 0");
     RF_REQUIRE(dtype == RF_DTYPE_F32 || dtype == RF_DTYPE_BF16, "rf_pool_rows_fwd: dtype must be F32 or BF16");
     RF_REQUIRE(out_dtype == RF_DTYPE_F32 || out_dtype == RF_DTYPE_BF16, "rf_pool_rows_fwd: out dtype must be F32 or BF16");
@@ -301,7 +301,9 @@ extern "C" int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, co
     RF_REQUIRE((flags & ~RF_FLAG_MASK_PADDING) == 0, "rf_pool_rows_fwd: only RF_FLAG_MASK_PADDING is accepted");
     const int64_t rows = 2 * n_tok + 2 * (int64_t)n_slots;
     RF_REQUIRE(rows <= (int64_t)0xffffffff, "rf_pool_rows_fwd: too many rows");
-    RF_REQUIRE(((uintptr_t)gathered & 15) == 0 && ((uintptr_t)out & 15) == 0, "rf_pool_rows_fwd: buffers must be 16-byte aligned");
+    RF_REQUIRE(((uintptr_t)gathered & 15) == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)local_table & 15) == 0,
+               "rf_pool_rows_fwd: buffers must be 16-byte aligned");
+    RF_REQUIRE(!local_table || row_map, "rf_pool_rows_fwd: local_table needs a row_map");
     const int64_t n_units = (int64_t)batch * n_slots;
     if (n_units == 0) return RF_OK;
     RF_REQUIRE(d_slots && bag_off && lmax && gathered && out, "rf_pool_rows_fwd: null pointer");
@@ -309,7 +311,8 @@ extern "C" int rf_pool_rows_fwd(const rf_slot_desc* d_slots, int32_t n_slots, co
     const int grid = grid_for(items, kWaves, 256 * 32 * 2);
     hipStream_t st = rf_stream(stream);
     const int fl = flags;
-    return launch_fused_any(true, dtype, out_dtype, d_slots, n_slots, nullptr, row_map, bag_off, lmax, n_units,
+    // the PRE kernel takes the local table through its (otherwise unused) token-bytes pointer
+    return launch_fused_any(true, dtype, out_dtype, d_slots, n_slots, (const uint8_t*)local_table, row_map, bag_off, lmax, n_units,
                             gathered, rows, dim, out, out_stride, fl, nullptr, grid, st);
 }
 

@@ -86,6 +86,23 @@ class SparseBatch:
         return (int(len(self.tok_bytes)) + 4 * self.n_tokens) / max(self.batch, 1)
 
 
+def split_examples(batch: SparseBatch, parts: int) -> List[SparseBatch]:
+    """Host CSR batch -> `parts` micro-batches of consecutive examples (re-based CSR), each keeping the WHOLE
+    batch's lmax: the reference pads to the batch max (dataloader.py:32-33), so a micro-batch pools exactly as
+    its examples do inside the full batch (the sharded encoder's pipelined forward)."""
+    h = batch.numpy()
+    S, B = h.n_slots, h.batch
+    bounds = [B * i // parts for i in range(parts + 1)]
+    out = []
+    for b0, b1 in zip(bounds[:-1], bounds[1:]):
+        t0, t1 = int(h.bag_off[b0 * S]), int(h.bag_off[b1 * S])
+        c0, c1 = int(h.tok_off[t0]), int(h.tok_off[t1])
+        out.append(SparseBatch(h.tok_bytes[c0:c1].copy(), (h.tok_off[t0:t1 + 1] - c0).astype(np.int32),
+                               (h.bag_off[b0 * S:b1 * S + 1] - t0).astype(np.int32), np.array(h.lmax, np.int32),
+                               b1 - b0, S))
+    return out
+
+
 def from_lists(rows: Sequence[Sequence[Sequence[bytes]]], lmax: Optional[Sequence[int]] = None) -> SparseBatch:
     """rows[b][s] = list of tokens (bytes or str) of example b, slot s."""
     B = len(rows)

@@ -94,6 +94,8 @@ def test_gloo_world2_bit_exact(O, tmp_path):
     mp.spawn(dist_worker, args=(2, port, DIM, SEED, str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         np.testing.assert_array_equal(np.load(tmp_path / f"out{r}.npy"), unsharded(O, r))
+        np.testing.assert_array_equal(np.load(tmp_path / f"pipe{r}.npy"), unsharded(O, r))  # pipelined, 3 micro
+        np.testing.assert_array_equal(np.load(tmp_path / f"radix{r}.npy"), unsharded(O, r))
     want = expected_grads(O, 2, [np.load(tmp_path / f"dout{r}.npy") for r in range(2)])
     for o in range(2):
         np.testing.assert_array_equal(np.load(tmp_path / f"gid{o}.npy"), want[o][0])

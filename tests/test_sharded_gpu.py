@@ -93,15 +93,37 @@ def test_route_rows_matches_oracle(O, cuda, P, n):
     np.testing.assert_array_equal(m.cpu().numpy(), wm)
 
 
-@pytest.mark.parametrize("P", [2, 4, 8])
+@pytest.mark.parametrize("P", [1, 2, 3, 8, 1000])
+@pytest.mark.parametrize("rank", [-1, 0, "last"])
+@pytest.mark.parametrize("n", [0, 1, 1000, 300001])
+def test_route_hash_matches_oracle(O, cuda, P, rank, n):
+    """rf_route_hash_build/finish (hash-table dedup; rows of `rank` left in place) == oracle.route_rows_local."""
+    rank = P - 1 if rank == "last" else rank
+    rng = np.random.default_rng(n + 3 * P)
+    R = 50_000_000
+    rows = (rng.zipf(1.2, n) * 7919 % R).astype(np.int64)
+    if n > 10:
+        rows[3] = -5          # invalid rows: routed to the last owner, local -1 (gathered as NaN)
+        rows[7] = R + 11
+    ops = GpuShardOps()
+    c, state = ops.route_hash_build(torch.from_numpy(rows).cuda(), P, rank, R)
+    wc, wl, wm = O.route_rows_local(rows, P, rank, R)
+    np.testing.assert_array_equal(c.cpu().numpy(), wc)
+    l, m = ops.route_hash_finish(state, int(wc.sum()))
+    np.testing.assert_array_equal(l.cpu().numpy(), wl)
+    np.testing.assert_array_equal(m.cpu().numpy(), wm)
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
 @pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("dedup", [False, True])
-def test_simulated_shards_bit_exact(cuda, P, tdt, dedup):
+@pytest.mark.parametrize("mode", ["bucketize", "radix", "hash", "hash_local"])
+def test_simulated_shards_bit_exact(cuda, P, tdt, mode):
     sp = slots(48, seed=P)
     full = FusedSparseEncoder(sp, 64, table_dtype=tdt, seed=21)
-    encs = [ShardedFusedEncoder(sp, 64, r, P, table_dtype=tdt, seed=21, dedup=dedup) for r in range(P)]
+    encs = [ShardedFusedEncoder(sp, 64, r, P, table_dtype=tdt, seed=21, dedup=mode != "bucketize",
+                                route="radix" if mode == "radix" else "hash") for r in range(P)]
     batches = [synthetic_batch(200 + 17 * r, [i % 3 == 0 for i in range(len(sp))], seed=40 + r) for r in range(P)]
-    outs = simulate_sharded_forward(encs, batches)
+    outs = simulate_sharded_forward(encs, batches, local_fast=mode == "hash_local")
     for r in range(P):
         want = full(batches[r].to("cuda"))
         np.testing.assert_array_equal(bits(outs[r]), bits(want))
@@ -121,9 +143,24 @@ def test_sharded_cfg2_layout(cuda):
     P = 4
     encs = [ShardedFusedEncoder(sp, 64, r, P, seed=2023) for r in range(P)]
     batches = [synthetic_batch(1024, [bool(f.multivalued) for f in feats], seed=7 + r) for r in range(P)]
-    outs = simulate_sharded_forward(encs, batches)
-    for r in range(P):
-        np.testing.assert_array_equal(bits(outs[r]), bits(full(batches[r].to("cuda"))))
+    for lf in (False, True):
+        outs = simulate_sharded_forward(encs, batches, local_fast=lf)
+        for r in range(P):
+            np.testing.assert_array_equal(bits(outs[r]), bits(full(batches[r].to("cuda"))))
+
+
+def test_local_comm_forward_pools_in_place(cuda):
+    """P = 1 through forward() (LocalComm): every row is rank-local, nothing routed, nothing exchanged; the
+    output equals the unsharded kernel's bit for bit."""
+    from recommendflow_amd.backend.encoder.sharded_encoder import LocalComm
+
+    sp = slots(30, seed=5)
+    full = FusedSparseEncoder(sp, 128, seed=8)
+    enc = ShardedFusedEncoder(sp, 128, 0, 1, comm=LocalComm(), seed=8)
+    hb = synthetic_batch(640, [i % 3 == 0 for i in range(len(sp))], seed=2).to("cuda")
+    st, recv = enc.route_exchange(hb, local_fast=True)
+    assert st.counts == [0] and st.n_requests == 0 and recv == [0]
+    np.testing.assert_array_equal(bits(enc(hb)), bits(full(hb)))
 
 
 def full_table(encs):
