@@ -596,11 +596,20 @@ def bench_sharded(args, specs, multi, rank, world):
     for i in range(2):
         enc.forward_pipelined(micro[i % 2], mouts)
     el_pipe = timed(lambda i: enc.forward_pipelined(micro[i % 2], mouts))
+    # the owner-side partial-pooling exchange (SURVEY §8e alternative): partial vectors per (unit, owner) return
+    try:
+        for i in range(2):
+            enc.forward_partial(batches[i % 2], out)
+        el_pp = timed(lambda i: enc.forward_partial(batches[i % 2], out))
+    except Exception as e:  # noqa: BLE001 — the variant's failure must not cost the leg
+        el_pp = None
+        pp_err = f"{type(e).__name__}: {e}"[:200]
     row_b = D * 4
     xgmi = (st["req"] * (8 + row_b)) * (P - 1) / P if P > 1 else 0
     res = {"examples_per_s": round(B * P * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
            "pipelined_examples_per_s": round(B * P * steps / el_pipe, 1),
            "pipelined_ms_per_step": round(el_pipe / steps * 1e3, 4),
+           "partial_pool_ms_per_step": round(el_pp / steps * 1e3, 4) if el_pp else pp_err,
            "stage_ms_rank0": stage, "gather_GBs": round(st["served"] * (2 * row_b + 8) / max(stage["gather"], 1e-6) / 1e6, 1),
            "a2a_bytes_per_rank_each_way": int(xgmi),
            "rows_read_by_pool": st["logical"], "rows_requested_after_dedup": st["req"],

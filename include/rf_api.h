@@ -324,6 +324,34 @@ int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nranks, int32_t 
                         int32_t* row_map, int32_t* counts, void* ws, size_t ws_bytes, void* stream);
 int rf_route_hash_finish(int64_t n, int32_t nranks, int64_t table_rows, int64_t n_uniq, int64_t* local_out,
                          int32_t* row_map, void* ws, size_t ws_bytes, void* stream);
+/*
+ * Owner-side partial pooling, the alternative exchange of the sharded lookup (SURVEY §8e "pool partial sums at
+ * the owner"; deviation D-partial-pool-order: sum / avg add the owners' partials in owner order, exact at P = 1).
+ * rf_pp_plan (requester): rows = rf_hash_rows + the 2*n_slots pad rows; for every unit u = 2*(b*n_slots + s) + k
+ *   its pooling entries in position order: (ent_row global row, ent_unit u, ent_mult multiplicity; the padding
+ *   positions of a unit are ONE entry of multiplicity Lmax - len; first / last: the one position). ent_off
+ *   int32 [2*batch*n_slots + 1] (exclusive scan of the entry counts), n_ent DEVICE int32. Capacity of the entry
+ *   arrays: 2*n_tok + 2*batch*n_slots. ws: rf_pp_ws_bytes(2*batch*n_slots).
+ * rf_pp_heads: over owner-major entries (rf_bucketize_owner order) with per-owner entry counts (DEVICE int32[P]):
+ *   seg_counts[P] (segments = runs of one unit inside an owner's chunk), and seg_of [n_units][P] (requester:
+ *   the global index of unit u's segment at owner o, or -1) and/or seg_start [n_seg] (owner: first entry of
+ *   each segment). ws: rf_pp_ws_bytes(n).
+ * rf_pp_owner_pool (owner): ent = int32 [n][3] (local row, unit, multiplicity) as received, segments from
+ *   rf_pp_heads -> part fp32 [n_seg][dim]: sum (fp32, entry order, multiplicity repeats) / max / min / the row.
+ * rf_pp_combine (requester): per unit the partials part[seg_of[u][o]] for o = 0 .. P-1 -> out (avg: / Lmax).
+ */
+size_t rf_pp_ws_bytes(int64_t n);
+int rf_pp_plan(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
+               int64_t n_tok, const int64_t* rows, int32_t flags, int32_t* ent_off, int64_t* ent_row, int32_t* ent_unit,
+               int32_t* ent_mult, int32_t* n_ent, void* ws, size_t ws_bytes, void* stream);
+int rf_pp_heads(const int32_t* unit, int64_t n, const int32_t* counts, int32_t nranks, int32_t* seg_counts,
+                int32_t* seg_of, int64_t n_units, int32_t* seg_start, void* ws, size_t ws_bytes, void* stream);
+int rf_pp_owner_pool(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* ent, int64_t n, const int32_t* seg_start,
+                     int64_t n_seg, const void* shard, int32_t dtype, int64_t shard_rows, int32_t dim, float* part,
+                     void* stream);
+int rf_pp_combine(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
+                  int32_t batch, int32_t flags, int32_t nranks, const int32_t* seg_of, const float* part, int32_t dim,
+                  void* out, int32_t out_dtype, int64_t out_stride, void* stream);
 int rf_route_rows(const int64_t* rows, int64_t n, int32_t nranks, int64_t table_rows, int32_t* counts,
                   int64_t* local_out, int32_t* row_map, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
 

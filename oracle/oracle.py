@@ -312,6 +312,74 @@ def route_rows_local(rows: np.ndarray, nranks: int, rank: int, table_rows: int):
     return counts, local, row_map
 
 
+def partial_pool(slots, tok_bytes, tok_off, bag_off, lmax, batch, table, dim, out_stride, nranks, flags=0):
+    """rf_pp_* (owner-side partial pooling) restated: unit (b, s, k) pools its positions l < L (L = len masked,
+    else max(Lmax, len); pad positions read the slot's pad row) per owner (row mod P) in position order from
+    +0.0 (sum) / -inf (max) / +inf (min), then adds / maxes / mins the owners' partials in owner order 0..P-1;
+    avg divides by L; first / last take position 0 / L-1; an empty unit (L = 0) gets 0 / NaN / -inf / +inf / 0
+    as rf_fused_hash_embed_fwd (zeros when masked). float32 arithmetic, fp32 table."""
+    f32 = np.float32
+    slots = np.ascontiguousarray(slots, dtype=SLOT_DTYPE)
+    S = len(slots)
+    rows = hash_rows(slots, tok_bytes, tok_off, bag_off, batch)
+    mask_pad = bool(flags & FLAG_MASK_PADDING)
+    table = np.asarray(table, np.float32)
+    out = np.zeros((batch, out_stride), np.float32)
+    for s in range(S):
+        sd = slots[s]
+        comb = int(sd["combiner"])
+        pads = []
+        for k in range(2):
+            nb = int(sd["num_bins"])
+            pb = 0 if int(sd["mask_empty"]) else hash_bucket(b"", nb, int(sd["salt"][k]), False)
+            pads.append(int(sd["row_base"][k]) + pb)
+        for b in range(batch):
+            u = b * S + s
+            t0, t1 = int(bag_off[u]), int(bag_off[u + 1])
+            ln = t1 - t0
+            L = ln if mask_pad else max(int(lmax[s]), ln)
+            for k in range(2):
+                pos = [int(rows[2 * t + k]) for t in range(t0, t1)] + [pads[k]] * (L - ln)
+                if comb == COMB["first"]:
+                    pos = pos[:1]
+                elif comb == COMB["last"]:
+                    pos = pos[L - 1:L] if L else []
+                if L == 0:
+                    v = np.full(dim, 0.0 if mask_pad else {COMB["avg"]: np.nan, COMB["max"]: -np.inf,
+                                                           COMB["min"]: np.inf}.get(comb, 0.0), f32)
+                else:
+                    init = {COMB["max"]: -np.inf, COMB["min"]: np.inf}.get(comb, 0.0)
+                    v = np.full(dim, init, f32)
+                    for o in range(nranks):
+                        mine = [g for g in pos if g % nranks == o]
+                        if not mine:
+                            continue
+                        p = np.full(dim, init, f32)
+                        for g in mine:
+                            x = table[g]
+                            if comb in (COMB["sum"], COMB["avg"]):
+                                p = (p + x).astype(f32)
+                            elif comb == COMB["max"]:
+                                p = np.where(x > p, x, p)
+                            elif comb == COMB["min"]:
+                                p = np.where(x < p, x, p)
+                            else:
+                                p = x.copy()
+                        if comb in (COMB["sum"], COMB["avg"]):
+                            v = (v + p).astype(f32)
+                        elif comb == COMB["max"]:
+                            v = np.where(p > v, p, v)
+                        elif comb == COMB["min"]:
+                            v = np.where(p < v, p, v)
+                        else:
+                            v = p
+                    if comb == COMB["avg"]:
+                        v = (v / f32(L)).astype(f32)
+                off = int(sd["out_off"]) + k * dim
+                out[b, off:off + dim] = v
+    return out
+
+
 def bf16_to_f32(u16: np.ndarray) -> np.ndarray:
     return (np.asarray(u16, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
 

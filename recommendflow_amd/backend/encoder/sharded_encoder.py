@@ -136,6 +136,64 @@ class GpuShardOps:
                L.stream_ptr(None))
         return local[:n_uniq], row_map[:n]
 
+    # -- owner-side partial pooling (rf_partial.hip) ---------------------------------------------------
+    def pp_plan(self, desc, n_slots: int, batch: SparseBatch, rows: torch.Tensor, flags: int, nranks: int):
+        """Requester: pooling entries in (unit, position) order, then owner-major (stable) ->
+        (ent int32 [n][3] = (local, unit, mult) owner-major, entry counts int32 [P], segment counts int32 [P],
+        seg_of int32 [n_units][P]). One host read (the entry count)."""
+        B, S = batch.batch, n_slots
+        n_units = 2 * B * S
+        cap = max(2 * batch.n_tokens + n_units, 1)
+        dev = self.device
+        ent_off = torch.empty(n_units + 1, dtype=torch.int32, device=dev)
+        ent_row = torch.empty(cap, dtype=torch.int64, device=dev)
+        ent_unit = torch.empty(cap, dtype=torch.int32, device=dev)
+        ent_mult = torch.empty(cap, dtype=torch.int32, device=dev)
+        n_ent = torch.empty(1, dtype=torch.int32, device=dev)
+        wsb = int(L.load().rf_pp_ws_bytes(max(n_units, cap)))
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+        L.call("rf_pp_plan", L.ptr(desc), S, L.ptr(batch.bag_off), L.ptr(batch.lmax), B, batch.n_tokens, L.ptr(rows),
+               flags, L.ptr(ent_off), L.ptr(ent_row), L.ptr(ent_unit), L.ptr(ent_mult), L.ptr(n_ent), L.ptr(ws), wsb,
+               L.stream_ptr(None))
+        n = int(n_ent.item())
+        counts, perm, local, _ = self.bucketize(ent_row[:n], nranks)
+        perm = perm.long()
+        ent = torch.stack([local.to(torch.int32), ent_unit[:n][perm], ent_mult[:n][perm]], dim=1).contiguous()
+        seg_counts = torch.empty(nranks, dtype=torch.int32, device=dev)
+        seg_of = torch.empty((max(n_units, 1), nranks), dtype=torch.int32, device=dev)
+        L.call("rf_pp_heads", L.ptr(ent[:, 1].contiguous()), n, L.ptr(counts), nranks, L.ptr(seg_counts), L.ptr(seg_of),
+               n_units, None, L.ptr(ws), wsb, L.stream_ptr(None))
+        return ent, counts, seg_counts, seg_of
+
+    def pp_owner_pool(self, desc, n_slots: int, ent: torch.Tensor, recv_counts: List[int], shard: torch.Tensor):
+        """Owner: one partial per segment of the received entries -> fp32 [n_seg, D]."""
+        n = ent.shape[0]
+        dev = self.device
+        P = len(recv_counts)
+        cnt = torch.tensor(recv_counts, dtype=torch.int32).to(dev)
+        seg_counts = torch.empty(P, dtype=torch.int32, device=dev)
+        seg_start = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        wsb = int(L.load().rf_pp_ws_bytes(max(n, 1)))
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+        L.call("rf_pp_heads", L.ptr(ent[:, 1].contiguous()) if n else None, n, L.ptr(cnt), P, L.ptr(seg_counts), None, 0,
+               L.ptr(seg_start), L.ptr(ws), wsb, L.stream_ptr(None))
+        return seg_counts, seg_start
+
+    def pp_owner_partials(self, desc, n_slots: int, ent, seg_start, n_seg: int, shard):
+        D = shard.shape[1]
+        part = torch.empty((max(n_seg, 1), D), dtype=torch.float32, device=self.device)
+        L.call("rf_pp_owner_pool", L.ptr(desc), n_slots, L.ptr(ent), ent.shape[0], L.ptr(seg_start), n_seg, L.ptr(shard),
+               L.torch_dtype_code(shard.dtype), shard.shape[0], D, L.ptr(part), L.stream_ptr(None))
+        return part[:n_seg]
+
+    def pp_combine(self, desc, n_slots: int, batch: SparseBatch, flags: int, nranks: int, seg_of, part, out):
+        if part.numel() == 0:
+            part = torch.zeros((1, out.shape[1] if out.dim() == 2 else 4), dtype=torch.float32, device=self.device)
+        L.call("rf_pp_combine", L.ptr(desc), n_slots, L.ptr(batch.bag_off), L.ptr(batch.lmax), batch.batch, flags, nranks,
+               L.ptr(seg_of), L.ptr(part), part.shape[1], L.ptr(out), L.torch_dtype_code(out.dtype), out.stride(0),
+               L.stream_ptr(None))
+        return out
+
     def gather(self, shard: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
         n = local.numel()
         out = torch.empty((max(n, 1), shard.shape[1]), dtype=shard.dtype, device=self.device)
@@ -399,6 +457,32 @@ class ShardedFusedEncoder(torch.nn.Module):
         back = self.comm.exchange(vec, recv_counts, st.counts)               # my rows, owner-major
         return self.combine(batch, st, back, out, local_fast=lf)
 
+    def forward_partial(self, batch: SparseBatch, out: Optional[torch.Tensor] = None):
+        """The owner-side partial-pooling exchange (SURVEY §8e alternative; rf_partial.hip): each unit's positions
+        go to their owners as (local row, unit, multiplicity) entries, every owner pools the positions it owns per
+        unit, one fp32 partial per (unit, owner) comes back and the requester combines them in owner order. Two
+        host reads (the entry total, then the exchanged entry / segment counts). Exact at P = 1 and for max / min /
+        first / last at any P; sum / avg add the owners' partials in owner order (D-partial-pool-order)."""
+        if self.comm is None:
+            raise RuntimeError("forward_partial needs a comm")
+        batch = self.ops.prepare_batch(batch)
+        if out is None:
+            out = torch.empty((batch.batch, self.out_width), dtype=self.out_dtype, device=self.ops.device)
+        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        S, P = len(self.slots), self.nranks
+        rows = torch.cat([self.ops.hash_rows(self.desc, S, batch), self.pad_rows])
+        ent, counts, seg_counts, seg_of = self.ops.pp_plan(self.desc, S, batch, rows, flags, P)
+        both = torch.stack([counts, seg_counts], dim=1).to(torch.int64)           # [P, 2]: entries, segments
+        recv = self.comm.exchange_counts(both.reshape(-1)).reshape(P, 2)
+        hb = [int(v) for v in torch.cat([both.reshape(-1), recv.reshape(-1).to(both.device)]).cpu().tolist()]
+        send_e, send_s = hb[0:2 * P:2], hb[1:2 * P:2]
+        recv_e, recv_s = hb[2 * P::2], hb[2 * P + 1::2]
+        r_ent = self.comm.exchange(ent, send_e, recv_e)                          # owner side from here
+        _, seg_start = self.ops.pp_owner_pool(self.desc, S, r_ent, recv_e, self.shard)
+        part = self.ops.pp_owner_partials(self.desc, S, r_ent, seg_start, sum(recv_s), self.shard)
+        back = self.comm.exchange(part, recv_s, send_s)                          # requester side again
+        return self.ops.pp_combine(self.desc, S, batch, flags, P, seg_of, back, out)
+
     def forward_pipelined(self, micro: Sequence[SparseBatch], outs: Optional[Sequence[torch.Tensor]] = None):
         """forward() over micro-batches (runtime.batch.split_examples: consecutive examples, the whole batch's
         lmax) with the all-to-alls of one micro-batch overlapping the local stages of the others (SURVEY §5.8
@@ -534,6 +618,38 @@ def simulate_sharded_backward(encoders: Sequence[ShardedFusedEncoder], batches: 
             gs.append(sent[r][1][a: a + cnt[o]])
         grads.append(encoders[o].owner_grad(torch.cat(ids), torch.cat(gs)))
     return [c.out for c in ctxs], grads
+
+
+def simulate_partial_forward(encoders: Sequence[ShardedFusedEncoder], batches: Sequence[SparseBatch]):
+    """forward_partial of all P ranks in one process (the exchanges done by slicing), for parity tests."""
+    P = len(encoders)
+    S = len(encoders[0].slots)
+    batches = [enc.ops.prepare_batch(b) for enc, b in zip(encoders, batches)]
+    plans = []
+    for enc, b in zip(encoders, batches):
+        flags = L.FLAG_MASK_PADDING if enc.mask_padding else 0
+        rows = torch.cat([enc.ops.hash_rows(enc.desc, S, b), enc.pad_rows])
+        ent, counts, seg_counts, seg_of = enc.ops.pp_plan(enc.desc, S, b, rows, flags, P)
+        plans.append((ent, [int(c) for c in counts.cpu().tolist()], [int(c) for c in seg_counts.cpu().tolist()], seg_of))
+    e_off = [np.concatenate([[0], np.cumsum(p[1])]) for p in plans]
+    s_off = [np.concatenate([[0], np.cumsum(p[2])]) for p in plans]
+    parts = []
+    for o, enc in enumerate(encoders):
+        r_ent = torch.cat([plans[r][0][e_off[r][o]: e_off[r][o + 1]] for r in range(P)])
+        recv_e = [plans[r][1][o] for r in range(P)]
+        _, seg_start = enc.ops.pp_owner_pool(enc.desc, S, r_ent, recv_e, enc.shard)
+        parts.append(enc.ops.pp_owner_partials(enc.desc, S, r_ent, seg_start, sum(plans[r][2][o] for r in range(P)),
+                                               enc.shard))
+    outs = []
+    for r, enc in enumerate(encoders):
+        flags = L.FLAG_MASK_PADDING if enc.mask_padding else 0
+        back = []
+        for o in range(P):
+            pos = sum(plans[q][2][o] for q in range(r))
+            back.append(parts[o][pos: pos + plans[r][2][o]])
+        out = torch.empty((batches[r].batch, enc.out_width), dtype=enc.out_dtype, device=enc.ops.device)
+        outs.append(enc.ops.pp_combine(enc.desc, S, batches[r], flags, P, plans[r][3], torch.cat(back), out))
+    return outs
 
 
 def simulate_sharded_forward(encoders: Sequence[ShardedFusedEncoder], batches: Sequence[SparseBatch],

@@ -49,6 +49,12 @@ _SIGS = {
     "rf_route_ws_bytes": (ctypes.c_size_t, [_i64, _i32, _i64]),
     "rf_route_rows": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_pool_rows_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _i32, _i32, _vp, _i32, _i64, _i32, _vp]),
+    "rf_pp_ws_bytes": (ctypes.c_size_t, [_i64]),
+    "rf_pp_plan": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  ctypes.c_size_t, _vp]),
+    "rf_pp_heads": (ctypes.c_int, [_vp, _i64, _vp, _i32, _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),
+    "rf_pp_owner_pool": (ctypes.c_int, [_vp, _i32, _vp, _i64, _vp, _i64, _vp, _i32, _i64, _i32, _vp, _vp]),
+    "rf_pp_combine": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32, _i64, _vp]),
     "rf_route_hash_ws_bytes": (ctypes.c_size_t, [_i64, _i32, _i64]),
     "rf_route_hash_build": (ctypes.c_int, [_vp, _i64, _i32, _i32, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_route_hash_finish": (ctypes.c_int, [_i64, _i32, _i64, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),

@@ -65,6 +65,113 @@ class OracleShardOps:
         out.copy_(torch.from_numpy(res))
         return out
 
+    # -- owner-side partial pooling, restated in numpy (rf_partial.hip) --------------------------------------------
+    def pp_plan(self, desc, n_slots, batch, rows, flags, nranks):
+        rows = rows.numpy()
+        S, B = n_slots, batch.batch
+        mask_pad = bool(flags & 1)
+        n_tok = batch.n_tokens
+        ent = []  # (global row, unit, mult) in (unit, position) order
+        for bs in range(B * S):
+            s = bs % S
+            comb = int(desc[s]["combiner"])
+            t0, t1 = int(batch.bag_off[bs]), int(batch.bag_off[bs + 1])
+            ln = t1 - t0
+            L = ln if mask_pad else max(int(batch.lmax[s]), ln)
+            for k in range(2):
+                u = 2 * bs + k
+                pad = int(rows[2 * n_tok + 2 * s + k])
+                if L == 0:
+                    continue
+                if comb == O.COMB["first"]:
+                    ent.append((int(rows[2 * t0 + k]) if ln > 0 else pad, u, 1))
+                elif comb == O.COMB["last"]:
+                    ent.append((int(rows[2 * (t0 + L - 1) + k]) if ln >= L else pad, u, 1))
+                else:
+                    ent += [(int(rows[2 * t + k]), u, 1) for t in range(t0, t1)]
+                    if L > ln:
+                        ent.append((pad, u, L - ln))
+        e = np.array(ent, np.int64).reshape(-1, 3)
+        owner = e[:, 0] % nranks
+        order = np.argsort(owner, kind="stable")
+        e, owner = e[order], owner[order]
+        counts = np.bincount(owner, minlength=nranks).astype(np.int32)
+        head = np.ones(len(e), bool)
+        head[1:] = (e[1:, 1] != e[:-1, 1]) | (owner[1:] != owner[:-1])
+        seg = np.cumsum(head) - 1
+        seg_counts = np.bincount(owner[head], minlength=nranks).astype(np.int32)
+        seg_of = np.full((2 * B * S, nranks), -1, np.int32)
+        seg_of[e[head, 1], owner[head]] = seg[head]
+        ent3 = np.stack([e[:, 0] // nranks, e[:, 1], e[:, 2]], axis=1).astype(np.int32)
+        return (torch.from_numpy(ent3), torch.from_numpy(counts), torch.from_numpy(seg_counts), torch.from_numpy(seg_of))
+
+    def pp_owner_pool(self, desc, n_slots, ent, recv_counts, shard):
+        e = ent.numpy()
+        src = np.repeat(np.arange(len(recv_counts)), recv_counts)
+        head = np.ones(len(e), bool)
+        head[1:] = (e[1:, 1] != e[:-1, 1]) | (src[1:] != src[:-1])
+        seg_counts = np.bincount(src[head], minlength=len(recv_counts)).astype(np.int32)
+        return torch.from_numpy(seg_counts), torch.from_numpy(np.nonzero(head)[0].astype(np.int32))
+
+    def pp_owner_partials(self, desc, n_slots, ent, seg_start, n_seg, shard):
+        e, st, sh = ent.numpy(), seg_start.numpy(), shard.numpy()
+        D = sh.shape[1]
+        part = np.zeros((n_seg, D), np.float32)
+        for g in range(n_seg):
+            a, b = int(st[g]), int(st[g + 1]) if g + 1 < n_seg else len(e)
+            comb = int(desc[(int(e[a, 1]) >> 1) % n_slots]["combiner"])
+            init = {O.COMB["max"]: -np.inf, O.COMB["min"]: np.inf}.get(comb, 0.0)
+            acc = np.full(D, init, np.float32)
+            for i in range(a, b):
+                x = sh[e[i, 0]]
+                if comb in (O.COMB["sum"], O.COMB["avg"]):
+                    for _ in range(int(e[i, 2])):
+                        acc = (acc + x).astype(np.float32)
+                elif comb == O.COMB["max"]:
+                    acc = np.where(x > acc, x, acc)
+                elif comb == O.COMB["min"]:
+                    acc = np.where(x < acc, x, acc)
+                else:
+                    acc = x.copy()
+            part[g] = acc
+        return torch.from_numpy(part)
+
+    def pp_combine(self, desc, n_slots, batch, flags, nranks, seg_of, part, out):
+        so, pt = seg_of.numpy(), part.numpy()
+        S, B = n_slots, batch.batch
+        D = out.shape[1] // (2 * S)
+        mask_pad = bool(flags & 1)
+        res = np.zeros((B, out.shape[1]), np.float32)
+        for bs in range(B * S):
+            b, s = divmod(bs, S)
+            comb = int(desc[s]["combiner"])
+            ln = int(batch.bag_off[bs + 1] - batch.bag_off[bs])
+            L = ln if mask_pad else max(int(batch.lmax[s]), ln)
+            for k in range(2):
+                init = {O.COMB["max"]: -np.inf, O.COMB["min"]: np.inf}.get(comb, 0.0)
+                a = np.full(D, init, np.float32)
+                for o in range(nranks):
+                    g = so[2 * bs + k, o]
+                    if g < 0:
+                        continue
+                    p = pt[g]
+                    if comb in (O.COMB["sum"], O.COMB["avg"]):
+                        a = (a + p).astype(np.float32)
+                    elif comb == O.COMB["max"]:
+                        a = np.where(p > a, p, a)
+                    elif comb == O.COMB["min"]:
+                        a = np.where(p < a, p, a)
+                    else:
+                        a = p
+                if comb == O.COMB["avg"]:
+                    a = (a / np.float32(L)).astype(np.float32) if L else np.full(D, np.nan, np.float32)
+                if L == 0 and mask_pad:
+                    a = np.zeros(D, np.float32)
+                off = int(desc[s]["out_off"]) + k * D
+                res[b, off:off + D] = a
+        out.copy_(torch.from_numpy(res))
+        return out
+
     def pool_bwd(self, desc, n_slots, batch, row_map, gathered, out, dout, flags, need_minmax):
         r, g = O.pool_rows_bwd(desc, batch.bag_off, batch.lmax, batch.batch, batch.n_tokens, row_map.numpy(),
                                gathered.numpy(), gathered.shape[1], out.numpy(), dout.numpy(), flags)
@@ -129,6 +236,7 @@ def dist_worker(rank, world, port, dim, seed, result_dir):
         enc_rx = ShardedFusedEncoder(small_slots(), dim, rank, world, comm=TorchDistComm(), ops=OracleShardOps(),
                                      seed=seed, device="cpu", route="radix")
         np.save(os.path.join(result_dir, f"radix{rank}.npy"), enc_rx(rank_batch(rank)).numpy())
+        np.save(os.path.join(result_dir, f"pp{rank}.npy"), enc.forward_partial(rank_batch(rank)).numpy())
         # one training step: forward_train, requester grads, reverse all-to-all, owner segment sum
         ctx = enc.forward_train(rank_batch(rank))
         dout = torch.from_numpy(np.random.default_rng(50 + rank).standard_normal(ctx.out.shape).astype(np.float32))

@@ -27,6 +27,17 @@ def unsharded(O, rank):
     return out
 
 
+def partial_desc():
+    return build_slot_desc(small_slots(), DIM)[0]
+
+
+def full_table():
+    from oracle import oracle as O
+
+    desc, rows = build_slot_desc(small_slots(), DIM)
+    return O.table_init_uniform(rows, DIM, seed=SEED)
+
+
 def test_shard_rows_partition():
     for R in (0, 1, 7, 100, 101):
         for P in (1, 2, 3, 8):
@@ -96,6 +107,11 @@ def test_gloo_world2_bit_exact(O, tmp_path):
         np.testing.assert_array_equal(np.load(tmp_path / f"out{r}.npy"), unsharded(O, r))
         np.testing.assert_array_equal(np.load(tmp_path / f"pipe{r}.npy"), unsharded(O, r))  # pipelined, 3 micro
         np.testing.assert_array_equal(np.load(tmp_path / f"radix{r}.npy"), unsharded(O, r))
+        b = rank_batch(r)  # owner-side partial pooling over gloo: the oracle's owner-ordered restatement, bit-exact
+        d = partial_desc()
+        want_pp = O.partial_pool(d, b.tok_bytes, b.tok_off, b.bag_off, b.lmax, b.batch, full_table(), DIM,
+                                 2 * DIM * len(d), 2)
+        np.testing.assert_array_equal(np.load(tmp_path / f"pp{r}.npy").view(np.uint32), want_pp.view(np.uint32))
     want = expected_grads(O, 2, [np.load(tmp_path / f"dout{r}.npy") for r in range(2)])
     for o in range(2):
         np.testing.assert_array_equal(np.load(tmp_path / f"gid{o}.npy"), want[o][0])
