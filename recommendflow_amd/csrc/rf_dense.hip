@@ -468,16 +468,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
 //   * block tile BM x 128 x 64 (BM = 128: 4 waves 2 x 2 of 64 x 64; BM = 64: 4 waves 1 x 4 of 64 x 32),
 //     v_mfma_f32_16x16x32_bf16 with fp32 accumulators;
 //   * A and B tiles land in LDS by global_load_lds_dwordx4 (no VGPR staging, no ds_write) in a ring of
-//     3 buffers: the loads of step k+2 are issued right after the barrier that opens step k, so two
-//     steps are in flight behind the MFMAs; each wave waits with a COUNTED vmcnt (never 0 inside the
-//     loop) and the buffer is read only after the raw s_barrier that follows the wait;
+//     kLdsStages buffers: the loads of step k + kLdsStages - 1 are issued right after the barrier that opens
+//     step k; each wave waits for its own copies of step k (vmcnt) and the buffer is read only after the raw
+//     s_barrier that follows the wait;
 //   * 128-byte tile rows, 16-byte chunk c of row r stored at chunk c ^ (r & 7): the ds_read_b128 lane
 //     groups of a 16 x 32 fragment touch 16 distinct (row parity, chunk) bank quads = conflict-free.
 //     LDS-DMA writes lane-linear, so the swizzle is applied on the SOURCE address (lane -> chunk);
 //   * XCD-aware tile order: the workgroups of one XCD (block ids congruent mod 8) take consecutive tiles,
 //     so the N-tiles sharing an A row panel share that XCD's L2.
 // ---------------------------------------------------------------------------------------------
-constexpr int kLdsK = 64, kLdsBN = 128, kLdsStages = 3;
+// 2 stages: the next step's tiles are in flight behind this step's MFMAs. Measured against 3- to 5-deep rings
+// on MI355X (tools/gemm_lab.hip, profiles/r03/gemm_lab_r03b.txt): the smaller LDS footprint (64 / 48 KB) lets two
+// or three workgroups share a CU, whose MFMAs then cover each other's load waits — 4096x1280->1024 16.2 vs
+// 16.9 us (64-row tiles), 51200x1280->1024 206 vs 248 us (128-row tiles); deeper rings only add LDS.
+constexpr int kLdsK = 64, kLdsBN = 128, kLdsStages = 2;
 
 template <int BM>
 __device__ __forceinline__ void glds_stage(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int64_t M, int N,
@@ -550,17 +554,19 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
 
     auto As = [&](int s) { return lds + s * (A_EL + B_EL); };
     auto Bs = [&](int s) { return lds + s * (A_EL + B_EL) + A_EL; };
-    glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, 0, As(0), Bs(0), tid);
-    if (nk > 1) glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, kLdsK, As(1), Bs(1), tid);
+#pragma unroll
+    for (int p = 0; p + 1 < kLdsStages; ++p)
+        if (p < nk) glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, p * kLdsK, As(p), Bs(p), tid);
     for (int kt = 0; kt < nk; ++kt) {
         const int s = kt % kLdsStages;
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+        // stage kt must have landed; the stages issued after it (at most kLdsStages - 2) may stay in flight
+        if (kLdsStages >= 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage kt landed for every wave; every wave is done reading stage kt - 1
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + 2 < nk) {
-            const int s2 = (kt + 2) % kLdsStages;
-            glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, (kt + 2) * kLdsK, As(s2), Bs(s2), tid);
+        if (kt + kLdsStages - 1 < nk) {
+            const int s2 = (kt + kLdsStages - 1) % kLdsStages;
+            glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, (kt + kLdsStages - 1) * kLdsK, As(s2), Bs(s2), tid);
         }
         const uint16_t* A = As(s);
         const uint16_t* B = Bs(s);

@@ -149,6 +149,39 @@ def test_sharded_cfg2_layout(cuda):
             np.testing.assert_array_equal(bits(outs[r]), bits(full(batches[r].to("cuda"))))
 
 
+@pytest.mark.parametrize("P", [1, 3])
+def test_partial_pool_stages_vs_numpy(O, cuda, P):
+    """Each rf_pp_* stage against the numpy restatement in tests/shard_helpers.py (plan entries, owner-major order,
+    segment counts, seg_of; the owner's segments and partials; the combine)."""
+    import sys
+    import os
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from shard_helpers import OracleShardOps
+
+    sp = slots(10, seed=P + 3)
+    enc = ShardedFusedEncoder(sp, 32, 0, P, seed=4)
+    hb = synthetic_batch(40, [i % 3 == 0 for i in range(len(sp))], seed=9, id_max=4000, max_len=7)
+    db = hb.to("cuda")
+    ops, ref = GpuShardOps(), OracleShardOps()
+    rows = torch.cat([ops.hash_rows(enc.desc, len(sp), db), enc.pad_rows])
+    got = ops.pp_plan(enc.desc, len(sp), db, rows, 0, P)
+    want = ref.pp_plan(enc.host_desc, len(sp), hb, rows.cpu(), 0, P)
+    for name, g, w in zip(("ent", "counts", "seg_counts", "seg_of"), got, want):
+        np.testing.assert_array_equal(g.cpu().numpy(), w.numpy(), err_msg=name)
+    ent = got[0]
+    counts = [int(c) for c in got[1].cpu().tolist()]
+    chunk = ent[: counts[0]]  # owner 0's entries from this requester
+    sc, ss = ops.pp_owner_pool(enc.desc, len(sp), chunk, [counts[0]], enc.shard)
+    wsc, wss = ref.pp_owner_pool(enc.host_desc, len(sp), chunk.cpu(), [counts[0]], enc.shard.cpu())
+    np.testing.assert_array_equal(sc.cpu().numpy(), wsc.numpy())
+    n_seg = int(wsc.sum())
+    np.testing.assert_array_equal(ss.cpu().numpy()[:n_seg], wss.numpy())
+    part = ops.pp_owner_partials(enc.desc, len(sp), chunk, ss, n_seg, enc.shard)
+    wpart = ref.pp_owner_partials(enc.host_desc, len(sp), chunk.cpu(), wss, n_seg, enc.shard.cpu())
+    np.testing.assert_array_equal(bits(part), wpart.numpy().view(np.uint32))
+
+
 @pytest.mark.parametrize("P", [1, 2, 3, 8])
 @pytest.mark.parametrize("mask_padding", [False, True])
 def test_partial_pool_vs_oracle(O, cuda, P, mask_padding):

@@ -8,7 +8,7 @@ if [ "${LAB:-1}" = 1 ]; then
   timeout -k 10 240 ./tools/gemm_lab 5 > "$OUT/gemm_lab.txt" 2>&1; rc=$?; echo "gemm_lab rc=$rc"; cat "$OUT/gemm_lab.txt"
   case $rc in 0) ;; *) exit $rc;; esac
 fi
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 ${TESTS:-tests/test_sharded_gpu.py tests/test_graphs_gpu.py tests/test_embed_gpu.py} -m gpu > "$OUT/pytest.log" 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 ${TESTS:-tests/test_sharded_gpu.py tests/test_graphs_gpu.py tests/test_embed_gpu.py tests/test_cfg1_gpu.py} -m gpu > "$OUT/pytest.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 "$OUT/pytest.log"
 case $rc in 0|1) ;; *) exit $rc;; esac
 timeout -k 10 600 python bench.py --no-extras --no-cascade --no-pipe --cpu-seconds 0 --no-probes --no-uniform-leg ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
