@@ -56,9 +56,7 @@ extern "C" {
 #define RF_FLAG_EMIT_IDX 0x2     /* also write the two bucket ids of every token to idx_out[2*t + k] */
 #define RF_FLAG_SINGLE_TOKEN 0x4 /* the caller knows every slot's batch Lmax is <= 1 (single-valued slots, e.g.
                                     cfg3): a low-register single-token kernel runs (same values); a slot whose
-                                    lmax is > 1 is then written as NaN. Not with RF_FLAG_EMIT_IDX. In this mode
-                                    idx_out may point to a caller scratch of batch * n_slots * 8 bytes (8-byte
-                                    aligned): the kernel then runs as two passes (hash -> row ids, ids -> rows). */
+                                    lmax is > 1 is then written as NaN. Not with RF_FLAG_EMIT_IDX. */
 #define RF_FLAG_DIAG_XCD_ORDER 0x0800      /* A/B switch: slot-interleaved XCD item order (measured slower); results identical */
 #define RF_FLAG_DIAG_GENERAL_PHASE2 0x8000 /* A/B switch: force the general pooling path for Lmax = 1 slots; results identical */
 /* Only these two result-preserving switches are accepted here; any other bit returns RF_EINVAL. Bits 12-14

@@ -110,8 +110,6 @@ class FusedSparseEncoder(torch.nn.Module):
         self.mask_padding = bool(mask_padding)
         self.seed = int(seed)
         self.single_token = True  # RF_FLAG_SINGLE_TOKEN when a batch's host-side Lmax allows it (A/B: False)
-        self.two_pass = True  # single-token batches: hash -> row ids -> gather, through a scratch (A/B: False)
-        self._st_scratch = None
         self.extra_flags = 0  # diagnostic bits (rf_api.h RF_FLAG_DIAG_*; ablations 12-14 go to rf_diag_fused_hash_embed_fwd)
         desc = np.zeros(len(self.slots), SLOT_DTYPE)
         base = int(row_base0)
@@ -172,11 +170,6 @@ class FusedSparseEncoder(torch.nn.Module):
         if not emit_idx and not self.extra_flags and self.single_token and self._single_token_batch(batch):
             flags |= L.FLAG_SINGLE_TOKEN  # every slot's batch Lmax <= 1: the low-register single-token kernel
         idx = torch.empty((max(batch.n_tokens, 1), 2), dtype=torch.int64, device=self.table.device) if emit_idx else None
-        if (flags & L.FLAG_SINGLE_TOKEN) and self.two_pass:
-            need = B * len(self.slots)  # uint2 per bag (rf_api.h RF_FLAG_SINGLE_TOKEN)
-            if self._st_scratch is None or self._st_scratch.numel() < need:
-                self._st_scratch = torch.empty(need, dtype=torch.int64, device=self.table.device)
-            idx = self._st_scratch
         entry = "rf_diag_fused_hash_embed_fwd" if self.extra_flags & L.DIAG_ABLATIONS else "rf_fused_hash_embed_fwd"
         L.call(entry, L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes),
                L.ptr(batch.tok_off), L.ptr(batch.bag_off), L.ptr(batch.lmax), B, L.ptr(self.table),

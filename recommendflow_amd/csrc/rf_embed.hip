@@ -247,10 +247,8 @@ static int fused_hash_embed_fwd_impl(uint32_t allowed_diag, const rf_slot_desc* 
     if (flags & RF_FLAG_SINGLE_TOKEN) {
         RF_REQUIRE(!(flags & RF_FLAG_EMIT_IDX), "rf_fused_hash_embed_fwd: RF_FLAG_SINGLE_TOKEN does not emit ids");
         RF_REQUIRE(!(flags & 0xF800), "rf_fused_hash_embed_fwd: RF_FLAG_SINGLE_TOKEN takes no diagnostic bits");
-        // idx_out, unused by this mode otherwise, may carry an n_units x 8-byte scratch: the two-pass form
         return launch_single_token_any(table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,
-                                       table, table_rows, dim, out, out_stride, flags, grid_for(items, 1, 256 * 32 * 2), st,
-                                       (void*)idx_out);
+                                       table, table_rows, dim, out, out_stride, flags, grid_for(items, 1, 256 * 32 * 2), st);
     }
     const int grid = grid_for(items, kWaves, 256 * 32 * 2);
     return launch_fused_any(false, table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,

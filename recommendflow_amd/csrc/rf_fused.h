@@ -688,145 +688,12 @@ __global__ __launch_bounds__(64) void single_token_embed_kernel(
     }
 }
 
-// Two-pass form of the single-token kernel (RF_FLAG_SINGLE_TOKEN with a caller scratch of n_units uint2):
-// pass 1 hashes (st_rows_kernel: lane j of an item = bag b0 + j of slot s, both keys in one read of the token;
-// the row pair lands slot-major in rows2[s * batch + b] — the pad rows for an empty bag, a 0xffffffff marker
-// when masked), pass 2 gathers (st_gather_kernel: a team per bag, the rows of GH bags in flight per team).
-// Each pass then has ONE dependent memory step per bag (token bytes -> ids, ids -> rows) instead of the four
-// in a row of the fused form (bag_off -> tok_off -> token -> rows), so the gather keeps its loads in flight
-// like a plain indexed copy. Values are identical to single_token_embed_kernel's.
-static __global__ __launch_bounds__(64) void st_rows_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
-                                                     const uint8_t* __restrict__ tok_bytes,
-                                                     const int32_t* __restrict__ tok_off,
-                                                     const int32_t* __restrict__ bag_off, int batch, int64_t table_rows,
-                                                     int flags, uint2* __restrict__ rows2) {
-    const int lane = threadIdx.x;
-    const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
-    const int nbb = (batch + kUnits - 1) / kUnits;
-    const int64_t n_items = (int64_t)n_slots * nbb;
-    for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-        const int s = (int)(item / nbb);
-        const int b0 = (int)(item - (int64_t)s * nbb) * kUnits;
-        if (b0 + lane >= batch) continue;
-        const rf_slot_desc* sd = slots + s;
-        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
-        const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
-        const int mask_empty = sd->mask_empty;
-        const BucketMod bmod = bucket_mod_init(nbins, mask_empty);
-        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
-        const int64_t u = (int64_t)(b0 + lane) * n_slots + s;
-        const int t = bag_off[u];
-        uint32_t r0, r1;
-        if (bag_off[u + 1] > t) {
-            const int tb = tok_off[t], n = tok_off[t + 1] - tb;
-            uint64_t h0, h1;
-            siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
-            r0 = ok ? (uint32_t)(rb0 + bucket_from_hash(h0, n, bmod)) : 0u;
-            r1 = ok ? (uint32_t)(rb1 + bucket_from_hash(h1, n, bmod)) : 0u;
-        } else if (mask_pad) {
-            r0 = r1 = 0xffffffffu;  // masked empty bag: zeros
-        } else {
-            int64_t pb0 = 0, pb1 = 0;
-            if (!mask_empty) {
-                pb0 = (int64_t)(siphash24_dev(salt0, salt0, tok_bytes, 0) % (uint64_t)nbins);
-                pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
-            }
-            r0 = ok ? (uint32_t)(rb0 + pb0) : 0u;
-            r1 = ok ? (uint32_t)(rb1 + pb1) : 0u;
-        }
-        rows2[(int64_t)s * batch + b0 + lane] = make_uint2(r0, r1);
-    }
-}
-
-template <int LPR, typename TT, typename OT>
-__global__ __launch_bounds__(64) void st_gather_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
-                                                       const int32_t* __restrict__ lmax, int batch,
-                                                       const TT* __restrict__ table, int64_t table_rows, int dim,
-                                                       OT* __restrict__ out, int64_t out_stride, int flags,
-                                                       const uint2* __restrict__ rows2) {
-    constexpr int EPV = Elem<TT>::EPV;
-    constexpr int TEAMS = 64 / LPR;
-    constexpr int G = kUnits / TEAMS;
-    constexpr int GH = G > 8 ? 8 : G;
-    const int lane = threadIdx.x, team = lane / LPR, tl = lane % LPR;
-    const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
-    const int nbb = (batch + kUnits - 1) / kUnits;
-    const int64_t n_items = (int64_t)n_slots * nbb;
-    for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-        const int s = (int)(item / nbb);
-        const int b0 = (int)(item - (int64_t)s * nbb) * kUnits;
-        const int nu = min(kUnits, batch - b0);
-        const rf_slot_desc* sd = slots + s;
-        const int comb = sd->combiner;
-        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
-        const int64_t out_off = sd->out_off;
-        const int lm = lmax[s];
-        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
-        if (lm == 0 && comb == RF_COMB_NULL) continue;
-        const float initv = comb_init(comb);
-        float special = 0.0f;
-        if (lm == 0 && !mask_pad)
-            special = comb == RF_COMB_AVG ? kMeanOfNothing : (comb == RF_COMB_MAX || comb == RF_COMB_MIN) ? initv : 0.0f;
-        if (lm > 1 || !ok) special = __builtin_nanf("");
-        const bool use_special = lm != 1 || !ok;
-        const uint2* rs = rows2 + (int64_t)s * batch + b0;
-#pragma unroll
-        for (int g0 = 0; g0 < G; g0 += GH) {
-            uint2 id[GH];
-#pragma unroll
-            for (int g = 0; g < GH; ++g) id[g] = rs[min(team + TEAMS * (g0 + g), nu - 1)];
-            uint4 v[GH][2];
-#pragma unroll
-            for (int g = 0; g < GH; ++g) {
-                const bool z = id[g].x == 0xffffffffu;  // masked empty bag: read row 0 (valid), store zeros
-                v[g][0] = row_chunk(table, z ? 0u : id[g].x, dim, tl);
-                v[g][1] = row_chunk(table, z ? 0u : id[g].y, dim, tl);
-            }
-#pragma unroll
-            for (int g = 0; g < GH; ++g) {
-                const int j = team + TEAMS * (g0 + g);
-                if (j >= nu) continue;
-                const bool zero = id[g].x == 0xffffffffu;
-                const int64_t ob = (int64_t)(b0 + j) * out_stride + out_off;
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    float f[EPV], a[EPV];
-                    unpack16<TT>(v[g][k], f);
-#pragma unroll
-                    for (int e = 0; e < EPV; ++e) {
-                        if (use_special) a[e] = special;
-                        else if (zero) a[e] = 0.0f;
-                        else if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) a[e] = __fadd_rn(0.0f, f[e]);
-                        else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) a[e] = comb_step(comb, initv, f[e]);
-                        else a[e] = f[e];
-                    }
-                    store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + tl * EPV, a);
-                }
-            }
-        }
-    }
-}
-
 template <typename TT, typename OT>
 int launch_single_token(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
                         const int32_t* bag_off, const int32_t* lmax, int64_t n_units, const void* table,
                         int64_t table_rows, int32_t dim, void* out, int64_t out_stride, int32_t flags, int grid,
-                        hipStream_t st, void* scratch) {
+                        hipStream_t st) {
     const int nchunks = dim / Elem<TT>::EPV;
-    if (scratch) {  // two passes through the caller's n_units x uint2 scratch
-        const int batch = (int)(n_units / n_slots);
-        hipLaunchKernelGGL(st_rows_kernel, dim3(grid), dim3(64), 0, st, d_slots, n_slots, tok_bytes, tok_off, bag_off,
-                           batch, table_rows, flags, (uint2*)scratch);
-#define RF_STG(L)                                                                                                      \
-    hipLaunchKernelGGL((st_gather_kernel<L, TT, OT>), dim3(grid), dim3(64), 0, st, d_slots, n_slots, lmax, batch,        \
-                       (const TT*)table, table_rows, dim, (OT*)out, out_stride, flags, (const uint2*)scratch)
-        if (nchunks == 4) RF_STG(4);
-        else if (nchunks == 8) RF_STG(8);
-        else if (nchunks == 16) RF_STG(16);
-        else return rf_set_error(RF_EINVAL, "single-token kernel: rows of %d 16-byte chunks (4, 8 or 16 supported)", nchunks);
-#undef RF_STG
-        return rf_check_launch("st_rows_kernel / st_gather_kernel");
-    }
 #define RF_ST(L)                                                                                                      \
     hipLaunchKernelGGL((single_token_embed_kernel<L, TT, OT>), dim3(grid), dim3(64), 0, st, d_slots, n_slots, tok_bytes, \
                        tok_off, bag_off, lmax, n_units, (const TT*)table, table_rows, dim, (OT*)out, out_stride, flags)
@@ -897,7 +764,7 @@ RF_FUSED_LAUNCH_DECL(launch_pool_bf16_obf16);
 int launch_single_token_any(int32_t table_dtype, int32_t out_dtype, const rf_slot_desc* d_slots, int32_t n_slots,
                             const uint8_t* tok_bytes, const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
                             int64_t n_units, const void* table, int64_t table_rows, int32_t dim, void* out,
-                            int64_t out_stride, int32_t flags, int grid, hipStream_t st, void* scratch);
+                            int64_t out_stride, int32_t flags, int grid, hipStream_t st);
 
 // picks the launcher for (table dtype, output dtype)
 inline int launch_fused_any(bool pre, int32_t table_dtype, int32_t out_dtype, const rf_slot_desc* d_slots,

@@ -123,9 +123,20 @@ __global__ __launch_bounds__(256) void pp_seg_kernel(const int32_t* __restrict__
         int owner = 0;
         int64_t c = counts[0];
         while (owner + 1 < P && i >= c) c += counts[++owner];
-        atomicAdd(seg_counts + owner, 1);
         if (seg_of) seg_of[(int64_t)unit[i] * P + owner] = seg;
         if (seg_start) seg_start[seg] = (int32_t)i;
+    }
+}
+
+// segments per owner chunk from the inclusive head scan at the chunk edges (no atomics: a counter shared by
+// millions of heads serialises at the memory side)
+__global__ void pp_segcount_kernel(const int32_t* __restrict__ scan, const int32_t* __restrict__ counts, int P,
+                                   int32_t* __restrict__ seg_counts) {
+    for (int o = threadIdx.x; o < P; o += blockDim.x) {
+        int64_t start = 0;
+        for (int p = 0; p < o; ++p) start += counts[p];
+        const int64_t end = start + counts[o];
+        seg_counts[o] = end > start ? scan[end - 1] - (start > 0 ? scan[start - 1] : 0) : 0;
     }
 }
 
@@ -297,6 +308,7 @@ extern "C" int rf_pp_heads(const int32_t* unit, int64_t n, const int32_t* counts
         return rf_set_error(RF_EHIP, "rf_pp_heads: scan failed");
     hipLaunchKernelGGL(pp_seg_kernel, dim3(grid_pp(n)), dim3(256), 0, st, unit, head, scan, n, counts, nranks, seg_counts,
                        seg_of, seg_start);
+    hipLaunchKernelGGL(pp_segcount_kernel, dim3(1), dim3(256), 0, st, scan, counts, nranks, seg_counts);
     return rf_check_launch("rf_pp_heads");
 }
 

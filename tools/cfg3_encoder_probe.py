@@ -21,13 +21,10 @@ def main():
     hb = synthetic_batch(B, [False] * Ls, seed=77, slot_ids=range(Ls)).to("cuda")
     out = torch.empty((B, enc.out_width), dtype=torch.bfloat16, device="cuda")
     res = {}
-    for name, fl, st, tp in (("single_token_two_pass", 0, True, True), ("single_token_fused", 0, True, False),
-                             ("single_token_two_pass_again", 0, True, True), ("general_kernel_lean", 0, False, False),
-                             ("general_phase2", 1 << 15, False, False), ("no_hash", 1 << 12, False, False),
-                             ("hash_only", 1 << 13, False, False)):
+    for name, fl, st in (("single_token_kernel", 0, True), ("general_kernel_lean", 0, False),
+                         ("general_phase2", 1 << 15, False), ("no_hash", 1 << 12, False), ("hash_only", 1 << 13, False)):
         enc.extra_flags = fl
         enc.single_token = st
-        enc.two_pass = tp
 
         def run():
             enc(hb, out=out)
@@ -65,8 +62,7 @@ def main():
         torch.cuda.synchronize()
         res[name] = round(sorted(a.elapsed_time(b) for a, b in zip(s, e))[25], 4)
     by = 2 * B * Ls * 128 + B * Ls * 256 + int(hb.tok_bytes.numel()) + 4 * hb.n_tokens
-    res["single_token_two_pass_GBs"] = round(by / res["single_token_two_pass"] / 1e6, 1)
-    res["single_token_fused_GBs"] = round(by / res["single_token_fused"] / 1e6, 1)
+    res["single_token_GBs"] = round(by / res["single_token_kernel"] / 1e6, 1)
     res["general_lean_GBs"] = round(by / res["general_kernel_lean"] / 1e6, 1)
     print(json.dumps(res))
 
