@@ -31,28 +31,35 @@ __device__ __forceinline__ int unit_len(int comb, int len, int lm, bool mask_pad
     return mask_pad ? len : max(lm, len);  // positions the combiner sees (the reference pads to the batch max)
 }
 
-// entries of unit (b, s, k); emit == false: count only
-template <bool EMIT>
-__device__ __forceinline__ int unit_entries(int comb, int len, int L, int t0, int k, int64_t pad_row,
-                                            const int64_t* __restrict__ rows, int64_t* er, int32_t* em) {
-    int n = 0;
-    auto put = [&](int64_t r, int m) {
-        if (EMIT) {
-            er[n] = r;
-            em[n] = m;
-        }
-        ++n;
-    };
+// number of pooling entries of a unit (no row is read: the count pass must not touch rows)
+__device__ __forceinline__ int unit_count(int comb, int len, int L) {
     if (L == 0) return 0;
-    if (comb == RF_COMB_FIRST) {
-        put(len > 0 ? rows[2 * (int64_t)t0 + k] : pad_row, 1);
-    } else if (comb == RF_COMB_LAST) {
-        put(len >= L ? rows[2 * (int64_t)(t0 + L - 1) + k] : pad_row, 1);
-    } else {
-        for (int l = 0; l < len; ++l) put(rows[2 * (int64_t)(t0 + l) + k], 1);
-        if (L > len) put(pad_row, L - len);
+    if (comb == RF_COMB_FIRST || comb == RF_COMB_LAST) return 1;
+    return len + (L > len ? 1 : 0);
+}
+
+// the entries of unit (b, s, k) in position order (padding collapsed into one entry of multiplicity L - len)
+__device__ __forceinline__ int unit_emit(int comb, int len, int L, int t0, int k, int64_t pad_row,
+                                         const int64_t* __restrict__ rows, int64_t* __restrict__ er,
+                                         int32_t* __restrict__ em) {
+    if (L == 0) return 0;
+    if (comb == RF_COMB_FIRST || comb == RF_COMB_LAST) {
+        const bool tok = comb == RF_COMB_FIRST ? len > 0 : len >= L;
+        const int l = comb == RF_COMB_FIRST ? 0 : L - 1;
+        er[0] = tok ? rows[2 * (int64_t)(t0 + l) + k] : pad_row;
+        em[0] = 1;
+        return 1;
     }
-    return n;
+    for (int l = 0; l < len; ++l) {
+        er[l] = rows[2 * (int64_t)(t0 + l) + k];
+        em[l] = 1;
+    }
+    if (L > len) {
+        er[len] = pad_row;
+        em[len] = L - len;
+        return len + 1;
+    }
+    return len;
 }
 
 __global__ __launch_bounds__(256) void pp_count_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
@@ -67,7 +74,7 @@ __global__ __launch_bounds__(256) void pp_count_kernel(const rf_slot_desc* __res
         const int t0 = bag_off[bs], len = bag_off[bs + 1] - t0;
         const int comb = slots[s].combiner;
         const int L = unit_len(comb, len, lmax[s], mask_pad);
-        cnt[u] = unit_entries<false>(comb, len, L, t0, 0, 0, nullptr, nullptr, nullptr);
+        cnt[u] = unit_count(comb, len, L);
     }
 }
 
@@ -88,7 +95,7 @@ __global__ __launch_bounds__(256) void pp_emit_kernel(const rf_slot_desc* __rest
         const int L = unit_len(comb, len, lmax[s], mask_pad);
         const int64_t pad = rows[2 * n_tok + 2 * (int64_t)s + k];
         const int32_t o = off[u];
-        const int n = unit_entries<true>(comb, len, L, t0, k, pad, rows, ent_row + o, ent_mult + o);
+        const int n = unit_emit(comb, len, L, t0, k, pad, rows, ent_row + o, ent_mult + o);
         for (int i = 0; i < n; ++i) ent_unit[o + i] = (int32_t)u;
     }
 }

@@ -25,6 +25,22 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
+__device__ __forceinline__ float gelu_erf(float x) {
+    const float z = x * 0.70710678118654752440f, a = fabsf(z);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, a, 1.0f));
+    float p = fmaf(t, 0.17087277f, -0.82215223f);
+    p = fmaf(t, p, 1.48851587f);
+    p = fmaf(t, p, -1.13520398f);
+    p = fmaf(t, p, 0.27886807f);
+    p = fmaf(t, p, -0.18628806f);
+    p = fmaf(t, p, 0.09678418f);
+    p = fmaf(t, p, 0.37409196f);
+    p = fmaf(t, p, 1.00002368f);
+    p = fmaf(t, p, -1.26551223f);
+    const float e = t * __expf(fmaf(-a, a, p));
+    return z >= 0.f ? x * fmaf(-0.5f, e, 1.0f) : 0.5f * x * e;
+}
+
 template <int N>
 __device__ __forceinline__ void vmcnt() {
     if constexpr (N >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
@@ -44,7 +60,10 @@ __device__ __forceinline__ void wait_stages(int pending) {
 // filled by global_load_lds_dwordx4 (one instruction = 8 rows x 128 B, lane-linear; chunk c of row r lands at
 // c ^ (r & 7) by swizzling the source). SCHED 0: all fragment reads, then all MFMAs; SCHED 1: reads of the
 // second k-half issued among the first half's MFMAs (compiler-scheduled).
-template <int BM, int BN, int STAGES, int WM, int WN, int SCHED>
+// EPI 0: raw fp32, lane-scattered stores; 1: bias + gelu fp32 scattered (rf_linear_fwd's epilogue); 2: the same
+// through an LDS transpose (16-byte row stores); 3: bias + gelu -> bf16 scattered (the stats GEMM's output);
+// 4: bf16 through the LDS transpose
+template <int BM, int BN, int STAGES, int WM, int WN, int SCHED, int EPI = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_v(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                        float* __restrict__ y, int M, int N, int K) {
     constexpr int NW = WM * WN, NT = 64 * NW;
@@ -135,17 +154,56 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_v(const uint16_t* __restric
             mm(1);
         }
     }
+    if constexpr (EPI == 0 || EPI == 1 || EPI == 3) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-        const int col = n0 + wn * TN + j * 16 + lr;
-        if (col >= N) continue;
+        for (int j = 0; j < FN; ++j) {
+            const int col = n0 + wn * TN + j * 16 + lr;
+            if (col >= N) continue;
+            const float bv = 0.001f * (col & 7);
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+            for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                if (row < M) y[(int64_t)row * N + col] = acc[i][j][r];
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                    if (row >= M) continue;
+                    if constexpr (EPI == 0) y[(int64_t)row * N + col] = acc[i][j][r];
+                    else if constexpr (EPI == 1) y[(int64_t)row * N + col] = gelu_erf(acc[i][j][r] + bv);
+                    else reinterpret_cast<__bf16*>(y)[(int64_t)row * N + col] = (__bf16)gelu_erf(acc[i][j][r] + bv);
+                }
+        }
+    } else {
+        // LDS transpose: the wave's TM x TN tile row-major in LDS (row pitch TN + 4 floats), then each lane
+        // stores 16-byte pieces of rows
+        __syncthreads();  // every wave is done with the ring
+        constexpr int PITCH = TN + 4;
+        float* t = reinterpret_cast<float*>(smem_raw) + wave * TM * PITCH;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int cl = j * 16 + lr;
+            const float bv = 0.001f * ((n0 + wn * TN + cl) & 7);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t[(i * 16 + lg * 4 + r) * PITCH + cl] = gelu_erf(acc[i][j][r] + bv);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes
+        constexpr int EL = EPI == 2 ? 4 : 8;   // elements per 16-byte store
+        constexpr int PER_ROW = TN / EL;
+        for (int q = lane; q < TM * PER_ROW; q += 64) {
+            const int rl = q / PER_ROW, c0 = (q % PER_ROW) * EL;
+            const int row = m0 + wm * TM + rl, col = n0 + wn * TN + c0;
+            if (row >= M || col >= N) continue;
+            const float* src = t + rl * PITCH + c0;
+            if constexpr (EPI == 2) {
+                *reinterpret_cast<float4*>(y + (int64_t)row * N + col) = make_float4(src[0], src[1], src[2], src[3]);
+            } else {
+                typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+                b8 v;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (__bf16)src[e];
+                *reinterpret_cast<b8*>(reinterpret_cast<__bf16*>(y) + (int64_t)row * N + col) = v;
             }
+        }
     }
 }
 
@@ -174,15 +232,16 @@ __global__ void fill_bf16(uint16_t* p, int64_t n, uint32_t seed) {
 struct Variant {
     std::string name;
     void (*fn)(const uint16_t*, const uint16_t*, float*, int, int, int);
-    int BM, BN, threads;
+    int BM, BN, threads, epi;
     size_t lds;
 };
 
-template <int BM, int BN, int STAGES, int WM, int WN, int SCHED>
+template <int BM, int BN, int STAGES, int WM, int WN, int SCHED, int EPI = 0>
 Variant mk(const char* nm) {
     Variant v;
     v.name = nm;
-    v.fn = gemm_v<BM, BN, STAGES, WM, WN, SCHED>;
+    v.fn = gemm_v<BM, BN, STAGES, WM, WN, SCHED, EPI>;
+    v.epi = EPI;
     v.BM = BM;
     v.BN = BN;
     v.threads = 64 * WM * WN;
@@ -193,21 +252,18 @@ Variant mk(const char* nm) {
 
 int main(int argc, char** argv) {
     std::vector<Variant> vs = {
-        mk<128, 128, 3, 2, 2, 0>("128x128 s3 w4 sched0 (r02)"),
-        mk<128, 128, 3, 2, 2, 1>("128x128 s3 w4 sched1"),
-        mk<128, 128, 2, 2, 2, 0>("128x128 s2 w4 sched0"),
-        mk<128, 128, 2, 2, 2, 1>("128x128 s2 w4 sched1"),
-        mk<128, 128, 4, 2, 2, 0>("128x128 s4 w4 sched0"),
-        mk<128, 128, 5, 2, 2, 0>("128x128 s5 w4 sched0"),
-        mk<128, 128, 5, 2, 2, 1>("128x128 s5 w4 sched1"),
-        mk<64, 128, 3, 1, 4, 0>("64x128 s3 w4 sched0 (r02 small)"),
-        mk<64, 128, 2, 1, 4, 1>("64x128 s2 w4 sched1"),
-        mk<64, 128, 4, 1, 4, 1>("64x128 s4 w4 sched1"),
-        mk<128, 128, 3, 4, 2, 1>("128x128 s3 w8 sched1"),
-        mk<128, 128, 2, 4, 2, 1>("128x128 s2 w8 sched1"),
-        mk<256, 128, 3, 4, 2, 1>("256x128 s3 w8 sched1"),
-        mk<256, 128, 2, 4, 2, 1>("256x128 s2 w8 sched1"),
-        mk<128, 256, 2, 2, 4, 1>("128x256 s2 w8 sched1"),
+        mk<64, 128, 3, 1, 4, 0, 0>("64x128 s3 epi0 raw f32"),
+        mk<64, 128, 2, 1, 4, 0, 0>("64x128 s2 epi0 raw f32"),
+        mk<64, 128, 3, 1, 4, 0, 1>("64x128 s3 epi1 gelu f32 scat"),
+        mk<64, 128, 2, 1, 4, 0, 1>("64x128 s2 epi1 gelu f32 scat"),
+        mk<64, 128, 2, 1, 4, 0, 2>("64x128 s2 epi2 gelu f32 lds"),
+        mk<64, 128, 3, 1, 4, 0, 3>("64x128 s3 epi3 gelu bf16 scat"),
+        mk<64, 128, 2, 1, 4, 0, 3>("64x128 s2 epi3 gelu bf16 scat"),
+        mk<64, 128, 2, 1, 4, 0, 4>("64x128 s2 epi4 gelu bf16 lds"),
+        mk<128, 128, 2, 2, 2, 0, 1>("128x128 s2 epi1 gelu f32 scat"),
+        mk<128, 128, 2, 2, 2, 0, 2>("128x128 s2 epi2 gelu f32 lds"),
+        mk<128, 128, 3, 2, 2, 0, 1>("128x128 s3 epi1 gelu f32 scat"),
+        mk<128, 128, 2, 4, 2, 1, 2>("128x128 s2 w8 epi2 gelu f32 lds"),
     };
     struct Shape { int M, K, N; };
     std::vector<Shape> shapes = {{4096, 1280, 1024}, {4096, 1024, 512}, {51200, 1280, 1024}};
@@ -238,7 +294,24 @@ int main(int argc, char** argv) {
             CK(hipMemcpy(hy.data(), y, hy.size() * 4, hipMemcpyDeviceToHost));
             double md = 0;
             for (size_t i = 0; i < hy.size(); ++i) md = std::max(md, (double)fabsf(hy[i] - hr[i]));
-            if (md > 1e-2) printf("MISMATCH %s M=%d: max|d| %g\n", vs[v].name.c_str(), M, md);
+            if (vs[v].epi == 0 && md > 1e-2) printf("MISMATCH %s M=%d: max|d| %g\n", vs[v].name.c_str(), M, md);
+            if (vs[v].epi != 0) {  // epilogue variants: gelu(ref + bias) within bf16 / fp32 tolerance
+                double me = 0;
+                for (int64_t i = 0; i < (int64_t)M * N; i += 9973) {
+                    const int col = i % N;
+                    const double g = hr[i] + 0.001 * (col & 7);
+                    const double want = 0.5 * g * (1.0 + erf(g / sqrt(2.0)));
+                    double got = hy[i];
+                    if (vs[v].epi >= 3) {
+                        const uint32_t u = (uint32_t)reinterpret_cast<uint16_t*>(hy.data())[i] << 16;
+                        float f;
+                        memcpy(&f, &u, 4);
+                        got = f;
+                    }
+                    me = std::max(me, fabs(got - want) / (1.0 + fabs(want)));
+                }
+                if (me > (vs[v].epi >= 3 ? 2e-2 : 1e-3)) printf("EPI MISMATCH %s M=%d: rel %g\n", vs[v].name.c_str(), M, me);
+            }
         }
         for (int r = 0; r < rounds; ++r)
             for (size_t v = 0; v < vs.size(); ++v) {
