@@ -557,6 +557,46 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
 #pragma unroll
     for (int p = 0; p + 1 < kLdsStages; ++p)
         if (p < nk) glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, p * kLdsK, As(p), Bs(p), tid);
+    // The epilogue's per-column parameters (bias, or the LN fold's s_c / t_c) are loaded now, under the first
+    // stage's copies, instead of as dependent loads after the last MFMA (one HBM round trip off the tail).
+    float pb[FN], pt[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int col = min(n0 + wn * TN + j * 16 + lr, N - 1);
+        if constexpr (EPI == kEpiLnFold) {
+            pb[j] = ea.fs[col];
+            pt[j] = ea.ft[col];
+        } else {
+            pb[j] = bias ? bias[col] : 0.f;
+            pt[j] = 0.f;
+        }
+    }
+    // LN fold: the tile's row statistics are reduced now too (their partials are complete: the previous
+    // launch wrote them), into an LDS area past the ring, read after the loop; the reduction order is fixed
+    // (TPR threads per row, each a strided subset, then a commutative shuffle combine: every lane the same bits)
+    float* srow = reinterpret_cast<float*>(smem_raw + (size_t)kLdsStages * (A_EL + B_EL) * 2);
+    if constexpr (EPI == kEpiLnFold) {
+        constexpr int TPR = 256 / BM;
+        const int rl = tid / TPR, part = tid % TPR;
+        const int64_t row = m0 + rl < M ? m0 + rl : M - 1;
+        float s1 = 0.f, s2 = 0.f;
+        for (int p = part; p < ea.P; p += TPR) {
+            const float2 v = *reinterpret_cast<const float2*>(ea.stats + 2 * (row * ea.P + p));
+            s1 += v.x;
+            s2 += v.y;
+        }
+#pragma unroll
+        for (int o = 1; o < TPR; o <<= 1) {
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+        }
+        if (part == 0) {
+            const float m = s1 / (float)K;
+            srow[2 * rl] = m;
+            srow[2 * rl + 1] = 1.0f / sqrtf(fmaxf(s2 / (float)K - m * m, 0.f) + ea.eps);
+        }
+        __syncthreads();  // srow visible to every wave (this also retires stage 0's copies: the loop waits for them first)
+    }
     for (int kt = 0; kt < nk; ++kt) {
         const int s = kt % kLdsStages;
         // stage kt must have landed; the stages issued after it (at most kLdsStages - 2) may stay in flight
@@ -603,7 +643,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
             for (int j = 0; j < FN; ++j) {
                 const int col = n0 + wn * TN + j * 16 + lr;
                 if (col >= N) continue;
-                const float bv = bias ? bias[col] : 0.f;
+                const float bv = pb[j];
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -624,7 +664,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
             for (int j = 0; j < FN; ++j) {
                 const int col = n0 + wn * TN + j * 16 + lr;
                 const bool cok = col < N;
-                const float bv = bias && cok ? bias[col] : 0.f;
+                const float bv = cok ? pb[j] : 0.f;
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -634,7 +674,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
                         if (cok) {
                             rs[i][r] += v;
                             rq[i][r] += v * v;
-                            if (row < M) ea.yb[row * ldy + col] = (uint16_t)f32_to_bf16_bits(v);
+                            if (row < M) reinterpret_cast<__bf16*>(ea.yb)[row * ldy + col] = (__bf16)v;  // v_cvt_pk_bf16_f32, RNE
                         }
                     }
             }
@@ -657,33 +697,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
                     if constexpr (WN == 2) *reinterpret_cast<float2*>(sp + 4) = make_float2(0.f, 0.f);
                 }
             }
-    } else {  // kEpiLnFold
-        // the tile's rows: P partials each, summed in a fixed order (TPR threads per row, each a strided
-        // subset, then a commutative shuffle combine that gives every lane the same bits) -> LDS
-        constexpr int TPR = 256 / BM;
-        float* srow = reinterpret_cast<float*>(smem_raw);
-        __syncthreads();  // every wave is done with the LDS ring
-        {
-            const int rl = tid / TPR, part = tid % TPR;
-            const int64_t row = m0 + rl < M ? m0 + rl : M - 1;
-            float s1 = 0.f, s2 = 0.f;
-            for (int p = part; p < ea.P; p += TPR) {
-                const float2 v = *reinterpret_cast<const float2*>(ea.stats + 2 * (row * ea.P + p));
-                s1 += v.x;
-                s2 += v.y;
-            }
-#pragma unroll
-            for (int o = 1; o < TPR; o <<= 1) {
-                s1 += __shfl_xor(s1, o, 64);
-                s2 += __shfl_xor(s2, o, 64);
-            }
-            if (part == 0) {
-                const float m = s1 / (float)K;
-                srow[2 * rl] = m;
-                srow[2 * rl + 1] = 1.0f / sqrtf(fmaxf(s2 / (float)K - m * m, 0.f) + ea.eps);
-            }
-        }
-        __syncthreads();
+    } else {  // kEpiLnFold: the row statistics were reduced into srow before the loop
         float mu[FM][4], rstd[FM][4];
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -698,7 +712,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
             for (int j = 0; j < FN; ++j) {
                 const int col = n0 + wn * TN + j * 16 + lr;
                 if (col >= N) continue;
-                const float sc = ea.fs[col], tc = ea.ft[col];
+                const float sc = pb[j], tc = pt[j];
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -713,7 +727,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
 
 template <int BM>
 constexpr size_t gemm_lds_bytes() {
-    return (size_t)kLdsStages * (BM + kLdsBN) * kLdsK * 2;
+    return (size_t)kLdsStages * (BM + kLdsBN) * kLdsK * 2 + (size_t)BM * 2 * sizeof(float);  // ring + LN-fold rows
 }
 
 // small-N head: one wave per row, fp32 dot products, optional row softmax (N <= 64)
