@@ -369,9 +369,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
     const char* w = reinterpret_cast<const char*>(wv);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int wm = wave >> 1, wn = wave & 1;
-    // XCD-aware tile order: consecutive tiles of one M row-panel on one XCD (guide T1)
+    // XCD-aware tile order (guide T1, bijective form): blocks b, b + 8, ... share an XCD and take consecutive
+    // tiles, so the N-tiles of one M row-panel read that panel through ONE XCD's L2 (the DSSM towers' 142 /
+    // 335 MB activations were otherwise fetched once per N-tile, from 8 different L2s)
     const int tiles_n = (N + BT - 1) / BT;
-    const int64_t tid_lin = blockIdx.x;
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+    const int64_t tid_lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
     const int64_t m0 = (tid_lin / tiles_n) * BT;
     const int n0 = (int)(tid_lin % tiles_n) * BT;
     f4 acc[FR][FR];
