@@ -205,6 +205,17 @@ int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t 
                   int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream);
 
 /*
+ * rf_linear_fwd with split-K for fp32 layers whose 128-tile grid leaves CUs half-occupied at deep K (the DSSM
+ * towers, K = 8704 / 20480 at B = 4096): S K-ranges as S workgroups per tile writing fp32 partials to ws, then
+ * y = act(sum_{s = 0..S-1} partial_s + b) in that fixed order (deterministic; not the unsplit fmaf chain).
+ * rf_linear_splitk_ws_bytes: the ws it needs (0 = no split for this shape); with a smaller ws (or none) it is
+ * exactly rf_linear_fwd. ws, x, W, b 16-byte aligned.
+ */
+size_t rf_linear_splitk_ws_bytes(int32_t x_dtype, int64_t M, int32_t K, int32_t N);
+int rf_linear_splitk_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t N,
+                         const float* b, int32_t act, float* y, int64_t ldy, void* ws, size_t ws_bytes, void* stream);
+
+/*
  * A two-layer create_mlp on a narrow input in ONE launch (the ESIM input_mlp [256, 512] over the dense
  * features, esim.py:45-48; mlp.py:4-15 with LayerNormalization):
  *   out = act(LN1(act(LN0(x) W0^T + b0)) W1^T + b1)

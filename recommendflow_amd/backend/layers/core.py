@@ -63,9 +63,23 @@ class Dense(torch.nn.Module):
             x = x.contiguous()
         if out is None:
             out = torch.empty((M, self.units), dtype=torch.float32, device=self.weight.device)
-        L.call("rf_linear_fwd", L.ptr(x), L.torch_dtype_code(self.dtype), M, self.in_features, x.stride(0),
-               L.ptr(self.weight), self.units, L.ptr(self.bias), L.ACT[self.activation], L.ptr(out), out.stride(0),
-               L.stream_ptr(stream))
+        return self._linear(x, self.weight, self.bias, out, stream)
+
+    def _linear(self, x, weight, bias, out, stream):
+        """rf_linear_fwd, or its split-K form when the shape asks for one (fp32 deep-K layers at a grid of at
+        most one 128-tile per CU: rf_linear_splitk_ws_bytes > 0); the partial-sum workspace comes from the
+        caching allocator on the launch stream."""
+        M, dt = x.shape[0], L.torch_dtype_code(self.dtype)
+        ws_bytes = int(L.load().rf_linear_splitk_ws_bytes(dt, M, self.in_features, self.units)) \
+            if self.dtype == torch.float32 else 0
+        if ws_bytes:
+            ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=self.weight.device)
+            L.call("rf_linear_splitk_fwd", L.ptr(x), dt, M, self.in_features, x.stride(0), L.ptr(weight), self.units,
+                   L.ptr(bias), L.ACT[self.activation], L.ptr(out), out.stride(0), L.ptr(ws), ws_bytes,
+                   L.stream_ptr(stream))
+            return out
+        L.call("rf_linear_fwd", L.ptr(x), dt, M, self.in_features, x.stride(0), L.ptr(weight), self.units,
+               L.ptr(bias), L.ACT[self.activation], L.ptr(out), out.stride(0), L.stream_ptr(stream))
         return out
 
 
@@ -80,10 +94,7 @@ class Dense(torch.nn.Module):
         M = x.shape[0]
         if out is None:
             out = torch.empty((M, self.units), dtype=torch.float32, device=self.weight.device)
-        L.call("rf_linear_fwd", L.ptr(x), L.torch_dtype_code(self.dtype), M, self.in_features, x.stride(0),
-               L.ptr(weight), self.units, L.ptr(bias), L.ACT[self.activation], L.ptr(out), out.stride(0),
-               L.stream_ptr(stream))
-        return out
+        return self._linear(x, weight, bias, out, stream)
 
 
 class LayerNormalization:

@@ -312,7 +312,7 @@ __device__ __forceinline__ v4u gload_asm(const char* p) {
 template <bool BF16, int BT, bool KTAIL>
 __device__ __forceinline__ void load_tile(v4u (&rg)[2][(GemmCfg<BF16, BT>::PER_THREAD)], uint32_t (&msk)[(GemmCfg<BF16, BT>::PER_THREAD)],
                                           const char* __restrict__ x, const char* __restrict__ w, int64_t M, int N, int K,
-                                          int64_t ldx, int64_t m0, int n0, int k0, int tid) {
+                                          int64_t ldx, int64_t ldw, int64_t m0, int n0, int k0, int tid) {
     using C = GemmCfg<BF16, BT>;
 #pragma unroll
     for (int i = 0; i < C::PER_THREAD; ++i) {
@@ -327,7 +327,7 @@ __device__ __forceinline__ void load_tile(v4u (&rg)[2][(GemmCfg<BF16, BT>::PER_T
             kc = kk < K ? kk : K - C::EPC;
         }
         rg[0][i] = gload_asm(x + (row * ldx + kc) * C::ESZ);
-        rg[1][i] = gload_asm(w + (col * K + kc) * C::ESZ);
+        rg[1][i] = gload_asm(w + (col * ldw + kc) * C::ESZ);
     }
 }
 
@@ -358,15 +358,23 @@ __device__ __forceinline__ void store_tile(char* __restrict__ As, char* __restri
     }
 }
 
-template <bool BF16, int BT, bool KTAIL>
+// SPLIT (split-K): blockIdx.y = s takes k in [s * kspan, min(K, (s + 1) * kspan)) and stores its raw partial sums
+// to y + s * M * ldy (no bias, no activation: splitk_reduce_kernel adds the partials in order s = 0, 1, ...).
+template <bool BF16, int BT, bool KTAIL, bool SPLIT = false>
 __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
                                                    const float* __restrict__ bias, float* __restrict__ y, int64_t M,
-                                                   int N, int K, int64_t ldx, int64_t ldy, int act) {
+                                                   int N, int K, int64_t ldx, int64_t ldy, int act, int kspan = 0) {
     using C = GemmCfg<BF16, BT>;
     constexpr int FR = C::FR, WT = BT / 2;
     __shared__ __attribute__((aligned(16))) char smem[2][2][BT * C::RS * C::ESZ];
-    const char* x = reinterpret_cast<const char*>(xv);
-    const char* w = reinterpret_cast<const char*>(wv);
+    const int64_t ldw = K;  // W rows are [N][K]
+    const int kb = SPLIT ? (int)blockIdx.y * kspan : 0;
+    const char* x = reinterpret_cast<const char*>(xv) + (int64_t)kb * C::ESZ;
+    const char* w = reinterpret_cast<const char*>(wv) + (int64_t)kb * C::ESZ;
+    if constexpr (SPLIT) {
+        K = min(kspan, K - kb);
+        y += (int64_t)blockIdx.y * M * ldy;
+    }
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int wm = wave >> 1, wn = wave & 1;
     // XCD-aware tile order (guide T1, bijective form): blocks b, b + 8, ... share an XCD and take consecutive
@@ -385,14 +393,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
     v4u rg[2][C::PER_THREAD];
     uint32_t msk[C::PER_THREAD];
     const int nk = (K + C::BK - 1) / C::BK;
-    load_tile<BF16, BT, KTAIL>(rg, msk, x, w, M, N, K, ldx, m0, n0, 0, tid);
+    load_tile<BF16, BT, KTAIL>(rg, msk, x, w, M, N, K, ldx, ldw, m0, n0, 0, tid);
     wait_tile<BF16, BT, KTAIL>(rg, msk);
     store_tile<BF16, BT>(smem[0][0], smem[0][1], rg, tid);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         // the last step re-loads its own stage into the idle buffer: no branch around the loads
-        load_tile<BF16, BT, KTAIL>(rg, msk, x, w, M, N, K, ldx, m0, n0, (kt + 1 < nk ? kt + 1 : kt) * C::BK, tid);
+        load_tile<BF16, BT, KTAIL>(rg, msk, x, w, M, N, K, ldx, ldw, m0, n0, (kt + 1 < nk ? kt + 1 : kt) * C::BK, tid);
         const char* As = smem[cur][0];
         const char* Bs = smem[cur][1];
         if constexpr (BF16) {
@@ -448,6 +456,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
         __syncthreads();
     }
     wait_tile<BF16, BT, KTAIL>(rg, msk);  // the last step's spare loads land before their registers are reused
+    if constexpr (SPLIT) {  // raw partial sums
+#pragma unroll
+        for (int j = 0; j < FR; ++j) {
+            const int col = n0 + wn * WT + j * 16 + lr;
+            if (col >= N) continue;
+#pragma unroll
+            for (int i = 0; i < FR; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t row = m0 + wm * WT + i * 16 + lg * 4 + r;
+                    if (row < M) y[row * ldy + col] = acc[i][j][r];
+                }
+        }
+        return;
+    }
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
     with_act(act, [&](auto A) {
 #pragma unroll
@@ -1204,6 +1227,84 @@ extern "C" int rf_linear_lnfold_fwd(const void* x, int64_t M, int32_t K, int64_t
     ea.eps = eps;
     ea.P = 4 * ((K + kLdsBN - 1) / kLdsBN);  // the stats call's N is this call's K
     return launch_lds_epi<kEpiLnFold>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, rf_stream(stream), "rf_linear_lnfold_fwd");
+}
+
+extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,
+                             int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream);
+
+namespace {
+// y = act(sum_s part[s] + b), partials added in order s = 0 .. S-1 (fixed: replay-deterministic), float4 columns
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int64_t M, int N,
+                                                            const float* __restrict__ bias, int act,
+                                                            float* __restrict__ y, int64_t ldy) {
+    const int n4 = N / 4;
+    const int64_t total = M * n4;
+    const int64_t plane = M * (int64_t)N;
+    with_act(act, [&](auto A) {
+        for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t m = e / n4;
+            const int c = (int)(e - m * n4) * 4;
+            float4 a = *reinterpret_cast<const float4*>(part + m * N + c);
+            for (int s2 = 1; s2 < S; ++s2) {
+                const float4 v = *reinterpret_cast<const float4*>(part + s2 * plane + m * N + c);
+                a.x += v.x;
+                a.y += v.y;
+                a.z += v.z;
+                a.w += v.w;
+            }
+            const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            float* d = y + m * ldy + c;
+            d[0] = A(a.x + bv.x);
+            d[1] = A(a.y + bv.y);
+            d[2] = A(a.z + bv.z);
+            d[3] = A(a.w + bv.w);
+        }
+    });
+}
+
+// split count for the fp32 register-staged GEMM: 128-tiles filling at most one workgroup per CU and a deep K
+// get S splits so two workgroups share each CU (their MFMAs cover each other's staging waits)
+int splitk_count(int32_t x_dtype, int64_t M, int32_t K, int32_t N) {
+    if (x_dtype != RF_DTYPE_F32 || N % 4 != 0 || N <= 16) return 1;
+    const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    if (tiles > 256 || K < 2048) return 1;
+    int S = 2;
+    while (S < 8 && tiles * S * 2 <= 512 && K / (S * 2) >= 1024) S *= 2;
+    return S;
+}
+}  // namespace
+
+extern "C" size_t rf_linear_splitk_ws_bytes(int32_t x_dtype, int64_t M, int32_t K, int32_t N) {
+    const int S = splitk_count(x_dtype, M, K, N);
+    return S > 1 ? (size_t)S * (size_t)M * (size_t)N * sizeof(float) : 0;
+}
+
+extern "C" int rf_linear_splitk_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,
+                                    int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* ws,
+                                    size_t ws_bytes, void* stream) {
+    const int S = splitk_count(x_dtype, M, K, N);
+    if (S == 1 || !ws || ws_bytes < rf_linear_splitk_ws_bytes(x_dtype, M, K, N) || act == RF_ACT_SOFTMAX)
+        return rf_linear_fwd(x, x_dtype, M, K, ldx, W, N, b, act, y, ldy, stream);
+    RF_REQUIRE(M > 0 && K % 4 == 0 && ldx % 4 == 0 && ldx >= K && ldy >= N && x && W && y, "rf_linear_splitk_fwd: bad shape");
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)y & 3) == 0,
+               "rf_linear_splitk_fwd: alignment");
+    RF_REQUIRE(!b || ((uintptr_t)b & 15) == 0, "rf_linear_splitk_fwd: bias must be 16-byte aligned");
+    hipStream_t st = rf_stream(stream);
+    const int kspan = ((K + S - 1) / S + BKF - 1) / BKF * BKF;
+    const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    const dim3 g((unsigned)tiles, (unsigned)S);
+    const bool ktail = K % BKF != 0 || kspan % BKF != 0;
+    if (ktail)
+        hipLaunchKernelGGL((gemm_kernel<false, 128, true, true>), g, dim3(256), 0, st, x, W, nullptr, (float*)ws, M, N, K,
+                           ldx, (int64_t)N, RF_ACT_NONE, kspan);
+    else
+        hipLaunchKernelGGL((gemm_kernel<false, 128, false, true>), g, dim3(256), 0, st, x, W, nullptr, (float*)ws, M, N, K,
+                           ldx, (int64_t)N, RF_ACT_NONE, kspan);
+    if (rf_check_launch("gemm_kernel (split-K)") != RF_OK) return RF_EHIP;
+    const int64_t total = M * (N / 4);
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, (const float*)ws, S, M, N, b, act, y, ldy);
+    return rf_check_launch("splitk_reduce_kernel");
 }
 
 extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,

@@ -76,6 +76,9 @@ _SIGS = {
     "rf_lookup_ids": (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
     "rf_bucketize_ids": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _i32, _f32, _vp, _vp]),
     "rf_attention_fusion_fwd": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i64, _vp, _i32, _vp, _i64, _vp, _vp]),
+    "rf_linear_splitk_ws_bytes": (ctypes.c_size_t, [_i32, _i64, _i32, _i32]),
+    "rf_linear_splitk_fwd": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _i64, _vp,
+                                            ctypes.c_size_t, _vp]),
     "rf_stream_copy": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp]),
     "rf_gather_probe": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, ctypes.c_uint64, _vp, _vp, _vp]),
     "rf_topk_merge": (ctypes.c_int, [_vp, _i64, _i32, _i32, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _i64, _vp]),

@@ -134,15 +134,23 @@ def test_dense_head_fp32_activations(O, cuda, M, K, N, act, wdt):
     np.testing.assert_allclose(y, want, rtol=1e-5, atol=2e-6 * np.sqrt(K))
 
 
-@pytest.mark.parametrize("M,K,N", [(100, 32, 64), (257, 8704, 1024), (64, 20480, 256)])
+@pytest.mark.parametrize("M,K,N", [(100, 32, 64), (257, 8704, 1024), (64, 20480, 256), (4096, 8704, 1024),
+                                   (300, 2052, 100)])
 def test_dense_fp32_exact_mfma(O, cuda, M, K, N):
-    """cfg2 towers run in fp32 (the reference's dtype): rtol 1e-5 / atol 1e-6 vs float64."""
+    """cfg2 towers run in fp32 (the reference's dtype): rtol 1e-5 / atol 1e-6 vs float64.
+    The deep-K shapes take the split-K form (rf_linear_splitk_fwd: 8 / 2 splits; 2052 a K tail per split)."""
+    import recommendflow_amd.runtime.lib as L
+
     x = rnd((M, K), K, 0.5, torch.float32)
-    dense = Dense(K, N, activation="selu", dtype=torch.float32, seed=1)
+    dense = Dense(K, N, activation="selu", dtype=torch.float32, seed=1, bias=torch.linspace(-0.3, 0.3, N))
+    split = L.load().rf_linear_splitk_ws_bytes(L.DT_F32, M, K, N) > 0
+    assert split == (K >= 2048), (M, K, N)
     y = dense(x.cuda()).cpu().numpy()
     W = dense.weight.cpu().numpy().astype(np.float64)
-    want = O.activation(x.numpy().astype(np.float64) @ W.T, "selu")
+    want = O.activation(x.numpy().astype(np.float64) @ W.T + dense.bias.cpu().numpy(), "selu")
     np.testing.assert_allclose(y, want, rtol=1e-5, atol=1e-6 * np.sqrt(K))
+    y2 = dense(x.cuda()).cpu().numpy()
+    assert np.array_equal(y, y2)  # fixed partial order: replays are bit-identical
 
 
 @pytest.mark.parametrize("cols", [16, 200, 256, 1024, 1280, 1400, 1536, 2048, 2050, 3000, 4100, 8704, 20480, 32768, 32772])

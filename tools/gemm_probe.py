@@ -17,8 +17,8 @@ from recommendflow_amd.backend.layers.core import Dense
 def main():
     res = {}
     g = torch.Generator(device="cuda").manual_seed(0)
-    for M, K, N in ((4096, 1280, 1024), (4096, 1024, 512), (51200, 1280, 1024), (4096, 256, 512), (4096, 8704, 1024)):
-        dt = torch.float32 if K == 8704 else torch.bfloat16
+    for M, K, N in ((4096, 1280, 1024), (4096, 1024, 512), (51200, 1280, 1024), (4096, 256, 512), (4096, 8704, 1024), (4096, 20480, 1024)):
+        dt = torch.float32 if K in (8704, 20480) else torch.bfloat16
         x = torch.randn((M, K), generator=g, device="cuda").to(dt)
         d = Dense(K, N, "gelu" if dt == torch.bfloat16 else "selu", dtype=dt, seed=1)
         fl = 2 * M * N * K
