@@ -374,7 +374,7 @@ def bench_esim(args):
     q = torch.empty((B, Ls * 128), dtype=torch.bfloat16, device="cuda")
     a = torch.empty_like(q)
     pooled = torch.empty((B, model.pooled_width), device="cuda")
-    from recommendflow_amd.backend.layers.attention_layers import esim_soft_attention_pool, esim_soft_attention_pool_ln
+    from recommendflow_amd.backend.layers.attention_layers import esim_soft_attention_pool
 
     par = {"s": 0, "f": 0, "e": 0}
 
@@ -382,25 +382,14 @@ def bench_esim(args):
         par[k] ^= 1
         return par[k]
 
-    fused_ln = model._ln_epilogue_ok()  # the output MLP's first LayerNorm runs in the attention kernel
-    n0 = model.output_mlp.norms[0]
-    hln = torch.empty((B, model.pooled_width), dtype=torch.bfloat16, device="cuda")
-
     def att():
-        if fused_ln:
-            esim_soft_attention_pool_ln(q.view(B, Ls, 128), a.view(B, Ls, 128), pooled, model.d_emb, None, None,
-                                        n0.eps, y=hln)
-        else:
-            esim_soft_attention_pool(q.view(B, Ls, 128), a.view(B, Ls, 128), out=pooled, out_col=model.d_emb)
+        esim_soft_attention_pool(q.view(B, Ls, 128), a.view(B, Ls, 128), out=pooled, out_col=model.d_emb)
 
     def in_mlp():  # on its side stream in the forward, concurrent with the encoders (off the critical path)
         model.input_mlp(dense, out=pooled[:, : model.d_emb])
 
     def mlp():  # the output MLP + Dense(2, softmax): the critical path after the attention
-        if fused_ln:
-            model.dense_output(model.output_mlp(hln, normed="unscaled"))
-        else:
-            model.dense_output(model.output_mlp(pooled))
+        model.dense_output(model.output_mlp(pooled))
 
     steps = max(10, args.steps // 2)
 
@@ -433,7 +422,6 @@ def bench_esim(args):
     return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4), "launch": "hipGraph",
             "eager_ms_per_step": round(eager_wall, 4), "cpu_baseline": cpu,
             "stage_ms": {k: round(v, 4) for k, v in per.items()},
-            "first_ln_in_attention_epilogue": fused_ln,
             "encoder_GBs": round(enc_bytes / per["sparse_encoders"] / 1e6, 1),
             "encoder_frac_of_measured_gather_ceiling": (
                 round(enc_bytes / per["sparse_encoders"] / 1e6 / args.probes["gather_copy_128B_GBs"], 4)
@@ -442,8 +430,7 @@ def bench_esim(args):
             "esim_mfma_frac_of_2500TF": round(att_flops / per["esim_attention"] / 1e9 / 2500, 4),
             "mlp_TFLOPs": round(mlp_flops / per["mlp_scorer"] / 1e9, 1),
             "stages_note": "input_mlp_concurrent runs on a side stream under the encoders in the forward; "
-                           "mlp_scorer = output MLP + Dense(2, softmax) (its first LayerNorm runs in the attention "
-                           "epilogue when first_ln_in_attention_epilogue); mlp_TFLOPs over those GEMMs",
+                           "mlp_scorer = output MLP + Dense(2, softmax); mlp_TFLOPs over those GEMMs",
             "config": "200 slots (100 q + 100 a) x 1M bins/hash, D=64 bf16 (tables 51.2 GB), L=100, d=128, "
                       "input_mlp 16->256->512, output_mlp 1280->1024->512, Dense(2, softmax), bf16 MFMA"}
 

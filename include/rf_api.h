@@ -161,21 +161,6 @@ int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int3
                                int32_t d, int64_t ex_stride, int64_t ld, float* out, int64_t out_stride,
                                int64_t out_off, float* att_out, void* stream);
 
-/*
- * rf_esim_soft_attention_fwd (without att_out) followed, in the same launch, by the LayerNormalization that
- * create_mlp puts in front of the output MLP's first Dense (backend/blocks/mlp.py:10-13 over the concat of
- * models/ranking/esim.py:84-85). Each out row is [head | pooled]: columns [0, out_off) are written
- * BEFORE this call by another producer (ESIM: the input MLP's d_emb columns, esim.py:75), the kernel writes
- * the 6d pooled features at out_off (F32, as above) and then normalises the whole row of out_off + 6d
- * values: y = (x - mean) / sqrt(var + eps) * gamma + beta (two-pass mean / variance, as rf_norm_fwd mode 0),
- * stored as BF16 into y_bf16 [batch][ldy] - the A operand of the next GEMM. gamma / beta may be NULL
- * (ones / zeros). Constraints as above plus 0 <= out_off <= 512.
- */
-int rf_esim_pool_ln_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d,
-                        int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
-                        const float* ln_gamma, const float* ln_beta, float eps, void* y_bf16, int64_t ldy,
-                        void* stream);
-
 /* activations for rf_linear_fwd */
 #define RF_ACT_NONE 0
 #define RF_ACT_GELU 1 /* exact erf gelu (tf.keras.activations.gelu, approximate=False) */
@@ -234,15 +219,15 @@ int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float 
  * A create_mlp layer pair with the second layer's LayerNormalization folded across the GEMMs (mlp.py:10-13:
  * Norm -> Dense(act) per hidden size; the reference normalises between the two Dense layers):
  *   rf_linear_stats_fwd   y = act(x W^T + b) stored as BF16 [M][N] (row stride ldy), and row_stats
- *                         [M][P][2], P = 4 * ceil(N / 128): partial (sum, sum of squares) of each row's fp32
- *                         values per column slice, written by the GEMM's epilogue (no pass over y, no
- *                         atomics: the fold sums the P partials in a fixed order, so results are
- *                         deterministic).
+ *                         [M][P][2], P = 4 * ceil(N / 128): for each 32-column slice p of a row (columns
+ *                         32p .. 32p + 31 below N, n_p of them) the pair (S_p, M2_p) of its fp32 values — their
+ *                         sum and their squared deviations from the slice mean S_p / n_p — written by the
+ *                         GEMM's epilogue (no pass over y, no atomics: fixed reduction order, deterministic).
  *   rf_linear_lnfold_fwd  y = act(rstd_r (x Wg^T - mu_r s) + t) = act(LN(x) W^T + b) for the raw BF16 x of
  *                         the previous call, with Wg = W diag(gamma) (BF16 [N][K]), s[c] = sum_k Wg[c][k],
- *                         t[c] = sum_k W[c][k] beta[k] + b[c] (F32 [N]), mu_r = sum_r / K and
- *                         rstd_r = 1 / sqrt(max(sumsq_r / K - mu_r^2, 0) + eps) from row_stats (the stats
- *                         call's N is this call's K).
+ *                         t[c] = sum_k W[c][k] beta[k] + b[c] (F32 [N]), mu_r = sum_p S_p / K and
+ *                         rstd_r = 1 / sqrt(var_r + eps), var_r = sum_p (M2_p + (S_p - n_p mu_r)^2 / n_p) / K
+ *                         (Chan's pairwise combine; the stats call's N is this call's K).
  * Both: x BF16 [M][K] (16-byte aligned, ldx % 8 == 0), K >= 512 and K % 64 == 0 (the LDS-DMA GEMM),
  * elementwise activations only. The pair replaces rf_norm_fwd -> rf_linear_fwd for the second layer.
  */

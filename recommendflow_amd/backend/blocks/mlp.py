@@ -65,9 +65,7 @@ class MLP(torch.nn.Module):
         """x [M, in] -> [M, hidden_units[-1]] fp32; `out` (optional) receives the last layer (any row stride).
         A two-layer LayerNorm MLP on a narrow input runs as ONE launch (rf_mlp2_small_fwd); otherwise
         each layer is rf_norm_fwd -> rf_linear_fwd. normed=True: x is the first layer's normalisation output
-        already (its producer applied norms[0]), in the layers' dtype; normed="unscaled": x is (row - mean) *
-        rstd without the LayerNorm's gamma / beta (rf_esim_pool_ln_fwd with NULL gamma / beta), which the
-        first Dense takes folded into its weights: W diag(gamma), W beta + b (_affine_folded)."""
+        already (its producer applied norms[0]), in the layers' dtype."""
         if not self.denses:
             self.build(x.shape[-1])
         if not normed and self._fusable(x):
@@ -76,10 +74,7 @@ class MLP(torch.nn.Module):
         i = 0
         while i <= last:
             norm, dense = self.norms[i], self.denses[i]
-            w_over = None
             if normed and i == 0:
-                if normed == "unscaled":
-                    w_over = self._affine_folded(0)
                 norm = None
             o = out if i == last else None
             if norm is not None and norm.mode == 1 and self.dtype == torch.float32 and x.dtype == torch.float32:
@@ -89,10 +84,10 @@ class MLP(torch.nn.Module):
                 continue
             h = norm(x, out_dtype=self.dtype, stream=stream) if norm is not None else x
             if self._ln_pair_ok(i, h):
-                x = self._ln_pair(i, h, out if i + 1 == last else None, stream, w_over)
+                x = self._ln_pair(i, h, out if i + 1 == last else None, stream)
                 i += 2
                 continue
-            x = dense.forward_with(h, *w_over, out=o, stream=stream) if w_over else dense(h, out=o, stream=stream)
+            x = dense(h, out=o, stream=stream)
             i += 1
         return x
 
@@ -109,15 +104,18 @@ class MLP(torch.nn.Module):
                 and h.dtype == torch.bfloat16 and h.dim() == 2 and h.stride(-1) == 1 and h.stride(0) % 8 == 0
                 and h.data_ptr() % 16 == 0)
 
-    def _ln_pair(self, i, h, out, stream, w_over=None):
+    def _ln_pair(self, i, h, out, stream):
         """act(LN(act(h W0^T + b0)) W1^T + b1) without the LayerNorm pass: the first GEMM writes its output
-        as bf16 plus per-row (sum, sum of squares) from its epilogue, the second applies the normalisation
-        after the product (W1 diag(gamma) and the per-column terms from _ln_folded)."""
+        as bf16 plus per-row, per-32-column-slice (sum, squared deviations from the slice mean) from its
+        epilogue, the second combines them (Chan) and applies the normalisation after the product (W1
+        diag(gamma) and the per-column terms from _ln_folded). Precision: the second GEMM multiplies the
+        UNCENTERED bf16 activations, so its error grows with |row mean| / row std (about 2^-9 of that ratio,
+        relative); fold_ln = False runs the LayerNorm as its own fp32 pass for such rows."""
         d0, d1, n1 = self.denses[i], self.denses[i + 1], self.norms[i + 1]
         M = h.shape[0]
         yb = torch.empty((M, d0.units), dtype=torch.bfloat16, device=h.device)
         st = torch.empty((M, 4 * ((d0.units + 127) // 128), 2), dtype=torch.float32, device=h.device)
-        w0, b0 = w_over if w_over else (d0.weight, d0.bias)
+        w0, b0 = d0.weight, d0.bias
         L.call("rf_linear_stats_fwd", L.ptr(h), M, d0.in_features, h.stride(0), L.ptr(w0), d0.units,
                L.ptr(b0), L.ACT[self.activation], L.ptr(yb), yb.stride(0), L.ptr(st), L.stream_ptr(stream))
         wg, sv, tv = self._ln_folded(i + 1)
@@ -145,25 +143,6 @@ class MLP(torch.nn.Module):
         tv = (w64 @ n.beta.double() + (d.bias.double() if d.bias is not None else 0.0)).float().contiguous()
         cache[("ln", i)] = (key, (wg, sv, tv))
         return wg, sv, tv
-
-    def _affine_folded(self, i: int):
-        """(W diag(gamma), W beta + b) of denses[i] behind LayerNorm norms[i], for an input that is already
-        (x - mean) * rstd: the LayerNorm's affine part moves into the weights. Cached until a parameter
-        changes (tensor identity or in-place version)."""
-        n, d = self.norms[i], self.denses[i]
-        ts = (d.weight, d.bias, n.gamma, n.beta)
-        key = _param_key(ts)
-        cache = getattr(self, "_fold_cache", None)
-        if cache is None:
-            cache = self._fold_cache = {}
-        hit = cache.get(("aff", i))
-        if hit is not None and _same_key(hit[0], key):
-            return hit[1]
-        w64 = d.weight.double()
-        w = (w64 * n.gamma.double()[None, :]).to(d.dtype).contiguous()
-        b = (w64 @ n.beta.double() + (d.bias.double() if d.bias is not None else 0.0)).float().contiguous()
-        cache[("aff", i)] = (key, (w, b))
-        return w, b
 
     def _bn_folded(self, i: int):
         """denses[i] with norms[i] folded in, for fp32 layers. BatchNormalization at inference is a per-column

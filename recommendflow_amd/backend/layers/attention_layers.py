@@ -53,30 +53,6 @@ def esim_soft_attention_pool(q: torch.Tensor, a: torch.Tensor, out: Optional[tor
     return out
 
 
-def esim_soft_attention_pool_ln(q: torch.Tensor, a: torch.Tensor, out: torch.Tensor, out_col: int, gamma: torch.Tensor,
-                                beta: torch.Tensor, eps: float, y: Optional[torch.Tensor] = None,
-                                stream=None) -> torch.Tensor:
-    """esim_soft_attention_pool into out[:, out_col:out_col+6d] (fp32), then the LayerNormalization of the
-    whole row out[:, :out_col+6d] in the same launch (rf_esim_pool_ln_fwd): columns [0, out_col) must already
-    hold the other producer's values. Returns y = LN(row) as bf16 [B, out_col+6d] (the next GEMM's input)."""
-    L.require_gpu()
-    q, a = _half(q), _half(a)
-    if a.dtype != q.dtype:
-        a = a.to(q.dtype)
-    if q.shape != a.shape:
-        raise ValueError(f"q {tuple(q.shape)} and a {tuple(a.shape)} must match (the reference needs L0 == L1)")
-    B, Ln, d = q.shape
-    if q.stride() != a.stride() or q.stride(2) != 1:
-        q, a = q.contiguous(), a.contiguous()
-    width = out_col + 6 * d
-    if y is None:
-        y = torch.empty((B, width), dtype=torch.bfloat16, device=q.device)
-    L.call("rf_esim_pool_ln_fwd", L.ptr(q), L.ptr(a), L.torch_dtype_code(q.dtype), B, Ln, d, q.stride(0), q.stride(1),
-           L.ptr(out), out.stride(0), out_col, L.ptr(gamma), L.ptr(beta), float(eps), L.ptr(y), y.stride(0),
-           L.stream_ptr(stream))
-    return y
-
-
 class SoftAttention:
     """SoftAttention()([x0, x1]) -> (S @ x0, S @ x1), E[n,i,j] = x1[n,i] . x0[n,j], S = softmax_j(E)."""
 

@@ -338,8 +338,11 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // LDS row stride (elements) of the ESIM v2 images: D + 16 puts the 8 rows of a ds_read_b64_tr_b16 lane
 // group (and the 16 rows of a ds_read_b128 fragment) on disjoint banks; D + 8 (2-way conflicts) only
 // where the wider images would push the workgroup past 80 KB (two per CU)
+// images + statistics + (d = 64) a 2 KB dummy area for the staging chunks of rows past the image (d = 64 rows
+// are 8 chunks, so a 256-chunk group can end mid-tile); it sits apart from the statistics, which the v6 loop
+// reduces while the next images are written
 __host__ __device__ constexpr size_t esim2_lds_bytes(int D, int ntt, int rs) {
-    return (size_t)2 * ntt * 16 * rs * 2 + (size_t)kEsim2Waves * 3 * 2 * D * 4;
+    return (size_t)2 * ntt * 16 * rs * 2 + (size_t)kEsim2Waves * 3 * 2 * D * 4 + (D == 64 ? 128 * 16 : 0);
 }
 __host__ __device__ constexpr int esim2_rs(int D, int ntt) {
     return esim2_lds_bytes(D, ntt, D + 16) <= 80 * 1024 ? D + 16 : D + 8;
@@ -458,7 +461,10 @@ __device__ __forceinline__ typename M::frag stripe_selector(int sp, int lr, int 
     return f;
 }
 
-template <typename M, int D, int NTT, bool TWO, int XM = 0>
+// KT0 = sp0 >> 1: the P @ V k-step holding stripe sp0's rows (sp1 = sp0 + 4: k-step KT0 + 2), a template
+// parameter so the selector MFMAs are placed at compile time and each half's P @ V is one basic block (a runtime
+// wave-uniform test split it into per-k-step blocks, each waiting out its own LDS reads before its MFMAs)
+template <typename M, int D, int NTT, bool TWO, int XM = 0, int KT0 = 0>
 __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
                                            int lane) {
     constexpr int nt = NTT;
@@ -548,7 +554,7 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
             // registers instead of 128, no spills next to the 64 prefetch registers)
             constexpr int NH = NT >= 8 ? 2 : 1, NC = NT / NH;
             const frag sel = stripe_selector<M>(sp0, lr, lg);  // sp1 = sp0 + 4: the same row half
-            const int kt0 = sp0 >> 1, kt1 = sp1 >> 1;  // kt0 in {0, 1}, kt1 in {2, 3}
+            constexpr int kt0 = KT0, kt1 = KT0 + 2;  // sp0 >> 1, sp1 >> 1
 #pragma unroll
             for (int h = 0; h < NH; ++h) {
                 f4 a0[NC], a1[NC], x0[NC], x1[NC];
@@ -616,31 +622,11 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
     }
 }
 
-// LayerNorm epilogue (rf_esim_pool_ln_fwd): the row of `out` is [head columns 0..out_off) | the 6d pooled
-// features], the head written beforehand by another producer (cfg3: the input MLP); the kernel normalises the
-// whole row (two-pass mean / variance, as rf_norm_fwd) and writes it as bf16 -> the output MLP's first GEMM
-struct EsimLn {
-    const float* gamma;  // [out_off + 6d] or null (ones)
-    const float* beta;   // [out_off + 6d] or null (zeros)
-    float eps;
-    uint16_t* y;         // [batch][ldy] bf16
-    int64_t ldy;
-};
-
-constexpr int kEsimLnHead = 2;  // head columns per thread: out_off <= 512
-
-// sum over the 64 lanes of a wave, every lane gets the total (same bits everywhere)
-__device__ __forceinline__ float wave_sum64(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-template <bool F16, int D, int NTT, int XM, bool LNE = false>
+template <bool F16, int D, int NTT, int XM>
 __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
                                                                      const uint16_t* __restrict__ a, int batch, int L,
                                                                      int64_t ex_stride, int64_t ld, float* __restrict__ out,
-                                                                     int64_t out_stride, int64_t out_off, EsimLn ln) {
+                                                                     int64_t out_stride, int64_t out_off) {
     using M = Mfma<F16>;
     constexpr int NTH = kEsim2Waves * 64;
     constexpr int RS = esim2_rs(D, NTT);
@@ -673,8 +659,8 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         }
     };
     // a chunk of a row past the image (only where 16-row tiles end inside a 256-chunk group: d = 64, odd
-    // tile counts) goes to this thread's dummy slot in the statistics area, rewritten after the barrier
-    uint16_t* dummy = reinterpret_cast<uint16_t*>(st) + (tid & 127) * 8;
+    // tile counts) goes to this thread's slot of the dummy area past the statistics
+    uint16_t* dummy = reinterpret_cast<uint16_t*>(st + kEsim2Waves * 3 * 2 * D) + (tid & 127) * 8;
     int64_t e = blockIdx.x;
     uint32_t it = 0;
     // the pooled features of the previous example, stored one example late (right before the next prefetch):
@@ -690,9 +676,12 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
 #pragma unroll
         for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pv[k]), ro, po[k], 0, 0);
     };
-    if (e < batch) prefetch(e);
-    for (; e < batch; e += gridDim.x) {
-        __syncthreads();
+    // v6 loop: two barriers per example. The images of example e + G are written right after the barrier that
+    // ends e's compute phase (nothing reads them after it; the prefetched registers landed under that compute),
+    // beside e's statistics reduction, which reads only the statistics area; the second barrier publishes the
+    // new images and retires the statistics reads before the next compute phase rewrites them (v5 had a third
+    // barrier before the staging writes).
+    auto stage_images = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int cm = tid + (i % HALF) * NTH;
@@ -702,19 +691,16 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                 *reinterpret_cast<uint4*>(dst) = pre[i];
             }
         }
+    };
+    if (e < batch) {
+        prefetch(e);
+        stage_images();
         __syncthreads();
+    }
+    for (; e < batch; e += gridDim.x) {
         if (pe >= 0) flush();
-        if (e + gridDim.x < batch) prefetch(e + gridDim.x);
-        // LN epilogue: this example's head columns (written by the other producer before the launch) are
-        // fetched now, in flight under the compute phase (2 registers)
-        float hv[LNE ? kEsimLnHead : 1];
-        if constexpr (LNE) {
-            int64_t hc = out_off;
-            asm volatile("" : "+s"(hc));
-            const float* orow = out + e * out_stride;
-#pragma unroll
-            for (int k = 0; k < kEsimLnHead; ++k) hv[k] = tid + k * NTH < hc ? orow[tid + k * NTH] : 0.f;
-        }
+        const bool more = e + gridDim.x < batch;
+        if (more) prefetch(e + gridDim.x);
 
         // v3: the stripe pairs rotate over the waves from one example to the next, so the wave left with one
         // stripe (7 tiles over 4 waves) is a different SIMD each time; statistics slots follow the stripe
@@ -723,10 +709,16 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         if (sp0 < nt) {
             float* wst = st + sp0 * 3 * 2 * D;
             // both-stripe / one-stripe waves are separate instantiations: no predicated MFMAs
-            if (sp1 < nt) esim3_wave<M, D, NTT, true, XM>(qs, as, wst, sp0, sp1, L, lane);
-            else esim3_wave<M, D, NTT, false, XM>(qs, as, wst, sp0, sp1, L, lane);
+            if (sp1 < nt) {
+                if (sp0 >> 1) esim3_wave<M, D, NTT, true, XM, 1>(qs, as, wst, sp0, sp1, L, lane);
+                else esim3_wave<M, D, NTT, true, XM, 0>(qs, as, wst, sp0, sp1, L, lane);
+            } else {
+                if (sp0 >> 1) esim3_wave<M, D, NTT, false, XM, 1>(qs, as, wst, sp0, sp1, L, lane);
+                else esim3_wave<M, D, NTT, false, XM, 0>(qs, as, wst, sp0, sp1, L, lane);
+            }
         }
-        __syncthreads();
+        __syncthreads();  // compute done: images free, statistics complete
+        if (more) stage_images();
 
         // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84)
         // every thread of the workgroup: lane l of wave w reduces side l >> 5 of the columns
@@ -761,77 +753,8 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                 po[3] = ok0 ? (5 * D + n) * 4 : kOff;
                 pe = e;
             }
-            if constexpr (LNE) {
-                static_assert(NTH / 2 >= D, "one column per thread and side");
-                int64_t hc = out_off;  // opaque: no loop-invariant index math hoisted into the compute phase
-                asm volatile("" : "+s"(hc));
-                // this thread's features (side 0: 4, side 1: 2; none past d) and up to 4 head columns
-                const bool own = n < D;
-                const float v[4] = {avg, m3, avg - avg_o, m3 - mx_o};
-                const int nv = own ? (side == 0 ? 4 : 2) : 0;
-                // the LN parameters of this thread's columns, all loads issued before the two reductions (their
-                // latency hides under the barriers); opaque pointer copies keep these loop-invariant loads out
-                // of the compute phase (hoisted, they hold 12 registers there and spill)
-                const float* lgam = ln.gamma;
-                const float* lbet = ln.beta;
-                asm volatile("" : "+s"(lgam), "+s"(lbet));
-                float gh[kEsimLnHead], bh[kEsimLnHead], gvv[4], bvv[4];
-#pragma unroll
-                for (int k = 0; k < kEsimLnHead; ++k) {
-                    const int c = tid + k * NTH < hc ? tid + k * NTH : 0;
-                    gh[k] = lgam ? lgam[c] : 1.f;
-                    bh[k] = lbet ? lbet[c] : 0.f;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int c = (int)hc + (k < 2 ? (2 * side + k) * D : (2 + k) * D) + (own ? n : 0);
-                    gvv[k] = lgam ? lgam[c] : 1.f;
-                    bvv[k] = lbet ? lbet[c] : 0.f;
-                }
-                // 2 x 4 wave partials in the q image: no wave reads the images between the post-compute barrier
-                // and the next example's staging (which follows the loop-top barrier)
-                float* red = reinterpret_cast<float*>(qs);
-                const float cols = (float)(hc + 6 * D);
-                float s1 = 0.f;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) s1 += k < nv ? v[k] : 0.f;
-#pragma unroll
-                for (int k = 0; k < kEsimLnHead; ++k) s1 += hv[k];
-                s1 = wave_sum64(s1);
-                if (lane == 0) red[wave] = s1;
-                __syncthreads();
-                const float mu = ((red[0] + red[1]) + (red[2] + red[3])) / cols;
-                float s2 = 0.f;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float dv = k < nv ? v[k] - mu : 0.f;
-                    s2 += dv * dv;
-                }
-#pragma unroll
-                for (int k = 0; k < kEsimLnHead; ++k) {
-                    const float dh = tid + k * NTH < hc ? hv[k] - mu : 0.f;
-                    s2 += dh * dh;
-                }
-                s2 = wave_sum64(s2);
-                if (lane == 0) red[4 + wave] = s2;
-                __syncthreads();
-                const float rstd = 1.0f / sqrtf(((red[4] + red[5]) + (red[6] + red[7])) / cols + ln.eps);
-                uint16_t* yr = ln.y + e * ln.ldy;
-#pragma unroll
-                for (int k = 0; k < kEsimLnHead; ++k) {
-                    const int c = tid + k * NTH;
-                    if (c < hc) yr[c] = (uint16_t)f32_to_bf16_bits((hv[k] - mu) * rstd * gh[k] + bh[k]);
-                }
-                // the pooled columns: side 0 avg, max, avg_q - avg_a, max_q - max_a; side 1 avg, max
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k < nv) {
-                        const int c = (int)hc + (k < 2 ? (2 * side + k) * D : (2 + k) * D) + n;
-                        yr[c] = (uint16_t)f32_to_bf16_bits((v[k] - mu) * rstd * gvv[k] + bvv[k]);
-                    }
-                }
-            }
         }
+        __syncthreads();  // next images visible; statistics reads retired
     }
     if (pe >= 0) flush();  // the last example's features
 }
@@ -965,26 +888,26 @@ int launch_big_lds(K kernel, int grid, size_t lds, hipStream_t st, const char* n
 
 template <bool F16, int D, int NTT>
 int launch_esim2_nt(int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L, int64_t ex_stride,
-                    int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimLn* ln) {
+                    int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
     // RF_ESIM_XM=0 keeps the v3 statistics (x read from LDS and converted on the VALU); A/B runs only
     static const int xm = [] {
         const char* e = getenv("RF_ESIM_XM");
         return e && e[0] == '0' ? 0 : 1;
     }();
-    auto kern = ln ? esim2_kernel<F16, D, NTT, 1, true> : xm == 0 ? esim2_kernel<F16, D, NTT, 0> : esim2_kernel<F16, D, NTT, 1>;
+    auto kern = xm == 0 ? esim2_kernel<F16, D, NTT, 0> : esim2_kernel<F16, D, NTT, 1>;
     const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, (const uint16_t*)q, (const uint16_t*)a, batch, L,
-                       ex_stride, ld, out, out_stride, out_off, ln ? *ln : EsimLn{});
+                       ex_stride, ld, out, out_stride, out_off);
     return RF_OK;
 }
 
 template <bool F16, int D>
 int launch_esim2(int nt, int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L,
-                 int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimLn* ln) {
+                 int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
     switch (nt) {
 #define RF_NT(N) \
-    case N: return launch_esim2_nt<F16, D, N>(grid, lds, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln);
+    case N: return launch_esim2_nt<F16, D, N>(grid, lds, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
         RF_NT(1) RF_NT(2) RF_NT(3) RF_NT(4) RF_NT(5) RF_NT(6) RF_NT(7) RF_NT(8)
 #undef RF_NT
         default: return rf_set_error(RF_EINVAL, "esim2: bad tile count %d", nt);
@@ -993,7 +916,7 @@ int launch_esim2(int nt, int grid, size_t lds, hipStream_t st, const void* q, co
 
 // the 4-wave persistent kernel (two workgroups per CU when the images fit 80 KB)
 int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d, int64_t ex_stride,
-                   int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimLn* ln, hipStream_t st) {
+                   int64_t ld, float* out, int64_t out_stride, int64_t out_off, hipStream_t st) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int nt = (L + 15) >> 4;
@@ -1001,10 +924,10 @@ int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, i
     const int per_cu = lds2 <= 80 * 1024 ? 2 : 1;
     const int grid2 = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
     if (dtype == RF_DTYPE_BF16)
-        return d == 64 ? launch_esim2<false, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln)
-                       : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln);
-    return d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln)
-                   : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ln);
+        return d == 64 ? launch_esim2<false, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
+                       : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
+    return d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
+                   : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
 }
 
 }  // namespace
@@ -1031,7 +954,7 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
         return e && e[0] == '1';
     }();
     if (!v1 && !att_out) {
-        const int rc = esim2_dispatch(q, a, dtype, batch, L, d, ex_stride, ld, out, out_stride, out_off, nullptr, st);
+        const int rc = esim2_dispatch(q, a, dtype, batch, L, d, ex_stride, ld, out, out_stride, out_off, st);
         if (rc) return rc;
         return rf_check_launch("rf_esim_soft_attention_fwd");
     }
@@ -1054,28 +977,6 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     }
 #undef RF_ESIM_LAUNCH
     return rf_check_launch("esim_kernel");
-}
-
-extern "C" int rf_esim_pool_ln_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d,
-                                   int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
-                                   const float* ln_gamma, const float* ln_beta, float eps, void* y_bf16, int64_t ldy,
-                                   void* stream) {
-    RF_REQUIRE(dtype == RF_DTYPE_BF16 || dtype == RF_DTYPE_F16, "rf_esim_pool_ln_fwd: dtype must be BF16 or F16");
-    RF_REQUIRE(L >= 1 && L <= 128, "rf_esim_pool_ln_fwd: need 1 <= L <= 128 (got %d)", L);
-    RF_REQUIRE(d == 64 || d == 128, "rf_esim_pool_ln_fwd: d must be 64 or 128 (got %d)", d);
-    RF_REQUIRE(batch >= 0, "rf_esim_pool_ln_fwd: batch < 0");
-    RF_REQUIRE(ld % 8 == 0 && ex_stride % 8 == 0 && ld >= d, "rf_esim_pool_ln_fwd: ld/ex_stride must be multiples of 8 elements (16-byte rows)");
-    RF_REQUIRE((int64_t)L * ld * 2 < ((int64_t)1 << 31), "rf_esim_pool_ln_fwd: one example's rows must span < 2 GiB");
-    RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)a & 15) == 0, "rf_esim_pool_ln_fwd: q/a must be 16-byte aligned");
-    RF_REQUIRE(out_off >= 0 && out_off <= kEsimLnHead * kEsim2Waves * 64, "rf_esim_pool_ln_fwd: need 0 <= out_off <= 512 head columns (got %lld)", (long long)out_off);
-    RF_REQUIRE(out_stride >= out_off + 6 * d && ldy >= out_off + 6 * d, "rf_esim_pool_ln_fwd: rows narrower than out_off + 6d");
-    RF_REQUIRE(eps >= 0.f, "rf_esim_pool_ln_fwd: eps < 0");
-    if (batch == 0) return RF_OK;
-    RF_REQUIRE(q && a && out && y_bf16, "rf_esim_pool_ln_fwd: null pointer");
-    const EsimLn ln{ln_gamma, ln_beta, eps, static_cast<uint16_t*>(y_bf16), ldy};
-    const int rc = esim2_dispatch(q, a, dtype, batch, L, d, ex_stride, ld, out, out_stride, out_off, &ln, rf_stream(stream));
-    if (rc) return rc;
-    return rf_check_launch("rf_esim_pool_ln_fwd");
 }
 
 extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int32_t batch, int32_t heads,

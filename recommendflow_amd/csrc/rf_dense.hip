@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 #include <cstdlib>
 
 #include "rf_common.h"
@@ -509,33 +510,44 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
 // 16.9 us (64-row tiles), 51200x1280->1024 206 vs 248 us (128-row tiles); deeper rings only add LDS.
 constexpr int kLdsK = 64, kLdsBN = 128, kLdsStages = 2;
 
-template <int BM>
-__device__ __forceinline__ void glds_stage(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, int64_t M, int N,
-                                           int64_t ldx, int K, int64_t m0, int n0, int k0, uint16_t* As, uint16_t* Bs,
+// T = uint16_t (bf16, 64 per 128-byte row) or float (fp32, 32 per row): the ring, the swizzle and the copies are
+// byte-identical for both; ldw = W's row stride (elements)
+// ESZ = 2 (bf16, 64 per 128-byte row) or 4 (fp32, 32 per row): the ring, the swizzle and the copies are
+// byte-identical for both; ldx / ldw (W's row stride) and k0 in elements
+template <int BM, int ESZ>
+__device__ __forceinline__ void glds_stage(const void* __restrict__ xv, const void* __restrict__ wv, int64_t M, int N,
+                                           int64_t ldx, int64_t ldw, int64_t m0, int n0, int k0, void* Asv, void* Bsv,
                                            int tid) {
+    const char* x = reinterpret_cast<const char*>(xv);
+    const char* w = reinterpret_cast<const char*>(wv);
+    char* As = reinterpret_cast<char*>(Asv);
+    char* Bs = reinterpret_cast<char*>(Bsv);
     // one wave-instruction = 8 tile rows x 8 chunks (1 KiB, lane-linear in LDS); 4 waves
     const int wave = tid >> 6, lane = tid & 63, rr = lane >> 3, pos = lane & 7;
 #pragma unroll
     for (int it = 0; it < BM / 32; ++it) {
         const int g = wave + 4 * it, r = g * 8 + rr;
         const int64_t row = m0 + r < M ? m0 + r : M - 1;  // rows past M: any valid row (never stored)
-        const uint16_t* src = x + row * ldx + k0 + ((pos ^ rr) << 3);
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + g * 512), 16, 0, 0);
+        const char* src = x + (row * ldx + k0) * ESZ + ((pos ^ rr) << 4);
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(As + g * 1024), 16, 0, 0);
     }
 #pragma unroll
     for (int it = 0; it < kLdsBN / 32; ++it) {
         const int g = wave + 4 * it, r = g * 8 + rr;
         const int64_t col = n0 + r < N ? n0 + r : N - 1;
-        const uint16_t* src = w + col * (int64_t)K + k0 + ((pos ^ rr) << 3);
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + g * 512), 16, 0, 0);
+        const char* src = w + (col * ldw + k0) * ESZ + ((pos ^ rr) << 4);
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(Bs + g * 1024), 16, 0, 0);
     }
 }
 
 // Epilogue variants of gemm_lds_kernel (the LayerNorm of the next layer folded across the pair):
 //   kEpiPlain  y = act(acc + b), fp32
-//   kEpiStats  y = act(acc + b) stored as bf16, and every row's (sum, sum of squares) of the fp32 values
-//              over the wave's columns written to stats[row][p] (p = column tile * 4 + wave column; 16-lane
-//              shuffle reduce); no atomics, so the reduction order (and the result) is fixed
+//   kEpiStats  y = act(acc + b) stored as bf16, and for every row and 32-column slice p of it (p = column tile
+//              * 4 + slice; n_p = its columns < N) the pair (S_p, M2_p) of the fp32 values: their sum and their
+//              squared deviations from the slice's own mean S_p / n_p (two 16-lane shuffle reduces), written to
+//              stats[row][p]; no atomics, so the reduction order (and the result) is fixed. Deviations from a
+//              local mean keep the variance exact-ish for rows whose mean is large against their spread (a
+//              single sum-of-squares pass loses it to cancellation)
 //   kEpiLnFold y = act(rstd_r (acc - mu_r s_c) + t_c): acc = x W'^T with x the previous layer's raw bf16
 //              output and W' = W diag(gamma); mu_r, rstd_r from stats over the K columns; s_c = sum_k W'[c][k],
 //              t_c = W beta + b. That is LN(x) W^T + b with the normalisation applied after the product.
@@ -551,17 +563,34 @@ struct EpiArgs {
     int P;               // partials per row (4 per 128-column tile of the stats GEMM)
 };
 
-template <int BM, int EPI = kEpiPlain>
-__global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+// F32: fp32 operands (x and W both fp32) on v_mfma_f32_16x16x4f32, 32 k per 128-byte row: a lane's two 16-byte
+// chunks (k = 4 lg .. 4 lg + 3 and 16 + 4 lg .. 16 + 4 lg + 3) feed 8 MFMAs, A and B in the same permuted k order.
+// SPLIT (split-K, EPI plain only): blockIdx.y = s takes k in [s kspan, min(K, (s + 1) kspan)) and stores raw
+// partial sums to y + s M ldy (splitk_reduce_kernel adds them in order s = 0, 1, ... with the bias / activation).
+template <int BM, int EPI = kEpiPlain, bool F32 = false, bool SPLIT = false>
+__global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
                                                        const float* __restrict__ bias, float* __restrict__ y, int64_t M,
-                                                       int N, int K, int64_t ldx, int64_t ldy, int act, EpiArgs ea) {
+                                                       int N, int K, int64_t ldx, int64_t ldy, int act, EpiArgs ea,
+                                                       int kspan = 0) {
+    using T = std::conditional_t<F32, float, uint16_t>;
+    constexpr int kK = 128 / (int)sizeof(T);                       // k per step (one 128-byte row)
+    constexpr int SH = F32 ? 2 : 3;
     constexpr int WM = BM == 128 ? 2 : 1, WN = 4 / WM;            // wave grid
     constexpr int TM = BM / WM, TN = kLdsBN / WN;                  // wave tile
     constexpr int FM = TM / 16, FN = TN / 16;                      // fragments per wave
-    constexpr int A_EL = BM * kLdsK, B_EL = kLdsBN * kLdsK;        // elements per stage
+    constexpr int A_EL = BM * kK, B_EL = kLdsBN * kK;              // elements per stage
     constexpr int LOADS = (BM / 8 + kLdsBN / 8) / 4;               // glds per thread per stage
+    static_assert(!SPLIT || EPI == kEpiPlain, "split-K: plain epilogue only");
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    uint16_t* lds = reinterpret_cast<uint16_t*>(smem_raw);
+    T* lds = reinterpret_cast<T*>(smem_raw);
+    const int64_t ldw = K;
+    const int kb = SPLIT ? (int)blockIdx.y * kspan : 0;
+    const T* x = reinterpret_cast<const T*>(xv) + kb;
+    const T* w = reinterpret_cast<const T*>(wv) + kb;
+    if constexpr (SPLIT) {
+        K = min(kspan, K - kb);
+        y += (int64_t)blockIdx.y * M * ldy;
+    }
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int wm = wave / WN, wn = wave % WN;
     // XCD-aware tile order (bijective): block b runs on XCD b % 8; give each XCD a contiguous tile range
@@ -570,7 +599,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
     const int tiles_n = (N + kLdsBN - 1) / kLdsBN;
     const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
     const int n0 = (tile % tiles_n) * kLdsBN;
-    const int nk = K / kLdsK;
+    const int nk = K / kK;
 
     f4 acc[FM][FN];
 #pragma unroll
@@ -582,7 +611,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
     auto Bs = [&](int s) { return lds + s * (A_EL + B_EL) + A_EL; };
 #pragma unroll
     for (int p = 0; p + 1 < kLdsStages; ++p)
-        if (p < nk) glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, p * kLdsK, As(p), Bs(p), tid);
+        if (p < nk) glds_stage<BM, (int)sizeof(T)>(x, w, M, N, ldx, ldw, m0, n0, p * kK, As(p), Bs(p), tid);
     // The epilogue's per-column parameters (bias, or the LN fold's s_c / t_c) are loaded now, under the first
     // stage's copies, instead of as dependent loads after the last MFMA (one HBM round trip off the tail).
     float pb[FN], pt[FN];
@@ -600,26 +629,32 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
     // LN fold: the tile's row statistics are reduced now too (their partials are complete: the previous
     // launch wrote them), into an LDS area past the ring, read after the loop; the reduction order is fixed
     // (TPR threads per row, each a strided subset, then a commutative shuffle combine: every lane the same bits)
-    float* srow = reinterpret_cast<float*>(smem_raw + (size_t)kLdsStages * (A_EL + B_EL) * 2);
+    float* srow = reinterpret_cast<float*>(smem_raw + (size_t)kLdsStages * (A_EL + B_EL) * sizeof(T));
     if constexpr (EPI == kEpiLnFold) {
         constexpr int TPR = 256 / BM;
         const int rl = tid / TPR, part = tid % TPR;
         const int64_t row = m0 + rl < M ? m0 + rl : M - 1;
-        float s1 = 0.f, s2 = 0.f;
+        // Chan's combine of the slices: mu = sum S_p / K, M2 = sum M2_p + (S_p - n_p mu)^2 / n_p
+        const float2* rs2 = reinterpret_cast<const float2*>(ea.stats) + row * ea.P;
+        float s1 = 0.f;
+        for (int p = part; p < ea.P; p += TPR) s1 += rs2[p].x;
+#pragma unroll
+        for (int o = 1; o < TPR; o <<= 1) s1 += __shfl_xor(s1, o, 64);
+        const float m = s1 / (float)K;
+        float s2 = 0.f;
         for (int p = part; p < ea.P; p += TPR) {
-            const float2 v = *reinterpret_cast<const float2*>(ea.stats + 2 * (row * ea.P + p));
-            s1 += v.x;
-            s2 += v.y;
+            const int np = min(max(K - p * 32, 0), 32);
+            if (np > 0) {
+                const float2 v = rs2[p];
+                const float dv = v.x - (float)np * m;
+                s2 += v.y + dv * dv / (float)np;
+            }
         }
 #pragma unroll
-        for (int o = 1; o < TPR; o <<= 1) {
-            s1 += __shfl_xor(s1, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
-        }
+        for (int o = 1; o < TPR; o <<= 1) s2 += __shfl_xor(s2, o, 64);
         if (part == 0) {
-            const float m = s1 / (float)K;
             srow[2 * rl] = m;
-            srow[2 * rl + 1] = 1.0f / sqrtf(fmaxf(s2 / (float)K - m * m, 0.f) + ea.eps);
+            srow[2 * rl + 1] = 1.0f / sqrtf(s2 / (float)K + ea.eps);
         }
         __syncthreads();  // srow visible to every wave (this also retires stage 0's copies: the loop waits for them first)
     }
@@ -632,35 +667,61 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
         __builtin_amdgcn_sched_barrier(0);
         if (kt + kLdsStages - 1 < nk) {
             const int s2 = (kt + kLdsStages - 1) % kLdsStages;
-            glds_stage<BM>(x, w, M, N, ldx, K, m0, n0, (kt + kLdsStages - 1) * kLdsK, As(s2), Bs(s2), tid);
+            glds_stage<BM, (int)sizeof(T)>(x, w, M, N, ldx, ldw, m0, n0, (kt + kLdsStages - 1) * kK, As(s2), Bs(s2), tid);
         }
-        const uint16_t* A = As(s);
-        const uint16_t* B = Bs(s);
-        // both 32-deep halves' fragments are read up front: the second half's reads run under the first
-        // half's MFMAs
-        bf16x8 af[2][FM], bfr[2][FN];
+        const T* A = As(s);
+        const T* B = Bs(s);
+        // both halves' fragments are read up front: the second half's reads run under the first half's MFMAs
+        using frag = std::conditional_t<F32, f4, bf16x8>;
+        frag af[2][FM], bfr[2][FN];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int ch = 4 * h + lg;  // 16-byte chunk of this lane's 8 k values
+            const int ch = 4 * h + lg;  // 16-byte chunk of this lane's k values
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
                 const int r = wm * TM + i * 16 + lr;
-                af[h][i] = *reinterpret_cast<const bf16x8*>(A + r * kLdsK + ((ch ^ (r & 7)) << 3));
+                af[h][i] = *reinterpret_cast<const frag*>(A + r * kK + ((ch ^ (r & 7)) << SH));
             }
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 const int r = wn * TN + j * 16 + lr;
-                bfr[h][j] = *reinterpret_cast<const bf16x8*>(B + r * kLdsK + ((ch ^ (r & 7)) << 3));
+                bfr[h][j] = *reinterpret_cast<const frag*>(B + r * kK + ((ch ^ (r & 7)) << SH));
             }
         }
         __builtin_amdgcn_sched_barrier(0);  // keep every read ahead of the MFMAs (hipcc would re-serialise them)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h) {
+            if constexpr (F32) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int j = 0; j < FN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[h][i][e], bfr[h][j][e], acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[h][i], bfr[h][j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    if constexpr (SPLIT) {  // raw partial sums
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int col = n0 + wn * TN + j * 16 + lr;
+            if (col >= N) continue;
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[h][i], bfr[h][j], acc[i][j], 0, 0, 0);
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                    if (row < M) y[row * ldy + col] = acc[i][j][r];
+                }
+        }
+        return;
     }
     // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
     if constexpr (EPI == kEpiPlain) {
@@ -680,11 +741,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
             }
         });
     } else if constexpr (EPI == kEpiStats) {
-        float rs[FM][4], rq[FM][4];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rs[i][r] = rq[i][r] = 0.f;
+        // pass 1: activation, bf16 store, and the fp32 value kept in acc (0 past N)
         with_act(act, [&](auto A) {
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
@@ -697,32 +754,38 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const uint16_t* __restric
                     for (int r = 0; r < 4; ++r) {
                         const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
                         const float v = A(acc[i][j][r] + bv);
-                        if (cok) {
-                            rs[i][r] += v;
-                            rq[i][r] += v * v;
-                            if (row < M) reinterpret_cast<__bf16*>(ea.yb)[row * ldy + col] = (__bf16)v;  // v_cvt_pk_bf16_f32, RNE
-                        }
+                        acc[i][j][r] = cok ? v : 0.f;
+                        if (cok && row < M) reinterpret_cast<__bf16*>(ea.yb)[row * ldy + col] = (__bf16)v;  // v_cvt_pk_bf16_f32, RNE
                     }
             }
         });
+        // pass 2: per 32-column slice (fragments 2q, 2q + 1 of this wave): sum, then squared deviations from the
+        // slice mean; slices past N hold (0, 0)
+        constexpr int SPW = FN / 2;  // slices per wave (TN = 64: 2; TN = 32: 1)
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int q = 0; q < SPW; ++q) {
+            const int c0 = n0 + wn * TN + q * 32;
+            const int nq = min(max(N - c0, 0), 32);
+            const float inv_n = nq > 0 ? 1.0f / (float)nq : 0.f;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int i = 0; i < FM; ++i)
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    rs[i][r] += __shfl_xor(rs[i][r], o, 64);
-                    rq[i][r] += __shfl_xor(rq[i][r], o, 64);
+                for (int r = 0; r < 4; ++r) {
+                    float sm = acc[i][2 * q][r] + acc[i][2 * q + 1][r];
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+                    const float mq = sm * inv_n;
+                    const float d0 = c0 + lr < N ? acc[i][2 * q][r] - mq : 0.f;
+                    const float d1 = c0 + 16 + lr < N ? acc[i][2 * q + 1][r] - mq : 0.f;
+                    float m2 = d0 * d0 + d1 * d1;
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+                    const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                    if (lr == 0 && row < M)
+                        *reinterpret_cast<float2*>(ea.stats + 2 * (row * ea.P + (n0 / kLdsBN) * 4 + wn * SPW + q)) =
+                            make_float2(sm, m2);
                 }
-                const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                if (lr == 0 && row < M) {
-                    float* sp = ea.stats + 2 * (row * ea.P + (n0 / kLdsBN) * 4 + wn);
-                    *reinterpret_cast<float2*>(sp) = make_float2(rs[i][r], rq[i][r]);
-                    // two wave columns per tile (128-row tiles): the tile's other two slots hold zeros, so
-                    // every slot of a row is written and the stats buffer needs no clearing launch
-                    if constexpr (WN == 2) *reinterpret_cast<float2*>(sp + 4) = make_float2(0.f, 0.f);
-                }
-            }
+        }
     } else {  // kEpiLnFold: the row statistics were reduced into srow before the loop
         float mu[FM][4], rstd[FM][4];
 #pragma unroll
@@ -1183,12 +1246,12 @@ int launch_lds_epi(const void* x, int64_t M, int32_t K, int64_t ldx, const void*
         auto kern = gemm_lds_kernel<128, EPI>;
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<128>());
         if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
-        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea);
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea, 0);
     } else {
         auto kern = gemm_lds_kernel<64, EPI>;
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64>());
         if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
-        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea);
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea, 0);
     }
     return rf_check_launch(who);
 }
@@ -1262,15 +1325,43 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     });
 }
 
-// split count for the fp32 register-staged GEMM: 128-tiles filling at most one workgroup per CU and a deep K
-// get S splits so two workgroups share each CU (their MFMAs cover each other's staging waits)
+// split count for the fp32 GEMM: 128-tiles filling at most one workgroup per CU and a deep K get S splits so
+// two workgroups share each CU (their MFMAs cover each other's load waits). RF_SPLITK=<S> overrides (A/B only).
 int splitk_count(int32_t x_dtype, int64_t M, int32_t K, int32_t N) {
     if (x_dtype != RF_DTYPE_F32 || N % 4 != 0 || N <= 16) return 1;
     const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    static const int force = [] {
+        const char* e = getenv("RF_SPLITK");
+        return e ? atoi(e) : 0;
+    }();
+    if (force > 0) return K >= 64 * force ? std::min(force, 8) : 1;
     if (tiles > 256 || K < 2048) return 1;
     int S = 2;
     while (S < 8 && tiles * S * 2 <= 512 && K / (S * 2) >= 1024) S *= 2;
     return S;
+}
+
+// the fp32 operand form of the LDS-DMA ring kernel (K % 32 == 0)
+template <int BM, bool SPLIT>
+int launch_lds_f32(const void* x, const void* W, const float* b, float* y, int64_t M, int N, int K, int64_t ldx,
+                   int64_t ldy, int act, int S, int kspan, hipStream_t st) {
+    auto kern = gemm_lds_kernel<BM, kEpiPlain, true, SPLIT>;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)gemm_lds_bytes<BM>());
+    if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel: %s", hipGetErrorString(e));
+    const int64_t tiles = ((M + BM - 1) / BM) * ((N + kLdsBN - 1) / kLdsBN);
+    RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_linear_fwd: too many tiles");
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles, (unsigned)S), dim3(256), gemm_lds_bytes<BM>(), st, x, W, b, y, M, N, K,
+                       ldx, ldy, act, EpiArgs{}, kspan);
+    return rf_check_launch("gemm_lds_kernel (fp32)");
+}
+
+bool lds_disabled() {  // RF_GEMM_LDS=0: the register-staged kernel everywhere (A/B measurement only)
+    static const bool off = [] {
+        const char* e = getenv("RF_GEMM_LDS");
+        return e && e[0] == '0';
+    }();
+    return off;
 }
 }  // namespace
 
@@ -1294,7 +1385,10 @@ extern "C" int rf_linear_splitk_fwd(const void* x, int32_t x_dtype, int64_t M, i
     const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
     const dim3 g((unsigned)tiles, (unsigned)S);
     const bool ktail = K % BKF != 0 || kspan % BKF != 0;
-    if (ktail)
+    if (!ktail && !lds_disabled()) {
+        const int rc = launch_lds_f32<128, true>(x, W, nullptr, (float*)ws, M, N, K, ldx, (int64_t)N, RF_ACT_NONE, S, kspan, st);
+        if (rc != RF_OK) return rc;
+    } else if (ktail)
         hipLaunchKernelGGL((gemm_kernel<false, 128, true, true>), g, dim3(256), 0, st, x, W, nullptr, (float*)ws, M, N, K,
                            ldx, (int64_t)N, RF_ACT_NONE, kspan);
     else
@@ -1330,10 +1424,13 @@ extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t 
     RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0, "rf_linear_fwd: x/W must be 16-byte aligned");
     // 128-tiles unless that grid would give fewer than 2 workgroups per CU (256 CUs): then 64-tiles
     // (4x the workgroups; same per-element accumulation order, so identical results)
-    static const bool lds_off = [] {  // A/B against the register-staged kernel (measurement only)
-        const char* e = getenv("RF_GEMM_LDS");
-        return e && e[0] == '0';
-    }();
+    const bool lds_off = lds_disabled();
+    // fp32 operands on the LDS-DMA ring (K % 32 == 0): 128-row tiles from one per CU, else 64-row tiles
+    if (!bf && !lds_off && K % 32 == 0 && K >= 256 && ((uintptr_t)y & 3) == 0) {
+        const int64_t t128 = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
+        if (t128 >= 256) return launch_lds_f32<128, false>(x, W, b, y, M, N, K, ldx, ldy, act, 1, 0, st);
+        return launch_lds_f32<64, false>(x, W, b, y, M, N, K, ldx, ldy, act, 1, 0, st);
+    }
     // the LDS-DMA kernel where it measured faster (profiles/r02/gemm_ab.txt): deep K, at most ~4 tiles of
     // 64 x 128 per CU (its per-CU load path is the limit on long grids; short K is all pipeline fill)
     const int64_t t64 = ((M + 63) / 64) * ((N + kLdsBN - 1) / kLdsBN);
@@ -1352,12 +1449,12 @@ extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t 
             auto kern = gemm_lds_kernel<128>;
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<128>());
             if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel: %s", hipGetErrorString(e));
-            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, EpiArgs{});
+            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, EpiArgs{}, 0);
         } else {
             auto kern = gemm_lds_kernel<64>;
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64>());
             if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel: %s", hipGetErrorString(e));
-            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, EpiArgs{});
+            hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<64>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, EpiArgs{}, 0);
         }
         return rf_check_launch("gemm_lds_kernel");
     }

@@ -18,7 +18,7 @@ import torch
 
 from ...backend.blocks.mlp import create_mlp
 from ...backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
-from ...backend.layers.attention_layers import esim_soft_attention_pool, esim_soft_attention_pool_ln
+from ...backend.layers.attention_layers import esim_soft_attention_pool
 from ...backend.layers.core import Dense, LayerNormalization
 from ...runtime.batch import SparseBatch
 
@@ -62,28 +62,9 @@ class Esim(torch.nn.Module):
         dense.record_stream(side)
         q = self.enc_q(user).view(B, self.L, self.d)
         a = self.enc_a(ad).view(B, self.L, self.d)
-        if self._ln_epilogue_ok():
-            # the output MLP's first LayerNorm in the attention kernel's epilogue (rf_esim_pool_ln_fwd): it needs
-            # the input MLP's columns, so the join comes first (that MLP finished long before, under the encoders)
-            # gamma / beta go into the first GEMM's weights (MLP._affine_folded): the epilogue only needs the
-            # row statistics, no parameter loads
-            n0 = self.output_mlp.norms[0]
-            cur.wait_stream(side)
-            h = esim_soft_attention_pool_ln(q, a, pooled, self.d_emb, None, None, n0.eps)
-            return self.dense_output(self.output_mlp(h, normed="unscaled"))
         esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
         cur.wait_stream(side)
         return self.dense_output(self.output_mlp(pooled))
-
-    # True: the output MLP's first LayerNorm runs in the attention kernel's epilogue (rf_esim_pool_ln_fwd, gamma /
-    # beta folded into the first GEMM). Measured a wash on cfg3 (forward 0.294 vs 0.2938 ms: the epilogue adds
-    # ~15 us to the attention kernel, the LN launch it removes cost the same), so off by default.
-    fuse_ln = False
-
-    def _ln_epilogue_ok(self) -> bool:
-        n0 = self.output_mlp.norms[0] if self.output_mlp.norms else None
-        return (self.fuse_ln and n0 is not None and n0.mode == 0 and self.output_mlp.dtype == torch.bfloat16
-                and self.d_emb <= 512 and self.d in (64, 128) and self.L <= 128)
 
     def _side_stream(self, device):
         s = getattr(self, "_side", None)

@@ -6,8 +6,8 @@ import pytest
 import torch
 
 from recommendflow_amd.backend.blocks.mlp import create_mlp
-from recommendflow_amd.backend.layers.attention_layers import (MultiHeadAttention, SoftAttention, esim_soft_attention_pool,
-                                                               esim_soft_attention_pool_ln)
+from recommendflow_amd.backend.layers.attention_layers import (MultiHeadAttention, SoftAttention,
+                                                               esim_soft_attention_pool)
 from recommendflow_amd.backend.layers.core import BatchNormalization, Dense, LayerNormalization
 from recommendflow_amd.backend.layers.layer_utils import scaled_dot_product_attention
 
@@ -52,37 +52,20 @@ def test_esim_pool_fast_path(O, cuda, L, d, dt):
         np.testing.assert_allclose(got, want, atol=tol * (scale + 1), rtol=0)
 
 
-@pytest.mark.parametrize("L,d", [(1, 64), (33, 128), (100, 128), (100, 64), (128, 128)])
-@pytest.mark.parametrize("head", [0, 130, 512])
-def test_esim_pool_ln_epilogue(O, cuda, L, d, head):
-    """rf_esim_pool_ln_fwd: the pooled features are the pooled-only kernel's bit for bit, and the bf16 row
-    LN([head | pooled]) equals a float64 LayerNorm of the kernel's own fp32 row within the bf16 rounding of
-    the output (|rel| <= 2^-8); against the oracle pooling at the ESIM bar of test_esim_pool_fast_path."""
-    B, scale, eps = 300, 0.5, 1e-6
-    q, a = rnd((B, L, d), L + d, scale), rnd((B, L, d), L + d + 9, scale)
-    W = head + 6 * d
-    out = torch.empty((B, W + 8), device="cuda")
-    hv = (torch.randn((B, max(head, 1)), generator=torch.Generator().manual_seed(head + 1)) * 0.7 + 0.2)[:, :head]
-    out[:, :head] = hv.cuda()
-    g = torch.Generator().manual_seed(L * 3 + d)
-    gamma = (torch.rand(W, generator=g) + 0.5).cuda()
-    beta = (torch.rand(W, generator=g) - 0.5).cuda()
-    y = esim_soft_attention_pool_ln(q.cuda(), a.cuda(), out, head, gamma, beta, eps)
-    plain = esim_soft_attention_pool(q.cuda(), a.cuda()).cpu().numpy()
-    row = out[:, :W].cpu().numpy()
-    assert np.array_equal(row[:, head:].view(np.uint32), plain.view(np.uint32))
-    np.testing.assert_array_equal(row[:, :head], hv.numpy())
-    want = O.layer_norm(row.astype(np.float64), gamma.double().cpu().numpy(), beta.double().cpu().numpy(), eps)
-    np.testing.assert_allclose(y.float().cpu().numpy(), want, rtol=2 ** -8, atol=1e-5)
-    want_p = O.esim_pool(q.float().numpy(), a.float().numpy())
-    np.testing.assert_allclose(row[:, head:], want_p, atol=2 ** -7 * scale * (scale + 1), rtol=0)
-
-
-def test_esim_pool_ln_rejects_wide_head(cuda):
-    q = rnd((2, 4, 64), 1).cuda()
-    out = torch.empty((2, 513 + 384), device="cuda")
-    with pytest.raises(Exception, match="out_off"):
-        esim_soft_attention_pool_ln(q, q, out, 513, None, None, 1e-6)
+@pytest.mark.parametrize("L,d", [(33, 64), (100, 128), (17, 64)])
+def test_esim_many_examples_per_workgroup(O, cuda, L, d):
+    """The persistent kernel's v6 loop (the next example's images staged beside this example's statistics
+    reduction; d = 64 at odd tile counts stages past-the-image chunks into the dummy area): B = 3000 gives
+    every workgroup 3 - 6 examples; pooled features against the float64 oracle at the ESIM bar, written at
+    an out_col offset with the head columns untouched."""
+    B, scale, head = 3000, 0.5, 24
+    q, a = rnd((B, L, d), L + 2 * d, scale), rnd((B, L, d), L + 2 * d + 5, scale)
+    out = torch.full((B, head + 6 * d), 7.0, device="cuda")
+    esim_soft_attention_pool(q.cuda(), a.cuda(), out=out, out_col=head)
+    got = out.cpu().numpy()
+    assert (got[:, :head] == 7.0).all()
+    want = O.esim_pool(q.float().numpy(), a.float().numpy())
+    np.testing.assert_allclose(got[:, head:], want, atol=2 ** -7 * scale * (scale + 1), rtol=0)
 
 
 def test_esim_strided_views(O, cuda):
@@ -276,6 +259,41 @@ def test_multi_head_attention_api(O, cuda):
     x = rnd((2, 20, 128), 8, 1.0, torch.float32).cuda()
     out = mha.call(x, x, x, None)
     assert tuple(out.shape) == (2, 20, 128) and torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("mean", [0.0, 40.0, 1000.0])
+def test_ln_fold_row_stats_large_mean(cuda, mean):
+    """rf_linear_stats_fwd's per-slice (S_p, M2_p) and the Chan combine of rf_linear_lnfold_fwd's prologue
+    (restated here in float64 over the kernel's own partials) against the float64 mean / variance of the same
+    GEMM's fp32 output (rf_linear_fwd, identical accumulation): rows whose mean is 1000x their spread keep a
+    relative variance error <= 1e-4 (fp32 slice sums), where a single sum-of-squares pass (sumsq / K - mu^2)
+    would be off by tens of percent."""
+    import recommendflow_amd.runtime.lib as L
+
+    M, K, N = 256, 512, 600  # N % 128 != 0: a partial last column tile (slices with n_p < 32 and n_p = 0)
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16).cuda()
+    W = (torch.randn(N, K, generator=g) * 0.04).to(torch.bfloat16).cuda()
+    b = (torch.full((N,), mean) + torch.randn(N, generator=g) * 0.1).cuda()
+    yb = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
+    P = 4 * ((N + 127) // 128)
+    st = torch.empty((M, P, 2), dtype=torch.float32, device="cuda")
+    L.call("rf_linear_stats_fwd", L.ptr(x), M, K, x.stride(0), L.ptr(W), N, L.ptr(b), L.ACT["relu"], L.ptr(yb),
+           yb.stride(0), L.ptr(st), L.stream_ptr(None))
+    y = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    L.call("rf_linear_fwd", L.ptr(x), L.DT_BF16, M, K, x.stride(0), L.ptr(W), N, L.ptr(b), L.ACT["relu"], L.ptr(y),
+           y.stride(0), L.stream_ptr(None))
+    torch.cuda.synchronize()
+    y64 = y.cpu().numpy().astype(np.float64)
+    S = st[..., 0].cpu().numpy().astype(np.float64)
+    M2 = st[..., 1].cpu().numpy().astype(np.float64)
+    n = np.clip(N - 32 * np.arange(P), 0, 32).astype(np.float64)
+    mu = S.sum(1) / N
+    ok = n > 0
+    var = (M2[:, ok] + (S[:, ok] - n[ok] * mu[:, None]) ** 2 / n[ok]).sum(1) / N
+    np.testing.assert_allclose(mu, y64.mean(1), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(var, y64.var(1), rtol=1e-4)
+    assert (S[:, ~ok] == 0).all() and (M2[:, ~ok] == 0).all()
 
 
 @pytest.mark.parametrize("M", [300, 4096])
