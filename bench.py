@@ -808,7 +808,7 @@ def bench_train(args, specs, multi):
     table, B = 4096, towers [1024, 512, 256], cosent_loss): fused encoder forward -> torch towers + our
     cosent kernel -> backward -> rf_fused_hash_embed_bwd (dedup sort-reduce) -> rf_adam_apply (Keras
     dense Adam over the whole table + m + v) and torch Adam on the towers. Also times the sparse stages
-    alone, and the lazy-Adam variant of the table update."""
+    alone, the towers' forward + backward alone, and the lazy-Adam variant of the table update."""
     import numpy as np
     import torch
 
@@ -862,14 +862,37 @@ def bench_train(args, specs, multi):
     ev[1].record()
     torch.cuda.synchronize()
     lazy_ms = ev[0].elapsed_time(ev[1]) / steps
+    # the towers alone: forward + l2norm + loss + backward to the embedding gradient, then the towers' Adam
+    xin = torch.randn((B, enc.out_width), generator=torch.Generator().manual_seed(3)).cuda() * 0.05
+    model.train()
+    tw = np.zeros(2)
+    for i in range(steps + 2):
+        xg = xin.detach().requires_grad_(True)
+        ev[0].record()
+        uu = torch.nn.functional.normalize(model.user_tower(xg[:, : model.wu]), dim=-1, eps=1e-6)
+        vv = torch.nn.functional.normalize(model.ad_tower(xg[:, model.wu:]), dim=-1, eps=1e-6)
+        model.loss_fn(y, uu, vv).backward()
+        ev[1].record()
+        model.dense_opt.step()
+        ev[2].record()
+        model.dense_opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        if i >= 2:
+            tw += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])]
+    tw /= steps
+    tower_flops = 3 * 2 * B * sum(t.W[l].numel() for t in (model.user_tower, model.ad_tower) for l in range(len(t.units)))
     adam_bytes = enc.table.numel() * 4 * 6 + enc.table.shape[0] * 4 + n_uniq * (args.dim * 4 + 8)
     res = {"examples_per_s": round(B / step_ms * 1e3, 1), "ms_per_step": round(step_ms, 4), "loss": round(float(loss), 4),
            "sparse_stage_ms": {"fwd": round(acc[0], 4), "bwd_dedup": round(acc[1], 4), "adam_dense": round(acc[2], 4),
                                "adam_lazy": round(lazy_ms, 4)},
+           "tower_stage_ms": {"fwd_bwd": round(tw[0], 4), "adam": round(tw[1], 4)},
+           "tower_fwd_bwd_TFLOPs": round(tower_flops / tw[0] / 1e9, 1),
            "distinct_rows_per_step": n_uniq,
            "adam_dense_GBs": round(adam_bytes / acc[2] / 1e6, 1),
            "config": "cfg2 DSSM train step: 229 slots, 9999972x64 fp32 table (+ m, v), B=4096, towers [1024,512,256] "
-                     "BN/selu/dropout (torch, library GEMMs), cosent_loss (HIP), Keras Adam (dense, exact) on the table"}
+                     "BatchNormalization(batch stats)/selu/dropout 0.3 on librf (train_mlp.TrainTower: BN folded into "
+                     "the fp32 MFMA forward GEMM, SELU/dropout/BN backward kernels, library GEMMs for dW and dx), "
+                     "cosent_loss (HIP), Keras Adam (dense, exact) on the table, Adam on the towers"}
     del model, enc, batches
     torch.cuda.empty_cache()
     return res

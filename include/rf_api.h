@@ -161,6 +161,40 @@ int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int3
                                int32_t d, int64_t ex_stride, int64_t ld, float* out, int64_t out_stride,
                                int64_t out_off, float* att_out, void* stream);
 
+/*
+ * DSSM tower training (models/matching/dssm.py:25-26: create_mlp([1024, 512, 256], 0.3, "selu",
+ * BatchNormalization(1e-6)) per tower, trained by model.fit, example/ranking_search/train.py:96-104). All F32.
+ * A layer's BatchNormalization in training mode (batch statistics; Keras tf.nn.moments, biased variance) folds
+ * into its Dense: W' = W diag(a), b' = b + W c, a = gamma / sqrt(var + eps), c = beta - mean a, so the forward
+ * GEMM (rf_linear_fwd / rf_linear_splitk_fwd with RF_ACT_SELU) reads the raw activations.
+ *   rf_col_stats         mean[K], var[K] of x [M][K] over the M rows (deterministic: fixed row chunks, per-chunk
+ *                        pivot, Chan's combine in chunk order)
+ *   rf_bn_fold           W' [N][K], b' [N] as above (b may be NULL)
+ *   rf_dropout_fwd       y = x / (1 - rate) where kept, 0 elsewhere; keep(r, c) = top 24 bits of
+ *                        splitmix64(seed ^ (r * N + c)) / 2^24 >= rate (Keras Dropout(rate) in training; the mask
+ *                        is recomputed in the backward, never stored); y may alias x (same strides)
+ *   rf_selu_dropout_bwd  dpre = dh * keep / (1 - rate) * SeluGrad(y) with y = h (1 - rate) the activation
+ *                        (h = the layer's dropout output), db[N] = column sums of dpre
+ *   rf_bn_fold_grad      dW = G diag(a) + db c^T for G = dpre^T x (the Dense weight's gradient)
+ *   rf_bn_bwd            dgamma = sum(dz xhat), dbeta = sum(dz), dx = gamma rstd (dz - dbeta / M - xhat dgamma / M)
+ * Column sums reduce fixed row chunks in chunk order (replay-deterministic). ws: rf_tower_ws_bytes(M, K) bytes
+ * (K = the reduced width). M <= 65535.
+ */
+size_t rf_tower_ws_bytes(int64_t M, int32_t K);
+int rf_col_stats(const float* x, int64_t M, int32_t K, int64_t ldx, float* mean, float* var, void* ws, size_t ws_bytes,
+                 void* stream);
+int rf_bn_fold(const float* W, int32_t N, int32_t K, const float* b, const float* gamma, const float* beta,
+               const float* mean, const float* var, float eps, float* W_out, float* b_out, void* stream);
+int rf_dropout_fwd(const float* x, int64_t M, int32_t N, int64_t ldx, float rate, uint64_t seed, float* y, int64_t ldy,
+                   void* stream);
+int rf_selu_dropout_bwd(const float* dh, int64_t lddh, const float* h, int64_t ldh, int64_t M, int32_t N, float rate,
+                        uint64_t seed, float* dpre, int64_t ldd, float* db, void* ws, size_t ws_bytes, void* stream);
+int rf_bn_fold_grad(const float* G, int32_t N, int32_t K, const float* db, const float* gamma, const float* beta,
+                    const float* mean, const float* var, float eps, float* dW, void* stream);
+int rf_bn_bwd(const float* dz, int64_t lddz, const float* x, int64_t ldx, int64_t M, int32_t K, const float* mean,
+              const float* var, const float* gamma, float eps, float* dx, int64_t lddx, float* dgamma, float* dbeta,
+              void* ws, size_t ws_bytes, void* stream);
+
 /* activations for rf_linear_fwd */
 #define RF_ACT_NONE 0
 #define RF_ACT_GELU 1 /* exact erf gelu (tf.keras.activations.gelu, approximate=False) */

@@ -582,6 +582,63 @@ def l2_normalize(x, eps=1e-12):
 
 
 # ----------------------------------------------------------------------------------------------
+# DSSM tower training (float64): create_mlp([..], rate, "selu", BatchNormalization(eps)) under model.fit
+# (dssm.py:25-26, mlp.py:4-15, train.py:96-104): per layer BatchNormalization with batch statistics (Keras
+# tf.nn.moments: biased variance) -> Dense -> SELU -> Dropout(rate); the keep mask restates rf_dropout_fwd's
+# ----------------------------------------------------------------------------------------------
+def _splitmix64_np(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def dropout_keep(seed: int, M: int, N: int, rate: float) -> np.ndarray:
+    """keep(r, c) = top 24 bits of splitmix64(seed ^ (r N + c)) / 2^24 >= rate (float32 compare)."""
+    idx = np.arange(M, dtype=np.uint64)[:, None] * np.uint64(N) + np.arange(N, dtype=np.uint64)[None, :]
+    h = _splitmix64_np(np.uint64(seed) ^ idx)
+    u = (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return u >= np.float32(rate)
+
+
+def tower_train_fwd(x, layers, rate: float, seeds, eps: float = 1e-6):
+    """layers: [{"W": [N][K], "b", "gamma", "beta"}]; returns (output, cache) in float64."""
+    h = np.asarray(x, np.float64)
+    cache = []
+    for p, seed in zip(layers, seeds):
+        W = np.asarray(p["W"], np.float64)
+        mean, var = h.mean(0), h.var(0)
+        xhat = (h - mean) / np.sqrt(var + eps)
+        z = xhat * p["gamma"] + p["beta"]
+        y = selu(z @ W.T + p["b"])
+        keep = dropout_keep(seed, h.shape[0], W.shape[0], rate)
+        out = np.where(keep, y / (1.0 - rate), 0.0)
+        cache.append({"h": h, "mean": mean, "var": var, "xhat": xhat, "z": z, "y": y, "keep": keep})
+        h = out
+    return h, cache
+
+
+def tower_train_bwd(dout, layers, cache, rate: float, eps: float = 1e-6):
+    """Backward of tower_train_fwd: returns (dx, [{"W", "b", "gamma", "beta"} gradients]); the SELU gradient is
+    TF's SeluGrad on the activations (y < 0: y + scale alpha, else scale)."""
+    scale, alpha = 1.0507009873554804934193349852946, 1.6732632423543772848170429916717
+    dh = np.asarray(dout, np.float64)
+    grads = []
+    for p, c in zip(reversed(layers), reversed(cache)):
+        W = np.asarray(p["W"], np.float64)
+        dy = np.where(c["keep"], dh / (1.0 - rate), 0.0)
+        dpre = dy * np.where(c["y"] < 0, c["y"] + scale * alpha, scale)
+        dz = dpre @ W
+        dxhat = dz * p["gamma"]
+        xh = c["xhat"]
+        dh = (dxhat - dxhat.mean(0) - xh * (dxhat * xh).mean(0)) / np.sqrt(c["var"] + eps)
+        grads.insert(0, {"W": dpre.T @ c["z"], "b": dpre.sum(0), "gamma": (dz * xh).sum(0), "beta": dz.sum(0)})
+    return dh, grads
+
+
+# ----------------------------------------------------------------------------------------------
 # training losses (float64), backend/losses/match_losses.py
 # ----------------------------------------------------------------------------------------------
 def cosent_loss(y: np.ndarray, s: np.ndarray, scale: float = 20.0):

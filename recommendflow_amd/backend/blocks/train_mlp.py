@@ -1,0 +1,181 @@
+"""create_mlp under model.fit for the DSSM towers (reference: backend/blocks/mlp.py:4-15 with
+models/matching/dssm.py:25-26 `create_mlp([1024, 512, 256], 0.3, "selu", BatchNormalization(1e-6))`, trained by
+example/ranking_search/train.py:96-104) on librf.so, replacing torch.nn.BatchNorm1d / Linear / SELU / Dropout.
+
+Per layer, forward (training):
+  mean, var = rf_col_stats(h)                          batch statistics (Keras tf.nn.moments: biased variance)
+  W', b'    = rf_bn_fold(W, b, gamma, beta, mean, var) BatchNormalization folded into the Dense
+  y         = selu(h W'^T + b')                        rf_linear_splitk_fwd / rf_linear_fwd, fp32 MFMA
+  h_next    = rf_dropout_fwd(y)                        Keras Dropout(rate): kept / (1 - rate), counter-hash mask
+and the moving statistics move as Keras does (moving = moving * momentum + batch * (1 - momentum), momentum
+0.99, the biased batch variance). Backward: rf_selu_dropout_bwd (dpre and the bias gradient), the Dense weight
+gradient G = dpre^T h (library GEMM) through rf_bn_fold_grad, dz = dpre W (library GEMM), rf_bn_bwd. In eval mode
+the moving statistics fold into the weights (no dropout).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import torch
+
+from ...runtime import lib as L
+
+_SEED_MIX = 0x9E3779B97F4A7C15
+
+
+def layer_seed(base: int, step: int, layer: int) -> int:
+    """The dropout mask seed of (tower seed, training step, layer): a 64-bit mix, any value is valid."""
+    x = (base * 0x100000001B3 + step * _SEED_MIX + layer * 0xC2B2AE3D27D4EB4F) & 0xFFFFFFFFFFFFFFFF
+    return x
+
+
+def _linear_f32(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int, out: torch.Tensor, stream: int):
+    M, K = x.shape
+    N = W.shape[0]
+    ws_bytes = int(L.load().rf_linear_splitk_ws_bytes(L.DT_F32, M, K, N))
+    if ws_bytes:
+        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device)
+        L.call("rf_linear_splitk_fwd", L.ptr(x), L.DT_F32, M, K, x.stride(0), L.ptr(W), N, L.ptr(b), act, L.ptr(out),
+               out.stride(0), L.ptr(ws), ws_bytes, stream)
+    else:
+        L.call("rf_linear_fwd", L.ptr(x), L.DT_F32, M, K, x.stride(0), L.ptr(W), N, L.ptr(b), act, L.ptr(out),
+               out.stride(0), stream)
+
+
+def _ws(M: int, K: int, device) -> torch.Tensor:
+    return torch.empty(max(int(L.load().rf_tower_ws_bytes(M, K)), 4), dtype=torch.uint8, device=device)
+
+
+class _TowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, tower: "TrainTower", *params):
+        if x.dim() != 2 or x.stride(1) != 1 or x.dtype != torch.float32:
+            raise ValueError("TrainTower input must be a 2-D fp32 tensor with unit column stride")
+        M = x.shape[0]
+        dev, st = x.device, L.stream_ptr(None)
+        step = tower.steps
+        tower.steps += 1
+        h = x
+        outs, means, vars_ = [], [], []
+        for l in range(len(tower.units)):
+            W, b, g, be = params[4 * l: 4 * l + 4]
+            N, K = W.shape
+            mean = torch.empty(K, dtype=torch.float32, device=dev)
+            var = torch.empty(K, dtype=torch.float32, device=dev)
+            ws = _ws(M, K, dev)
+            L.call("rf_col_stats", L.ptr(h), M, K, h.stride(0), L.ptr(mean), L.ptr(var), L.ptr(ws), ws.numel(), st)
+            Wf = torch.empty_like(W)
+            bf = torch.empty(N, dtype=torch.float32, device=dev)
+            L.call("rf_bn_fold", L.ptr(W), N, K, L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(mean), L.ptr(var), tower.eps,
+                   L.ptr(Wf), L.ptr(bf), st)
+            y = torch.empty((M, N), dtype=torch.float32, device=dev)
+            _linear_f32(h, Wf, bf, L.ACT["selu"], y, st)
+            L.call("rf_dropout_fwd", L.ptr(y), M, N, N, tower.rate, layer_seed(tower.seed, step, l), L.ptr(y), N, st)
+            with torch.no_grad():
+                tower.moving_mean[l].mul_(tower.momentum).add_(mean, alpha=1.0 - tower.momentum)
+                tower.moving_var[l].mul_(tower.momentum).add_(var, alpha=1.0 - tower.momentum)
+            outs.append(y)
+            means.append(mean)
+            vars_.append(var)
+            h = y
+        ctx.tower, ctx.step, ctx.n = tower, step, len(tower.units)
+        ctx.save_for_backward(x, *params, *outs, *means, *vars_)
+        return outs[-1]
+
+    @staticmethod
+    def backward(ctx, dout):
+        tower, n = ctx.tower, ctx.n
+        saved = ctx.saved_tensors
+        x = saved[0]
+        params = saved[1: 1 + 4 * n]
+        outs = saved[1 + 4 * n: 1 + 5 * n]
+        means = saved[1 + 5 * n: 1 + 6 * n]
+        vars_ = saved[1 + 6 * n: 1 + 7 * n]
+        dev, st = x.device, L.stream_ptr(None)
+        M = x.shape[0]
+        dh = dout if dout.stride(1) == 1 else dout.contiguous()
+        grads: List[Optional[torch.Tensor]] = [None] * (4 * n)
+        for l in reversed(range(n)):
+            W, b, g, be = params[4 * l: 4 * l + 4]
+            N, K = W.shape
+            h_in = x if l == 0 else outs[l - 1]
+            ws = _ws(M, max(K, N), dev)
+            dpre = torch.empty((M, N), dtype=torch.float32, device=dev)
+            db = torch.empty(N, dtype=torch.float32, device=dev)
+            L.call("rf_selu_dropout_bwd", L.ptr(dh), dh.stride(0), L.ptr(outs[l]), N, M, N, tower.rate,
+                   layer_seed(tower.seed, ctx.step, l), L.ptr(dpre), N, L.ptr(db), L.ptr(ws), ws.numel(), st)
+            G = torch.mm(dpre.t(), h_in)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
+            dW = torch.empty_like(W)
+            L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]), L.ptr(vars_[l]),
+                   tower.eps, L.ptr(dW), st)
+            dz = torch.mm(dpre, W)  # [M][K] (library GEMM)
+            dx = torch.empty((M, K), dtype=torch.float32, device=dev)
+            dgamma = torch.empty(K, dtype=torch.float32, device=dev)
+            dbeta = torch.empty(K, dtype=torch.float32, device=dev)
+            L.call("rf_bn_bwd", L.ptr(dz), K, L.ptr(h_in), h_in.stride(0), M, K, L.ptr(means[l]), L.ptr(vars_[l]), L.ptr(g),
+                   tower.eps, L.ptr(dx), K, L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), ws.numel(), st)
+            grads[4 * l: 4 * l + 4] = [dW, db, dgamma, dbeta]
+            dh = dx
+        return (dh, None, *grads)
+
+
+class TrainTower(torch.nn.Module):
+    """One DSSM tower: [BatchNormalization(eps) -> Dense(units, selu) -> Dropout(rate)] per hidden size, fp32,
+    glorot_uniform kernels and zero biases (Keras Dense defaults), gamma 1 / beta 0 / moving stats 0 and 1."""
+
+    def __init__(self, in_features: int, units: Sequence[int], rate: float = 0.3, eps: float = 1e-6,
+                 momentum: float = 0.99, seed: int = 0, generator: Optional[torch.Generator] = None, device="cuda"):
+        super().__init__()
+        L.load()
+        L.require_gpu()
+        self.units, self.rate, self.eps, self.momentum, self.seed = list(units), float(rate), float(eps), float(momentum), int(seed)
+        self.steps = 0
+        g = generator if generator is not None else torch.Generator().manual_seed(seed)
+        self.W, self.b, self.gamma, self.beta = (torch.nn.ParameterList() for _ in range(4))
+        self.moving_mean, self.moving_var = [], []
+        width = int(in_features)
+        for i, u in enumerate(self.units):
+            lim = math.sqrt(6.0 / (width + u))
+            self.W.append(torch.nn.Parameter(((torch.rand(u, width, generator=g) * 2 - 1) * lim).to(device)))
+            self.b.append(torch.nn.Parameter(torch.zeros(u, device=device)))
+            self.gamma.append(torch.nn.Parameter(torch.ones(width, device=device)))
+            self.beta.append(torch.nn.Parameter(torch.zeros(width, device=device)))
+            mm = torch.zeros(width, device=device)
+            mv = torch.ones(width, device=device)
+            self.register_buffer(f"moving_mean_{i}", mm)
+            self.register_buffer(f"moving_var_{i}", mv)
+            self.moving_mean.append(mm)
+            self.moving_var.append(mv)
+            width = u
+        self.out_features = width
+
+    def _apply(self, fn, *args, **kw):  # keep the moving-stat lists pointing at the registered buffers
+        r = super()._apply(fn, *args, **kw)
+        self.moving_mean = [getattr(self, f"moving_mean_{i}") for i in range(len(self.units))]
+        self.moving_var = [getattr(self, f"moving_var_{i}") for i in range(len(self.units))]
+        return r
+
+    def params(self) -> List[torch.nn.Parameter]:
+        out = []
+        for l in range(len(self.units)):
+            out += [self.W[l], self.b[l], self.gamma[l], self.beta[l]]
+        return out
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.training:
+            return _TowerFn.apply(x, self, *self.params())
+        # inference: the moving statistics folded into the weights, no dropout
+        st = L.stream_ptr(None)
+        h = x if x.stride(1) == 1 else x.contiguous()
+        for l in range(len(self.units)):
+            W = self.W[l].detach()
+            N, K = W.shape
+            Wf = torch.empty_like(W)
+            bf = torch.empty(N, dtype=torch.float32, device=x.device)
+            L.call("rf_bn_fold", L.ptr(W), N, K, L.ptr(self.b[l]), L.ptr(self.gamma[l]), L.ptr(self.beta[l]),
+                   L.ptr(self.moving_mean[l]), L.ptr(self.moving_var[l]), self.eps, L.ptr(Wf), L.ptr(bf), st)
+            y = torch.empty((h.shape[0], N), dtype=torch.float32, device=x.device)
+            _linear_f32(h, Wf, bf, L.ACT["selu"], y, st)
+            h = y
+        return h

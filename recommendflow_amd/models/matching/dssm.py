@@ -55,15 +55,18 @@ class Dssm(torch.nn.Module):
 
 class TrainableDssm(torch.nn.Module):
     """DSSM training graph (deviation D-dssm-wiring as above): ONE fused encoder over the user slots then
-    the ad slots (one forward and one backward launch for both towers), torch towers
-    [BatchNorm(eps 1e-6, Keras momentum 0.99) -> Dense(selu) -> Dropout(0.3)] x [1024, 512, 256]
-    (dssm.py:25-26, mlp.py:4-15; library GEMMs), l2 normalisation (dssm.py:35-36), and the
-    configured loss (cosent_loss for base_recall_sdpa.yaml). step() = forward, backward, SparseAdam on
-    the table (rf_adam_apply) and torch Adam on the towers, Keras defaults (lr 1e-3, 0.9, 0.999, 1e-7)."""
+    the ad slots (one forward and one backward launch for both towers), towers
+    [BatchNormalization(eps 1e-6, Keras momentum 0.99) -> Dense(selu) -> Dropout(0.3)] x [1024, 512, 256]
+    (dssm.py:25-26, mlp.py:4-15) on librf.so (backend.blocks.train_mlp.TrainTower: batch statistics folded
+    into the fp32 MFMA GEMM, SELU / dropout / BatchNormalization backward kernels, library GEMMs for the two
+    backward products), l2 normalisation (dssm.py:35-36), and the configured loss (cosent_loss for
+    base_recall_sdpa.yaml). step() = forward, backward, SparseAdam on the table (rf_adam_apply) and Adam on
+    the towers, Keras defaults (lr 1e-3, 0.9, 0.999, 1e-7)."""
 
     def __init__(self, encoder: FusedSparseEncoder, n_user_slots: int, units=(1024, 512, 256), dropout=0.3,
                  learning_rate=1e-3, loss="cosent", lazy_adam=False, seed=0):
         super().__init__()
+        from ...backend.blocks.train_mlp import TrainTower
         from ...backend.losses import match_losses
         from ...backend.optim import SparseAdam
 
@@ -71,23 +74,9 @@ class TrainableDssm(torch.nn.Module):
         self.wu = 2 * encoder.dim * n_user_slots
         self.wa = encoder.out_width - self.wu
         g = torch.Generator().manual_seed(seed)
-
-        def tower(width):
-            layers = []
-            for u in units:
-                lin = torch.nn.Linear(width, u)
-                with torch.no_grad():  # glorot_uniform kernel, zero bias (Keras Dense defaults)
-                    lim = (6.0 / (width + u)) ** 0.5
-                    lin.weight.copy_(torch.rand(u, width, generator=g) * 2 * lim - lim)
-                    lin.bias.zero_()
-                layers += [torch.nn.BatchNorm1d(width, eps=1e-6, momentum=0.01), lin, torch.nn.SELU(),
-                           torch.nn.Dropout(dropout)]
-                width = u
-            return torch.nn.Sequential(*layers)
-
         dev = encoder.table.device
-        self.user_tower = tower(self.wu).to(dev)
-        self.ad_tower = tower(self.wa).to(dev)
+        self.user_tower = TrainTower(self.wu, units, rate=dropout, eps=1e-6, seed=2 * seed + 1, generator=g, device=dev)
+        self.ad_tower = TrainTower(self.wa, units, rate=dropout, eps=1e-6, seed=2 * seed + 2, generator=g, device=dev)
         self.loss_fn = {"cosent": match_losses.cosent_loss,
                         "inbatch_ce": match_losses.batch_neg_sample_scaled_multi_class_ce_loss}[loss]
         self.sparse_opt = SparseAdam(encoder.table, learning_rate=learning_rate, lazy=lazy_adam)
@@ -98,9 +87,9 @@ class TrainableDssm(torch.nn.Module):
         from ...runtime.train import embed
 
         x = embed(self.enc, batch)
-        # contiguous column blocks: BatchNorm's backward on a strided view falls off torch's fast path
-        u = torch.nn.functional.normalize(self.user_tower(x[:, : self.wu].contiguous()), dim=-1, eps=1e-6)
-        v = torch.nn.functional.normalize(self.ad_tower(x[:, self.wu:].contiguous()), dim=-1, eps=1e-6)
+        # the towers read their column blocks of x in place (row stride = the full width)
+        u = torch.nn.functional.normalize(self.user_tower(x[:, : self.wu]), dim=-1, eps=1e-6)
+        v = torch.nn.functional.normalize(self.ad_tower(x[:, self.wu:]), dim=-1, eps=1e-6)
         return u, v
 
     def step(self, batch: SparseBatch, labels: torch.Tensor, dp=None) -> torch.Tensor:

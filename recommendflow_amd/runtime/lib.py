@@ -77,6 +77,15 @@ _SIGS = {
     "rf_linear_splitk_ws_bytes": (ctypes.c_size_t, [_i32, _i64, _i32, _i32]),
     "rf_linear_splitk_fwd": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _i64, _vp,
                                             ctypes.c_size_t, _vp]),
+    "rf_tower_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
+    "rf_col_stats": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "rf_bn_fold": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp]),
+    "rf_dropout_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _f32, ctypes.c_uint64, _vp, _i64, _vp]),
+    "rf_selu_dropout_bwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _f32, ctypes.c_uint64, _vp, _i64, _vp, _vp,
+                                           ctypes.c_size_t, _vp]),
+    "rf_bn_fold_grad": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp]),
+    "rf_bn_bwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _vp,
+                                 ctypes.c_size_t, _vp]),
     "rf_stream_copy": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp]),
     "rf_gather_probe": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, ctypes.c_uint64, _vp, _vp, _vp]),
     "rf_topk_merge": (ctypes.c_int, [_vp, _i64, _i32, _i32, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _i64, _vp]),
