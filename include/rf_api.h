@@ -412,6 +412,24 @@ int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const 
                             int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
 
 /*
+ * rf_fused_hash_embed_bwd in two halves on one workspace: _plan (enumerate, sort, segment: the batch alone
+ * decides it) writes uniq_rows / n_uniq and keeps the plan in ws; _reduce (the same ws, untouched in between)
+ * reads dout and writes uniq_grad. plan + reduce == rf_fused_hash_embed_bwd, bit for bit. The plan can run
+ * while the dense layers still compute dout (the DSSM train step runs it, and rf_adam_untouched, on a side stream).
+ */
+int rf_fused_hash_embed_bwd_plan(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                 const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
+                                 int64_t n_positions, int64_t table_rows, int32_t dim, int64_t out_stride, int32_t flags,
+                                 int64_t* uniq_rows, int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes,
+                                 void* stream);
+int rf_fused_hash_embed_bwd_reduce(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                   const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
+                                   int64_t n_positions, const float* table, int64_t table_rows, int32_t dim,
+                                   const float* out, const float* dout, int64_t out_stride, int32_t flags,
+                                   int32_t* minmax_count, int64_t* uniq_rows, float* uniq_grad, int64_t uniq_cap,
+                                   int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
+
+/*
  * Backward of rf_pool_rows_fwd (the requester side of the sharded lookup): the same
  * per-position gradients and (b, l) summation order as rf_fused_hash_embed_bwd, keyed by the distinct
  * gathered row each logical row maps to (row_map, as in the forward; n_rows = number of gathered rows).
@@ -444,6 +462,16 @@ int rf_segment_sum_rows(const int64_t* ids, const float* vals, int64_t n, int32_
  * ws: rf_adam_ws_bytes(table_rows, lazy) bytes (dense mode: a row -> gradient map).
  */
 size_t rf_adam_ws_bytes(int64_t table_rows, int32_t lazy);
+/*
+ * The dense step split in time: rf_adam_untouched updates every row NOT listed in uniq_rows[:n_uniq] (their
+ * Keras update needs no gradient: m, v decay, var moves by lr m / (sqrt(v) + eps)), so it can run as soon as
+ * the row set is known (rf_fused_hash_embed_bwd_plan); rf_adam_apply(lazy = 1) on the gradient then updates
+ * the listed rows with the same lr. Together: rf_adam_apply(lazy = 0), bit for bit.
+ * ws: rf_adam_ws_bytes(table_rows, 0).
+ */
+int rf_adam_untouched(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                      const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1, float beta2, float epsilon, void* ws,
+                      size_t ws_bytes, void* stream);
 int rf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
                   const float* uniq_grad, const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1,
                   float beta2, float epsilon, int32_t lazy, void* ws, size_t ws_bytes, void* stream);

@@ -47,77 +47,118 @@ def _ws(M: int, K: int, device) -> torch.Tensor:
     return torch.empty(max(int(L.load().rf_tower_ws_bytes(M, K)), 4), dtype=torch.uint8, device=device)
 
 
-class _TowerFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, tower: "TrainTower", *params):
-        if x.dim() != 2 or x.stride(1) != 1 or x.dtype != torch.float32:
-            raise ValueError("TrainTower input must be a 2-D fp32 tensor with unit column stride")
-        M = x.shape[0]
-        dev, st = x.device, L.stream_ptr(None)
-        step = tower.steps
-        tower.steps += 1
-        h = x
-        outs, means, vars_ = [], [], []
-        for l in range(len(tower.units)):
-            W, b, g, be = params[4 * l: 4 * l + 4]
-            N, K = W.shape
-            mean = torch.empty(K, dtype=torch.float32, device=dev)
-            var = torch.empty(K, dtype=torch.float32, device=dev)
-            ws = _ws(M, K, dev)
-            L.call("rf_col_stats", L.ptr(h), M, K, h.stride(0), L.ptr(mean), L.ptr(var), L.ptr(ws), ws.numel(), st)
-            Wf = torch.empty_like(W)
-            bf = torch.empty(N, dtype=torch.float32, device=dev)
-            L.call("rf_bn_fold", L.ptr(W), N, K, L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(mean), L.ptr(var), tower.eps,
-                   L.ptr(Wf), L.ptr(bf), st)
-            y = torch.empty((M, N), dtype=torch.float32, device=dev)
-            _linear_f32(h, Wf, bf, L.ACT["selu"], y, st)
-            L.call("rf_dropout_fwd", L.ptr(y), M, N, N, tower.rate, layer_seed(tower.seed, step, l), L.ptr(y), N, st)
-            with torch.no_grad():
-                tower.moving_mean[l].mul_(tower.momentum).add_(mean, alpha=1.0 - tower.momentum)
-                tower.moving_var[l].mul_(tower.momentum).add_(var, alpha=1.0 - tower.momentum)
-            outs.append(y)
-            means.append(mean)
-            vars_.append(var)
-            h = y
-        ctx.tower, ctx.step, ctx.n = tower, step, len(tower.units)
-        ctx.save_for_backward(x, *params, *outs, *means, *vars_)
-        return outs[-1]
+def _tower_forward(tower: "TrainTower", x: torch.Tensor, params):
+    """The training forward of one tower on x (a 2-D fp32 view with unit column stride; any row stride).
+    Returns (outputs per layer, batch means, batch variances, the step number that seeded the masks)."""
+    if x.dim() != 2 or x.stride(1) != 1 or x.dtype != torch.float32:
+        raise ValueError("TrainTower input must be a 2-D fp32 tensor with unit column stride")
+    M = x.shape[0]
+    dev, st = x.device, L.stream_ptr(None)
+    step = tower.steps
+    tower.steps += 1
+    h = x
+    outs, means, vars_ = [], [], []
+    for l in range(len(tower.units)):
+        W, b, g, be = params[4 * l: 4 * l + 4]
+        N, K = W.shape
+        mean = torch.empty(K, dtype=torch.float32, device=dev)
+        var = torch.empty(K, dtype=torch.float32, device=dev)
+        ws = _ws(M, K, dev)
+        L.call("rf_col_stats", L.ptr(h), M, K, h.stride(0), L.ptr(mean), L.ptr(var), L.ptr(ws), ws.numel(), st)
+        Wf = torch.empty_like(W)
+        bf = torch.empty(N, dtype=torch.float32, device=dev)
+        L.call("rf_bn_fold", L.ptr(W), N, K, L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(mean), L.ptr(var), tower.eps,
+               L.ptr(Wf), L.ptr(bf), st)
+        y = torch.empty((M, N), dtype=torch.float32, device=dev)
+        _linear_f32(h, Wf, bf, L.ACT["selu"], y, st)
+        L.call("rf_dropout_fwd", L.ptr(y), M, N, N, tower.rate, layer_seed(tower.seed, step, l), L.ptr(y), N, st)
+        with torch.no_grad():
+            tower.moving_mean[l].mul_(tower.momentum).add_(mean, alpha=1.0 - tower.momentum)
+            tower.moving_var[l].mul_(tower.momentum).add_(var, alpha=1.0 - tower.momentum)
+        outs.append(y)
+        means.append(mean)
+        vars_.append(var)
+        h = y
+    return outs, means, vars_, step
+
+
+def _tower_backward(tower: "TrainTower", step: int, x: torch.Tensor, params, outs, means, vars_, dout: torch.Tensor,
+                    dx_out: torch.Tensor):
+    """Backward of _tower_forward: parameter gradients (W, b, gamma, beta per layer) returned, the input gradient
+    written into dx_out (a view of x's shape; any row stride)."""
+    n = len(tower.units)
+    dev, st = x.device, L.stream_ptr(None)
+    M = x.shape[0]
+    dh = dout if dout.stride(1) == 1 else dout.contiguous()
+    grads: List[Optional[torch.Tensor]] = [None] * (4 * n)
+    for l in reversed(range(n)):
+        W, b, g, be = params[4 * l: 4 * l + 4]
+        N, K = W.shape
+        h_in = x if l == 0 else outs[l - 1]
+        ws = _ws(M, max(K, N), dev)
+        dpre = torch.empty((M, N), dtype=torch.float32, device=dev)
+        db = torch.empty(N, dtype=torch.float32, device=dev)
+        L.call("rf_selu_dropout_bwd", L.ptr(dh), dh.stride(0), L.ptr(outs[l]), N, M, N, tower.rate,
+               layer_seed(tower.seed, step, l), L.ptr(dpre), N, L.ptr(db), L.ptr(ws), ws.numel(), st)
+        G = torch.mm(dpre.t(), h_in)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
+        dW = torch.empty_like(W)
+        L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]), L.ptr(vars_[l]),
+               tower.eps, L.ptr(dW), st)
+        del G
+        dz = torch.mm(dpre, W)  # [M][K] (library GEMM)
+        dx = dx_out if l == 0 else torch.empty((M, K), dtype=torch.float32, device=dev)
+        dgamma = torch.empty(K, dtype=torch.float32, device=dev)
+        dbeta = torch.empty(K, dtype=torch.float32, device=dev)
+        L.call("rf_bn_bwd", L.ptr(dz), K, L.ptr(h_in), h_in.stride(0), M, K, L.ptr(means[l]), L.ptr(vars_[l]), L.ptr(g),
+               tower.eps, L.ptr(dx), dx.stride(0), L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), ws.numel(), st)
+        grads[4 * l: 4 * l + 4] = [dW, db, dgamma, dbeta]
+        dh = dx
+    return grads
+
+
+class _TowersFn(torch.autograd.Function):
+    """Towers over column blocks of ONE input (the DSSM user and ad blocks of the fused encoder's output):
+    the backward writes every tower's input gradient into its block of one full-width gradient, so autograd
+    never materialises zero-filled slice gradients and adds them."""
 
     @staticmethod
-    def backward(ctx, dout):
-        tower, n = ctx.tower, ctx.n
-        saved = ctx.saved_tensors
-        x = saved[0]
-        params = saved[1: 1 + 4 * n]
-        outs = saved[1 + 4 * n: 1 + 5 * n]
-        means = saved[1 + 5 * n: 1 + 6 * n]
-        vars_ = saved[1 + 6 * n: 1 + 7 * n]
-        dev, st = x.device, L.stream_ptr(None)
-        M = x.shape[0]
-        dh = dout if dout.stride(1) == 1 else dout.contiguous()
-        grads: List[Optional[torch.Tensor]] = [None] * (4 * n)
-        for l in reversed(range(n)):
-            W, b, g, be = params[4 * l: 4 * l + 4]
-            N, K = W.shape
-            h_in = x if l == 0 else outs[l - 1]
-            ws = _ws(M, max(K, N), dev)
-            dpre = torch.empty((M, N), dtype=torch.float32, device=dev)
-            db = torch.empty(N, dtype=torch.float32, device=dev)
-            L.call("rf_selu_dropout_bwd", L.ptr(dh), dh.stride(0), L.ptr(outs[l]), N, M, N, tower.rate,
-                   layer_seed(tower.seed, ctx.step, l), L.ptr(dpre), N, L.ptr(db), L.ptr(ws), ws.numel(), st)
-            G = torch.mm(dpre.t(), h_in)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
-            dW = torch.empty_like(W)
-            L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]), L.ptr(vars_[l]),
-                   tower.eps, L.ptr(dW), st)
-            dz = torch.mm(dpre, W)  # [M][K] (library GEMM)
-            dx = torch.empty((M, K), dtype=torch.float32, device=dev)
-            dgamma = torch.empty(K, dtype=torch.float32, device=dev)
-            dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-            L.call("rf_bn_bwd", L.ptr(dz), K, L.ptr(h_in), h_in.stride(0), M, K, L.ptr(means[l]), L.ptr(vars_[l]), L.ptr(g),
-                   tower.eps, L.ptr(dx), K, L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), ws.numel(), st)
-            grads[4 * l: 4 * l + 4] = [dW, db, dgamma, dbeta]
-            dh = dx
-        return (dh, None, *grads)
+    def forward(ctx, x, blocks, *params):
+        outs_all, saved, meta = [], [], []
+        p0 = 0
+        for tower, off, width in blocks:
+            np_ = 4 * len(tower.units)
+            ps = params[p0: p0 + np_]
+            outs, means, vars_, step = _tower_forward(tower, x[:, off: off + width], ps)
+            meta.append((tower, off, width, step, p0, np_, len(saved)))
+            saved += [*outs, *means, *vars_]
+            outs_all.append(outs[-1])
+            p0 += np_
+        ctx.meta = meta
+        ctx.save_for_backward(x, *params, *saved)
+        return tuple(outs_all)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        x = ctx.saved_tensors[0]
+        nparams = sum(m[5] for m in ctx.meta)
+        params = ctx.saved_tensors[1: 1 + nparams]
+        saved = ctx.saved_tensors[1 + nparams:]
+        dx = torch.zeros_like(x) if sum(m[2] for m in ctx.meta) != x.shape[1] else torch.empty_like(x)
+        grads: List[Optional[torch.Tensor]] = [None] * nparams
+        for (tower, off, width, step, p0, np_, s0), dout in zip(ctx.meta, douts):
+            n = len(tower.units)
+            outs, means, vars_ = saved[s0: s0 + n], saved[s0 + n: s0 + 2 * n], saved[s0 + 2 * n: s0 + 3 * n]
+            if dout is None:
+                dout = torch.zeros_like(outs[-1])
+            grads[p0: p0 + np_] = _tower_backward(tower, step, x[:, off: off + width], params[p0: p0 + np_], outs, means,
+                                                  vars_, dout, dx[:, off: off + width])
+        return (dx, None, *grads)
+
+
+def towers_forward(x: torch.Tensor, blocks) -> tuple:
+    """blocks: [(TrainTower, column offset, width)]: each tower's training forward on its block of x."""
+    params = [p for t, _, _ in blocks for p in t.params()]
+    return _TowersFn.apply(x, list(blocks), *params)
 
 
 class TrainTower(torch.nn.Module):
@@ -164,7 +205,9 @@ class TrainTower(torch.nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.training:
-            return _TowerFn.apply(x, self, *self.params())
+            if x.stride(1) != 1:
+                x = x.contiguous()
+            return towers_forward(x, [(self, 0, x.shape[1])])[0]
         # inference: the moving statistics folded into the weights, no dropout
         st = L.stream_ptr(None)
         h = x if x.stride(1) == 1 else x.contiguous()

@@ -77,6 +77,19 @@ def init_table(table: torch.Tensor, row0: int = 0, row_stride: int = 1, seed: in
 
 
 @dataclass
+class BwdPlan:
+    """FusedSparseEncoder.backward_plan's state: the device batch, the distinct rows (rows[:n_uniq]) and the
+    workspace the reduce half continues from."""
+    batch: SparseBatch
+    n_pos: int
+    cap: int
+    rows: torch.Tensor
+    n_uniq: torch.Tensor
+    ws: torch.Tensor
+    flags: int
+
+
+@dataclass
 class SparseGrad:
     """Deduplicated gradient of a fused table (device): rows[:n] ascending, grad[:n] [n, dim]; n = n_uniq
     (a device int32; negative = invalid batch, see rf_fused_hash_embed_bwd)."""
@@ -214,6 +227,50 @@ class FusedSparseEncoder(torch.nn.Module):
                L.ptr(out) if need_mm else None, L.ptr(dout), dout.stride(0), flags, L.ptr(cnt), L.ptr(rows), L.ptr(grad),
                cap, L.ptr(n_uniq), L.ptr(ws), ws.numel(), L.stream_ptr(stream))
         return SparseGrad(rows, grad, n_uniq, cap)
+
+    def backward_plan(self, batch: SparseBatch, uniq_cap: Optional[int] = None, stream=None) -> "BwdPlan":
+        """The batch-only half of backward() (rf_fused_hash_embed_bwd_plan): the distinct rows the gradient will
+        hold (plan.rows[:n], ascending; n = plan.n_uniq on the device), before dout exists."""
+        if batch.n_slots != len(self.slots):
+            raise ValueError(f"batch has {batch.n_slots} slots, encoder {len(self.slots)}")
+        lm = batch.lmax_numpy()
+        if not batch.is_device():
+            batch = batch.to(self.table.device)
+        B, dev = batch.batch, self.table.device
+        n_pos = B * int(2 * np.asarray(lm, np.int64).sum())
+        cap = int(uniq_cap) if uniq_cap is not None else max(1, min(n_pos, self.table.shape[0]))
+        rows = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+        wsb = L.load().rf_embed_bwd_ws_bytes(n_pos, len(self.slots), self.table.shape[0])
+        ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=dev)
+        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        L.call("rf_fused_hash_embed_bwd_plan", L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes),
+               L.ptr(batch.tok_off), L.ptr(batch.bag_off), L.ptr(batch.lmax), B, n_pos, self.table.shape[0], self.dim,
+               self.out_width, flags, L.ptr(rows), cap, L.ptr(n_uniq), L.ptr(ws), ws.numel(), L.stream_ptr(stream))
+        return BwdPlan(batch, n_pos, cap, rows, n_uniq, ws, flags)
+
+    def backward_reduce(self, plan: "BwdPlan", dout: torch.Tensor, out: Optional[torch.Tensor] = None,
+                        stream=None) -> "SparseGrad":
+        """The dout half of backward() on a plan from backward_plan (same stream order or joined): the result
+        equals backward(plan.batch, dout, out) bit for bit."""
+        if self.table.dtype != torch.float32 or dout.dtype != torch.float32:
+            raise ValueError("backward needs an fp32 table and an fp32 output gradient")
+        dout = dout.contiguous()
+        if dout.stride(0) != self.out_width:
+            raise ValueError("backward_reduce: dout must be [B, out_width] (the plan's row stride)")
+        need_mm = any(sp.combiner in ("max", "min") for sp in self.slots)
+        if need_mm and out is None:
+            raise ValueError("max/min pooling: backward needs the forward output `out`")
+        if out is not None and (out.stride(0) != dout.stride(0) or out.dtype != torch.float32):
+            out = out.contiguous().float()
+        cnt = torch.empty(dout.shape, dtype=torch.int32, device=dout.device) if need_mm else None
+        grad = torch.empty((max(plan.cap, 1), self.dim), dtype=torch.float32, device=dout.device)
+        b = plan.batch
+        L.call("rf_fused_hash_embed_bwd_reduce", L.ptr(self.desc), len(self.slots), L.ptr(b.tok_bytes), L.ptr(b.tok_off),
+               L.ptr(b.bag_off), L.ptr(b.lmax), b.batch, plan.n_pos, L.ptr(self.table), self.table.shape[0], self.dim,
+               L.ptr(out) if need_mm else None, L.ptr(dout), dout.stride(0), plan.flags, L.ptr(cnt), L.ptr(plan.rows),
+               L.ptr(grad), plan.cap, L.ptr(plan.n_uniq), L.ptr(plan.ws), plan.ws.numel(), L.stream_ptr(stream))
+        return SparseGrad(plan.rows, grad, plan.n_uniq, plan.cap)
 
     def algorithmic_bytes(self, batch: SparseBatch) -> int:
         """HBM bytes one forward must move: rows read (every occurrence, padding positions

@@ -41,6 +41,20 @@ class SparseAdam:
         b1p, b2p = np.power(f(self.beta_1), t), np.power(f(self.beta_2), t)
         return float(f(self.learning_rate) * (np.sqrt(f(1) - b2p) / (f(1) - b1p)))
 
+    def apply_untouched(self, rows: torch.Tensor, n_uniq: torch.Tensor, cap: int, stream=None):
+        """The first half of this iteration's dense step: every row not in rows[:n_uniq] (rf_adam_untouched). The
+        second half is apply_touched() with the gradient over exactly those rows; together they equal apply()."""
+        L.call("rf_adam_untouched", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0],
+               self.table.shape[1], L.ptr(rows), L.ptr(n_uniq), cap, self.step_lr(), self.beta_1, self.beta_2,
+               self.epsilon, L.ptr(self._ws), self._ws.numel(), L.stream_ptr(stream))
+
+    def apply_touched(self, g: SparseGrad, stream=None):
+        """The second half (after apply_untouched on g's row set): the listed rows with their gradient."""
+        L.call("rf_adam_apply", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0], self.table.shape[1],
+               L.ptr(g.rows), L.ptr(g.grad), L.ptr(g.n_uniq), g.cap, self.step_lr(), self.beta_1, self.beta_2,
+               self.epsilon, 1, L.ptr(self._ws), self._ws.numel(), L.stream_ptr(stream))
+        self.iterations += 1
+
     def apply(self, g: SparseGrad, stream=None):
         L.call("rf_adam_apply", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0], self.table.shape[1],
                L.ptr(g.rows), L.ptr(g.grad), L.ptr(g.n_uniq), g.cap, self.step_lr(), self.beta_1, self.beta_2,

@@ -7,8 +7,8 @@
 // batch_neg_sample_scaled_multi_class_ce_loss (match_losses.py:150-165, Que2Search):
 //   loss = mean_i( -log(exp(s P_ii) / sum_j exp(s P_ij)) * y_i ),  P = query . doc^T (a library GEMM)
 //   dloss/dP_ij = s * y_i / B * (softmax_j(s P_i.) - [i == j])
-// Deterministic: fixed-order block reductions, no atomics. cosent: a thread per i walks every j, the j
-// scores and labels staged through LDS 256 at a time.
+// Deterministic: fixed-order block reductions, no atomics. cosent: (i block, j chunk) tiles of 256 x 256 pairs,
+// the j scores and labels staged through LDS; the tile partials are summed in tile order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,25 +30,25 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// pass A: per-block max of the valid x_ij (thread per i, loop over all j through LDS)
+// The B x B pairs run as (i block, j chunk) tiles: grid (ceil(B / 256), ceil(B / 256)), a thread per i walking
+// its tile's 256 j through LDS, so a 4096 batch fills 256 workgroups (a thread per i over every j kept 16 busy).
+// pass A: per-tile max of the valid x_ij
 __global__ __launch_bounds__(kRows) void cosent_max_kernel(const float* __restrict__ s, const float* __restrict__ y,
                                                            int B, float scale, float* __restrict__ part) {
     __shared__ float sj[kRows], yj[kRows];
     __shared__ float red[kRows / 64];
     const int i = blockIdx.x * kRows + threadIdx.x;
     const float si = i < B ? s[i] : 0.f, yi = i < B ? y[i] : 0.f;
+    const int j0 = blockIdx.y * kRows;
+    const int j = j0 + threadIdx.x;
+    sj[threadIdx.x] = j < B ? s[j] : 0.f;
+    yj[threadIdx.x] = j < B ? y[j] : -INFINITY;
+    __syncthreads();
     float m = -INFINITY;
-    for (int j0 = 0; j0 < B; j0 += kRows) {
-        __syncthreads();
-        const int j = j0 + threadIdx.x;
-        sj[threadIdx.x] = j < B ? s[j] : 0.f;
-        yj[threadIdx.x] = j < B ? y[j] : -INFINITY;
-        __syncthreads();
-        if (i < B) {
-            const int n = min(kRows, B - j0);
-            for (int k = 0; k < n; ++k)
-                if (yi < yj[k]) m = fmaxf(m, scale * si - scale * sj[k]);
-        }
+    if (i < B) {
+        const int n = min(kRows, B - j0);
+        for (int k = 0; k < n; ++k)
+            if (yi < yj[k]) m = fmaxf(m, scale * si - scale * sj[k]);
     }
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -56,50 +56,50 @@ __global__ __launch_bounds__(kRows) void cosent_max_kernel(const float* __restri
     if (threadIdx.x == 0) {
         float r = red[0];
         for (int w = 1; w < kRows / 64; ++w) r = fmaxf(r, red[w]);
-        part[blockIdx.x] = r;
+        part[blockIdx.y * gridDim.x + blockIdx.x] = r;
     }
 }
 
-// pass B: R_i and C_i with the global m (m = max(0, all partial maxima), recomputed by every block)
+// pass B: per-tile partials of R_i and C_i with the global m (m = max(0, every tile maximum))
 __global__ __launch_bounds__(kRows) void cosent_sums_kernel(const float* __restrict__ s, const float* __restrict__ y,
                                                             int B, float scale, const float* __restrict__ part, int nparts,
-                                                            float* __restrict__ R, float* __restrict__ C) {
+                                                            float* __restrict__ Rp, float* __restrict__ Cp) {
     __shared__ float sj[kRows], yj[kRows];
     float m = 0.f;
     for (int p = 0; p < nparts; ++p) m = fmaxf(m, part[p]);
     const int i = blockIdx.x * kRows + threadIdx.x;
     const float si = i < B ? s[i] : 0.f, yi = i < B ? y[i] : 0.f;
+    const int j0 = blockIdx.y * kRows;
+    const int j = j0 + threadIdx.x;
+    sj[threadIdx.x] = j < B ? s[j] : 0.f;
+    yj[threadIdx.x] = j < B ? y[j] : 0.f;
+    __syncthreads();
+    if (i >= B) return;
     float r = 0.f, c = 0.f;
-    for (int j0 = 0; j0 < B; j0 += kRows) {
-        __syncthreads();
-        const int j = j0 + threadIdx.x;
-        sj[threadIdx.x] = j < B ? s[j] : 0.f;
-        yj[threadIdx.x] = j < B ? y[j] : 0.f;
-        __syncthreads();
-        if (i < B) {
-            const int n = min(kRows, B - j0);
-            for (int k = 0; k < n; ++k) {
-                if (yi < yj[k]) r += expf(scale * si - scale * sj[k] - m);
-                if (yj[k] < yi) c += expf(scale * sj[k] - scale * si - m);
-            }
-        }
+    const int n = min(kRows, B - j0);
+    for (int k = 0; k < n; ++k) {
+        if (yi < yj[k]) r += expf(scale * si - scale * sj[k] - m);
+        if (yj[k] < yi) c += expf(scale * sj[k] - scale * si - m);
     }
-    if (i < B) {
-        R[i] = r;
-        C[i] = c;
-    }
+    Rp[(int64_t)blockIdx.y * B + i] = r;
+    Cp[(int64_t)blockIdx.y * B + i] = c;
 }
 
-// pass C (one block): Z, loss, gradient
-__global__ __launch_bounds__(1024) void cosent_final_kernel(const float* __restrict__ R, const float* __restrict__ C, int B,
-                                                            float scale, const float* __restrict__ part, int nparts,
+// pass C (one block): R_i, C_i = the tile partials summed in tile order; Z, loss, gradient
+__global__ __launch_bounds__(1024) void cosent_final_kernel(const float* __restrict__ Rp, const float* __restrict__ Cp, int B,
+                                                            int nj, float scale, const float* __restrict__ part, int nparts,
                                                             float* __restrict__ loss, float* __restrict__ ds) {
     __shared__ float red[16];
     __shared__ float s_z;
     float m = 0.f;
     for (int p = 0; p < nparts; ++p) m = fmaxf(m, part[p]);
+    auto rsum = [&](const float* P, int i) {
+        float a = 0.f;
+        for (int t = 0; t < nj; ++t) a += P[(int64_t)t * B + i];
+        return a;
+    };
     float acc = 0.f;
-    for (int i = threadIdx.x; i < B; i += 1024) acc += R[i];
+    for (int i = threadIdx.x; i < B; i += 1024) acc += rsum(Rp, i);
     acc = wave_sum(acc);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(1024) void cosent_final_kernel(const float* __restr
     __syncthreads();
     const float z = s_z;
     if (ds)
-        for (int i = threadIdx.x; i < B; i += 1024) ds[i] = scale * (R[i] - C[i]) / z;
+        for (int i = threadIdx.x; i < B; i += 1024) ds[i] = scale * (rsum(Rp, i) - rsum(Cp, i)) / z;
 }
 
 // in-batch CE: one block per row i (256 threads), logits row of length B
@@ -165,7 +165,7 @@ size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 extern "C" size_t rf_loss_ws_bytes(int32_t batch) {
     if (batch < 0) return 0;
     const size_t nb = (size_t)(batch + kRows - 1) / kRows + 1;
-    return a256(nb * 4) + 2 * a256((size_t)std::max(batch, 1) * 4);
+    return a256(nb * nb * 4) + 2 * a256(nb * (size_t)std::max(batch, 1) * 4);
 }
 
 extern "C" int rf_cosent_loss(const float* score, const float* label, int32_t batch, float scale, float* loss, float* dscore,
@@ -177,11 +177,12 @@ extern "C" int rf_cosent_loss(const float* score, const float* label, int32_t ba
     const int nb = (batch + kRows - 1) / kRows;
     char* w = static_cast<char*>(ws);
     float* part = reinterpret_cast<float*>(w);
-    float* R = reinterpret_cast<float*>(w + a256((size_t)(nb + 1) * 4));
-    float* C = R + a256((size_t)batch * 4) / 4;
-    hipLaunchKernelGGL(cosent_max_kernel, dim3(nb), dim3(kRows), 0, st, score, label, batch, scale, part);
-    hipLaunchKernelGGL(cosent_sums_kernel, dim3(nb), dim3(kRows), 0, st, score, label, batch, scale, part, nb, R, C);
-    hipLaunchKernelGGL(cosent_final_kernel, dim3(1), dim3(1024), 0, st, R, C, batch, scale, part, nb, loss, dscore);
+    float* Rp = reinterpret_cast<float*>(w + a256((size_t)(nb + 1) * (nb + 1) * 4));
+    float* Cp = Rp + a256((size_t)(nb + 1) * batch * 4) / 4;
+    const dim3 g(nb, nb);
+    hipLaunchKernelGGL(cosent_max_kernel, g, dim3(kRows), 0, st, score, label, batch, scale, part);
+    hipLaunchKernelGGL(cosent_sums_kernel, g, dim3(kRows), 0, st, score, label, batch, scale, part, nb * nb, Rp, Cp);
+    hipLaunchKernelGGL(cosent_final_kernel, dim3(1), dim3(1024), 0, st, Rp, Cp, batch, nb, scale, part, nb * nb, loss, dscore);
     return rf_check_launch("rf_cosent_loss");
 }
 

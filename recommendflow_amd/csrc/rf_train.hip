@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 
 #include "rf_common.h"
@@ -529,6 +530,26 @@ __global__ __launch_bounds__(256) void adam_dense_kernel(float* __restrict__ w, 
     }
 }
 
+// the rows NOT in the gradient (map < 0) only: their Keras update needs no gradient, so it can run before the
+// gradient exists; the listed rows then take the lazy kernel with their gradient (together: exactly the dense step)
+__global__ __launch_bounds__(256) void adam_untouched_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                                             int64_t n4, int D4, const int32_t* __restrict__ map, AdamCoef c) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / D4;
+        if (map[row] >= 0) continue;
+        float4 wv = reinterpret_cast<float4*>(w)[i];
+        float4 mv = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+        adam_elem(wv.x, mv.x, vv.x, false, 0.f, c);
+        adam_elem(wv.y, mv.y, vv.y, false, 0.f, c);
+        adam_elem(wv.z, mv.z, vv.z, false, 0.f, c);
+        adam_elem(wv.w, mv.w, vv.w, false, 0.f, c);
+        reinterpret_cast<float4*>(w)[i] = wv;
+        reinterpret_cast<float4*>(m)[i] = mv;
+        reinterpret_cast<float4*>(v)[i] = vv;
+    }
+}
+
 // lazy: touched rows only
 __global__ __launch_bounds__(256) void adam_lazy_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                                                         int D4, const int64_t* __restrict__ uniq_rows,
@@ -570,7 +591,10 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
                    const int32_t* row_map, int64_t n_tok, const int32_t* bag_off, const int32_t* lmax, int32_t batch,
                    int64_t n_positions, const float* table, int64_t table_rows, int32_t dim, const float* out,
                    const float* dout, int64_t out_stride, int32_t flags, int32_t* minmax_count, int64_t* uniq_rows,
-                   float* uniq_grad, int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream) {
+                   float* uniq_grad, int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream,
+                   int mode = 0) {
+    // mode 0: everything; 1: the plan (enumerate, sort, segment, classify: the batch alone decides it, so it can
+    // run before dout exists); 2: the reduce of a plan already in ws (minmax counts, segment sums, flag)
     RF_REQUIRE(n_slots >= 1 && batch >= 0 && n_positions >= 0, "rf_fused_hash_embed_bwd: need n_slots >= 1, batch >= 0, n_positions >= 0");
     RF_REQUIRE(n_positions < ((int64_t)1 << 32) - 1, "rf_fused_hash_embed_bwd: n_positions must be < 2^32 - 1");
     RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 32) - 1, "rf_fused_hash_embed_bwd: table_rows must be in [1, 2^32 - 1)");
@@ -585,11 +609,13 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
         if (hipMemsetAsync(n_uniq, 0, sizeof(int32_t), st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
         return RF_OK;
     }
-    RF_REQUIRE(d_slots && (row_map || (tok_bytes && tok_off)) && bag_off && lmax && table && dout && uniq_rows && uniq_grad,
-               "rf_fused_hash_embed_bwd: null pointer");
-    RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)dout & 15) == 0 && ((uintptr_t)uniq_grad & 15) == 0 &&
-               (!out || ((uintptr_t)out & 15) == 0) && (!minmax_count || ((uintptr_t)minmax_count & 15) == 0),
-               "rf_fused_hash_embed_bwd: buffers must be 16-byte aligned");
+    RF_REQUIRE(d_slots && (row_map || (tok_bytes && tok_off)) && bag_off && lmax && uniq_rows, "rf_fused_hash_embed_bwd: null pointer");
+    if (mode != 1) {
+        RF_REQUIRE(table && dout && uniq_grad, "rf_fused_hash_embed_bwd: null pointer");
+        RF_REQUIRE(((uintptr_t)table & 15) == 0 && ((uintptr_t)dout & 15) == 0 && ((uintptr_t)uniq_grad & 15) == 0 &&
+                   (!out || ((uintptr_t)out & 15) == 0) && (!minmax_count || ((uintptr_t)minmax_count & 15) == 0),
+                   "rf_fused_hash_embed_bwd: buffers must be 16-byte aligned");
+    }
     const int masked = (flags & RF_FLAG_MASK_PADDING) ? 1 : 0;
     char* w = static_cast<char*>(ws);
     auto* kin = reinterpret_cast<uint32_t*>(w + lay.off_kin);
@@ -603,6 +629,12 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
     void* tmp = w + lay.off_tmp;
     const int64_t n = n_positions;
     const uint32_t sentinel = (uint32_t)table_rows;
+    uint32_t* src = kin;
+    uint32_t* aux = vin;
+    int32_t* long_list = scan;
+    int32_t* long_cnt = flag + 1;
+    const int64_t max_u = std::min<int64_t>(std::min<int64_t>(n, table_rows), uniq_cap);
+    if (mode != 2) {
     if (hipMemsetAsync(flag, 0, 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
     hipLaunchKernelGGL(posoff_kernel, dim3(1), dim3(1024), 0, st, lmax, n_slots, pos_off);
     hipLaunchKernelGGL(enum_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_slots, n_slots, tok_bytes, tok_off, bag_off,
@@ -616,22 +648,19 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
         return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: scan failed");
     hipLaunchKernelGGL(emit_kernel, dim3(grid_of(n)), dim3(256), 0, st, kout, scan, n, sentinel, uniq_cap, uniq_rows, seg);
     hipLaunchKernelGGL(count_kernel, dim3(1), dim3(64), 0, st, kout, scan, n, sentinel, flag, seg, n_uniq);
+    // prep (src/aux into the now-free pre-sort buffers) and the long-segment list (into the free scan buffer)
+    if (hipMemsetAsync(long_cnt, 0, 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
+    hipLaunchKernelGGL(prep_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_slots, n_slots, bag_off, lmax, pos_off, masked,
+                       vout, seg, n_uniq, dim, out_stride, src, aux, flag);
+    hipLaunchKernelGGL(classify_kernel, dim3(grid_of(max_u)), dim3(256), 0, st, seg, n_uniq, uniq_cap, long_list, long_cnt);
+    }
+    if (mode == 1) return rf_check_launch("rf_fused_hash_embed_bwd_plan");
     if (minmax_count) {
         RF_REQUIRE(out, "rf_fused_hash_embed_bwd: max/min pooling needs the forward output");
         hipLaunchKernelGGL(minmax_count_kernel, dim3(grid_of((int64_t)batch * n_slots * 2)), dim3(256), 0, st, d_slots,
                            n_slots, tok_bytes, tok_off, bag_off, lmax, batch, masked, row_map, n_tok, table, table_rows, dim, out,
                            out_stride, minmax_count);
     }
-    // prep (src/aux into the now-free pre-sort buffers) and the long-segment list (into the free scan buffer)
-    uint32_t* src = kin;
-    uint32_t* aux = vin;
-    int32_t* long_list = scan;
-    int32_t* long_cnt = flag + 1;
-    if (hipMemsetAsync(long_cnt, 0, 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_fused_hash_embed_bwd: memset failed");
-    hipLaunchKernelGGL(prep_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_slots, n_slots, bag_off, lmax, pos_off, masked,
-                       vout, seg, n_uniq, dim, out_stride, src, aux, flag);
-    const int64_t max_u = std::min<int64_t>(std::min<int64_t>(n, table_rows), uniq_cap);
-    hipLaunchKernelGGL(classify_kernel, dim3(grid_of(max_u)), dim3(256), 0, st, seg, n_uniq, uniq_cap, long_list, long_cnt);
     auto launch = [&](auto tpr) {
         constexpr int TPR = decltype(tpr)::value;
         const int teams = 256 / TPR;
@@ -664,6 +693,27 @@ extern "C" int rf_fused_hash_embed_bwd(const rf_slot_desc* d_slots, int32_t n_sl
     return embed_bwd_impl(d_slots, n_slots, tok_bytes, tok_off, nullptr, 0, bag_off, lmax, batch, n_positions, table,
                           table_rows, dim, out, dout, out_stride, flags, minmax_count, uniq_rows, uniq_grad, uniq_cap,
                           n_uniq, ws, ws_bytes, stream);
+}
+
+extern "C" int rf_fused_hash_embed_bwd_plan(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                            const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                                            int32_t batch, int64_t n_positions, int64_t table_rows, int32_t dim,
+                                            int64_t out_stride, int32_t flags, int64_t* uniq_rows, int64_t uniq_cap,
+                                            int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream) {
+    return embed_bwd_impl(d_slots, n_slots, tok_bytes, tok_off, nullptr, 0, bag_off, lmax, batch, n_positions, nullptr,
+                          table_rows, dim, nullptr, nullptr, out_stride, flags, nullptr, uniq_rows, nullptr, uniq_cap, n_uniq,
+                          ws, ws_bytes, stream, 1);
+}
+
+extern "C" int rf_fused_hash_embed_bwd_reduce(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                              const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                                              int32_t batch, int64_t n_positions, const float* table, int64_t table_rows,
+                                              int32_t dim, const float* out, const float* dout, int64_t out_stride,
+                                              int32_t flags, int32_t* minmax_count, int64_t* uniq_rows, float* uniq_grad,
+                                              int64_t uniq_cap, int32_t* n_uniq, void* ws, size_t ws_bytes, void* stream) {
+    return embed_bwd_impl(d_slots, n_slots, tok_bytes, tok_off, nullptr, 0, bag_off, lmax, batch, n_positions, table,
+                          table_rows, dim, out, dout, out_stride, flags, minmax_count, uniq_rows, uniq_grad, uniq_cap,
+                          n_uniq, ws, ws_bytes, stream, 2);
 }
 
 extern "C" int rf_pool_rows_bwd(const rf_slot_desc* d_slots, int32_t n_slots, const int32_t* bag_off, const int32_t* lmax,
@@ -784,4 +834,36 @@ extern "C" int rf_adam_apply(float* table, float* m, float* v, int64_t table_row
     hipLaunchKernelGGL(adam_dense_kernel, dim3(grid_of(table_rows * D4, 256 * 256)), dim3(256), 0, st, table, m, v,
                        table_rows * D4, D4, map, uniq_grad, c);
     return rf_check_launch("adam_dense_kernel");
+}
+
+extern "C" int rf_adam_untouched(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                                 const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1, float beta2, float epsilon,
+                                 void* ws, size_t ws_bytes, void* stream) {
+    RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 31), "rf_adam_untouched: table_rows must be in [1, 2^31)");
+    RF_REQUIRE(dim >= 4 && dim % 4 == 0, "rf_adam_untouched: dim must be a multiple of 4");
+    RF_REQUIRE(table && m && v && n_uniq && (uniq_cap == 0 || uniq_rows), "rf_adam_untouched: null pointer");
+    RF_REQUIRE((((uintptr_t)table | (uintptr_t)m | (uintptr_t)v) & 15) == 0, "rf_adam_untouched: buffers must be 16-byte aligned");
+    RF_REQUIRE(ws && ws_bytes >= rf_adam_ws_bytes(table_rows, 0), "rf_adam_untouched: workspace too small");
+    hipStream_t st = rf_stream(stream);
+    AdamCoef c;
+    c.lr = lr;
+    c.b1 = beta1;
+    c.b2 = beta2;
+    c.omb1 = 1.0f - beta1;
+    c.omb2 = 1.0f - beta2;
+    c.eps = epsilon;
+    auto* map = static_cast<int32_t*>(ws);
+    if (hipMemsetAsync(map, 0xff, (size_t)table_rows * 4, st) != hipSuccess) return rf_set_error(RF_EHIP, "rf_adam_untouched: memset failed");
+    if (uniq_cap > 0)
+        hipLaunchKernelGGL(map_fill_kernel, dim3(grid_of(uniq_cap)), dim3(256), 0, st, uniq_rows, n_uniq, uniq_cap, map);
+    // a persistent-size grid (one workgroup per CU; 128 / 256 / 512 / 65536 measured 16.2 / 13.2 / 13.4 / 13.9 ms
+    // per cfg2 train step, profiles/r03/r03y_train_ab.txt): this runs beside the towers' GEMMs on another stream, so it
+    // takes a bounded share of every CU instead of queueing 65,536 workgroups ahead of them
+    static const int gmax = [] {
+        const char* e = getenv("RF_ADAM_SIDE_GRID");
+        return e ? std::max(1, atoi(e)) : 256;
+    }();
+    hipLaunchKernelGGL(adam_untouched_kernel, dim3(grid_of(table_rows * (dim / 4), gmax)), dim3(256), 0, st, table, m, v,
+                       table_rows * (dim / 4), dim / 4, map, c);
+    return rf_check_launch("rf_adam_untouched");
 }

@@ -83,13 +83,29 @@ class TrainableDssm(torch.nn.Module):
         self.dense_opt = torch.optim.Adam(list(self.user_tower.parameters()) + list(self.ad_tower.parameters()),
                                           lr=learning_rate, betas=(0.9, 0.999), eps=1e-7)
 
-    def forward(self, batch: SparseBatch):
+    overlap_table_adam = True  # False: the table's dense Adam runs after the backward in one launch (A/B)
+
+    def _side_stream(self):
+        s = getattr(self, "_side", None)
+        if s is None:
+            s = self._side = torch.cuda.Stream(device=self.enc.table.device)
+        return s
+
+    def forward(self, batch: SparseBatch, after_embed=None):
+        from ...backend.blocks.train_mlp import towers_forward
         from ...runtime.train import embed
 
         x = embed(self.enc, batch)
-        # the towers read their column blocks of x in place (row stride = the full width)
-        u = torch.nn.functional.normalize(self.user_tower(x[:, : self.wu]), dim=-1, eps=1e-6)
-        v = torch.nn.functional.normalize(self.ad_tower(x[:, self.wu:]), dim=-1, eps=1e-6)
+        if after_embed is not None:
+            after_embed()
+        if self.training:
+            # both towers read their column blocks of x in place (row stride = the full width); the backward
+            # writes both input gradients into one full-width buffer
+            tu, ta = towers_forward(x, [(self.user_tower, 0, self.wu), (self.ad_tower, self.wu, self.wa)])
+        else:
+            tu, ta = self.user_tower(x[:, : self.wu]), self.ad_tower(x[:, self.wu:])
+        u = torch.nn.functional.normalize(tu, dim=-1, eps=1e-6)
+        v = torch.nn.functional.normalize(ta, dim=-1, eps=1e-6)
         return u, v
 
     def step(self, batch: SparseBatch, labels: torch.Tensor, dp=None) -> torch.Tensor:
@@ -99,14 +115,33 @@ class TrainableDssm(torch.nn.Module):
         BatchNorm moving statistics are then averaged over the replicas (DataParallel.sync_buffers)."""
         self.train()
         self.dense_opt.zero_grad(set_to_none=True)
-        u, v = self(batch)
+        # single replica, dense (exact Keras) Adam: the table rows NOT in this batch's gradient take their update
+        # on a side stream while the towers run (their Keras step needs no gradient); the gradient's rows get
+        # theirs after the backward (SparseAdam.apply_untouched / apply_touched == apply, bit for bit)
+        split = dp is None and not self.sparse_opt.lazy and self.overlap_table_adam
+
+        def launch_untouched():
+            main = torch.cuda.current_stream()
+            side = self._side_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                plan = self.enc.backward_plan(batch)
+                self.sparse_opt.apply_untouched(plan.rows, plan.n_uniq, plan.cap)
+            for t in (plan.rows, plan.n_uniq, plan.ws):
+                t.record_stream(main)
+            self.enc._plan, self.enc._plan_batch, self.enc._plan_stream = plan, batch, side
+
+        u, v = self(batch, after_embed=launch_untouched if split else None)
         loss = self.loss_fn(labels, u, v)
         (loss * dp.loss_scale() if dp is not None else loss).backward()
         sg = self.enc.grad
         if dp is not None:
             dp.allreduce_dense(list(self.user_tower.parameters()) + list(self.ad_tower.parameters()))
             sg = dp.allgather_sparse(sg, self.enc.table_rows)
-        self.sparse_opt.apply(sg)
+        if split:
+            self.sparse_opt.apply_touched(sg)
+        else:
+            self.sparse_opt.apply(sg)
         self.dense_opt.step()
         if dp is not None:  # BN moving statistics: ON_READ / MEAN across replicas (MirroredStrategy)
             dp.sync_buffers([self.user_tower, self.ad_tower])

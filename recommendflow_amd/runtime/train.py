@@ -27,7 +27,17 @@ class _EmbedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         (out,) = ctx.saved_tensors
-        ctx.enc.grad = ctx.enc.backward(ctx.batch, dout.float().contiguous(), out=out)
+        enc = ctx.enc
+        plan = getattr(enc, "_plan", None)
+        if plan is not None and getattr(enc, "_plan_batch", None) is ctx.batch:
+            # the batch-only half already ran (possibly on a side stream): join it, reduce dout on this stream
+            side = getattr(enc, "_plan_stream", None)
+            if side is not None:
+                torch.cuda.current_stream().wait_stream(side)
+            enc.grad = enc.backward_reduce(plan, dout.float().contiguous(), out=out)
+            enc._plan = enc._plan_batch = enc._plan_stream = None
+        else:
+            enc.grad = enc.backward(ctx.batch, dout.float().contiguous(), out=out)
         return None, None, None
 
 

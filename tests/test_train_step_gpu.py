@@ -80,3 +80,41 @@ def test_data_parallel_world1_matches_single(cuda):
             assert torch.equal(a, b)
     finally:
         dist.destroy_process_group()
+
+
+def test_backward_plan_reduce_equals_backward(cuda):
+    """rf_fused_hash_embed_bwd_plan + _reduce (the halves the train step splits across streams) give the
+    one-call backward's rows and gradient bit for bit."""
+    S = 12
+    specs = [SlotSpec(f"f{s}", 700, (2022, 2023), ["sum", "avg", "max"][s % 3]) for s in range(S)]
+    enc = FusedSparseEncoder(specs, 16, seed=6)
+    b = synthetic_batch(200, [s % 3 == 0 for s in range(S)], seed=12, id_max=500).to("cuda")
+    out = enc(b)
+    dout = torch.randn(out.shape, generator=torch.Generator().manual_seed(2)).cuda()
+    g1 = enc.backward(b, dout, out=out)
+    plan = enc.backward_plan(b)
+    g2 = enc.backward_reduce(plan, dout, out=out)
+    n = g1.count()
+    assert g2.count() == n
+    assert torch.equal(g1.rows[:n], g2.rows[:n])
+    assert torch.equal(g1.grad[:n], g2.grad[:n])
+
+
+def test_overlapped_table_adam_equals_dense(cuda):
+    """TrainableDssm.step with the table's dense Adam split (untouched rows on a side stream during the towers,
+    the gradient's rows after the backward) against the one-launch dense Adam: three steps, bit-identical
+    tables, Adam moments and towers."""
+    S = 16
+    hb = synthetic_batch(128, [s % 4 == 0 for s in range(S)], seed=21, id_max=400).to("cuda")
+    y = (torch.arange(128, device="cuda") % 2).float()
+    models = [_model()[0] for _ in range(2)]
+    models[1].overlap_table_adam = False
+    for _ in range(3):
+        for m in models:
+            m.step(hb, y)
+    torch.cuda.synchronize()
+    a, b = models
+    assert torch.equal(a.enc.table, b.enc.table)
+    assert torch.equal(a.sparse_opt.m, b.sparse_opt.m) and torch.equal(a.sparse_opt.v, b.sparse_opt.v)
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)

@@ -1,0 +1,40 @@
+"""The bench's cfg2 DSSM train-step leg alone (diagnostics): prints its JSON object."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from recommendflow_amd.backend.encoder.sparse_encoder import SlotSpec  # noqa: E402
+from recommendflow_amd.config_parser.configuration import Configuration  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--table-rows", type=int, default=10_000_000)
+    a = ap.parse_args()
+    conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "base_recall_sdpa.yaml"))
+    feats = conf.features.hashing_features
+    n_bins = a.table_rows // (2 * len(feats))
+    specs = [SlotSpec(f.name, n_bins, tuple(f.hash_seeds), f.pooling.value) for f in feats]
+    multi = [bool(f.multivalued) for f in feats]
+    from recommendflow_amd.models.matching.dssm import TrainableDssm
+
+    TrainableDssm.overlap_table_adam = os.environ.get("RF_TRAIN_OVERLAP", "1") != "0"
+    r = bench.bench_train(a, specs, multi)
+    r["overlap_table_adam"] = TrainableDssm.overlap_table_adam
+    r["side_grid"] = os.environ.get("RF_ADAM_SIDE_GRID", "512")
+    print(json.dumps(r))
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
