@@ -7,8 +7,8 @@
 // batch_neg_sample_scaled_multi_class_ce_loss (match_losses.py:150-165, Que2Search):
 //   loss = mean_i( -log(exp(s P_ii) / sum_j exp(s P_ij)) * y_i ),  P = query . doc^T (a library GEMM)
 //   dloss/dP_ij = s * y_i / B * (softmax_j(s P_i.) - [i == j])
-// Deterministic: fixed-order block reductions, no atomics. cosent: (i block, j chunk) tiles of 256 x 256 pairs,
-// the j scores and labels staged through LDS; the tile partials are summed in tile order.
+// Deterministic: fixed-order block reductions, no atomics. cosent: (i block, j chunk) tiles of 256 x 64 pairs,
+// the j scores and labels staged through LDS; the tile partials are summed in tile order, then row blocks in order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,23 +30,27 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// The B x B pairs run as (i block, j chunk) tiles: grid (ceil(B / 256), ceil(B / 256)), a thread per i walking
-// its tile's 256 j through LDS, so a 4096 batch fills 256 workgroups (a thread per i over every j kept 16 busy).
+// The B x B pairs run as (i block, j chunk) tiles: grid (ceil(B / 256), ceil(B / 64)), a thread per i walking its
+// tile's 64 j through LDS, so a 4096 batch fills 1,024 workgroups (a thread per i over every j kept 16 busy).
+constexpr int kCols = 64;  // j per tile
+
 // pass A: per-tile max of the valid x_ij
 __global__ __launch_bounds__(kRows) void cosent_max_kernel(const float* __restrict__ s, const float* __restrict__ y,
                                                            int B, float scale, float* __restrict__ part) {
-    __shared__ float sj[kRows], yj[kRows];
+    __shared__ float sj[kCols], yj[kCols];
     __shared__ float red[kRows / 64];
     const int i = blockIdx.x * kRows + threadIdx.x;
     const float si = i < B ? s[i] : 0.f, yi = i < B ? y[i] : 0.f;
-    const int j0 = blockIdx.y * kRows;
-    const int j = j0 + threadIdx.x;
-    sj[threadIdx.x] = j < B ? s[j] : 0.f;
-    yj[threadIdx.x] = j < B ? y[j] : -INFINITY;
+    const int j0 = blockIdx.y * kCols;
+    if (threadIdx.x < kCols) {
+        const int j = j0 + threadIdx.x;
+        sj[threadIdx.x] = j < B ? s[j] : 0.f;
+        yj[threadIdx.x] = j < B ? y[j] : -INFINITY;
+    }
     __syncthreads();
     float m = -INFINITY;
     if (i < B) {
-        const int n = min(kRows, B - j0);
+        const int n = min(kCols, B - j0);
         for (int k = 0; k < n; ++k)
             if (yi < yj[k]) m = fmaxf(m, scale * si - scale * sj[k]);
     }
@@ -60,23 +64,31 @@ __global__ __launch_bounds__(kRows) void cosent_max_kernel(const float* __restri
     }
 }
 
-// pass B: per-tile partials of R_i and C_i with the global m (m = max(0, every tile maximum))
+// m = max(0, every tile maximum): a wave-parallel max over the tile maxima (max is order-free)
+__device__ __forceinline__ float cosent_m(const float* __restrict__ part, int nparts) {
+    float m = 0.f;
+    for (int p = threadIdx.x & 63; p < nparts; p += 64) m = fmaxf(m, part[p]);
+    return wave_max(m);
+}
+
+// pass B: per-tile partials of R_i and C_i with the global m
 __global__ __launch_bounds__(kRows) void cosent_sums_kernel(const float* __restrict__ s, const float* __restrict__ y,
                                                             int B, float scale, const float* __restrict__ part, int nparts,
                                                             float* __restrict__ Rp, float* __restrict__ Cp) {
-    __shared__ float sj[kRows], yj[kRows];
-    float m = 0.f;
-    for (int p = 0; p < nparts; ++p) m = fmaxf(m, part[p]);
+    __shared__ float sj[kCols], yj[kCols];
+    const float m = cosent_m(part, nparts);
     const int i = blockIdx.x * kRows + threadIdx.x;
     const float si = i < B ? s[i] : 0.f, yi = i < B ? y[i] : 0.f;
-    const int j0 = blockIdx.y * kRows;
-    const int j = j0 + threadIdx.x;
-    sj[threadIdx.x] = j < B ? s[j] : 0.f;
-    yj[threadIdx.x] = j < B ? y[j] : 0.f;
+    const int j0 = blockIdx.y * kCols;
+    if (threadIdx.x < kCols) {
+        const int j = j0 + threadIdx.x;
+        sj[threadIdx.x] = j < B ? s[j] : 0.f;
+        yj[threadIdx.x] = j < B ? y[j] : 0.f;
+    }
     __syncthreads();
     if (i >= B) return;
     float r = 0.f, c = 0.f;
-    const int n = min(kRows, B - j0);
+    const int n = min(kCols, B - j0);
     for (int k = 0; k < n; ++k) {
         if (yi < yj[k]) r += expf(scale * si - scale * sj[k] - m);
         if (yj[k] < yi) c += expf(scale * sj[k] - scale * si - m);
@@ -85,34 +97,40 @@ __global__ __launch_bounds__(kRows) void cosent_sums_kernel(const float* __restr
     Cp[(int64_t)blockIdx.y * B + i] = c;
 }
 
-// pass C (one block): R_i, C_i = the tile partials summed in tile order; Z, loss, gradient
-__global__ __launch_bounds__(1024) void cosent_final_kernel(const float* __restrict__ Rp, const float* __restrict__ Cp, int B,
-                                                            int nj, float scale, const float* __restrict__ part, int nparts,
-                                                            float* __restrict__ loss, float* __restrict__ ds) {
-    __shared__ float red[16];
-    __shared__ float s_z;
-    float m = 0.f;
-    for (int p = 0; p < nparts; ++p) m = fmaxf(m, part[p]);
-    auto rsum = [&](const float* P, int i) {
-        float a = 0.f;
-        for (int t = 0; t < nj; ++t) a += P[(int64_t)t * B + i];
-        return a;
-    };
-    float acc = 0.f;
-    for (int i = threadIdx.x; i < B; i += 1024) acc += rsum(Rp, i);
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+// pass C: R_i, C_i = the tile partials summed in tile order; D_i = R_i - C_i and the block's sum of R_i
+__global__ __launch_bounds__(kRows) void cosent_rows_kernel(const float* __restrict__ Rp, const float* __restrict__ Cp, int B,
+                                                            int nj, float* __restrict__ D, float* __restrict__ rpart) {
+    __shared__ float red[kRows / 64];
+    const int i = blockIdx.x * kRows + threadIdx.x;
+    float r = 0.f, c = 0.f;
+    if (i < B)
+        for (int t = 0; t < nj; ++t) {
+            r += Rp[(int64_t)t * B + i];
+            c += Cp[(int64_t)t * B + i];
+        }
+    if (i < B) D[i] = r - c;
+    r = wave_sum(r);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = r;
     __syncthreads();
+    if (threadIdx.x == 0) rpart[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// pass D (one block): Z = e^-m + the row blocks' sums in block order, the loss, ds_i = scale D_i / Z
+__global__ __launch_bounds__(1024) void cosent_final_kernel(const float* __restrict__ D, const float* __restrict__ rpart,
+                                                            int B, int ni, float scale, const float* __restrict__ part,
+                                                            int nparts, float* __restrict__ loss, float* __restrict__ ds) {
+    __shared__ float s_z;
+    const float m = cosent_m(part, nparts);
     if (threadIdx.x == 0) {
         float z = expf(-m);
-        for (int w = 0; w < 16; ++w) z += red[w];
+        for (int b = 0; b < ni; ++b) z += rpart[b];
         s_z = z;
         *loss = m + logf(z);
     }
     __syncthreads();
     const float z = s_z;
     if (ds)
-        for (int i = threadIdx.x; i < B; i += 1024) ds[i] = scale * (rsum(Rp, i) - rsum(Cp, i)) / z;
+        for (int i = threadIdx.x; i < B; i += 1024) ds[i] = scale * D[i] / z;
 }
 
 // in-batch CE: one block per row i (256 threads), logits row of length B
@@ -162,10 +180,11 @@ size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
+// tile maxima (ni x nj) | Rp, Cp (nj x B each) | D (B) | row-block sums (ni); also the in-batch CE's row losses
 extern "C" size_t rf_loss_ws_bytes(int32_t batch) {
     if (batch < 0) return 0;
-    const size_t nb = (size_t)(batch + kRows - 1) / kRows + 1;
-    return a256(nb * nb * 4) + 2 * a256(nb * (size_t)std::max(batch, 1) * 4);
+    const size_t B = (size_t)std::max(batch, 1), ni = (B + kRows - 1) / kRows, nj = (B + kCols - 1) / kCols;
+    return a256(ni * nj * 4) + 2 * a256(nj * B * 4) + a256(B * 4) + a256(ni * 4);
 }
 
 extern "C" int rf_cosent_loss(const float* score, const float* label, int32_t batch, float scale, float* loss, float* dscore,
@@ -174,15 +193,23 @@ extern "C" int rf_cosent_loss(const float* score, const float* label, int32_t ba
     RF_REQUIRE(score && label && loss && ws, "rf_cosent_loss: null pointer");
     RF_REQUIRE(ws_bytes >= rf_loss_ws_bytes(batch), "rf_cosent_loss: workspace too small");
     hipStream_t st = rf_stream(stream);
-    const int nb = (batch + kRows - 1) / kRows;
+    const size_t B = (size_t)batch;
+    const int ni = (batch + kRows - 1) / kRows, nj = (batch + kCols - 1) / kCols;
     char* w = static_cast<char*>(ws);
     float* part = reinterpret_cast<float*>(w);
-    float* Rp = reinterpret_cast<float*>(w + a256((size_t)(nb + 1) * (nb + 1) * 4));
-    float* Cp = Rp + a256((size_t)(nb + 1) * batch * 4) / 4;
-    const dim3 g(nb, nb);
+    w += a256((size_t)ni * nj * 4);
+    float* Rp = reinterpret_cast<float*>(w);
+    w += a256((size_t)nj * B * 4);
+    float* Cp = reinterpret_cast<float*>(w);
+    w += a256((size_t)nj * B * 4);
+    float* D = reinterpret_cast<float*>(w);
+    w += a256(B * 4);
+    float* rpart = reinterpret_cast<float*>(w);
+    const dim3 g(ni, nj);
     hipLaunchKernelGGL(cosent_max_kernel, g, dim3(kRows), 0, st, score, label, batch, scale, part);
-    hipLaunchKernelGGL(cosent_sums_kernel, g, dim3(kRows), 0, st, score, label, batch, scale, part, nb * nb, Rp, Cp);
-    hipLaunchKernelGGL(cosent_final_kernel, dim3(1), dim3(1024), 0, st, Rp, Cp, batch, nb, scale, part, nb * nb, loss, dscore);
+    hipLaunchKernelGGL(cosent_sums_kernel, g, dim3(kRows), 0, st, score, label, batch, scale, part, ni * nj, Rp, Cp);
+    hipLaunchKernelGGL(cosent_rows_kernel, dim3(ni), dim3(kRows), 0, st, Rp, Cp, batch, nj, D, rpart);
+    hipLaunchKernelGGL(cosent_final_kernel, dim3(1), dim3(1024), 0, st, D, rpart, batch, ni, scale, part, ni * nj, loss, dscore);
     return rf_check_launch("rf_cosent_loss");
 }
 

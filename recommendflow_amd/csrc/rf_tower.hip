@@ -8,12 +8,17 @@
 // SELU + dropout gradient with the bias gradient's column sums, the folded weight gradient dW = G diag(a) + db c^T
 // from G = dpre^T x, and the BatchNormalization backward (column sums of dz and dz * xhat, then dx).
 //
-// Column reductions are deterministic: a thread per column walks a fixed chunk of rows (coalesced: consecutive
-// threads, consecutive columns), chunk partials land in a workspace, and a finish kernel combines them in chunk
-// order. Statistics use a per-chunk pivot (the chunk's first value) and Chan's combine across chunks.
+// Column reductions are deterministic: a thread per 4 columns (one float4; 1 when a row is not 16-byte aligned)
+// walks a fixed chunk of rows with 4-8 rows' loads in flight (coalesced: consecutive threads, consecutive
+// columns), chunk partials land in a workspace, and a finish kernel combines them in chunk order. The chunk
+// count depends only on (M, K) and is sized for ~4K workgroups: at cfg2's 4096 x 256 that is 512 chunks of 8
+// rows where a fixed 128-row chunk left 32 workgroups on 256 CUs. Statistics use a per-chunk pivot (the chunk's
+// first value) and Chan's combine across chunks.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
+#include <utility>
 #include <cmath>
 
 #include "rf_common.h"
@@ -21,9 +26,38 @@
 namespace {
 
 constexpr int kColThreads = 256;
-constexpr int kRowsPerChunk = 128;
+constexpr int kUnroll = 8;  // rows loaded ahead of the in-order accumulation
 
-__host__ __device__ inline int tower_chunks(int64_t M) { return (int)std::min<int64_t>(64, (M + kRowsPerChunk - 1) / kRowsPerChunk); }
+// Row chunks of a column reduction: enough chunks that the float4 launch has ~4K workgroups (a thread per 4
+// columns walks its chunk's rows in order), at least 8 rows a chunk, at most 512 chunks. Depends only on
+// (M, K), so a reduction is replay-deterministic whichever vector width runs it.
+__host__ inline int tower_chunks(int64_t M, int K) {
+    const int64_t colblocks = std::max<int64_t>(1, ((int64_t)K + 4 * kColThreads - 1) / (4 * kColThreads));
+    const int64_t want = (4096 + colblocks - 1) / colblocks;
+    const int64_t cap = std::min<int64_t>(512, std::max<int64_t>(1, (M + 7) / 8));
+    return (int)std::max<int64_t>(1, std::min(want, cap));
+}
+
+// columns a thread owns: 4 (one float4) when every operand's rows are 16-byte aligned, else 1
+__host__ inline bool vec4_ok(int K, std::initializer_list<std::pair<const void*, int64_t>> ops) {
+    if (K % 4) return false;
+    for (auto& o : ops)
+        if (((uintptr_t)o.first & 15) || (o.second % 4)) return false;
+    return true;
+}
+
+template <int V> struct vec_t;
+template <> struct vec_t<1> { using T = float; };
+template <> struct vec_t<4> { using T = float4; };
+template <int V> __device__ __forceinline__ float& lane(typename vec_t<V>::T& v, int i);
+template <> __device__ __forceinline__ float& lane<1>(float& v, int) { return v; }
+template <> __device__ __forceinline__ float& lane<4>(float4& v, int i) { return (&v.x)[i]; }
+template <int V> __device__ __forceinline__ typename vec_t<V>::T ld(const float* p) {
+    return *reinterpret_cast<const typename vec_t<V>::T*>(p);
+}
+template <int V> __device__ __forceinline__ void st(float* p, const typename vec_t<V>::T& v) {
+    *reinterpret_cast<typename vec_t<V>::T*>(p) = v;
+}
 
 // keep mask of Keras Dropout(rate) in training: u = top 24 bits of splitmix64(seed ^ (row * N + col)) / 2^24,
 // kept when u >= rate (oracle.dropout_keep restates it)
@@ -37,55 +71,164 @@ __device__ __forceinline__ float bn_scale(const float* gamma, const float* var, 
 }
 
 // ---- column statistics -----------------------------------------------------------------------------------
-// chunk partials: (n, mean, M2) around the chunk's first value (pivot p: S = sum(x - p), Q = sum((x - p)^2),
+// chunk partials: (mean, M2) around the chunk's first value (pivot p: S = sum(x - p), Q = sum((x - p)^2),
 // mean = p + S / n, M2 = Q - S^2 / n)
+template <int V>
 __global__ __launch_bounds__(kColThreads) void col_stats_partial_kernel(const float* __restrict__ x, int64_t M, int K,
                                                                         int64_t ldx, int rows_per, float* __restrict__ part) {
-    const int k = blockIdx.x * kColThreads + threadIdx.x;
-    if (k >= K) return;
+    const int k0 = (blockIdx.x * kColThreads + threadIdx.x) * V;
+    if (k0 >= K) return;
     const int64_t r0 = (int64_t)blockIdx.y * rows_per;
     const int64_t r1 = std::min<int64_t>(M, r0 + rows_per);
-    float mean = 0.f, m2 = 0.f;
+    float mean[V], m2[V];
+    for (int i = 0; i < V; ++i) mean[i] = m2[i] = 0.f;
     if (r0 < r1) {
-        const float p = x[r0 * ldx + k];
-        float s = 0.f, q = 0.f;
-        for (int64_t r = r0; r < r1; ++r) {
-            const float d = x[r * ldx + k] - p;
-            s += d;
-            q = fmaf(d, d, q);
+        typename vec_t<V>::T p = ld<V>(x + r0 * ldx + k0);
+        float s[V], q[V];
+        for (int i = 0; i < V; ++i) s[i] = q[i] = 0.f;
+        int64_t r = r0;
+        for (; r + kUnroll <= r1; r += kUnroll) {
+            typename vec_t<V>::T v[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) v[u] = ld<V>(x + (r + u) * ldx + k0);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    const float d = lane<V>(v[u], i) - lane<V>(p, i);
+                    s[i] += d;
+                    q[i] = fmaf(d, d, q[i]);
+                }
+        }
+        for (; r < r1; ++r) {
+            typename vec_t<V>::T v = ld<V>(x + r * ldx + k0);
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const float d = lane<V>(v, i) - lane<V>(p, i);
+                s[i] += d;
+                q[i] = fmaf(d, d, q[i]);
+            }
         }
         const float n = (float)(r1 - r0);
-        mean = p + s / n;
-        m2 = fmaxf(q - s * s / n, 0.f);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            mean[i] = lane<V>(p, i) + s[i] / n;
+            m2[i] = fmaxf(q[i] - s[i] * s[i] / n, 0.f);
+        }
     }
-    float* o = part + ((int64_t)blockIdx.y * K + k) * 2;
-    o[0] = mean;
-    o[1] = m2;
+    // layout [chunk][2][K]: the finish kernel reads both planes coalesced
+    float* o = part + (int64_t)blockIdx.y * 2 * K + k0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        o[i] = mean[i];
+        o[K + i] = m2[i];
+    }
 }
 
-__global__ __launch_bounds__(kColThreads) void col_stats_finish_kernel(const float* __restrict__ part, int64_t M, int K,
-                                                                       int chunks, int rows_per, float* __restrict__ mean,
-                                                                       float* __restrict__ var) {
-    const int k = blockIdx.x * kColThreads + threadIdx.x;
-    if (k >= K) return;
+// ---- chunk-partial finish ---------------------------------------------------------------------------------
+// A workgroup per 32 columns: 8 groups of 32 lanes each combine a contiguous run of chunks (8 loads in flight per
+// lane), then group 0 combines the 8 group results in group order. A fixed tree, so replay-deterministic; a
+// thread walking all (up to 512) chunks alone was latency-bound at 120-230 us a launch.
+constexpr int kFinCols = 32, kFinGroups = 8;
+
+// sums of P planes: part[c][p][K] (P = 1 or 2)
+template <int P>
+__device__ __forceinline__ void finish_sums(const float* __restrict__ part, int K, int chunks, float (&out)[P]) {
+    __shared__ float red[kFinGroups][P][kFinCols];
+    const int cl = threadIdx.x % kFinCols, grp = threadIdx.x / kFinCols;
+    const int k = blockIdx.x * kFinCols + cl;
+    const int per = (chunks + kFinGroups - 1) / kFinGroups, c0 = grp * per, c1 = std::min(chunks, c0 + per);
+    float acc[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc[p] = 0.f;
+    if (k < K) {
+        int c = c0;
+        for (; c + 8 <= c1; c += 8) {
+            float v[8][P];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int p = 0; p < P; ++p) v[u][p] = part[((int64_t)(c + u) * P + p) * K + k];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int p = 0; p < P; ++p) acc[p] += v[u][p];
+        }
+        for (; c < c1; ++c)
+#pragma unroll
+            for (int p = 0; p < P; ++p) acc[p] += part[((int64_t)c * P + p) * K + k];
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) red[grp][p][cl] = acc[p];
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        float t = 0.f;
+        for (int g = 0; g < kFinGroups; ++g) t += red[g][p][cl];
+        out[p] = t;
+    }
+}
+
+__global__ __launch_bounds__(kFinCols * kFinGroups) void col_stats_finish_kernel(const float* __restrict__ part, int64_t M, int K,
+                                                                                 int chunks, int rows_per, float* __restrict__ mean,
+                                                                                 float* __restrict__ var) {
+    __shared__ float red[kFinGroups][3][kFinCols];
+    const int cl = threadIdx.x % kFinCols, grp = threadIdx.x / kFinCols;
+    const int k = blockIdx.x * kFinCols + cl;
+    const int per = (chunks + kFinGroups - 1) / kFinGroups, c0 = grp * per, c1 = std::min(chunks, c0 + per);
     float n = 0.f, mu = 0.f, m2 = 0.f;
-    for (int c = 0; c < chunks; ++c) {
-        const int64_t r0 = (int64_t)c * rows_per;
-        const float nb = (float)std::max<int64_t>(0, std::min<int64_t>(M, r0 + rows_per) - r0);
-        if (nb <= 0.f) continue;
-        const float mb = part[((int64_t)c * K + k) * 2], m2b = part[((int64_t)c * K + k) * 2 + 1];
+    auto combine = [&](float nb, float mb, float m2b) {
+        if (nb <= 0.f) return;
         const float nn = n + nb, d = mb - mu;
         mu += d * (nb / nn);
         m2 += m2b + d * d * (n * nb / nn);
         n = nn;
+    };
+    auto rows = [&](int c) {
+        const int64_t r0 = (int64_t)c * rows_per;
+        return (float)std::max<int64_t>(0, std::min<int64_t>(M, r0 + rows_per) - r0);
+    };
+    if (k < K) {
+        int c = c0;
+        for (; c + 8 <= c1; c += 8) {
+            float mb[8], m2b[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                mb[u] = part[(int64_t)(c + u) * 2 * K + k];
+                m2b[u] = part[(int64_t)(c + u) * 2 * K + K + k];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) combine(rows(c + u), mb[u], m2b[u]);
+        }
+        for (; c < c1; ++c) combine(rows(c), part[(int64_t)c * 2 * K + k], part[(int64_t)c * 2 * K + K + k]);
     }
+    red[grp][0][cl] = n;
+    red[grp][1][cl] = mu;
+    red[grp][2][cl] = m2;
+    __syncthreads();
+    if (grp != 0 || k >= K) return;
+    n = mu = m2 = 0.f;
+    for (int g = 0; g < kFinGroups; ++g) combine(red[g][0][cl], red[g][1][cl], red[g][2][cl]);
     mean[k] = mu;
     var[k] = m2 / (float)M;
 }
 
 // ---- BatchNormalization folded into the Dense that follows it ----------------------------------------------
+// the fold's per-column affine a_k = gamma_k rstd_k, c_k = beta_k - mean_k a_k for columns k .. k + V
+template <int V>
+__device__ __forceinline__ void bn_affine(const float* gamma, const float* beta, const float* mean, const float* var, float eps,
+                                          int k, typename vec_t<V>::T& a, typename vec_t<V>::T& c) {
+    typename vec_t<V>::T g = ld<V>(gamma + k), be = ld<V>(beta + k), mu = ld<V>(mean + k), vr = ld<V>(var + k);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        lane<V>(a, i) = lane<V>(g, i) * (1.0f / sqrtf(lane<V>(vr, i) + eps));
+        lane<V>(c, i) = lane<V>(be, i) - lane<V>(mu, i) * lane<V>(a, i);
+    }
+}
+
 // one workgroup per output row n: W'[n][k] = W[n][k] a_k; b'[n] = b[n] + sum_k W[n][k] c_k (fixed order: each
 // thread its strided subset, then a fixed tree)
+template <int V>
 __global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ W, int K, const float* __restrict__ b,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       const float* __restrict__ mean, const float* __restrict__ var,
@@ -95,12 +238,15 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ 
     const float* w = W + n * K;
     float* wo = Wo + n * K;
     float acc = 0.f;
-    for (int k = threadIdx.x; k < K; k += 256) {
-        const float a = bn_scale(gamma, var, eps, k);
-        const float c = beta[k] - mean[k] * a;
-        const float v = w[k];
-        wo[k] = v * a;
-        acc = fmaf(v, c, acc);
+    for (int k = threadIdx.x * V; k < K; k += 256 * V) {
+        typename vec_t<V>::T v = ld<V>(w + k), a, c, o;
+        bn_affine<V>(gamma, beta, mean, var, eps, k, a, c);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            lane<V>(o, i) = lane<V>(v, i) * lane<V>(a, i);
+            acc = fmaf(lane<V>(v, i), lane<V>(c, i), acc);
+        }
+        st<V>(wo + k, o);
     }
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -112,149 +258,223 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(const float* __restrict__ 
 }
 
 // dW[n][k] = G[n][k] a_k + db[n] c_k  (grid: x = column blocks, y = rows)
+template <int V>
 __global__ __launch_bounds__(256) void bn_fold_grad_kernel(const float* __restrict__ G, int N, int K, const float* __restrict__ db,
                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
                                                            const float* __restrict__ mean, const float* __restrict__ var,
                                                            float eps, float* __restrict__ dW) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int k = (blockIdx.x * 256 + threadIdx.x) * V;
     if (k >= K) return;
     const int64_t e = (int64_t)blockIdx.y * K + k;
-    const float a = bn_scale(gamma, var, eps, k);
-    const float c = beta[k] - mean[k] * a;
-    dW[e] = fmaf(G[e], a, db[blockIdx.y] * c);
+    typename vec_t<V>::T g = ld<V>(G + e), a, c, o;
+    bn_affine<V>(gamma, beta, mean, var, eps, k, a, c);
+    const float d = db[blockIdx.y];
+#pragma unroll
+    for (int i = 0; i < V; ++i) lane<V>(o, i) = fmaf(lane<V>(g, i), lane<V>(a, i), d * lane<V>(c, i));
+    st<V>(dW + e, o);
 }
 
 // ---- dropout ------------------------------------------------------------------------------------------------
+template <int V>
 __global__ __launch_bounds__(256) void dropout_fwd_kernel(const float* __restrict__ x, int64_t M, int N, int64_t ldx,
-                                                          float rate, uint64_t seed, float* __restrict__ y, int64_t ldy) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
+                                                          float rate, uint64_t seed, float* y, int64_t ldy) {
+    const int c = (blockIdx.x * 256 + threadIdx.x) * V;
     if (c >= N) return;
     const int64_t r = blockIdx.y;
-    const float v = x[r * ldx + c];
-    y[r * ldy + c] = keep_elem(seed, r, N, c, rate) ? v * (1.0f / (1.0f - rate)) : 0.f;
+    typename vec_t<V>::T v = ld<V>(x + r * ldx + c);
+    const float s = 1.0f / (1.0f - rate);
+#pragma unroll
+    for (int i = 0; i < V; ++i) lane<V>(v, i) = keep_elem(seed, r, N, c + i, rate) ? lane<V>(v, i) * s : 0.f;
+    st<V>(y + r * ldy + c, v);
 }
 
 // ---- SELU + dropout backward, bias-gradient column partials ----------------------------------------------
 // h = dropout(selu(pre)): for a kept element y = selu(pre) = h (1 - rate), and the gradient factor is TF's SeluGrad
 // on the activations: y + scale alpha where y < 0, scale elsewhere; dropped elements get dpre = 0
+template <int V>
 __global__ __launch_bounds__(kColThreads) void selu_dropout_bwd_kernel(const float* __restrict__ dh, int64_t lddh,
                                                                        const float* __restrict__ h, int64_t ldh, int64_t M,
                                                                        int N, float rate, uint64_t seed, int rows_per,
                                                                        float* __restrict__ dpre, int64_t ldd,
                                                                        float* __restrict__ part) {
     constexpr float kScale = 1.0507009873554804934193349852946f, kAlpha = 1.6732632423543772848170429916717f;
-    const int c = blockIdx.x * kColThreads + threadIdx.x;
+    const int c = (blockIdx.x * kColThreads + threadIdx.x) * V;
     if (c >= N) return;
     const float s = 1.0f / (1.0f - rate), keepv = 1.0f - rate;
     const int64_t r0 = (int64_t)blockIdx.y * rows_per;
     const int64_t r1 = std::min<int64_t>(M, r0 + rows_per);
-    float acc = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        float g = 0.f;
-        if (keep_elem(seed, r, N, c, rate)) {
-            const float y = h[r * ldh + c] * keepv;
-            const float d = y < 0.f ? y + kScale * kAlpha : kScale;
-            g = dh[r * lddh + c] * s * d;
+    float acc[V];
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+    constexpr int U = kUnroll / 2;
+    int64_t r = r0;
+    auto row = [&](int64_t rr, typename vec_t<V>::T g, typename vec_t<V>::T hv) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            float o = 0.f;
+            if (keep_elem(seed, rr, N, c + i, rate)) {
+                const float y = lane<V>(hv, i) * keepv;
+                o = lane<V>(g, i) * s * (y < 0.f ? y + kScale * kAlpha : kScale);
+            }
+            lane<V>(g, i) = o;
+            acc[i] += o;
         }
-        dpre[r * ldd + c] = g;
-        acc += g;
+        st<V>(dpre + rr * ldd + c, g);
+    };
+    for (; r + U <= r1; r += U) {
+        typename vec_t<V>::T g[U], hv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            g[u] = ld<V>(dh + (r + u) * lddh + c);
+            hv[u] = ld<V>(h + (r + u) * ldh + c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) row(r + u, g[u], hv[u]);
     }
-    part[(int64_t)blockIdx.y * N + c] = acc;
+    for (; r < r1; ++r) row(r, ld<V>(dh + r * lddh + c), ld<V>(h + r * ldh + c));
+    float* o = part + (int64_t)blockIdx.y * N + c;
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = acc[i];
 }
 
-__global__ __launch_bounds__(kColThreads) void col_sum_finish_kernel(const float* __restrict__ part, int N, int chunks,
-                                                                     float* __restrict__ out) {
-    const int c = blockIdx.x * kColThreads + threadIdx.x;
-    if (c >= N) return;
-    float acc = 0.f;
-    for (int i = 0; i < chunks; ++i) acc += part[(int64_t)i * N + c];
-    out[c] = acc;
+__global__ __launch_bounds__(kFinCols * kFinGroups) void col_sum_finish_kernel(const float* __restrict__ part, int N, int chunks,
+                                                                               float* __restrict__ out) {
+    float t[1];
+    finish_sums<1>(part, N, chunks, t);
+    const int k = blockIdx.x * kFinCols + threadIdx.x;
+    if (threadIdx.x < kFinCols && k < N) out[k] = t[0];
 }
 
 // ---- BatchNormalization backward -------------------------------------------------------------------------
 // column partials of sum(dz) and sum(dz * xhat), xhat = (x - mean) rstd
+template <int V>
 __global__ __launch_bounds__(kColThreads) void bn_bwd_partial_kernel(const float* __restrict__ dz, int64_t lddz,
                                                                      const float* __restrict__ x, int64_t ldx, int64_t M, int K,
                                                                      const float* __restrict__ mean, const float* __restrict__ var,
                                                                      float eps, int rows_per, float* __restrict__ part) {
-    const int k = blockIdx.x * kColThreads + threadIdx.x;
-    if (k >= K) return;
-    const float mu = mean[k], rstd = 1.0f / sqrtf(var[k] + eps);
+    const int k0 = (blockIdx.x * kColThreads + threadIdx.x) * V;
+    if (k0 >= K) return;
+    float mu[V], rstd[V], s1[V], s2[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        mu[i] = mean[k0 + i];
+        rstd[i] = 1.0f / sqrtf(var[k0 + i] + eps);
+        s1[i] = s2[i] = 0.f;
+    }
     const int64_t r0 = (int64_t)blockIdx.y * rows_per;
     const int64_t r1 = std::min<int64_t>(M, r0 + rows_per);
-    float s1 = 0.f, s2 = 0.f;
-    for (int64_t r = r0; r < r1; ++r) {
-        const float g = dz[r * lddz + k];
-        s1 += g;
-        s2 = fmaf(g, (x[r * ldx + k] - mu) * rstd, s2);
+    constexpr int U = kUnroll / 2;
+    int64_t r = r0;
+    auto row = [&](typename vec_t<V>::T g, typename vec_t<V>::T xv) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            s1[i] += lane<V>(g, i);
+            s2[i] = fmaf(lane<V>(g, i), (lane<V>(xv, i) - mu[i]) * rstd[i], s2[i]);
+        }
+    };
+    for (; r + U <= r1; r += U) {
+        typename vec_t<V>::T g[U], xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            g[u] = ld<V>(dz + (r + u) * lddz + k0);
+            xv[u] = ld<V>(x + (r + u) * ldx + k0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) row(g[u], xv[u]);
     }
-    float* o = part + ((int64_t)blockIdx.y * K + k) * 2;
-    o[0] = s1;
-    o[1] = s2;
+    for (; r < r1; ++r) row(ld<V>(dz + r * lddz + k0), ld<V>(x + r * ldx + k0));
+    float* o = part + (int64_t)blockIdx.y * 2 * K + k0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        o[i] = s1[i];
+        o[K + i] = s2[i];
+    }
 }
 
-__global__ __launch_bounds__(kColThreads) void bn_bwd_finish_kernel(const float* __restrict__ part, int K, int chunks,
-                                                                    float* __restrict__ dbeta, float* __restrict__ dgamma) {
-    const int k = blockIdx.x * kColThreads + threadIdx.x;
-    if (k >= K) return;
-    float s1 = 0.f, s2 = 0.f;
-    for (int c = 0; c < chunks; ++c) {
-        s1 += part[((int64_t)c * K + k) * 2];
-        s2 += part[((int64_t)c * K + k) * 2 + 1];
-    }
-    dbeta[k] = s1;
-    dgamma[k] = s2;
+// dbeta, dgamma in chunk order; then the apply kernel's per-column constants: p_k = gamma_k rstd_k,
+// q_k = dbeta_k / M, t_k = dgamma_k / M (written after dbeta, dgamma into ac[0..3K))
+__global__ __launch_bounds__(kFinCols * kFinGroups) void bn_bwd_finish_kernel(const float* __restrict__ part, int64_t M, int K,
+                                                                              int chunks, const float* __restrict__ gamma,
+                                                                              const float* __restrict__ var, float eps,
+                                                                              float* __restrict__ dbeta, float* __restrict__ dgamma,
+                                                                              float* __restrict__ ac) {
+    float t[2];
+    finish_sums<2>(part, K, chunks, t);
+    const int k = blockIdx.x * kFinCols + threadIdx.x;
+    if (threadIdx.x >= kFinCols || k >= K) return;
+    dbeta[k] = t[0];
+    dgamma[k] = t[1];
+    const float invM = 1.0f / (float)M;
+    ac[k] = gamma[k] * (1.0f / sqrtf(var[k] + eps));
+    ac[K + k] = t[0] * invM;
+    ac[2 * K + k] = t[1] * invM;
 }
 
 // dx = gamma rstd (dz - dbeta / M - xhat dgamma / M)  (grid: x = column blocks, y = rows)
+template <int V>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dz, int64_t lddz, const float* __restrict__ x,
-                                                           int64_t ldx, int64_t M, int K, const float* __restrict__ mean,
-                                                           const float* __restrict__ var, const float* __restrict__ gamma,
-                                                           float eps, const float* __restrict__ dbeta,
-                                                           const float* __restrict__ dgamma, float* __restrict__ dx, int64_t lddx) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
+                                                           int64_t ldx, int K, const float* __restrict__ mean,
+                                                           const float* __restrict__ var, float eps,
+                                                           const float* __restrict__ ac, float* dx, int64_t lddx) {
+    const int k = (blockIdx.x * 256 + threadIdx.x) * V;
     if (k >= K) return;
     const int64_t r = blockIdx.y;
-    const float invM = 1.0f / (float)M;
-    const float rstd = 1.0f / sqrtf(var[k] + eps);
-    const float xh = (x[r * ldx + k] - mean[k]) * rstd;
-    const float g = dz[r * lddz + k] - dbeta[k] * invM - xh * dgamma[k] * invM;
-    dx[r * lddx + k] = gamma[k] * rstd * g;
+    typename vec_t<V>::T g = ld<V>(dz + r * lddz + k), xv = ld<V>(x + r * ldx + k), mu = ld<V>(mean + k), vr = ld<V>(var + k),
+                         p = ld<V>(ac + k), q = ld<V>(ac + K + k), t = ld<V>(ac + 2 * K + k), o;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const float xh = (lane<V>(xv, i) - lane<V>(mu, i)) * (1.0f / sqrtf(lane<V>(vr, i) + eps));
+        lane<V>(o, i) = lane<V>(p, i) * (lane<V>(g, i) - lane<V>(q, i) - xh * lane<V>(t, i));
+    }
+    st<V>(dx + r * lddx + k, o);
 }
-
 
 }  // namespace
 
+// chunk partials ([chunk][2][K] floats) + rf_bn_bwd's per-column constants (3 K floats)
 extern "C" size_t rf_tower_ws_bytes(int64_t M, int32_t K) {
-    return (size_t)tower_chunks(M) * (size_t)std::max(K, 1) * 2 * sizeof(float);
+    const size_t k = (size_t)std::max(K, 1);
+    return ((size_t)tower_chunks(std::max<int64_t>(M, 1), (int)k) * 2 + 3) * k * sizeof(float);
 }
+
+#define RF_TOWER_LAUNCH(kern, V, grid, ...)                                                    \
+    do {                                                                                       \
+        if (V == 4)                                                                            \
+            hipLaunchKernelGGL(kern<4>, grid(4), dim3(256), 0, st, __VA_ARGS__);               \
+        else                                                                                   \
+            hipLaunchKernelGGL(kern<1>, grid(1), dim3(256), 0, st, __VA_ARGS__);               \
+    } while (0)
 
 extern "C" int rf_col_stats(const float* x, int64_t M, int32_t K, int64_t ldx, float* mean, float* var, void* ws,
                             size_t ws_bytes, void* stream) {
     RF_REQUIRE(M > 0 && K > 0 && ldx >= K && x && mean && var, "rf_col_stats: bad arguments");
     RF_REQUIRE(ws && ws_bytes >= rf_tower_ws_bytes(M, K), "rf_col_stats: workspace too small");
-    const int chunks = tower_chunks(M), rows_per = (int)((M + chunks - 1) / chunks);
+    const int chunks = tower_chunks(M, K), rows_per = (int)((M + chunks - 1) / chunks);
     hipStream_t st = rf_stream(stream);
-    const dim3 g((K + kColThreads - 1) / kColThreads, chunks);
-    hipLaunchKernelGGL(col_stats_partial_kernel, g, dim3(kColThreads), 0, st, x, M, K, ldx, rows_per, (float*)ws);
-    hipLaunchKernelGGL(col_stats_finish_kernel, dim3(g.x), dim3(kColThreads), 0, st, (const float*)ws, M, K, chunks, rows_per,
-                       mean, var);
+    const int V = vec4_ok(K, {{x, ldx}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((K / v + kColThreads - 1) / kColThreads, chunks); };
+    RF_TOWER_LAUNCH(col_stats_partial_kernel, V, grid, x, M, K, ldx, rows_per, (float*)ws);
+    hipLaunchKernelGGL(col_stats_finish_kernel, dim3((K + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinGroups), 0, st,
+                       (const float*)ws, M, K, chunks, rows_per, mean, var);
     return rf_check_launch("rf_col_stats");
 }
 
 extern "C" int rf_bn_fold(const float* W, int32_t N, int32_t K, const float* b, const float* gamma, const float* beta,
                           const float* mean, const float* var, float eps, float* W_out, float* b_out, void* stream) {
     RF_REQUIRE(N > 0 && K > 0 && W && gamma && beta && mean && var && W_out && b_out, "rf_bn_fold: bad arguments");
-    hipLaunchKernelGGL(bn_fold_kernel, dim3(N), dim3(256), 0, rf_stream(stream), W, K, b, gamma, beta, mean, var, eps, W_out,
-                       b_out);
+    hipStream_t st = rf_stream(stream);
+    const int V = vec4_ok(K, {{W, K}, {W_out, K}, {gamma, 0}, {beta, 0}, {mean, 0}, {var, 0}}) ? 4 : 1;
+    auto grid = [&](int) { return dim3(N); };
+    RF_TOWER_LAUNCH(bn_fold_kernel, V, grid, W, K, b, gamma, beta, mean, var, eps, W_out, b_out);
     return rf_check_launch("rf_bn_fold");
 }
 
 extern "C" int rf_bn_fold_grad(const float* G, int32_t N, int32_t K, const float* db, const float* gamma, const float* beta,
                                const float* mean, const float* var, float eps, float* dW, void* stream) {
-    RF_REQUIRE(N > 0 && K > 0 && G && db && gamma && beta && mean && var && dW, "rf_bn_fold_grad: bad arguments");
-    hipLaunchKernelGGL(bn_fold_grad_kernel, dim3((K + 255) / 256, N), dim3(256), 0, rf_stream(stream), G, N, K, db, gamma, beta,
-                       mean, var, eps, dW);
+    RF_REQUIRE(N > 0 && N <= 65535 && K > 0 && G && db && gamma && beta && mean && var && dW, "rf_bn_fold_grad: bad arguments");
+    hipStream_t st = rf_stream(stream);
+    const int V = vec4_ok(K, {{G, K}, {dW, K}, {gamma, 0}, {beta, 0}, {mean, 0}, {var, 0}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((K / v + 255) / 256, N); };
+    RF_TOWER_LAUNCH(bn_fold_grad_kernel, V, grid, G, N, K, db, gamma, beta, mean, var, eps, dW);
     return rf_check_launch("rf_bn_fold_grad");
 }
 
@@ -264,8 +484,10 @@ extern "C" int rf_dropout_fwd(const float* x, int64_t M, int32_t N, int64_t ldx,
                "rf_dropout_fwd: bad arguments");
     if (M == 0) return RF_OK;
     RF_REQUIRE(x && y, "rf_dropout_fwd: null pointer");
-    hipLaunchKernelGGL(dropout_fwd_kernel, dim3((N + 255) / 256, (unsigned)M), dim3(256), 0, rf_stream(stream), x, M, N, ldx, rate,
-                       seed, y, ldy);
+    hipStream_t st = rf_stream(stream);
+    const int V = vec4_ok(N, {{x, ldx}, {y, ldy}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((N / v + 255) / 256, (unsigned)M); };
+    RF_TOWER_LAUNCH(dropout_fwd_kernel, V, grid, x, M, N, ldx, rate, seed, y, ldy);
     return rf_check_launch("rf_dropout_fwd");
 }
 
@@ -276,12 +498,13 @@ extern "C" int rf_selu_dropout_bwd(const float* dh, int64_t lddh, const float* h
                "rf_selu_dropout_bwd: bad arguments");
     RF_REQUIRE(dh && h && dpre && db, "rf_selu_dropout_bwd: null pointer");
     RF_REQUIRE(ws && ws_bytes >= rf_tower_ws_bytes(M, N), "rf_selu_dropout_bwd: workspace too small");
-    const int chunks = tower_chunks(M), rows_per = (int)((M + chunks - 1) / chunks);
+    const int chunks = tower_chunks(M, N), rows_per = (int)((M + chunks - 1) / chunks);
     hipStream_t st = rf_stream(stream);
-    const dim3 g((N + kColThreads - 1) / kColThreads, chunks);
-    hipLaunchKernelGGL(selu_dropout_bwd_kernel, g, dim3(kColThreads), 0, st, dh, lddh, h, ldh, M, N, rate, seed, rows_per, dpre,
-                       ldd, (float*)ws);
-    hipLaunchKernelGGL(col_sum_finish_kernel, dim3(g.x), dim3(kColThreads), 0, st, (const float*)ws, N, chunks, db);
+    const int V = vec4_ok(N, {{dh, lddh}, {h, ldh}, {dpre, ldd}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((N / v + kColThreads - 1) / kColThreads, chunks); };
+    RF_TOWER_LAUNCH(selu_dropout_bwd_kernel, V, grid, dh, lddh, h, ldh, M, N, rate, seed, rows_per, dpre, ldd, (float*)ws);
+    hipLaunchKernelGGL(col_sum_finish_kernel, dim3((N + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinGroups), 0, st,
+                       (const float*)ws, N, chunks, db);
     return rf_check_launch("rf_selu_dropout_bwd");
 }
 
@@ -291,13 +514,16 @@ extern "C" int rf_bn_bwd(const float* dz, int64_t lddz, const float* x, int64_t 
     RF_REQUIRE(M > 0 && M <= 65535 && K > 0 && lddz >= K && ldx >= K && lddx >= K, "rf_bn_bwd: bad arguments");
     RF_REQUIRE(dz && x && mean && var && gamma && dx && dgamma && dbeta, "rf_bn_bwd: null pointer");
     RF_REQUIRE(ws && ws_bytes >= rf_tower_ws_bytes(M, K), "rf_bn_bwd: workspace too small");
-    const int chunks = tower_chunks(M), rows_per = (int)((M + chunks - 1) / chunks);
+    const int chunks = tower_chunks(M, K), rows_per = (int)((M + chunks - 1) / chunks);
     hipStream_t st = rf_stream(stream);
-    const dim3 g((K + kColThreads - 1) / kColThreads, chunks);
-    hipLaunchKernelGGL(bn_bwd_partial_kernel, g, dim3(kColThreads), 0, st, dz, lddz, x, ldx, M, K, mean, var, eps, rows_per,
-                       (float*)ws);
-    hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3(g.x), dim3(kColThreads), 0, st, (const float*)ws, K, chunks, dbeta, dgamma);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((K + 255) / 256, (unsigned)M), dim3(256), 0, st, dz, lddz, x, ldx, M, K, mean, var,
-                       gamma, eps, dbeta, dgamma, dx, lddx);
+    float* part = (float*)ws;
+    float* ac = part + (size_t)chunks * 2 * K;
+    const int V = vec4_ok(K, {{dz, lddz}, {x, ldx}, {dx, lddx}, {mean, 0}, {var, 0}, {ac, 0}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((K / v + kColThreads - 1) / kColThreads, chunks); };
+    RF_TOWER_LAUNCH(bn_bwd_partial_kernel, V, grid, dz, lddz, x, ldx, M, K, mean, var, eps, rows_per, part);
+    hipLaunchKernelGGL(bn_bwd_finish_kernel, dim3((K + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinGroups), 0, st,
+                       (const float*)part, M, K, chunks, gamma, var, eps, dbeta, dgamma, ac);
+    auto grid2 = [&](int v) { return dim3((K / v + 255) / 256, (unsigned)M); };
+    RF_TOWER_LAUNCH(bn_bwd_apply_kernel, V, grid2, dz, lddz, x, ldx, K, mean, var, eps, (const float*)ac, dx, lddx);
     return rf_check_launch("rf_bn_bwd");
 }

@@ -532,21 +532,40 @@ __global__ __launch_bounds__(256) void adam_dense_kernel(float* __restrict__ w, 
 
 // the rows NOT in the gradient (map < 0) only: their Keras update needs no gradient, so it can run before the
 // gradient exists; the listed rows then take the lazy kernel with their gradient (together: exactly the dense step)
+// U float4 slots per thread per pass, every load issued before the first update: this kernel runs on a capped
+// grid beside the towers' GEMMs, so its bandwidth comes from loads in flight per wave, not from more waves
+template <int U>
 __global__ __launch_bounds__(256) void adam_untouched_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                                                              int64_t n4, int D4, const int32_t* __restrict__ map, AdamCoef c) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t row = i / D4;
-        if (map[row] >= 0) continue;
-        float4 wv = reinterpret_cast<float4*>(w)[i];
-        float4 mv = reinterpret_cast<float4*>(m)[i];
-        float4 vv = reinterpret_cast<float4*>(v)[i];
-        adam_elem(wv.x, mv.x, vv.x, false, 0.f, c);
-        adam_elem(wv.y, mv.y, vv.y, false, 0.f, c);
-        adam_elem(wv.z, mv.z, vv.z, false, 0.f, c);
-        adam_elem(wv.w, mv.w, vv.w, false, 0.f, c);
-        reinterpret_cast<float4*>(w)[i] = wv;
-        reinterpret_cast<float4*>(m)[i] = mv;
-        reinterpret_cast<float4*>(v)[i] = vv;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += stride) {
+        bool act[U];
+        float4 wv[U], mv[U], vv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + (int64_t)u * blockDim.x;
+            act[u] = i < n4 && map[i / D4] < 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (act[u]) {
+                const int64_t i = base + (int64_t)u * blockDim.x;
+                wv[u] = reinterpret_cast<float4*>(w)[i];
+                mv[u] = reinterpret_cast<float4*>(m)[i];
+                vv[u] = reinterpret_cast<float4*>(v)[i];
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (act[u]) {
+                const int64_t i = base + (int64_t)u * blockDim.x;
+                adam_elem(wv[u].x, mv[u].x, vv[u].x, false, 0.f, c);
+                adam_elem(wv[u].y, mv[u].y, vv[u].y, false, 0.f, c);
+                adam_elem(wv[u].z, mv[u].z, vv[u].z, false, 0.f, c);
+                adam_elem(wv[u].w, mv[u].w, vv[u].w, false, 0.f, c);
+                reinterpret_cast<float4*>(w)[i] = wv[u];
+                reinterpret_cast<float4*>(m)[i] = mv[u];
+                reinterpret_cast<float4*>(v)[i] = vv[u];
+            }
     }
 }
 
@@ -863,7 +882,7 @@ extern "C" int rf_adam_untouched(float* table, float* m, float* v, int64_t table
         const char* e = getenv("RF_ADAM_SIDE_GRID");
         return e ? std::max(1, atoi(e)) : 256;
     }();
-    hipLaunchKernelGGL(adam_untouched_kernel, dim3(grid_of(table_rows * (dim / 4), gmax)), dim3(256), 0, st, table, m, v,
+    hipLaunchKernelGGL(adam_untouched_kernel<4>, dim3(grid_of(table_rows * (dim / 4), gmax)), dim3(256), 0, st, table, m, v,
                        table_rows * (dim / 4), dim / 4, map, c);
     return rf_check_launch("rf_adam_untouched");
 }

@@ -126,10 +126,14 @@ class TrainableDssm(torch.nn.Module):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 plan = self.enc.backward_plan(batch)
+                planned = torch.cuda.Event()
+                planned.record(side)
                 self.sparse_opt.apply_untouched(plan.rows, plan.n_uniq, plan.cap)
             for t in (plan.rows, plan.n_uniq, plan.ws):
                 t.record_stream(main)
-            self.enc._plan, self.enc._plan_batch, self.enc._plan_stream = plan, batch, side
+            # the backward's reduce waits for the plan only: the untouched rows' update keeps running through the
+            # towers' backward, the reduce and the touched rows' update (disjoint rows), and the step joins it last
+            self.enc._plan, self.enc._plan_batch, self.enc._plan_stream = plan, batch, planned
 
         u, v = self(batch, after_embed=launch_untouched if split else None)
         loss = self.loss_fn(labels, u, v)
@@ -143,6 +147,8 @@ class TrainableDssm(torch.nn.Module):
         else:
             self.sparse_opt.apply(sg)
         self.dense_opt.step()
+        if split:  # the next step's lookup reads every row
+            torch.cuda.current_stream().wait_stream(self._side_stream())
         if dp is not None:  # BN moving statistics: ON_READ / MEAN across replicas (MirroredStrategy)
             dp.sync_buffers([self.user_tower, self.ad_tower])
         return loss.detach()

@@ -30,9 +30,12 @@ class _EmbedFn(torch.autograd.Function):
         enc = ctx.enc
         plan = getattr(enc, "_plan", None)
         if plan is not None and getattr(enc, "_plan_batch", None) is ctx.batch:
-            # the batch-only half already ran (possibly on a side stream): join it, reduce dout on this stream
+            # the batch-only half already ran (possibly on a side stream: _plan_stream is then that stream or an
+            # event recorded on it after the plan): join it, reduce dout on this stream
             side = getattr(enc, "_plan_stream", None)
-            if side is not None:
+            if isinstance(side, torch.cuda.Event):
+                torch.cuda.current_stream().wait_event(side)
+            elif side is not None:
                 torch.cuda.current_stream().wait_stream(side)
             enc.grad = enc.backward_reduce(plan, dout.float().contiguous(), out=out)
             enc._plan = enc._plan_batch = enc._plan_stream = None

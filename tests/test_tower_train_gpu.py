@@ -35,15 +35,15 @@ def _oracle_layers(t):
              "beta": t.beta[l].detach().cpu().numpy().astype(np.float64)} for l in range(len(t.units))]
 
 
-@pytest.mark.parametrize("M,in_f,units,rate", [(512, 384, (128, 64, 32), 0.3), (300, 2048, (256, 64), 0.0),
-                                               (1024, 8704, (1024, 512, 256), 0.3)])
-def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate):
+@pytest.mark.parametrize("M,in_f,units,rate,off", [(512, 384, (128, 64, 32), 0.3, 4), (300, 2048, (256, 64), 0.0, 4),
+                                                   (1024, 8704, (1024, 512, 256), 0.3, 4)])
+def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate, off):
     """Output, input gradient and every parameter gradient vs float64; the last shape is cfg2's user tower
     (K = 8704: the split-K forward)."""
     t = _tower(in_f, units, rate)
     g = torch.Generator().manual_seed(M + in_f)
     xfull = (torch.randn(M, in_f + 8, generator=g) * 0.05 + 0.01).cuda()
-    x = xfull[:, 4: 4 + in_f].detach().requires_grad_(True)  # a strided view, as the DSSM column blocks
+    x = xfull[:, off: off + in_f].detach().requires_grad_(True)  # a strided view, as the DSSM column blocks
     step = t.steps
     out = t(x)
     dout = torch.randn(out.shape, generator=g).cuda()
@@ -104,15 +104,18 @@ def test_two_tower_loss_and_gradients_vs_oracle(O, cuda):
             close(t.beta[l].grad.cpu().numpy(), gs[l]["beta"])
 
 
-def test_col_stats_large_mean_and_dropout_mask(O, cuda):
+@pytest.mark.parametrize("M,K,off", [(3000, 700, 0), (3000, 701, 1), (37, 5, 0), (4096, 256, 0), (5, 2048, 4)])
+def test_col_stats_large_mean_and_dropout_mask(O, cuda, M, K, off):
     """rf_col_stats on columns whose mean is 1000x their spread (pivoted chunks + Chan combine) and
-    rf_dropout_fwd's mask bit-exact against oracle.dropout_keep."""
-    M, K = 3000, 700
+    rf_dropout_fwd's mask bit-exact against oracle.dropout_keep; the float4 path (16-byte aligned rows) and
+    the scalar one (odd K, a view starting one float in), tiny and cfg2-shaped chunkings."""
     g = torch.Generator().manual_seed(4)
-    x = (torch.randn(M, K, generator=g) + 1000.0).cuda()
+    ld = K + 4
+    xfull = (torch.randn(M, ld, generator=g) + 1000.0).cuda()
+    x = xfull[:, off: off + K]
     mean, var = torch.empty(K, device="cuda"), torch.empty(K, device="cuda")
     ws = torch.empty(int(L.load().rf_tower_ws_bytes(M, K)), dtype=torch.uint8, device="cuda")
-    L.call("rf_col_stats", L.ptr(x), M, K, K, L.ptr(mean), L.ptr(var), L.ptr(ws), ws.numel(), L.stream_ptr(None))
+    L.call("rf_col_stats", L.ptr(x), M, K, ld, L.ptr(mean), L.ptr(var), L.ptr(ws), ws.numel(), L.stream_ptr(None))
     x64 = x.cpu().numpy().astype(np.float64)
     close(mean.cpu().numpy(), x64.mean(0), rtol=1e-6)
     close(var.cpu().numpy(), x64.var(0), rtol=2e-4)
@@ -120,6 +123,44 @@ def test_col_stats_large_mean_and_dropout_mask(O, cuda):
     L.call("rf_dropout_fwd", L.ptr(y), M, K, K, 0.3, 987654321, L.ptr(y), K, L.stream_ptr(None))
     keep = O.dropout_keep(987654321, M, K, 0.3)
     assert np.array_equal(y.cpu().numpy() != 0, keep)
+
+
+@pytest.mark.parametrize("M,K", [(4096, 256), (333, 520)])
+def test_column_kernels_float4_equals_scalar(cuda, M, K):
+    """The column kernels pick float4 lanes when every row is 16-byte aligned and scalar lanes otherwise; both
+    walk the same row chunks in the same order, so the results are bit-identical (a view one float in forces the
+    scalar path)."""
+    g = torch.Generator().manual_seed(M)
+    st = L.stream_ptr(None)
+    ws = torch.empty(int(L.load().rf_tower_ws_bytes(M, K)), dtype=torch.uint8, device="cuda")
+
+    def views(t):  # the same values, aligned and one float in
+        a = torch.zeros(M, K + 4, device="cuda")
+        b = torch.zeros(M, K + 4, device="cuda")
+        a[:, :K] = t
+        b[:, 1:K + 1] = t
+        return a[:, :K], b[:, 1:K + 1]
+
+    x = torch.randn(M, K, generator=g).cuda() * 0.3 + 0.1
+    dz = torch.randn(M, K, generator=g).cuda()
+    gamma, var = torch.rand(K).cuda() + 0.5, torch.rand(K).cuda() + 0.1
+    mean = torch.randn(K).cuda() * 0.1
+    outs = []
+    for xv, dv in zip(views(x), views(dz)):
+        ld = K + 4
+        mu, va = torch.empty(K, device="cuda"), torch.empty(K, device="cuda")
+        L.call("rf_col_stats", L.ptr(xv), M, K, ld, L.ptr(mu), L.ptr(va), L.ptr(ws), ws.numel(), st)
+        dpre, db = torch.zeros(M, K + 4, device="cuda"), torch.empty(K, device="cuda")
+        dp = dpre[:, 1:K + 1] if xv.data_ptr() % 16 else dpre[:, :K]
+        L.call("rf_selu_dropout_bwd", L.ptr(dv), ld, L.ptr(xv), ld, M, K, 0.3, 77, L.ptr(dp), ld, L.ptr(db), L.ptr(ws),
+               ws.numel(), st)
+        dx, dg, dbe = torch.zeros(M, K + 4, device="cuda"), torch.empty(K, device="cuda"), torch.empty(K, device="cuda")
+        dxv = dx[:, 1:K + 1] if xv.data_ptr() % 16 else dx[:, :K]
+        L.call("rf_bn_bwd", L.ptr(dv), ld, L.ptr(xv), ld, M, K, L.ptr(mean), L.ptr(var), L.ptr(gamma), 1e-6, L.ptr(dxv), ld,
+               L.ptr(dg), L.ptr(dbe), L.ptr(ws), ws.numel(), st)
+        outs.append([t.clone() for t in (mu, va, dp, db, dxv, dg, dbe)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_eval_mode_folds_moving_statistics(O, cuda):

@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU: train-step tests, then the train-step probe at several side-stream Adam grids (RF_ADAM_SIDE_GRID).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-sidegrid}
+mkdir -p "$OUT"
+timeout -k 10 400 python -u -m pytest -q --timeout 300 tests/test_train_step_gpu.py tests/test_tower_train_gpu.py -m gpu > "$OUT/pytest.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest.log"
+case $rc in 0|1) ;; *) exit $rc;; esac
+for g in ${GRIDS:-256 512 1024}; do
+  RF_ADAM_SIDE_GRID=$g timeout -k 10 300 python tools/train_step_probe.py > "$OUT/probe_$g.json" 2>&1 || exit $?
+  echo "grid $g: $(tail -1 "$OUT/probe_$g.json" | cut -c1-260)"
+done
