@@ -462,6 +462,13 @@ int rf_segment_sum_rows(const int64_t* ids, const float* vals, int64_t n, int32_
  * ws: rf_adam_ws_bytes(table_rows, lazy) bytes (dense mode: a row -> gradient map).
  */
 size_t rf_adam_ws_bytes(int64_t table_rows, int32_t lazy);
+/* Keras Adam on a dense fp32 variable of n elements (the towers' weights; Adam._resource_apply_dense ->
+ * ResourceApplyAdam): m += (g - m)(1 - beta1); v += (g^2 - v)(1 - beta2); w -= m lr / (sqrt(v) + epsilon), with lr
+ * the bias-corrected step size lr * sqrt(1 - beta2^t) / (1 - beta1^t) in fp32. In place, one launch.
+ */
+int rf_adam_dense(float* w, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float epsilon,
+                  void* stream);
+
 /*
  * The dense step split in time: rf_adam_untouched updates every row NOT listed in uniq_rows[:n_uniq] (their
  * Keras update needs no gradient: m, v decay, var moves by lr m / (sqrt(v) + eps)), so it can run as soon as

@@ -223,6 +223,18 @@ def adam_apply(table, m, v, uniq_rows, uniq_grad, lr, beta1, beta2, eps, lazy=Fa
                          len(uniq_rows), lr, beta1, beta2, eps, int(lazy))
 
 
+def adam_dense(w, g, m, v, lr, beta1, beta2, eps):
+    """Keras Adam._resource_apply_dense (TF ResourceApplyAdam, training_ops: ApplyAdamNonCuda) in place on fp32
+    numpy arrays, lr the bias-corrected step size (keras_adam_lr): m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);
+    w -= m lr / (sqrt(v) + eps). numpy float32 ops round each step (no fused multiply-add), as the kernel does."""
+    f = np.float32
+    for a in (w, g, m, v):
+        assert a.dtype == np.float32
+    m += (g - m) * (f(1) - f(beta1))
+    v += (g * g - v) * (f(1) - f(beta2))
+    w -= (m * f(lr)) / (np.sqrt(v) + f(eps))
+
+
 def keras_adam_lr(lr: float, beta1: float, beta2: float, step: int) -> float:
     """Keras Adam's bias-corrected step size in float32: lr * (sqrt(1 - b2^t) / (1 - b1^t))."""
     f = np.float32

@@ -7,7 +7,8 @@ Adam._resource_apply_sparse to the deduplicated IndexedSlices gradient: m and v 
 variable, the scaled gradient is scatter-added, and every row moves (dense semantics). ``lazy=True``
 touches only the rows in the gradient (TF-Addons LazyAdam; deviation D-lazy-adam, opt-in).
 
-Dense parameters (towers, attention) use torch.optim.Adam with the same hyper-parameters.
+Dense variables (the towers) take Keras' Adam._resource_apply_dense (TF ResourceApplyAdam) through
+``KerasAdam`` (rf_adam_dense, one launch per variable).
 """
 from __future__ import annotations
 
@@ -59,4 +60,50 @@ class SparseAdam:
         L.call("rf_adam_apply", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0], self.table.shape[1],
                L.ptr(g.rows), L.ptr(g.grad), L.ptr(g.n_uniq), g.cap, self.step_lr(), self.beta_1, self.beta_2,
                self.epsilon, int(self.lazy), L.ptr(self._ws), self._ws.numel(), L.stream_ptr(stream))
+        self.iterations += 1
+
+
+class KerasAdam:
+    """tf.keras.optimizers.Adam on dense fp32 parameters (Adam._resource_apply_dense -> ResourceApplyAdam):
+    m += (g - m)(1 - beta_1); v += (g^2 - v)(1 - beta_2); var -= m lr_t / (sqrt(v) + epsilon) with Keras'
+    bias-corrected lr_t in float32. The torch.optim-style surface (zero_grad, step, param_groups) the
+    training loops use; parameters without a gradient are skipped, as Keras skips None gradients."""
+
+    def __init__(self, params, learning_rate: float = 0.001, beta_1: float = 0.9, beta_2: float = 0.999,
+                 epsilon: float = 1e-7):
+        self.params = [p for p in params]
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise ValueError("KerasAdam needs contiguous fp32 parameters")
+        self.learning_rate, self.beta_1, self.beta_2, self.epsilon = learning_rate, beta_1, beta_2, epsilon
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.iterations = 0
+        self.param_groups = [{"params": self.params, "lr": learning_rate}]
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
+
+    def step_lr(self) -> float:
+        f = np.float32
+        t = f(self.iterations + 1)
+        b1p, b2p = np.power(f(self.beta_1), t), np.power(f(self.beta_2), t)
+        return float(f(self.learning_rate) * (np.sqrt(f(1) - b2p) / (f(1) - b1p)))
+
+    @torch.no_grad()
+    def step(self, stream=None):
+        lr = self.step_lr()
+        st = L.stream_ptr(stream)
+        for p, m, v in zip(self.params, self.m, self.v):
+            g = p.grad
+            if g is None:
+                continue
+            if g.dtype != torch.float32 or not g.is_contiguous():
+                g = g.float().contiguous()
+            L.call("rf_adam_dense", L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr, self.beta_1, self.beta_2,
+                   self.epsilon, st)
         self.iterations += 1

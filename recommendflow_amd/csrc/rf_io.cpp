@@ -1,6 +1,8 @@
 // rf_io.cpp — TFRecord(GZIP) <-> batched-CSR feature pipe (include/rf_io.h). Host code only.
 //
-// Reader: per-file decompression threads (zlib inflate + TFRecord framing with masked CRC-32C)
+// Reader: per-file decompression threads (inflate + TFRecord framing with masked CRC-32C; a
+// single-member GZIP file is inflated whole by libdeflate when the system has it, zlib streams
+// everything else)
 // feed a deterministic block_length-1 interleave (tf.data TFRecordDataset(num_parallel_reads),
 // backend/core/dataloader.py:567-570); a fork-join parse pool turns a batch of serialized
 // tf.train.Example records into the columns parse_example would produce
@@ -10,6 +12,8 @@
 //
 // Writer: tf.io.TFRecordWriter(path, "GZIP") (utils/make_tfrecord.py:142) and the
 // tf.train.Example serialisation of build_tfrecord (make_tfrecord.py:94-119).
+#include <dlfcn.h>
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -18,6 +22,7 @@
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -125,6 +130,37 @@ struct Status {
 Status fail(int code, std::string msg) { return Status{code, std::move(msg)}; }
 
 // ------------------------------------------------------------------------------------------------
+// libdeflate (the system's libdeflate.so.0, loaded at run time; its whole-buffer gzip decoder runs
+// ~2-3x zlib's streaming inflate). Only the three entry points the reader needs; absent library or
+// RF_TFR_INFLATE=zlib -> zlib for every file.
+// ------------------------------------------------------------------------------------------------
+struct Deflate {
+    using alloc_t = void* (*)();
+    using free_t = void (*)(void*);
+    // libdeflate_gzip_decompress_ex(d, in, in_n, out, out_avail, &in_used, &out_n) -> 0 success,
+    // 1 bad data, 2 short output, 3 insufficient space
+    using gunzip_t = int (*)(void*, const void*, size_t, void*, size_t, size_t*, size_t*);
+    alloc_t alloc = nullptr;
+    free_t release = nullptr;
+    gunzip_t gunzip = nullptr;
+    Deflate() {
+        const char* e = std::getenv("RF_TFR_INFLATE");
+        if (e && std::string(e) == "zlib") return;
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = reinterpret_cast<alloc_t>(dlsym(h, "libdeflate_alloc_decompressor"));
+        release = reinterpret_cast<free_t>(dlsym(h, "libdeflate_free_decompressor"));
+        gunzip = reinterpret_cast<gunzip_t>(dlsym(h, "libdeflate_gzip_decompress_ex"));
+        if (!alloc || !release || !gunzip) alloc = nullptr;
+    }
+    bool ok() const { return alloc != nullptr; }
+};
+const Deflate& deflate_lib() {
+    static const Deflate d;
+    return d;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Byte stream over a file, plain or gzip (concatenated members allowed), read straight into the
 // caller's buffer (fread, or inflate with the buffer as its output window).
 // ------------------------------------------------------------------------------------------------
@@ -138,6 +174,7 @@ class InStream {
     Status open() {
         f_ = std::fopen(path_.c_str(), "rb");
         if (!f_) return fail(RF_EIO, "cannot open " + path_ + ": " + std::strerror(errno));
+        if (gz_ && whole_file()) return {};
         if (gz_) {
             in_.resize(1 << 20);
             std::memset(&zs_, 0, sizeof(zs_));
@@ -151,6 +188,13 @@ class InStream {
     // Fills dst[0, n) as far as the stream allows; *got < n only at the end of the stream.
     Status read(uint8_t* dst, size_t n, size_t* got) {
         *got = 0;
+        if (whole_) {
+            const size_t k = std::min(n, out_n_ - out_pos_);
+            std::memcpy(dst, out_.get() + out_pos_, k);
+            out_pos_ += k;
+            *got = k;
+            return {};
+        }
         if (!gz_) {
             while (*got < n) {
                 const size_t k = std::fread(dst + *got, 1, n - *got, f_);
@@ -191,12 +235,72 @@ class InStream {
     }
 
   private:
+    // One gzip member spanning the whole file (what tf.io.TFRecordWriter and this build's writer
+    // produce), at most 256 MiB decoded: inflate it in one libdeflate call, sized by the member's
+    // ISIZE trailer. Anything else — several members, a bad or truncated stream, no libdeflate — leaves
+    // the file to the zlib stream from its first byte, so errors and partial reads are zlib's.
+    bool whole_file() {
+        const Deflate& lib = deflate_lib();
+        if (!lib.ok()) return false;
+        if (std::fseek(f_, 0, SEEK_END) != 0) return false;
+        const long sz = std::ftell(f_);
+        std::rewind(f_);
+        if (sz < 18 || sz > (1l << 30)) return false;
+        std::unique_ptr<uint8_t[]> in(new uint8_t[static_cast<size_t>(sz)]);  // not zero-initialised
+        if (std::fread(in.get(), 1, static_cast<size_t>(sz), f_) != static_cast<size_t>(sz)) {
+            std::rewind(f_);
+            return false;
+        }
+        const uint8_t* t = in.get() + sz - 4;
+        const size_t isize = static_cast<size_t>(t[0]) | static_cast<size_t>(t[1]) << 8 | static_cast<size_t>(t[2]) << 16 |
+                             static_cast<size_t>(t[3]) << 24;
+        bool ok = false;
+        if (isize <= (256u << 20)) {
+            void* d = lib.alloc();
+            if (d) {
+                std::unique_ptr<uint8_t[]> out(new uint8_t[std::max<size_t>(isize, 1)]);
+                huge_pages(out.get(), isize);
+                size_t used = 0, n = 0;
+                ok = lib.gunzip(d, in.get(), static_cast<size_t>(sz), out.get(), isize, &used, &n) == 0 &&
+                     used == static_cast<size_t>(sz) && n == isize;
+                lib.release(d);
+                if (ok) {
+                    out_ = std::move(out);
+                    out_n_ = n;
+                }
+            }
+        }
+        if (!ok) std::rewind(f_);
+        whole_ = ok;
+        return ok;
+    }
+
     std::string path_;
     bool gz_;
     FILE* f_ = nullptr;
     z_stream zs_;
     bool z_init_ = false, member_open_ = false;
     std::vector<uint8_t> in_;
+    bool whole_ = false;
+    std::unique_ptr<uint8_t[]> out_;  // the whole file's decoded bytes (whole_)
+    size_t out_n_ = 0, out_pos_ = 0;
+
+  public:
+    // whole-file mode: hand the decoded bytes over (the producer frames them in place, no block copies)
+    bool take_whole(std::unique_ptr<uint8_t[]>* buf, size_t* n) {
+        if (!whole_ || out_pos_ != 0) return false;
+        *buf = std::move(out_);
+        *n = out_n_;
+        out_pos_ = out_n_;
+        return true;
+    }
+    // transparent huge pages for a large decode buffer: 2 MiB faults instead of 4 KiB ones when 16
+    // producers fill fresh buffers at once
+    static void huge_pages(void* p, size_t n) {
+        const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + (2u << 20) - 1) & ~static_cast<uintptr_t>((2u << 20) - 1);
+        const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + n) & ~static_cast<uintptr_t>((2u << 20) - 1);
+        if (e > a) madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
+    }
 };
 
 // A block of one file's decoded bytes and the records framed inside it (payloads in place).
@@ -206,6 +310,7 @@ struct Chunk {
     std::vector<uint64_t> start;  // record i = buf[start[i], start[i] + len[i])
     std::vector<uint32_t> len;
     explicit Chunk(size_t c) : buf(new uint8_t[c]), cap(c) {}
+    Chunk(std::unique_ptr<uint8_t[]> b, size_t c) : buf(std::move(b)), cap(c) {}
     size_t size() const { return start.size(); }
 };
 
@@ -261,8 +366,18 @@ class FileProducer {
         Status s = in.open();
         if (!s.ok()) return s;
         uint64_t rec_no = 0;
-        auto chunk = std::make_shared<Chunk>(kBlockBytes);
+        std::shared_ptr<Chunk> chunk;
         size_t have = 0;  // bytes in chunk->buf
+        {
+            std::unique_ptr<uint8_t[]> whole;
+            size_t n = 0;
+            if (in.take_whole(&whole, &n)) {  // the decoded file is one chunk; the loop below frames it and sees EOF
+                chunk = std::make_shared<Chunk>(std::move(whole), n + 1);
+                have = n;
+            } else {
+                chunk = std::make_shared<Chunk>(kBlockBytes);
+            }
+        }
         for (;;) {
             size_t got = 0;
             s = in.read(chunk->buf.get() + have, chunk->cap - have, &got);
@@ -744,9 +859,16 @@ class Reader {
             auto& slot = cycle_[cursor_];
             if (!slot) {
                 if (next_path_ < paths_.size()) {
-                    slot = std::make_unique<FileProducer>(paths_[next_path_++], gz_);
-                    ++n_open_;
-                    any_open_ = true;
+                    // open a file for this slot and for every other empty slot, in the order the cursor reaches
+                    // them (the order they would take files one visit at a time), so their producers decode in
+                    // parallel instead of each starting only when the round-robin first asks it for a record
+                    for (size_t k = 0; k < cycle_.size() && next_path_ < paths_.size(); ++k) {
+                        auto& sl = cycle_[(cursor_ + k) % cycle_.size()];
+                        if (sl) continue;
+                        sl = take_producer();
+                        ++n_open_;
+                        any_open_ = true;
+                    }
                     continue;  // the new file produces in this same turn
                 }
                 cursor_ = (cursor_ + 1) % cycle_.size();
@@ -770,6 +892,23 @@ class Reader {
             }
         }
         return {};
+    }
+
+    // The producer of paths_[next_path_]: files go to slots in path order whatever the slot, so the next
+    // cycle_.size() paths are opened ahead (their threads decode while the current files are consumed;
+    // a whole-file inflate otherwise stalls its slot at every file boundary).
+    std::unique_ptr<FileProducer> take_producer() {
+        std::unique_ptr<FileProducer> p;
+        if (!ahead_.empty()) {
+            p = std::move(ahead_.front());
+            ahead_.pop_front();
+        } else {
+            p = std::make_unique<FileProducer>(paths_[next_path_], gz_);
+        }
+        ++next_path_;
+        while (ahead_.size() < cycle_.size() && next_path_ + ahead_.size() < paths_.size())
+            ahead_.push_back(std::make_unique<FileProducer>(paths_[next_path_ + ahead_.size()], gz_));
+        return p;
     }
 
     Status parse(const Schema& sc, int32_t B, rf_tfr_columns* c) {
@@ -954,6 +1093,7 @@ class Reader {
     }
 
     std::vector<std::string> paths_;
+    std::deque<std::unique_ptr<FileProducer>> ahead_;  // opened ahead, in path order
     bool gz_;
     Pool pool_;
     std::vector<std::unique_ptr<FileProducer>> cycle_;

@@ -373,7 +373,8 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
     constexpr int PT = 1024 / TPR;     // positions per pass of the block
     constexpr int P = PPT * PT;        // positions per chunk (one barrier)
     constexpr int kDepth = 8 / PPT;
-    constexpr int G = 8;  // LDS reads per add group
+    constexpr int G = 8;  // LDS reads in flight per add group
+    constexpr int KD = TPR >= 16 ? TPR / 16 : 1;  // float columns per lane of the adding wave (TPR * 4 floats a row)
     __shared__ float4 buf[2][PPT * 1024];
     const int t = threadIdx.x, pi = t / TPR, lane = t % TPR;
     const bool active = lane * 4 < D;
@@ -411,7 +412,9 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
                 rs[k][h] = i >= 0 ? src[i] : kZero;
                 ra[k][h] = i >= 0 ? aux[i] : 0u;
             }
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        float acc[KD];
+#pragma unroll
+        for (int k = 0; k < KD; ++k) acc[k] = 0.f;
         for (int c0 = 0; c0 < nch; c0 += kDepth) {
 #pragma unroll
             for (int k = 0; k < kDepth; ++k) {
@@ -428,32 +431,35 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
                         rs[k][h] = i >= 0 ? src[i] : kZero;
                         ra[k][h] = i >= 0 ? aux[i] : 0u;
                     }
-                    if (t < TPR && active) {
+                    if (t < 64) {  // wave 0, a lane per float column: one add per position and column
                         const int np = min(P, i1 - (i0 + c * P));
+                        const float* bf = reinterpret_cast<const float*>(b);
+                        int col[KD];  // this lane's float columns (a dead lane re-reads column 0; never stored)
+#pragma unroll
+                        for (int k = 0; k < KD; ++k) col[k] = k * 64 + t < D ? k * 64 + t : 0;
                         int q = 0;
-                        if (np == P) {  // full chunk: reads of group g + 1 in flight while group g is added
-                            float4 cur[G], nxt[G];
+                        for (; q + G <= np; q += G) {
+                            float v[G][KD];
 #pragma unroll
-                            for (int r = 0; r < G; ++r) cur[r] = b[r * TPR + t];
+                            for (int r = 0; r < G; ++r)
 #pragma unroll
-                            for (int g = 0; g < P / G; ++g) {
-                                if (g + 1 < P / G) {
+                                for (int k = 0; k < KD; ++k) v[r][k] = bf[(q + r) * (TPR * 4) + col[k]];
 #pragma unroll
-                                    for (int r = 0; r < G; ++r) nxt[r] = b[((g + 1) * G + r) * TPR + t];
-                                }
+                            for (int r = 0; r < G; ++r)
 #pragma unroll
-                                for (int r = 0; r < G; ++r) add4(acc, cur[r]);
-#pragma unroll
-                                for (int r = 0; r < G; ++r) cur[r] = nxt[r];
-                            }
-                            q = P;
+                                for (int k = 0; k < KD; ++k) acc[k] += v[r][k];
                         }
-                        for (; q < np; ++q) add4(acc, b[q * TPR + t]);
+                        for (; q < np; ++q)
+#pragma unroll
+                            for (int k = 0; k < KD; ++k) acc[k] += bf[q * (TPR * 4) + col[k]];
                     }
                 }
             }
         }
-        if (t < TPR && active) reinterpret_cast<float4*>(uniq_grad + (int64_t)u * D)[t] = acc;
+        if (t < 64)
+#pragma unroll
+            for (int k = 0; k < KD; ++k)
+                if (k * 64 + t < D) uniq_grad[(int64_t)u * D + k * 64 + t] = acc[k];
         __syncthreads();
     }
 }
@@ -591,6 +597,35 @@ __global__ __launch_bounds__(256) void adam_lazy_kernel(float* __restrict__ w, f
         reinterpret_cast<float4*>(w)[e] = wv;
         reinterpret_cast<float4*>(m)[e] = mv;
         reinterpret_cast<float4*>(v)[e] = vv;
+    }
+}
+
+// Dense variables (the towers): ResourceApplyAdam, the form Keras' Adam._resource_apply_dense runs —
+// m += (g - m)(1 - beta_1); v += (g^2 - v)(1 - beta_2); var -= m lr / (sqrt(v) + epsilon)
+__device__ __forceinline__ void adam_dense_elem(float& w, float& m, float& v, float g, const AdamCoef& c) {
+    m = m + (g - m) * c.omb1;
+    v = v + (g * g - v) * c.omb2;
+    w = w - (m * c.lr) / (sqrtf(v) + c.eps);
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void adam_dense_flat_kernel(float* __restrict__ w, const float* __restrict__ g,
+                                                              float* __restrict__ m, float* __restrict__ v, int64_t n, AdamCoef c) {
+    const int64_t nv = n / V;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+        if constexpr (V == 4) {
+            float4 wv = reinterpret_cast<float4*>(w)[i], mv = reinterpret_cast<float4*>(m)[i], vv = reinterpret_cast<float4*>(v)[i];
+            const float4 gv = reinterpret_cast<const float4*>(g)[i];
+            adam_dense_elem(wv.x, mv.x, vv.x, gv.x, c);
+            adam_dense_elem(wv.y, mv.y, vv.y, gv.y, c);
+            adam_dense_elem(wv.z, mv.z, vv.z, gv.z, c);
+            adam_dense_elem(wv.w, mv.w, vv.w, gv.w, c);
+            reinterpret_cast<float4*>(w)[i] = wv;
+            reinterpret_cast<float4*>(m)[i] = mv;
+            reinterpret_cast<float4*>(v)[i] = vv;
+        } else {
+            adam_dense_elem(w[i], m[i], v[i], g[i], c);
+        }
     }
 }
 
@@ -885,4 +920,25 @@ extern "C" int rf_adam_untouched(float* table, float* m, float* v, int64_t table
     hipLaunchKernelGGL(adam_untouched_kernel<4>, dim3(grid_of(table_rows * (dim / 4), gmax)), dim3(256), 0, st, table, m, v,
                        table_rows * (dim / 4), dim / 4, map, c);
     return rf_check_launch("rf_adam_untouched");
+}
+
+extern "C" int rf_adam_dense(float* w, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                             float epsilon, void* stream) {
+    RF_REQUIRE(n >= 0, "rf_adam_dense: n must be >= 0");
+    if (n == 0) return RF_OK;
+    RF_REQUIRE(w && g && m && v, "rf_adam_dense: null pointer");
+    AdamCoef c;
+    c.lr = lr;
+    c.b1 = beta1;
+    c.b2 = beta2;
+    c.omb1 = 1.0f - beta1;
+    c.omb2 = 1.0f - beta2;
+    c.eps = epsilon;
+    hipStream_t st = rf_stream(stream);
+    const bool v4 = n % 4 == 0 && ((((uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
+    if (v4)
+        hipLaunchKernelGGL(adam_dense_flat_kernel<4>, dim3(grid_of(n / 4, 4096)), dim3(256), 0, st, w, g, m, v, n, c);
+    else
+        hipLaunchKernelGGL(adam_dense_flat_kernel<1>, dim3(grid_of(n, 4096)), dim3(256), 0, st, w, g, m, v, n, c);
+    return rf_check_launch("rf_adam_dense");
 }

@@ -60,15 +60,15 @@ class TrainableDssm(torch.nn.Module):
     (dssm.py:25-26, mlp.py:4-15) on librf.so (backend.blocks.train_mlp.TrainTower: batch statistics folded
     into the fp32 MFMA GEMM, SELU / dropout / BatchNormalization backward kernels, library GEMMs for the two
     backward products), l2 normalisation (dssm.py:35-36), and the configured loss (cosent_loss for
-    base_recall_sdpa.yaml). step() = forward, backward, SparseAdam on the table (rf_adam_apply) and Adam on
-    the towers, Keras defaults (lr 1e-3, 0.9, 0.999, 1e-7)."""
+    base_recall_sdpa.yaml). step() = forward, backward, SparseAdam on the table (rf_adam_apply) and KerasAdam
+    on the towers (rf_adam_dense), Keras defaults (lr 1e-3, 0.9, 0.999, 1e-7)."""
 
     def __init__(self, encoder: FusedSparseEncoder, n_user_slots: int, units=(1024, 512, 256), dropout=0.3,
                  learning_rate=1e-3, loss="cosent", lazy_adam=False, seed=0):
         super().__init__()
         from ...backend.blocks.train_mlp import TrainTower
         from ...backend.losses import match_losses
-        from ...backend.optim import SparseAdam
+        from ...backend.optim import KerasAdam, SparseAdam
 
         self.enc = encoder
         self.wu = 2 * encoder.dim * n_user_slots
@@ -80,8 +80,8 @@ class TrainableDssm(torch.nn.Module):
         self.loss_fn = {"cosent": match_losses.cosent_loss,
                         "inbatch_ce": match_losses.batch_neg_sample_scaled_multi_class_ce_loss}[loss]
         self.sparse_opt = SparseAdam(encoder.table, learning_rate=learning_rate, lazy=lazy_adam)
-        self.dense_opt = torch.optim.Adam(list(self.user_tower.parameters()) + list(self.ad_tower.parameters()),
-                                          lr=learning_rate, betas=(0.9, 0.999), eps=1e-7)
+        self.dense_opt = KerasAdam(list(self.user_tower.parameters()) + list(self.ad_tower.parameters()),
+                                   learning_rate=learning_rate)
 
     overlap_table_adam = True  # False: the table's dense Adam runs after the backward in one launch (A/B)
 

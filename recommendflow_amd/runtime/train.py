@@ -3,8 +3,8 @@
 The fused encoder joins torch autograd through `embed()`: forward = rf_fused_hash_embed_fwd, backward =
 rf_fused_hash_embed_bwd, whose deduplicated row gradient is parked on the encoder (`enc.grad`) for
 SparseAdam (rf_adam_apply) — the table is never a dense torch gradient. Dense parameters (towers) train
-with torch autograd + torch.optim.Adam using Keras' Adam defaults (reference: model.fit with
-tf.keras.optimizers.Adam, example/recall_search/train.py:96-104).
+with torch autograd + backend.optim.KerasAdam (rf_adam_dense: Keras' dense Adam update, Keras defaults;
+reference: model.fit with tf.keras.optimizers.Adam, example/recall_search/train.py:96-104).
 """
 from __future__ import annotations
 

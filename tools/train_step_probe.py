@@ -31,7 +31,7 @@ def main():
     TrainableDssm.overlap_table_adam = os.environ.get("RF_TRAIN_OVERLAP", "1") != "0"
     r = bench.bench_train(a, specs, multi)
     r["overlap_table_adam"] = TrainableDssm.overlap_table_adam
-    r["side_grid"] = os.environ.get("RF_ADAM_SIDE_GRID", "512")
+    r["side_grid"] = os.environ.get("RF_ADAM_SIDE_GRID", "256")
     print(json.dumps(r))
     torch.cuda.synchronize()
 
