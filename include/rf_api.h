@@ -468,6 +468,17 @@ size_t rf_adam_ws_bytes(int64_t table_rows, int32_t lazy);
  */
 int rf_adam_dense(float* w, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2, float epsilon,
                   void* stream);
+/* rf_adam_dense over a list of variables in one launch. tensors: a DEVICE array of n_tensors descriptors
+ * (every n <= max_n); the same update, bit for bit, as one rf_adam_dense per entry. */
+typedef struct rf_adam_tensor {
+    float* w;
+    const float* g;
+    float* m;
+    float* v;
+    int64_t n;
+} rf_adam_tensor;
+int rf_adam_dense_multi(const rf_adam_tensor* tensors, int32_t n_tensors, int64_t max_n, float lr, float beta1, float beta2,
+                        float epsilon, void* stream);
 
 /*
  * The dense step split in time: rf_adam_untouched updates every row NOT listed in uniq_rows[:n_uniq] (their

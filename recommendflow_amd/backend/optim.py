@@ -96,14 +96,37 @@ class KerasAdam:
 
     @torch.no_grad()
     def step(self, stream=None):
+        """One launch for every parameter with a gradient (rf_adam_dense_multi): descriptors (w, g, m, v, n)
+        written into a pinned ring slot and copied to the device on the step's stream."""
         lr = self.step_lr()
-        st = L.stream_ptr(stream)
+        rows, grads = [], []
         for p, m, v in zip(self.params, self.m, self.v):
             g = p.grad
             if g is None:
                 continue
             if g.dtype != torch.float32 or not g.is_contiguous():
                 g = g.float().contiguous()
-            L.call("rf_adam_dense", L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr, self.beta_1, self.beta_2,
-                   self.epsilon, st)
+            grads.append(g)
+            rows.append((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel()))
+        if rows:
+            dev = self.params[0].device
+            if not hasattr(self, "_ring"):
+                self._ring = [torch.empty((len(self.params), 5), dtype=torch.int64).pin_memory() for _ in range(2)]
+                self._ring_ev = [None, None]
+                self._desc = torch.empty((len(self.params), 5), dtype=torch.int64, device=dev)
+            k = self.iterations % 2
+            if self._ring_ev[k] is not None:
+                self._ring_ev[k].synchronize()  # the copy that last read this slot is done
+            host = self._ring[k]
+            host[: len(rows)].copy_(torch.tensor(rows, dtype=torch.int64))
+            cur = torch.cuda.current_stream(dev) if stream is None else stream
+            with torch.cuda.stream(cur):
+                self._desc[: len(rows)].copy_(host[: len(rows)], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cur)
+            self._ring_ev[k] = ev
+            L.call("rf_adam_dense_multi", L.ptr(self._desc), len(rows), max(r[4] for r in rows), lr, self.beta_1,
+                   self.beta_2, self.epsilon, L.stream_ptr(cur))
+            for g in grads:  # the kernel reads them on `cur`
+                g.record_stream(cur)
         self.iterations += 1

@@ -629,6 +629,31 @@ __global__ __launch_bounds__(256) void adam_dense_flat_kernel(float* __restrict_
     }
 }
 
+// every tensor of a list in one launch: blockIdx.y = tensor, blockIdx.x strides its elements (float4 when the
+// tensor's four pointers are 16-byte aligned and n % 4 == 0)
+__global__ __launch_bounds__(256) void adam_dense_multi_kernel(const rf_adam_tensor* __restrict__ ts, AdamCoef c) {
+    const rf_adam_tensor t = ts[blockIdx.y];
+    const bool v4 = t.n % 4 == 0 && ((((uintptr_t)t.w | (uintptr_t)t.g | (uintptr_t)t.m | (uintptr_t)t.v) & 15) == 0);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (v4) {
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n / 4; i += stride) {
+            float4 wv = reinterpret_cast<float4*>(t.w)[i], mv = reinterpret_cast<float4*>(t.m)[i],
+                   vv = reinterpret_cast<float4*>(t.v)[i];
+            const float4 gv = reinterpret_cast<const float4*>(t.g)[i];
+            adam_dense_elem(wv.x, mv.x, vv.x, gv.x, c);
+            adam_dense_elem(wv.y, mv.y, vv.y, gv.y, c);
+            adam_dense_elem(wv.z, mv.z, vv.z, gv.z, c);
+            adam_dense_elem(wv.w, mv.w, vv.w, gv.w, c);
+            reinterpret_cast<float4*>(t.w)[i] = wv;
+            reinterpret_cast<float4*>(t.m)[i] = mv;
+            reinterpret_cast<float4*>(t.v)[i] = vv;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n; i += stride)
+            adam_dense_elem(t.w[i], t.m[i], t.v[i], t.g[i], c);
+    }
+}
+
 int grid_of(int64_t n, int cap = 256 * 64) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)); }
 
 }  // namespace
@@ -719,10 +744,10 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
         constexpr int TPR = decltype(tpr)::value;
         const int teams = 256 / TPR;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((max_u + teams - 1) / teams, 256 * 64));
-        hipLaunchKernelGGL(reduce_short_kernel<TPR>, dim3(grid), dim3(256), 0, st, src, aux, seg, n_uniq, uniq_cap,
-                           uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
         const int lgrid = (int)std::max<int64_t>(1, std::min<int64_t>(n / kLong + 1, 1024));
         hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
+                           uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
+        hipLaunchKernelGGL(reduce_short_kernel<TPR>, dim3(grid), dim3(256), 0, st, src, aux, seg, n_uniq, uniq_cap,
                            uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
     };
     const int d4 = dim / 4;
@@ -941,4 +966,21 @@ extern "C" int rf_adam_dense(float* w, const float* g, float* m, float* v, int64
     else
         hipLaunchKernelGGL(adam_dense_flat_kernel<1>, dim3(grid_of(n, 4096)), dim3(256), 0, st, w, g, m, v, n, c);
     return rf_check_launch("rf_adam_dense");
+}
+
+extern "C" int rf_adam_dense_multi(const rf_adam_tensor* tensors, int32_t n_tensors, int64_t max_n, float lr, float beta1,
+                                   float beta2, float epsilon, void* stream) {
+    RF_REQUIRE(n_tensors >= 0 && n_tensors <= 65535 && max_n >= 0, "rf_adam_dense_multi: bad arguments");
+    if (n_tensors == 0 || max_n == 0) return RF_OK;
+    RF_REQUIRE(tensors, "rf_adam_dense_multi: null pointer");
+    AdamCoef c;
+    c.lr = lr;
+    c.b1 = beta1;
+    c.b2 = beta2;
+    c.omb1 = 1.0f - beta1;
+    c.omb2 = 1.0f - beta2;
+    c.eps = epsilon;
+    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((max_n / 4 + 255) / 256, 1024));
+    hipLaunchKernelGGL(adam_dense_multi_kernel, dim3(gx, n_tensors), dim3(256), 0, rf_stream(stream), tensors, c);
+    return rf_check_launch("rf_adam_dense_multi");
 }

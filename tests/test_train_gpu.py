@@ -156,3 +156,30 @@ def test_keras_adam_dense_matches_oracle(O, cuda, n):
     assert np.array_equal(bits(p.detach().cpu().numpy()), bits(w))
     assert np.array_equal(bits(opt.m[0].cpu().numpy()), bits(m))
     assert np.array_equal(bits(opt.v[0].cpu().numpy()), bits(v))
+
+
+def test_keras_adam_multi_tensor_list(O, cuda):
+    """One rf_adam_dense_multi launch over parameters of mixed sizes (scalar and float4 paths) and a parameter
+    without a gradient (skipped, as Keras skips None gradients): each bit-exact vs oracle.adam_dense."""
+    from recommendflow_amd.backend.optim import KerasAdam
+
+    g = torch.Generator().manual_seed(3)
+    sizes = [7, 4096, 1000003, 64]
+    ps = [torch.nn.Parameter(torch.randn(n, generator=g).cuda()) for n in sizes]
+    ref = [(p.detach().cpu().numpy().copy(), np.zeros(p.numel(), np.float32), np.zeros(p.numel(), np.float32)) for p in ps]
+    opt = KerasAdam(ps, learning_rate=0.003)
+    for step in range(1, 4):
+        opt.zero_grad()
+        for i, p in enumerate(ps):
+            if i == 3 and step == 2:
+                continue  # no gradient this step
+            gr = torch.randn(p.numel(), generator=g)
+            p.grad = gr.cuda()
+            w, m, v = ref[i]
+            O.adam_dense(w, gr.numpy(), m, v, O.keras_adam_lr(0.003, 0.9, 0.999, step), 0.9, 0.999, 1e-7)
+        opt.step()
+    torch.cuda.synchronize()
+    for p, (w, m, v), om, ov in zip(ps, ref, opt.m, opt.v):
+        assert np.array_equal(bits(p.detach().cpu().numpy()), bits(w))
+        assert np.array_equal(bits(om.cpu().numpy()), bits(m))
+        assert np.array_equal(bits(ov.cpu().numpy()), bits(v))
