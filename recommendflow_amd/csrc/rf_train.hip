@@ -373,9 +373,12 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
     constexpr int PT = 1024 / TPR;     // positions per pass of the block
     constexpr int P = PPT * PT;        // positions per chunk (one barrier)
     constexpr int kDepth = 8 / PPT;
-    constexpr int G = 8;  // LDS reads in flight per add group
+    constexpr int G4 = 4;  // 16-byte LDS reads in flight per add group (16 positions)
     constexpr int KD = TPR >= 16 ? TPR / 16 : 1;  // float columns per lane of the adding wave (TPR * 4 floats a row)
-    __shared__ float4 buf[2][PPT * 1024];
+    // chunk image transposed, column-major: column j's P values at buf[j * PS + q] (PS = P + 4 keeps the
+    // columns 16-byte aligned for the adding wave's ds_read_b128 of 4 positions and spreads their banks)
+    constexpr int PS = P + 4;
+    __shared__ __attribute__((aligned(16))) float buf[2][TPR * 4 * PS];
     const int t = threadIdx.x, pi = t / TPR, lane = t % TPR;
     const bool active = lane * 4 < D;
     const auto* dout4 = reinterpret_cast<const float4*>(dout);
@@ -420,9 +423,15 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
             for (int k = 0; k < kDepth; ++k) {
                 const int c = c0 + k;
                 if (c < nch) {  // block-uniform
-                    float4* b = buf[c & 1];
+                    float* b = buf[c & 1];
 #pragma unroll
-                    for (int h = 0; h < PPT; ++h) b[h * 1024 + t] = rv[k][h];  // = b[q * TPR + lane]
+                    for (int h = 0; h < PPT; ++h) {  // position q = h * PT + pi, columns lane * 4 .. + 3
+                        float* o = b + (lane * 4) * PS + h * PT + pi;
+                        o[0] = rv[k][h].x;
+                        o[PS] = rv[k][h].y;
+                        o[2 * PS] = rv[k][h].z;
+                        o[3 * PS] = rv[k][h].w;
+                    }
                     __syncthreads();
 #pragma unroll
                     for (int h = 0; h < PPT; ++h) {
@@ -431,27 +440,32 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
                         rs[k][h] = i >= 0 ? src[i] : kZero;
                         ra[k][h] = i >= 0 ? aux[i] : 0u;
                     }
-                    if (t < 64) {  // wave 0, a lane per float column: one add per position and column
+                    if (t < 64) {  // wave 0, a lane per float column: one add per position and column, reading
+                                   // 4 positions of its column per ds_read_b128
                         const int np = min(P, i1 - (i0 + c * P));
-                        const float* bf = reinterpret_cast<const float*>(b);
-                        int col[KD];  // this lane's float columns (a dead lane re-reads column 0; never stored)
+                        const float* col[KD];  // this lane's columns (a dead lane re-reads column 0; never stored)
 #pragma unroll
-                        for (int k = 0; k < KD; ++k) col[k] = k * 64 + t < D ? k * 64 + t : 0;
+                        for (int k = 0; k < KD; ++k) col[k] = b + (k * 64 + t < D ? k * 64 + t : 0) * PS;
                         int q = 0;
-                        for (; q + G <= np; q += G) {
-                            float v[G][KD];
+                        for (; q + 4 * G4 <= np; q += 4 * G4) {
+                            float4 v[G4][KD];
 #pragma unroll
-                            for (int r = 0; r < G; ++r)
+                            for (int r = 0; r < G4; ++r)
 #pragma unroll
-                                for (int k = 0; k < KD; ++k) v[r][k] = bf[(q + r) * (TPR * 4) + col[k]];
+                                for (int k = 0; k < KD; ++k) v[r][k] = *reinterpret_cast<const float4*>(col[k] + q + 4 * r);
 #pragma unroll
-                            for (int r = 0; r < G; ++r)
+                            for (int r = 0; r < G4; ++r)
 #pragma unroll
-                                for (int k = 0; k < KD; ++k) acc[k] += v[r][k];
+                                for (int k = 0; k < KD; ++k) {
+                                    acc[k] += v[r][k].x;
+                                    acc[k] += v[r][k].y;
+                                    acc[k] += v[r][k].z;
+                                    acc[k] += v[r][k].w;
+                                }
                         }
                         for (; q < np; ++q)
 #pragma unroll
-                            for (int k = 0; k < KD; ++k) acc[k] += bf[q * (TPR * 4) + col[k]];
+                            for (int k = 0; k < KD; ++k) acc[k] += col[k][q];
                     }
                 }
             }
