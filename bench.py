@@ -937,19 +937,25 @@ def bench_pipe(args, enc, specs, multi):
                 w.write_many(data, off)
         return int(off[-1])
 
-    def e2e(comp, parse):
+    steady = {}
+
+    def e2e(comp, parse, leg=None):
         out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
         pipe = T.FeaturePipe(paths[comp] * passes, fspecs, B, thread_num=thr, prefetch=3, compression_type=comp,
                              parse=parse)
         torch.cuda.synchronize()
-        t0, m = time.perf_counter(), 0
+        t0, m, t1, m1 = time.perf_counter(), 0, None, 0
         for fb in pipe:
             enc(fb.sparse, out=out[: fb.batch])
             m += fb.batch
+            if t1 is None:  # the pipeline is full once the first batch is out
+                t1, m1 = time.perf_counter(), m
         torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        t2 = time.perf_counter()
         pipe.close()
-        return round(m / dt, 1)
+        if leg is not None and t1 is not None and t2 > t1:
+            steady[leg] = round((m - m1) / (t2 - t1), 1)
+        return round(m / (t2 - t0), 1)
 
     try:
         with ThreadPoolExecutor(n_files) as ex:
@@ -968,10 +974,11 @@ def bench_pipe(args, enc, specs, multi):
         dec = time.perf_counter() - t0
         rd.close()
         e2e("GZIP", "host")  # warm the pinned pools and the allocator
-        legs = {"gzip_host": e2e("GZIP", "host"), "gzip_device": e2e("GZIP", "device")}
+        legs = {"gzip_host": e2e("GZIP", "host", "gzip_host"), "gzip_device": e2e("GZIP", "device", "gzip_device")}
         e2e(None, "device")
-        legs["none_device"] = e2e(None, "device")
+        legs["none_device"] = e2e(None, "device", "none_device")
         return {"pipe_to_encoder_examples_per_s": max(legs.values()), "legs_examples_per_s": legs,
+                "legs_after_first_batch_examples_per_s": steady,
                 "decode_examples_per_s": round(n / dec, 1), "decode_raw_GBs": round(raw / dec / 1e9, 3),
                 "none_device_raw_GBs": round(legs["none_device"] * raw / n / 1e9, 3),
                 "examples": n, "examples_e2e": passes * n, "threads": thr,
@@ -980,7 +987,8 @@ def bench_pipe(args, enc, specs, multi):
                           f"{thr} reader threads, pinned ring of 3, side-stream H2D, fused encoder consumes; end-to-end legs read "
                           f"the file list {passes} times; single-member GZIP inflated by libdeflate (whole file, next files "
                           f"opened ahead); "
-                          f"decode_* = host C++ parse alone on the GZIP files"}
+                          f"decode_* = host C++ parse alone on the GZIP files; legs_after_first_batch_* = the same runs timed from "
+                          f"the first batch out (pipeline full: every slot has inflated its first file) to the last"}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -373,3 +373,18 @@ def test_schema_blob_and_device_check_messages():
     assert msg(b=1, err_type=3, err_feat=3)[1] == "rf_tfr_next_batch: Key: disc. malformed float list (record 41)"
     assert msg(b=1, err_type=4, err_feat=4, err_count=2)[1] == \
         "rf_tfr_next_batch: Key: label. Number of values != expected. Values size: 2 but output shape: [] (record 41)"
+
+
+@pytest.mark.parametrize("compression", [None, "GZIP"])
+def test_writer_crc_every_length_class(tmp_path, compression):
+    """The build's CRC-32C (three interleaved streams over 1024- and 128-byte blocks, then single steps) against
+    the oracle's bitwise CRC on payloads around every block boundary."""
+    rng = np.random.default_rng(8)
+    sizes = [0, 1, 7, 8, 9, 383, 384, 385, 1000, 3071, 3072, 3073, 3456, 3457, 4000, 20000, 65537]
+    recs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    data = np.frombuffer(b"".join(recs), np.uint8)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    p = str(tmp_path / ("c.gz" if compression else "c"))
+    with T.TFRecordWriter(p, compression) as w:
+        w.write_many(data, off)
+    assert TO.read_file(p, compression or "NONE") == recs
