@@ -44,9 +44,25 @@ struct ActRelu { __device__ __forceinline__ float operator()(float x) const { re
 struct ActSelu {
     __device__ __forceinline__ float operator()(float x) const {
         const float alpha = 1.6732632423543772848170429916717f, scale = 1.0507009873554804934193349852946f;
-        return x > 0.f ? scale * x : scale * alpha * (__expf(x) - 1.0f);
+        const float neg = scale * alpha * (__expf(fminf(x, 0.f)) - 1.0f);  // both sides, then a select: no branch
+        return x > 0.f ? scale * x : neg;
     }
 };
+
+// Sum over each 16-lane row of the wave, result in every lane of the row, by DPP (no LDS round trips):
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror. Lane 0's value is bit-identical to
+// the xor butterfly (offsets 1, 2, 4, 8): every step adds the same two partial sums, only commuted.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);  // row_half_mirror
+    v += dpp_mov<0x140>(v);  // row_mirror
+    return v;
+}
 
 // Runs f(Act{}) with the activation resolved once, outside the element loops f contains.
 template <class F>
@@ -472,22 +488,44 @@ __global__ __launch_bounds__(256) void gemm_kernel(const void* __restrict__ xv, 
         }
         return;
     }
-    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r. Values first, stores after (a store in a
+    // per-element branch next to a loaded bias made hipcc wait for every previous store; see gemm_lds_kernel)
+    const int64_t rbase = m0 + wm * WT + lg * 4;
+    const int cbase = n0 + wn * WT + lr;
+    float bv[FR];
+#pragma unroll
+    for (int j = 0; j < FR; ++j) bv[j] = bias ? bias[min(cbase + j * 16, N - 1)] : 0.f;
     with_act(act, [&](auto A) {
 #pragma unroll
-        for (int j = 0; j < FR; ++j) {
-            const int col = n0 + wn * WT + j * 16 + lr;
-            if (col >= N) continue;
-            const float bv = bias ? bias[col] : 0.f;
+        for (int j = 0; j < FR; ++j)
 #pragma unroll
             for (int i = 0; i < FR; ++i)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t row = m0 + wm * WT + i * 16 + lg * 4 + r;
-                    if (row < M) y[row * ldy + col] = A(acc[i][j][r] + bv);
-                }
-        }
+                for (int r = 0; r < 4; ++r) acc[i][j][r] = A(acc[i][j][r] + bv[j]);
     });
+    if (m0 + BT <= M && n0 + BT <= N) {
+#pragma unroll
+        for (int i = 0; i < FR; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float* yr = y + (rbase + i * 16 + r) * ldy + cbase;
+#pragma unroll
+                for (int j = 0; j < FR; ++j) yr[j * 16] = acc[i][j][r];
+            }
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < FR; ++j) {
+        const int col = cbase + j * 16;
+        if (col >= N) continue;
+#pragma unroll
+        for (int i = 0; i < FR; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = rbase + i * 16 + r;
+                if (row < M) y[row * ldy + col] = acc[i][j][r];
+            }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -563,6 +601,40 @@ struct EpiArgs {
     int P;               // partials per row (4 per 128-column tile of the stats GEMM)
 };
 
+// Sum over aligned groups of G consecutive lanes (G = 1, 2, 4), the xor-butterfly order (offsets 1, 2) by DPP
+template <int G>
+__device__ __forceinline__ float lane_group_sum(float v) {
+    static_assert(G == 1 || G == 2 || G == 4, "quad-local groups only");
+    if constexpr (G >= 2) v += dpp_mov<0xB1>(v);  // quad_perm [1,0,3,2]: xor 1
+    if constexpr (G >= 4) v += dpp_mov<0x4E>(v);  // quad_perm [2,3,0,1]: xor 2
+    return v;
+}
+
+// The LN fold's per-row (mu, rstd) from the stats GEMM's P slice partials, TPR threads per row (rows whose
+// partials do not fit gemm_lds_kernel's registers): Chan's combine, the same order as the register path.
+template <int TPR>
+__device__ __forceinline__ void ln_fold_row_stats(const float2* rs2, int P, int K, float eps, int part, int rl,
+                                                  float* srow) {
+    float s1 = 0.f;
+    for (int p = part; p < P; p += TPR) s1 += rs2[p].x;
+    s1 = lane_group_sum<TPR>(s1);
+    const float m = s1 / (float)K;
+    float s2 = 0.f;
+    for (int p = part; p < P; p += TPR) {
+        const int np = min(max(K - p * 32, 0), 32);
+        if (np > 0) {
+            const float2 v = rs2[p];
+            const float dv = v.x - (float)np * m;
+            s2 += v.y + dv * dv / (float)np;
+        }
+    }
+    s2 = lane_group_sum<TPR>(s2);
+    if (part == 0) {
+        srow[2 * rl] = m;
+        srow[2 * rl + 1] = 1.0f / sqrtf(s2 / (float)K + eps);
+    }
+}
+
 // F32: fp32 operands (x and W both fp32) on v_mfma_f32_16x16x4f32, 32 k per 128-byte row: a lane's two 16-byte
 // chunks (k = 4 lg .. 4 lg + 3 and 16 + 4 lg .. 16 + 4 lg + 3) feed 8 MFMAs, A and B in the same permuted k order.
 // SPLIT (split-K, EPI plain only): blockIdx.y = s takes k in [s kspan, min(K, (s + 1) kspan)) and stores raw
@@ -626,37 +698,32 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             pt[j] = 0.f;
         }
     }
-    // LN fold: the tile's row statistics are reduced now too (their partials are complete: the previous
-    // launch wrote them), into an LDS area past the ring, read after the loop; the reduction order is fixed
-    // (TPR threads per row, each a strided subset, then a commutative shuffle combine: every lane the same bits)
+    // LN-fold row statistics (mu, rstd per tile row), in an LDS area past the ring
     float* srow = reinterpret_cast<float*>(smem_raw + (size_t)kLdsStages * (A_EL + B_EL) * sizeof(T));
+    // LN fold: the tile's row statistics (complete: the previous launch wrote them) are combined in a fixed order
+    // (TPR threads per row, each a strided subset, then a commutative lane combine: every lane the same bits).
+    // Their loads are issued here, into registers, and the combine runs after the k-loop, so the two dependent
+    // global round trips are hidden under the MFMAs instead of delaying the first one (P <= NPR * TPR, i.e.
+    // K <= 2048 at BM = 64; longer rows combine before the loop)
+    constexpr int TPR = 256 / BM, NPR = 16;
+    const int rl = tid / TPR, part = tid % TPR;
+    const float2* rs2 = nullptr;
+    float2 sp[NPR];
+    bool stats_late = false;
     if constexpr (EPI == kEpiLnFold) {
-        constexpr int TPR = 256 / BM;
-        const int rl = tid / TPR, part = tid % TPR;
         const int64_t row = m0 + rl < M ? m0 + rl : M - 1;
-        // Chan's combine of the slices: mu = sum S_p / K, M2 = sum M2_p + (S_p - n_p mu)^2 / n_p
-        const float2* rs2 = reinterpret_cast<const float2*>(ea.stats) + row * ea.P;
-        float s1 = 0.f;
-        for (int p = part; p < ea.P; p += TPR) s1 += rs2[p].x;
+        rs2 = reinterpret_cast<const float2*>(ea.stats) + row * ea.P;
+        stats_late = ea.P <= NPR * TPR;
+        if (stats_late) {
 #pragma unroll
-        for (int o = 1; o < TPR; o <<= 1) s1 += __shfl_xor(s1, o, 64);
-        const float m = s1 / (float)K;
-        float s2 = 0.f;
-        for (int p = part; p < ea.P; p += TPR) {
-            const int np = min(max(K - p * 32, 0), 32);
-            if (np > 0) {
-                const float2 v = rs2[p];
-                const float dv = v.x - (float)np * m;
-                s2 += v.y + dv * dv / (float)np;
+            for (int u = 0; u < NPR; ++u) {
+                const int p = part + u * TPR;
+                sp[u] = p < ea.P ? rs2[p] : make_float2(0.f, 0.f);
             }
+        } else {
+            ln_fold_row_stats<TPR>(rs2, ea.P, K, ea.eps, part, rl, srow);
+            __syncthreads();  // srow visible to every wave (this also retires stage 0's copies: the loop waits for them first)
         }
-#pragma unroll
-        for (int o = 1; o < TPR; o <<= 1) s2 += __shfl_xor(s2, o, 64);
-        if (part == 0) {
-            srow[2 * rl] = m;
-            srow[2 * rl + 1] = 1.0f / sqrtf(s2 / (float)K + ea.eps);
-        }
-        __syncthreads();  // srow visible to every wave (this also retires stage 0's copies: the loop waits for them first)
     }
     for (int kt = 0; kt < nk; ++kt) {
         const int s = kt % kLdsStages;
@@ -708,6 +775,32 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             }
         }
     }
+    if constexpr (EPI == kEpiLnFold) {
+        if (stats_late) {
+            // Chan's combine of the slices: mu = sum S_p / K, M2 = sum M2_p + (S_p - n_p mu)^2 / n_p
+            float s1 = 0.f;
+#pragma unroll
+            for (int u = 0; u < NPR; ++u) s1 += sp[u].x;  // zeros past P: the same sum as the strided loop
+            s1 = lane_group_sum<TPR>(s1);
+            const float m = s1 / (float)K;
+            float s2 = 0.f;
+#pragma unroll
+            for (int u = 0; u < NPR; ++u) {
+                const int p = part + u * TPR;
+                const int np = min(max(K - p * 32, 0), 32);
+                if (p < ea.P && np > 0) {
+                    const float dv = sp[u].x - (float)np * m;
+                    s2 += sp[u].y + dv * dv / (float)np;
+                }
+            }
+            s2 = lane_group_sum<TPR>(s2);
+            if (part == 0) {
+                srow[2 * rl] = m;
+                srow[2 * rl + 1] = 1.0f / sqrtf(s2 / (float)K + ea.eps);
+            }
+            __syncthreads();  // srow visible to every wave
+        }
+    }
     if constexpr (SPLIT) {  // raw partial sums
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
@@ -723,42 +816,84 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
         }
         return;
     }
-    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r
+    // epilogue: C/D layout col = lane & 15, row = (lane >> 4) * 4 + r. Values first (straight-line, in acc), stores
+    // after: a store inside a per-element branch next to a use of a loaded value (bias, s_c, t_c) made hipcc put
+    // an s_waitcnt vmcnt(0) in every branch block, so each store waited for the previous one to land
+    // (4096x1280->1024: 20.7 vs 16.8 us with the same main loop). Interior tiles (block-uniform) store unguarded.
+    const bool full = m0 + BM <= M && n0 + kLdsBN <= N;
+    const int64_t rbase = m0 + wm * TM + lg * 4;
+    const int cbase = n0 + wn * TN + lr;
     if constexpr (EPI == kEpiPlain) {
         with_act(act, [&](auto A) {
 #pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] = A(acc[i][j][r] + pb[j]);
+        });
+        if (full) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float* yr = y + (rbase + i * 16 + r) * ldy + cbase;
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) yr[j * 16] = acc[i][j][r];
+                }
+        } else {
+#pragma unroll
             for (int j = 0; j < FN; ++j) {
-                const int col = n0 + wn * TN + j * 16 + lr;
+                const int col = cbase + j * 16;
                 if (col >= N) continue;
-                const float bv = pb[j];
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                        if (row < M) y[row * ldy + col] = A(acc[i][j][r] + bv);
+                        const int64_t row = rbase + i * 16 + r;
+                        if (row < M) y[row * ldy + col] = acc[i][j][r];
                     }
             }
-        });
+        }
     } else if constexpr (EPI == kEpiStats) {
-        // pass 1: activation, bf16 store, and the fp32 value kept in acc (0 past N)
+        // pass 1: activation, the fp32 value kept in acc (0 past N); then the bf16 stores
         with_act(act, [&](auto A) {
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
-                const int col = n0 + wn * TN + j * 16 + lr;
-                const bool cok = col < N;
-                const float bv = cok ? pb[j] : 0.f;
+                const bool cok = cbase + j * 16 < N;
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                        const float v = A(acc[i][j][r] + bv);
+                        const float v = A(acc[i][j][r] + pb[j]);
                         acc[i][j][r] = cok ? v : 0.f;
-                        if (cok && row < M) reinterpret_cast<__bf16*>(ea.yb)[row * ldy + col] = (__bf16)v;  // v_cvt_pk_bf16_f32, RNE
                     }
             }
         });
+        __bf16* yb = reinterpret_cast<__bf16*>(ea.yb);
+        if (full) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    __bf16* yr = yb + (rbase + i * 16 + r) * ldy + cbase;
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) yr[j * 16] = (__bf16)acc[i][j][r];  // v_cvt_pk_bf16_f32, RNE
+                }
+        } else {
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int col = cbase + j * 16;
+                if (col >= N) continue;
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t row = rbase + i * 16 + r;
+                        if (row < M) yb[row * ldy + col] = (__bf16)acc[i][j][r];
+                    }
+            }
+        }
         // pass 2: per 32-column slice (fragments 2q, 2q + 1 of this wave): sum, then squared deviations from the
         // slice mean; slices past N hold (0, 0)
         constexpr int SPW = FN / 2;  // slices per wave (TN = 64: 2; TN = 32: 1)
@@ -771,46 +906,52 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float sm = acc[i][2 * q][r] + acc[i][2 * q + 1][r];
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+                    const float sm = row16_sum(acc[i][2 * q][r] + acc[i][2 * q + 1][r]);
                     const float mq = sm * inv_n;
                     const float d0 = c0 + lr < N ? acc[i][2 * q][r] - mq : 0.f;
                     const float d1 = c0 + 16 + lr < N ? acc[i][2 * q + 1][r] - mq : 0.f;
-                    float m2 = d0 * d0 + d1 * d1;
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) m2 += __shfl_xor(m2, o, 64);
-                    const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
+                    const float m2 = row16_sum(d0 * d0 + d1 * d1);
+                    const int64_t row = rbase + i * 16 + r;
                     if (lr == 0 && row < M)
                         *reinterpret_cast<float2*>(ea.stats + 2 * (row * ea.P + (n0 / kLdsBN) * 4 + wn * SPW + q)) =
                             make_float2(sm, m2);
                 }
         }
     } else {  // kEpiLnFold: the row statistics were reduced into srow before the loop
-        float mu[FM][4], rstd[FM][4];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rl = wm * TM + i * 16 + lg * 4 + r;
-                mu[i][r] = srow[2 * rl];
-                rstd[i][r] = srow[2 * rl + 1];
-            }
         with_act(act, [&](auto A) {
 #pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rl = wm * TM + i * 16 + lg * 4 + r;
+                    const float mu = srow[2 * rl], rstd = srow[2 * rl + 1];
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) acc[i][j][r] = A(rstd * (acc[i][j][r] - mu * pb[j]) + pt[j]);
+                }
+        });
+        if (full) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float* yr = y + (rbase + i * 16 + r) * ldy + cbase;
+#pragma unroll
+                    for (int j = 0; j < FN; ++j) yr[j * 16] = acc[i][j][r];
+                }
+        } else {
+#pragma unroll
             for (int j = 0; j < FN; ++j) {
-                const int col = n0 + wn * TN + j * 16 + lr;
+                const int col = cbase + j * 16;
                 if (col >= N) continue;
-                const float sc = pb[j], tc = pt[j];
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int64_t row = m0 + wm * TM + i * 16 + lg * 4 + r;
-                        if (row < M) y[row * ldy + col] = A(rstd[i][r] * (acc[i][j][r] - mu[i][r] * sc) + tc);
+                        const int64_t row = rbase + i * 16 + r;
+                        if (row < M) y[row * ldy + col] = acc[i][j][r];
                     }
             }
-        });
+        }
     }
 }
 
