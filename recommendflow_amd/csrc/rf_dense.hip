@@ -1155,8 +1155,7 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             xv[j] = 4 * j + sub < K0 ? xv[j] : 0.f;
             s += xv[j];
         }
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
+        s = lane_group_sum<4>(s);
         const float mu = s / (float)K0;
         float q = 0.f;
 #pragma unroll
@@ -1164,8 +1163,7 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             const float d = 4 * j + sub < K0 ? xv[j] - mu : 0.f;
             q += d * d;
         }
-        q += __shfl_xor(q, 1, 64);
-        q += __shfl_xor(q, 2, 64);
+        q = lane_group_sum<4>(q);
         const float rstd = 1.0f / sqrtf(q / (float)K0 + eps);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1214,14 +1212,12 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
     float mu[4], rstd[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) psum[r] += __shfl_xor(psum[r], o, 64);
+        psum[r] = row16_sum(psum[r]);
         mu[r] = psum[r] / (float)H;
         float q = 0.f;
 #pragma unroll
         for (int t = 0; t < T0; ++t) q += (hv[t][r] - mu[r]) * (hv[t][r] - mu[r]);
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+        q = row16_sum(q);
         rstd[r] = 1.0f / sqrtf(q / (float)H + eps);
     }
 #pragma unroll

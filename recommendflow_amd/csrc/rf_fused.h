@@ -652,38 +652,48 @@ __global__ __launch_bounds__(64) void single_token_embed_kernel(
             special = comb == RF_COMB_AVG ? kMeanOfNothing : (comb == RF_COMB_MAX || comb == RF_COMB_MIN) ? initv : 0.0f;
         if (lm > 1 || !ok) special = __builtin_nanf("");
         const bool use_special = lm != 1 || !ok;
+        const bool full = nu == kUnits;  // every team's bag exists: no per-bag guard on the stores
+        // the element rule is wave-uniform per item: resolved once here, not per element (a chain of uniform
+        // branches per element was most of this loop's issue)
+        auto body = [&](auto rule, auto zero_ok) {  // zero_ok: mask_pad zeros apply (not to the special values)
 #pragma unroll
-        for (int g0 = 0; g0 < G; g0 += GH) {
-            uint4 v[GH][2];
+            for (int g0 = 0; g0 < G; g0 += GH) {
+                uint4 v[GH][2];
 #pragma unroll
-            for (int g = 0; g < GH; ++g) {
-                const int j = team + TEAMS * (g0 + g);
-                const uint32_t q0 = (uint32_t)__shfl((int)r0, j, 64), q1 = (uint32_t)__shfl((int)r1, j, 64);
-                v[g][0] = row_chunk(table, q0, dim, tl);
-                v[g][1] = row_chunk(table, q1, dim, tl);
-            }
+                for (int g = 0; g < GH; ++g) {
+                    const int j = team + TEAMS * (g0 + g);
+                    const uint32_t q0 = (uint32_t)__shfl((int)r0, j, 64), q1 = (uint32_t)__shfl((int)r1, j, 64);
+                    v[g][0] = row_chunk(table, q0, dim, tl);
+                    v[g][1] = row_chunk(table, q1, dim, tl);
+                }
 #pragma unroll
-            for (int g = 0; g < GH; ++g) {
-                const int j = team + TEAMS * (g0 + g);
-                const int hj = __shfl(has, j, 64);
-                if (j >= nu) continue;
-                const bool zero = mask_pad && !hj;
-                const int64_t ob = (int64_t)(b0 + j) * out_stride + out_off;
+                for (int g = 0; g < GH; ++g) {
+                    const int j = team + TEAMS * (g0 + g);
+                    const int hj = __shfl(has, j, 64);
+                    if (!full && j >= nu) continue;
+                    const bool zero = mask_pad && !hj;
+                    const int64_t ob = (int64_t)(b0 + j) * out_stride + out_off;
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    float f[EPV], a[EPV];
-                    unpack16<TT>(v[g][k], f);
+                    for (int k = 0; k < 2; ++k) {
+                        float f[EPV], a[EPV];
+                        unpack16<TT>(v[g][k], f);
 #pragma unroll
-                    for (int e = 0; e < EPV; ++e) {
-                        if (use_special) a[e] = special;
-                        else if (zero) a[e] = 0.0f;
-                        else if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) a[e] = __fadd_rn(0.0f, f[e]);
-                        else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) a[e] = comb_step(comb, initv, f[e]);
-                        else a[e] = f[e];
+                        for (int e = 0; e < EPV; ++e) a[e] = (decltype(zero_ok)::value && zero) ? 0.0f : rule(f[e]);
+                        store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + tl * EPV, a);
                     }
-                    store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + tl * EPV, a);
                 }
             }
+        };
+        if (use_special) {
+            body([=](float) { return special; }, std::false_type{});
+        } else if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) {
+            body([](float x) { return __fadd_rn(0.0f, x); }, std::true_type{});
+        } else if (comb == RF_COMB_MAX) {
+            body([](float x) { return comb_step(RF_COMB_MAX, -INFINITY, x); }, std::true_type{});
+        } else if (comb == RF_COMB_MIN) {
+            body([](float x) { return comb_step(RF_COMB_MIN, INFINITY, x); }, std::true_type{});
+        } else {
+            body([](float x) { return x; }, std::true_type{});
         }
     }
 }

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU iteration: encoder / model / graph parity tests, then the full bench line.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-g3}
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread ${TESTS:-tests/test_embed_gpu.py tests/test_models_gpu.py tests/test_graphs_gpu.py tests/test_factory_gpu.py tests/test_cfg1_gpu.py} -m gpu > "$OUT/pytest.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest.log"
+[ $rc = 0 ] || exit $rc
+timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench.log" > "$OUT/bench.json"; exit $rc
