@@ -64,6 +64,14 @@ __device__ __forceinline__ float row16_sum(float v) {
     return v;
 }
 
+// Sum over the whole wave, the same bits in every lane: 16-lane rows by DPP, then rows (0+1) + (2+3)
+__device__ __forceinline__ float wave_sum(float v) {
+    v = row16_sum(v);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+}
+
 // Runs f(Act{}) with the activation resolved once, outside the element loops f contains.
 template <class F>
 __device__ __forceinline__ void with_act(int act, F&& f) {
@@ -138,41 +146,47 @@ __global__ __launch_bounds__(256) void norm_vec_kernel(const float* __restrict__
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
     const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
-    float4 v[NV];
+    // every load first (x, then gamma / beta at clamped columns): the stores below then wait on nothing, and
+    // rows whose NV chunks are all in range store without a branch (a loaded value used inside a per-chunk
+    // branch made hipcc wait for every previous store there)
+    const bool full = 4 * 64 * NV == cols;
+    float4 v[NV], g[NV], bb[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int c4 = lane + 64 * k;
-        v[k] = 4 * c4 < cols ? xr[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k] = full || 4 * c4 < cols ? xr[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int c4 = min(lane + 64 * k, cols / 4 - 1);
+        g[k] = gamma ? reinterpret_cast<const float4*>(gamma)[c4] : make_float4(1.f, 1.f, 1.f, 1.f);
+        bb[k] = beta ? reinterpret_cast<const float4*>(beta)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     float mu = 0.f, rstd = 1.f;
     if (mode == 0) {
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < NV; ++k) s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        s = wave_sum(s);
         mu = s / (float)cols;
         float q = 0.f;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            if (4 * (lane + 64 * k) < cols) {
+            if (full || 4 * (lane + 64 * k) < cols) {
                 const float a = v[k].x - mu, b = v[k].y - mu, c = v[k].z - mu, d = v[k].w - mu;
                 q += (a * a + b * b) + (c * c + d * d);
             }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        q = wave_sum(q);
         rstd = 1.0f / sqrtf(q / (float)cols + eps);
     }
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int c4 = lane + 64 * k;
-        if (4 * c4 >= cols) continue;
-        const float4 g = gamma ? reinterpret_cast<const float4*>(gamma)[c4] : make_float4(1.f, 1.f, 1.f, 1.f);
-        const float4 bb = beta ? reinterpret_cast<const float4*>(beta)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!full && 4 * c4 >= cols) continue;
         float o[4];
         const float xv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-        const float gv[4] = {g.x, g.y, g.z, g.w}, bv[4] = {bb.x, bb.y, bb.z, bb.w};
+        const float gv[4] = {g[k].x, g[k].y, g[k].z, g[k].w}, bv[4] = {bb[k].x, bb[k].y, bb[k].z, bb[k].w};
         if (mode == 0) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (xv[e] - mu) * rstd * gv[e] + bv[e];
@@ -1108,34 +1122,11 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int64_t r0 = (int64_t)blockIdx.x * kMlp2Rows;
     const int c0 = blockIdx.y * kMlp2Cols;
-    // ---- W1 slice and W0 straight into LDS (no registers, nothing for the compiler to sink) ----
-#pragma unroll
-    for (int i = 0; i < NI1 / 4; ++i) {
-        const int g = wave + 4 * i, e = g * 64 + lane;  // chunk index in the LDS image
-        const int row = e / CPR, cp = e % CPR;
-        const int col = c0 + row < O ? c0 + row : O - 1;  // columns past O: any valid row (never stored)
-        const uint16_t* src = W1 + (int64_t)col * H + 8 * (cp ^ (row & 7));
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(w1s + g * 512), 16, 0, 0);
-    }
-    if (VEC0) {
-        const int ni0 = H * K0 * 2 / 1024;
-        for (int g = wave; g < ni0; g += 4)
-            __builtin_amdgcn_global_load_lds(W0 + g * 512 + lane * 8, (__attribute__((address_space(3))) void*)(w0s + g * 512), 16, 0, 0);
-    }
-    // ---- per-column parameters -> LDS (NULL bias / affine: 0 / 1); a dummy valid address, then a select ----
-    {
-        const int n = tid < H ? tid : H - 1;
-        const float vb0 = (b0 ? b0 : g0)[b0 ? n : 0], vg1 = (g1 ? g1 : g0)[g1 ? n : 0], vbe1 = (be1 ? be1 : g0)[be1 ? n : 0];
-        const int n1 = tid & (kMlp2Cols - 1), col = c0 + n1 < O ? c0 + n1 : O - 1;
-        const float vb1 = (b1 ? b1 : g0)[b1 ? col : 0];
-        if (tid < H) {
-            pb0[tid] = b0 ? vb0 : 0.f;
-            pg1[tid] = g1 ? vg1 : 1.f;
-            pbe1[tid] = be1 ? vbe1 : 0.f;
-        }
-        if (tid < kMlp2Cols) pb1[tid] = b1 ? vb1 : 0.f;
-    }
-    // ---- LN0: each wave its 16 rows, 4 lanes per row ----
+    // Issue order: the LN0 inputs first, then W0 and the per-column parameters (LDS-DMA), LN0 itself, and the
+    // 64 KiB W1 slice last, so layer 0 and LN1 (this wave's own rows: no barrier between them) run while the W1
+    // slice lands; vmcnt retires in issue order, so the wait before layer 0 leaves exactly this wave's W1
+    // pieces in flight.
+    // ---- LN0 inputs: each wave its 16 rows, 4 lanes per row ----
     float xv[8], gv[8], bv[8];
     const int xr = 16 * wave + (lane >> 2), sub = lane & 3;
     {
@@ -1146,6 +1137,33 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             xv[j] = x[row * ldx + k];
             gv[j] = g0[k];
             bv[j] = be0[k];
+        }
+    }
+    if (VEC0) {  // W0 as it lies in memory (2 pieces per wave at cfg3)
+        const int ni0 = H * K0 * 2 / 1024;
+        for (int g = wave; g < ni0; g += 4)
+            __builtin_amdgcn_global_load_lds(W0 + g * 512 + lane * 8, (__attribute__((address_space(3))) void*)(w0s + g * 512), 16, 0, 0);
+    }
+    // ---- per-column parameters by LDS-DMA too (one dword per lane, lane-linear; NULL bias / affine: 0 / 1 by
+    //      plain LDS writes): nothing here waits, and vmcnt keeps them ahead of the W1 pieces ----
+    {
+        auto dma4 = [&](const float* src, float* dst) {
+            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+        };
+        if (wave * 64 < H) {
+            if (b0) dma4(b0 + tid, pb0 + wave * 64); else pb0[tid] = 0.f;
+            if (g1) dma4(g1 + tid, pg1 + wave * 64); else pg1[tid] = 1.f;
+            if (be1) dma4(be1 + tid, pbe1 + wave * 64); else pbe1[tid] = 0.f;
+        }
+        if (wave * 64 < kMlp2Cols) {
+            const int col = c0 + tid < O ? c0 + tid : O - 1;  // columns past O: any valid entry (never stored)
+            if (b1) dma4(b1 + col, pb1 + wave * 64); else pb1[tid] = 0.f;
+        }
+    }
+    if (!VEC0) {  // W0 [H][K0] -> LDS [H][32], k zero-padded
+        for (int i = tid; i < H * 32; i += 256) {
+            const int n = i >> 5, k = i & 31;
+            w0s[n * 32 + k] = k < K0 ? W0[(int64_t)n * K0 + k] : (uint16_t)0;
         }
     }
     {
@@ -1171,14 +1189,20 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             xs[xr * RS0 + k] = k < K0 ? (uint16_t)f32_to_bf16_bits((xv[j] - mu) * rstd * gv[j] + bv[j]) : (uint16_t)0;
         }
     }
-    if (!VEC0) {  // W0 [H][K0] -> LDS [H][32], k zero-padded
-        for (int i = tid; i < H * 32; i += 256) {
-            const int n = i >> 5, k = i & 31;
-            w0s[n * 32 + k] = k < K0 ? W0[(int64_t)n * K0 + k] : (uint16_t)0;
-        }
+    __builtin_amdgcn_sched_barrier(0);  // LN0 (it waits for x) stays ahead of the W1 pieces
+    // ---- the W1 slice straight into LDS, last ----
+#pragma unroll
+    for (int i = 0; i < NI1 / 4; ++i) {
+        const int g = wave + 4 * i, e = g * 64 + lane;  // chunk index in the LDS image
+        const int row = e / CPR, cp = e % CPR;
+        const int col = c0 + row < O ? c0 + row : O - 1;  // columns past O: any valid row (never stored)
+        const uint16_t* src = W1 + (int64_t)col * H + 8 * (cp ^ (row & 7));
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(w1s + g * 512), 16, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
-    __syncthreads();
+    // this wave's W0 and parameter pieces landed (its W1 pieces may stay in flight); then every wave's
+    // (a raw s_barrier: __syncthreads' release fence would wait for the W1 pieces too)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI1 / 4) : "memory");
+    __builtin_amdgcn_s_barrier();
     // ---- layer 0 + LN1: this wave's 16 rows x all H columns ----
     const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xs + (16 * wave + lr) * RS0 + lg * 8);
     float hv[T0][4];
@@ -1228,7 +1252,8 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
         for (int r = 0; r < 4; ++r)
             hs[(16 * wave + 4 * lg + r) * RSH + n] = (uint16_t)f32_to_bf16_bits((hv[t][r] - mu[r]) * rstd[r] * gg + bb);
     }
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's W1 pieces landed
+    __syncthreads();                                   // every wave's W1 pieces (hs rows are wave-local)
     // ---- layer 1: this wave's 16 rows x the block's 128 columns ----
     bf16x8 ha[KS];
 #pragma unroll

@@ -54,6 +54,12 @@ class Esim(torch.nn.Module):
         B = user.batch
         cur = torch.cuda.current_stream(dense.device)
         pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=dense.device)
+        if not self.concurrent_input_mlp:
+            self.input_mlp(dense, out=pooled[:, : self.d_emb])
+            q = self.enc_q(user).view(B, self.L, self.d)
+            a = self.enc_a(ad).view(B, self.L, self.d)
+            esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
+            return self.dense_output(self.output_mlp(pooled))
         side = self._side_stream(dense.device)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
@@ -65,6 +71,8 @@ class Esim(torch.nn.Module):
         esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
         cur.wait_stream(side)
         return self.dense_output(self.output_mlp(pooled))
+
+    concurrent_input_mlp = True  # False: the input MLP runs on the current stream ahead of the encoders (A/B)
 
     def _side_stream(self, device):
         s = getattr(self, "_side", None)

@@ -1,7 +1,7 @@
 """rocprof target (diagnostics): the cfg3 ESIM forward as the bench runs it (one hipGraph per forward, two
 resident batches alternating), replayed 40 times; `rocprofv3 --kernel-trace` of this run gives every kernel's
 start/end, so tools/trace_gaps.py can split a forward into kernel time and the idle gaps between kernels.
-    python tools/cfg3_gaps.py [--eager]
+    python tools/cfg3_gaps.py [--eager] [--serial-mlp]
 """
 import os
 import sys
@@ -23,6 +23,8 @@ model = Esim(user, ad, n_dense=16, dim=64, table_dtype=torch.bfloat16, seed=3)
 hu = [synthetic_batch(B, [False] * Ls, seed=77 + i, slot_ids=range(Ls)).to("cuda") for i in range(2)]
 ha = [synthetic_batch(B, [False] * Ls, seed=99 + i, slot_ids=range(Ls, 2 * Ls)).to("cuda") for i in range(2)]
 dense = torch.randn(B, 16, device="cuda")
+if "--serial-mlp" in sys.argv:
+    model.concurrent_input_mlp = False
 if "--eager" in sys.argv:
     run = [lambda p=p: model(hu[p], ha[p], dense) for p in (0, 1)]
 else:

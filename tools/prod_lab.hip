@@ -100,5 +100,64 @@ int main(int argc, char** argv) {
         CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(y)); CK(hipFree(yb)); CK(hipFree(b));
         CK(hipFree(sv)); CK(hipFree(tv)); CK(hipFree(st));
     }
+    // chain: the cfg3 output MLP pair as the forward runs it (stats GEMM 1280 -> 1024 writes bf16 + row statistics,
+    // the LN-fold GEMM 1024 -> 512 consumes them), 20 pairs back to back; under rocprofv3 --kernel-trace each
+    // kernel's duration in the chain can be compared with its isolated, repeated timing above
+    {
+        const int M = 4096, K = 1280, N1 = 1024, N2 = 512;
+        uint16_t *x, *w1, *w2, *yb;
+        float *b1, *st, *sv, *tv, *y;
+        CK(hipMalloc(&x, (size_t)M * K * 2));
+        CK(hipMalloc(&w1, (size_t)N1 * K * 2));
+        CK(hipMalloc(&w2, (size_t)N2 * N1 * 2));
+        CK(hipMalloc(&yb, (size_t)M * N1 * 2));
+        CK(hipMalloc(&y, (size_t)M * N2 * 4));
+        CK(hipMalloc(&b1, (size_t)N1 * 4));
+        CK(hipMalloc(&sv, (size_t)N2 * 4));
+        CK(hipMalloc(&tv, (size_t)N2 * 4));
+        CK(hipMalloc(&st, (size_t)M * 4 * (N1 / 128) * 8));
+        CK(hipMemset(b1, 0, (size_t)N1 * 4));
+        CK(hipMemset(sv, 0, (size_t)N2 * 4));
+        CK(hipMemset(tv, 0, (size_t)N2 * 4));
+        fill_bf16<<<(M * (int64_t)K + 255) / 256, 256>>>(x, (int64_t)M * K, 1, 1.f);
+        fill_bf16<<<(N1 * (int64_t)K + 255) / 256, 256>>>(w1, (int64_t)N1 * K, 2, 0.05f);
+        fill_bf16<<<(N2 * (int64_t)N1 + 255) / 256, 256>>>(w2, (int64_t)N2 * N1, 3, 0.05f);
+        auto pair = [&] {
+            rf_linear_stats_fwd(x, M, K, K, w1, N1, b1, RF_ACT_GELU, yb, N1, st, nullptr);
+            rf_linear_lnfold_fwd(yb, M, N1, N1, w2, N2, sv, tv, st, 1e-6f, RF_ACT_GELU, y, N2, nullptr);
+        };
+        for (int i = 0; i < 3; ++i) pair();
+        hipEvent_t a, e;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&e));
+        std::vector<float> t;
+        for (int r = 0; r < rounds; ++r) {
+            CK(hipEventRecord(a));
+            for (int i = 0; i < 20; ++i) pair();
+            CK(hipEventRecord(e));
+            CK(hipEventSynchronize(e));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, e));
+            t.push_back(ms / 20 * 1000.f);
+        }
+        std::sort(t.begin(), t.end());
+        printf("== chain stats(4096x1280->1024) + lnfold(->512): median %.2f us per pair\n", t[t.size() / 2]);
+        // sustained: 2000 pairs back to back (~70 ms of continuous MFMA load), per-200-pair windows
+        hipEvent_t ev[11];
+        for (auto& x : ev) CK(hipEventCreate(&x));
+        CK(hipEventRecord(ev[0]));
+        for (int w = 0; w < 10; ++w) {
+            for (int i = 0; i < 200; ++i) pair();
+            CK(hipEventRecord(ev[w + 1]));
+        }
+        CK(hipEventSynchronize(ev[10]));
+        printf("   sustained windows (us per pair):");
+        for (int w = 0; w < 10; ++w) {
+            float ms;
+            CK(hipEventElapsedTime(&ms, ev[w], ev[w + 1]));
+            printf(" %.2f", ms / 200 * 1000.f);
+        }
+        printf("\n");
+    }
     return 0;
 }
