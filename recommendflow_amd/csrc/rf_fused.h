@@ -304,51 +304,53 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         if (lean) {
             constexpr int UPT = kUnits / TEAMS;     // bags per team
             constexpr int GU = CPL >= 2 ? 2 : 4;    // bags per load group
-            const float initv = comb_init(comb);
+            // the element rule is wave-uniform per item: resolved once here, not as a chain of uniform branches
+            // per element (as the single-token kernel)
+            auto lean_body = [&](auto rule) __attribute__((always_inline)) {
 #pragma unroll 1
-            for (int q0 = 0; q0 < UPT; q0 += GU) {
-                uint4 v[GU][2][CPL];
-                bool has[GU];
+                for (int q0 = 0; q0 < UPT; q0 += GU) {
+                    uint4 v[GU][2][CPL];
+                    bool has[GU];
 #pragma unroll
-                for (int g = 0; g < GU; ++g) {
-                    const int jj = min(team + TEAMS * (q0 + g), nu - 1);
-                    const int i = s_loc[wave][jj];
-                    has[g] = s_loc[wave][jj + 1] - i == 1;
-                    const uint32_t r0 = has[g] ? s_row[wave][0][i] : pad0;
-                    const uint32_t r1 = has[g] ? s_row[wave][1][i] : pad1;
-#pragma unroll
-                    for (int cc = 0; cc < CPL; ++cc) {
-                        v[g][0][cc] = row_chunk_src<PRE>(table, local_tab, r0, dim, cidx[cc]);
-                        v[g][1][cc] = row_chunk_src<PRE>(table, local_tab, r1, dim, cidx[cc]);
-                    }
-                }
-#pragma unroll
-                for (int g = 0; g < GU; ++g) {
-                    const int j = team + TEAMS * (q0 + g);
-                    if (j >= nu) continue;
-                    const int64_t ob = (int64_t)(b0 + j) * out_stride + out_off;
-                    const bool zero = !has[g] && mask_pad;
-#pragma unroll
-                    for (int k = 0; k < 2; ++k)
+                    for (int g = 0; g < GU; ++g) {
+                        const int jj = min(team + TEAMS * (q0 + g), nu - 1);
+                        const int i = s_loc[wave][jj];
+                        has[g] = s_loc[wave][jj + 1] - i == 1;
+                        const uint32_t r0 = has[g] ? s_row[wave][0][i] : pad0;
+                        const uint32_t r1 = has[g] ? s_row[wave][1][i] : pad1;
 #pragma unroll
                         for (int cc = 0; cc < CPL; ++cc) {
-                            float f[EPV], a[EPV];
-                            unpack16<TT>(v[g][k][cc], f);
-#pragma unroll
-                            for (int e = 0; e < EPV; ++e) {
-                                if (zero) a[e] = 0.0f;
-                                else if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) a[e] = __fadd_rn(0.0f, f[e]);
-                                else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) a[e] = comb_step(comb, initv, f[e]);
-                                else a[e] = f[e];
-                            }
-                            if (!ok) {
-#pragma unroll
-                                for (int e = 0; e < EPV; ++e) a[e] = __builtin_nanf("");
-                            }
-                            if (cown[cc]) store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + cidx[cc] * EPV, a);
+                            v[g][0][cc] = row_chunk_src<PRE>(table, local_tab, r0, dim, cidx[cc]);
+                            v[g][1][cc] = row_chunk_src<PRE>(table, local_tab, r1, dim, cidx[cc]);
                         }
+                    }
+#pragma unroll
+                    for (int g = 0; g < GU; ++g) {
+                        const int j = team + TEAMS * (q0 + g);
+                        if (j >= nu) continue;
+                        const int64_t ob = (int64_t)(b0 + j) * out_stride + out_off;
+                        const bool zero = !has[g] && mask_pad;
+#pragma unroll
+                        for (int k = 0; k < 2; ++k)
+#pragma unroll
+                            for (int cc = 0; cc < CPL; ++cc) {
+                                float f[EPV], a[EPV];
+                                unpack16<TT>(v[g][k][cc], f);
+#pragma unroll
+                                for (int e = 0; e < EPV; ++e) a[e] = zero ? 0.0f : rule(f[e]);
+                                if (!ok) {
+#pragma unroll
+                                    for (int e = 0; e < EPV; ++e) a[e] = __builtin_nanf("");
+                                }
+                                if (cown[cc]) store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + cidx[cc] * EPV, a);
+                            }
+                    }
                 }
-            }
+            };
+            if (comb == RF_COMB_SUM || comb == RF_COMB_AVG) lean_body([](float x) { return __fadd_rn(0.0f, x); });
+            else if (comb == RF_COMB_MAX) lean_body([](float x) { return comb_step(RF_COMB_MAX, -INFINITY, x); });
+            else if (comb == RF_COMB_MIN) lean_body([](float x) { return comb_step(RF_COMB_MIN, INFINITY, x); });
+            else lean_body([](float x) { return x; });
             continue;
         }
 
