@@ -1077,59 +1077,58 @@ __global__ __launch_bounds__(256) void dense_head_kernel(const float* __restrict
 
 // ---------------------------------------------------------------------------------------------
 // Two-layer create_mlp on a narrow input, one launch (the ESIM input_mlp: 16 -> 256 -> 512, LayerNorm,
-// gelu; esim.py:45-48, mlp.py:4-15). A workgroup owns 64 rows x 128 output columns (grid: row blocks x
-// column blocks, 256 workgroups at cfg3), so W1 is read once per workgroup into LDS instead of once per
-// 16 rows from L2:
-//   W1[c0 .. c0+127][:] loads are issued first (registers), then LN0 (K0 <= 32 columns, a 4-lane group
-//   per row, each wave its 16 rows) -> bf16 A tile in LDS (k zero-padded to 32), W0 and the W1 slice
-//   -> LDS;
-//   H = act(A W0^T + b0): wave w computes its 16 rows x all H columns (one 16x16x32 MFMA per column
-//   tile), LN1 over the row entirely inside the wave (16-lane shuffles) -> bf16 rows in LDS
-//   (the layer-0 work is repeated by the O/128 column blocks of a row block: 16 x 256 x 32 per row);
-//   O = act(LN1(H) W1^T + b1) for the wave's 16 rows x the block's 128 columns, fp32 stores into the
-//   caller's strided output.
+// gelu; esim.py:45-48, mlp.py:4-15). v2 (round 3): a workgroup owns 16 rows and EVERY output column
+// (grid = row blocks), 4 waves:
+//   * wave 0 runs LN0 for the 16 rows (4 lanes per row) into a bf16 A tile in LDS (k zero-padded to 32);
+//   * layer 0 H = act(A W0^T + b0) is split over the waves by columns (wave w: H/4 of them), so no
+//     workgroup recomputes it (v1's 64-row x 128-column blocks each redid layer 0 for their column block:
+//     4x the gelu work, and one wave per SIMD left it VALU-issue-bound, 4.4 K VALU per wave, 21.7 us);
+//   * LN1 over the H columns: per-wave row partials (16-lane DPP sums) meet in LDS in wave order (fixed:
+//     deterministic), two passes (mean, then squared deviations) -> bf16 rows in LDS;
+//   * layer 1 O = act(LN1(H) W1^T + b1): wave w takes 128-column blocks w, w + 4, ...; its W1 fragments
+//     (16 B per lane per MFMA) are loaded from L2 into registers at kernel start, so they land while
+//     LN0 / layer 0 / LN1 run (one workgroup per CU: the register budget is the whole SIMD's).
 // ---------------------------------------------------------------------------------------------
-constexpr int kMlp2Rows = 64, kMlp2Cols = 128;
+constexpr int kMlp2Rows = 16, kMlp2Cols = 128;
 
 template <int H>
 constexpr size_t mlp2_lds_bytes() {
-    return 2 * ((size_t)kMlp2Rows * 40 + (size_t)H * 32 + (size_t)kMlp2Rows * (H + 8) + (size_t)kMlp2Cols * H) +
-           4 * (3 * (size_t)H + kMlp2Cols);
+    // xs [16][40] bf16, w0s [H][32] bf16, hs [16][H + 8] bf16, params 3 H floats, row partials [4][16] x 2
+    return 2 * ((size_t)kMlp2Rows * 40 + (size_t)H * 32 + (size_t)kMlp2Rows * (H + 8)) + 4 * (3 * (size_t)H) +
+           4 * 2 * 4 * kMlp2Rows;
 }
 
 // VEC0: K0 % 8 == 0 and H * K0 * 2 a multiple of 1 KiB, so W0 moves by LDS-DMA as it lies in memory.
+// NB: column blocks of 128 per wave pass (O <= 512 in one pass at cfg3).
 template <int H, bool VEC0>
-__global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict__ x, int64_t M, int K0, int64_t ldx, float eps,
-                                                         const float* __restrict__ g0, const float* __restrict__ be0,
-                                                         const uint16_t* __restrict__ W0, const float* __restrict__ b0,
-                                                         const float* __restrict__ g1, const float* __restrict__ be1,
-                                                         const uint16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                         int O, int act, float* __restrict__ out, int64_t ldo) {
+__global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restrict__ x, int64_t M, int K0, int64_t ldx, float eps,
+                                                            const float* __restrict__ g0, const float* __restrict__ be0,
+                                                            const uint16_t* __restrict__ W0, const float* __restrict__ b0,
+                                                            const float* __restrict__ g1, const float* __restrict__ be1,
+                                                            const uint16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                            int O, int act, float* __restrict__ out, int64_t ldo) {
     constexpr int RS0 = 32 + 8, RSH = H + 8;  // LDS row strides (elements) of the A tiles: 16-byte row pad
-    constexpr int T0 = H / 16;                // layer-0 column tiles (all of them, per wave)
+    constexpr int TW = H / 64;                // layer-0 column tiles per wave (H / 4 columns)
     constexpr int KS = H / 32;                // layer-1 k steps
-    constexpr int CPR = H / 8;                // 16-byte chunks per W1 row
-    constexpr int NI1 = kMlp2Cols * H * 2 / 1024;  // W1-slice LDS-DMA wave-instructions (1 KiB each)
+    constexpr int NT = kMlp2Cols / 16;        // layer-1 column tiles per block
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem_raw);
     uint16_t* w0s = xs + kMlp2Rows * RS0;
     uint16_t* hs = w0s + H * 32;
-    uint16_t* w1s = hs + kMlp2Rows * RSH;  // [128][H], chunk c of row r at chunk c ^ (r & 7)
-    float* pb0 = reinterpret_cast<float*>(w1s + kMlp2Cols * H);
+    float* pb0 = reinterpret_cast<float*>(hs + kMlp2Rows * RSH);
     float* pg1 = pb0 + H;
     float* pbe1 = pg1 + H;
-    float* pb1 = pbe1 + H;
+    float* red = pbe1 + H;  // [2][4 waves][16 rows]
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int64_t r0 = (int64_t)blockIdx.x * kMlp2Rows;
-    const int c0 = blockIdx.y * kMlp2Cols;
-    // Issue order: the LN0 inputs first, then W0 and the per-column parameters (LDS-DMA), LN0 itself, and the
-    // 64 KiB W1 slice last, so layer 0 and LN1 (this wave's own rows: no barrier between them) run while the W1
-    // slice lands; vmcnt retires in issue order, so the wait before layer 0 leaves exactly this wave's W1
-    // pieces in flight.
-    // ---- LN0 inputs: each wave its 16 rows, 4 lanes per row ----
+    const int nblk = (O + kMlp2Cols - 1) / kMlp2Cols;
+    // Issue order: wave 0's LN0 inputs, W0 and the per-column parameters by LDS-DMA, then this wave's first
+    // layer-1 block of W1 fragments and bias into registers (16 B per lane per MFMA, from L2): everything is
+    // in flight together and lands in about one memory latency (a wave stalls issuing past 63 outstanding
+    // loads, so the oldest, wave 0's x, must go first).
     float xv[8], gv[8], bv[8];
-    const int xr = 16 * wave + (lane >> 2), sub = lane & 3;
-    {
+    const int xr = lane >> 2, sub = lane & 3;
+    if (wave == 0) {
         const int64_t row = r0 + xr < M ? r0 + xr : M - 1;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1139,14 +1138,17 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             bv[j] = be0[k];
         }
     }
-    if (VEC0) {  // W0 as it lies in memory (2 pieces per wave at cfg3)
+    if (VEC0) {  // W0 as it lies in memory
         const int ni0 = H * K0 * 2 / 1024;
         for (int g = wave; g < ni0; g += 4)
             __builtin_amdgcn_global_load_lds(W0 + g * 512 + lane * 8, (__attribute__((address_space(3))) void*)(w0s + g * 512), 16, 0, 0);
+    } else {  // W0 [H][K0] -> LDS [H][32], k zero-padded
+        for (int i = tid; i < H * 32; i += 256) {
+            const int n = i >> 5, k = i & 31;
+            w0s[n * 32 + k] = k < K0 ? W0[(int64_t)n * K0 + k] : (uint16_t)0;
+        }
     }
-    // ---- per-column parameters by LDS-DMA too (one dword per lane, lane-linear; NULL bias / affine: 0 / 1 by
-    //      plain LDS writes): nothing here waits, and vmcnt keeps them ahead of the W1 pieces ----
-    {
+    {  // per-column parameters by LDS-DMA (one dword per lane, lane-linear; NULL: 0 / 1 by plain LDS writes)
         auto dma4 = [&](const float* src, float* dst) {
             __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
         };
@@ -1155,18 +1157,22 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             if (g1) dma4(g1 + tid, pg1 + wave * 64); else pg1[tid] = 1.f;
             if (be1) dma4(be1 + tid, pbe1 + wave * 64); else pbe1[tid] = 0.f;
         }
-        if (wave * 64 < kMlp2Cols) {
-            const int col = c0 + tid < O ? c0 + tid : O - 1;  // columns past O: any valid entry (never stored)
-            if (b1) dma4(b1 + col, pb1 + wave * 64); else pb1[tid] = 0.f;
-        }
     }
-    if (!VEC0) {  // W0 [H][K0] -> LDS [H][32], k zero-padded
-        for (int i = tid; i < H * 32; i += 256) {
-            const int n = i >> 5, k = i & 31;
-            w0s[n * 32 + k] = k < K0 ? W0[(int64_t)n * K0 + k] : (uint16_t)0;
+    const int cb0 = wave;  // layer-1 column blocks wave, wave + 4, ...
+    bf16x8 wf[NT][KS];
+    float bb1[NT];
+    auto load_w1 = [&](int cb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int col = min(cb * kMlp2Cols + nt * 16 + lr, O - 1);  // columns past O: never stored
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk)
+                wf[nt][kk] = *reinterpret_cast<const bf16x8*>(W1 + (int64_t)col * H + kk * 32 + lg * 8);
+            bb1[nt] = b1 ? b1[col] : 0.f;
         }
-    }
-    {
+    };
+    if (cb0 < nblk) load_w1(cb0);
+    if (wave == 0) {
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1189,27 +1195,14 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
             xs[xr * RS0 + k] = k < K0 ? (uint16_t)f32_to_bf16_bits((xv[j] - mu) * rstd * gv[j] + bv[j]) : (uint16_t)0;
         }
     }
-    __builtin_amdgcn_sched_barrier(0);  // LN0 (it waits for x) stays ahead of the W1 pieces
-    // ---- the W1 slice straight into LDS, last ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's W0 / parameter pieces (and W1 fragments) landed
+    __syncthreads();
+    // ---- layer 0: the 16 rows x this wave's H / 4 columns ----
+    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xs + lr * RS0 + lg * 8);
+    float hv[TW][4];
 #pragma unroll
-    for (int i = 0; i < NI1 / 4; ++i) {
-        const int g = wave + 4 * i, e = g * 64 + lane;  // chunk index in the LDS image
-        const int row = e / CPR, cp = e % CPR;
-        const int col = c0 + row < O ? c0 + row : O - 1;  // columns past O: any valid row (never stored)
-        const uint16_t* src = W1 + (int64_t)col * H + 8 * (cp ^ (row & 7));
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(w1s + g * 512), 16, 0, 0);
-    }
-    // this wave's W0 and parameter pieces landed (its W1 pieces may stay in flight); then every wave's
-    // (a raw s_barrier: __syncthreads' release fence would wait for the W1 pieces too)
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NI1 / 4) : "memory");
-    __builtin_amdgcn_s_barrier();
-    // ---- layer 0 + LN1: this wave's 16 rows x all H columns ----
-    const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xs + (16 * wave + lr) * RS0 + lg * 8);
-    float hv[T0][4];
-    float psum[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < T0; ++t) {
-        const int n = t * 16 + lr;
+    for (int t = 0; t < TW; ++t) {
+        const int n = wave * (H / 4) + t * 16 + lr;
         bf16x8 bw;
         if (VEC0) {
             const bool live = lg * 8 < K0;  // k chunk lg exists; else its A lanes are zero and B must be too
@@ -1225,60 +1218,101 @@ __global__ __launch_bounds__(256) void mlp2_small_kernel(const float* __restrict
     }
     with_act(act, [&](auto A) {
 #pragma unroll
-        for (int t = 0; t < T0; ++t)
+        for (int t = 0; t < TW; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) hv[t][r] = A(hv[t][r]);
     });
-#pragma unroll
-    for (int t = 0; t < T0; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) psum[r] += hv[t][r];
+    // ---- LN1: row partials of this wave's columns (C layout: row = 4 lg + r, column lr) meet in LDS ----
     float mu[4], rstd[4];
+    {
+        float ps[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        psum[r] = row16_sum(psum[r]);
-        mu[r] = psum[r] / (float)H;
-        float q = 0.f;
+        for (int r = 0; r < 4; ++r) {
+            float t0 = 0.f;
 #pragma unroll
-        for (int t = 0; t < T0; ++t) q += (hv[t][r] - mu[r]) * (hv[t][r] - mu[r]);
-        q = row16_sum(q);
-        rstd[r] = 1.0f / sqrtf(q / (float)H + eps);
+            for (int t = 0; t < TW; ++t) t0 += hv[t][r];
+            ps[r] = row16_sum(t0);
+        }
+        if (lr == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[wave * kMlp2Rows + 4 * lg + r] = ps[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * lg + r;
+            mu[r] = (((red[row] + red[kMlp2Rows + row]) + red[2 * kMlp2Rows + row]) + red[3 * kMlp2Rows + row]) / (float)H;
+            float t0 = 0.f;
+#pragma unroll
+            for (int t = 0; t < TW; ++t) t0 += (hv[t][r] - mu[r]) * (hv[t][r] - mu[r]);
+            ps[r] = row16_sum(t0);
+        }
+        float* red2 = red + 4 * kMlp2Rows;
+        if (lr == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red2[wave * kMlp2Rows + 4 * lg + r] = ps[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 4 * lg + r;
+            const float q = ((red2[row] + red2[kMlp2Rows + row]) + red2[2 * kMlp2Rows + row]) + red2[3 * kMlp2Rows + row];
+            rstd[r] = 1.0f / sqrtf(q / (float)H + eps);
+        }
     }
 #pragma unroll
-    for (int t = 0; t < T0; ++t) {
-        const int n = t * 16 + lr;
+    for (int t = 0; t < TW; ++t) {
+        const int n = wave * (H / 4) + t * 16 + lr;
         const float gg = pg1[n], bb = pbe1[n];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            hs[(16 * wave + 4 * lg + r) * RSH + n] = (uint16_t)f32_to_bf16_bits((hv[t][r] - mu[r]) * rstd[r] * gg + bb);
+            hs[(4 * lg + r) * RSH + n] = (uint16_t)f32_to_bf16_bits((hv[t][r] - mu[r]) * rstd[r] * gg + bb);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's W1 pieces landed
-    __syncthreads();                                   // every wave's W1 pieces (hs rows are wave-local)
-    // ---- layer 1: this wave's 16 rows x the block's 128 columns ----
+    __syncthreads();
+    // ---- layer 1: the 16 rows x this wave's 128-column blocks ----
     bf16x8 ha[KS];
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) ha[kk] = *reinterpret_cast<const bf16x8*>(hs + (16 * wave + lr) * RSH + kk * 32 + lg * 8);
-    with_act(act, [&](auto A) {
-    #pragma unroll
-        for (int nt = 0; nt < kMlp2Cols / 16; ++nt) {
-            const int rr = nt * 16 + lr;
-            f4 c = f4{0.f, 0.f, 0.f, 0.f};
-    #pragma unroll
-            for (int kk = 0; kk < KS; ++kk) {
-                const bf16x8 bw = *reinterpret_cast<const bf16x8*>(w1s + rr * H + 8 * ((kk * 4 + lg) ^ (rr & 7)));
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[kk], bw, c, 0, 0, 0);
+    for (int kk = 0; kk < KS; ++kk) ha[kk] = *reinterpret_cast<const bf16x8*>(hs + lr * RSH + kk * 32 + lg * 8);
+    const bool rows_full = r0 + kMlp2Rows <= M;
+    for (int cb = cb0; cb < nblk; cb += 4) {
+        if (cb != cb0) {
+            load_w1(cb);
+        }
+        f4 c[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            c[nt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) c[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[kk], wf[nt][kk], c[nt], 0, 0, 0);
+        }
+        with_act(act, [&](auto A) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) c[nt][r] = A(c[nt][r] + bb1[nt]);
+        });
+        // values first, stores after (see gemm_lds_kernel's epilogue)
+        const int c0 = cb * kMlp2Cols;
+        if (rows_full && c0 + kMlp2Cols <= O) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float* yr = out + (r0 + 4 * lg + r) * ldo + c0 + lr;
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) yr[nt * 16] = c[nt][r];
             }
-            const int n = c0 + rr;
-            const float bb = pb1[rr];
-            if (n < O) {
-    #pragma unroll
+        } else {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int n = c0 + nt * 16 + lr;
+                if (n >= O) continue;
+#pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int64_t row = r0 + 16 * wave + 4 * lg + r;
-                    if (row < M) out[row * ldo + n] = A(c[r] + bb);
+                    const int64_t row = r0 + 4 * lg + r;
+                    if (row < M) out[row * ldo + n] = c[nt][r];
                 }
             }
         }
-    });
+    }
 }
 
 }  // namespace
@@ -1294,7 +1328,7 @@ extern "C" int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t 
     if (M == 0) return RF_OK;
     RF_REQUIRE(x && W0 && W1 && out && ln0_gamma && ln0_beta, "rf_mlp2_small_fwd: null pointer");
     RF_REQUIRE(((uintptr_t)W1 & 15) == 0 && ((uintptr_t)W0 & 15) == 0, "rf_mlp2_small_fwd: W0 / W1 must be 16-byte aligned");
-    const dim3 grid((unsigned)((M + kMlp2Rows - 1) / kMlp2Rows), (unsigned)((O + kMlp2Cols - 1) / kMlp2Cols));
+    const dim3 grid((unsigned)((M + kMlp2Rows - 1) / kMlp2Rows));
     hipStream_t st = rf_stream(stream);
     const bool vec0 = (K0 & 7) == 0 && (H * K0 * 2) % 1024 == 0;
     auto kern = H == 256 ? (vec0 ? mlp2_small_kernel<256, true> : mlp2_small_kernel<256, false>)

@@ -47,10 +47,10 @@ class Esim(torch.nn.Module):
                                   seed=seed + 30, device=device)
 
     def forward(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor) -> torch.Tensor:
-        """The input MLP (dense features only) runs on a side stream, concurrently with the two encoders and
-        the attention: it is a latency-bound launch of 256 workgroups that the encoders' tails leave room
-        for. It writes pooled[:, :d_emb], the attention pooled[:, d_emb:]; the output MLP waits for both
-        (also inside a hipGraph capture: the fork/join become graph edges)."""
+        """The input MLP (dense features only) writes pooled[:, :d_emb], the attention pooled[:, d_emb:]. By
+        default it runs first on the current stream; concurrent_input_mlp = True puts it on a side stream
+        beside the two encoders (the output MLP waits for both; inside a hipGraph capture the fork/join
+        become graph edges)."""
         B = user.batch
         cur = torch.cuda.current_stream(dense.device)
         pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=dense.device)
@@ -72,7 +72,10 @@ class Esim(torch.nn.Module):
         cur.wait_stream(side)
         return self.dense_output(self.output_mlp(pooled))
 
-    concurrent_input_mlp = True  # False: the input MLP runs on the current stream ahead of the encoders (A/B)
+    # True: the input MLP on a side stream beside the encoders. Measured (tools/cfg3_gaps.py, graph-replayed
+    # forward, profiles/r03/r03b6_*): with mlp2_small v2 the serial order is faster (0.2601-0.2604 vs
+    # 0.2638-0.2665 ms: the side launch slowed both encoder launches by ~2.4 us each and adds a fork/join)
+    concurrent_input_mlp = False
 
     def _side_stream(self, device):
         s = getattr(self, "_side", None)

@@ -81,9 +81,9 @@ def test_esim_cfg3_shape_vs_oracle(O, cuda):
     assert (p.argmax(1) == want.argmax(1)).mean() >= 0.999
     fwd = model.graphed(du, da, dd)
     assert torch.equal(fwd(du, da, dd), p_gpu)
-    # the input MLP on the current stream ahead of the encoders (the A/B switch) gives the same bits
-    model.concurrent_input_mlp = False
+    # the input MLP on a side stream beside the encoders (the A/B switch) gives the same bits
+    model.concurrent_input_mlp = True
     try:
         assert torch.equal(model(du, da, dd), p_gpu)
     finally:
-        model.concurrent_input_mlp = True
+        model.concurrent_input_mlp = False

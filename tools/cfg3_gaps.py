@@ -23,8 +23,7 @@ model = Esim(user, ad, n_dense=16, dim=64, table_dtype=torch.bfloat16, seed=3)
 hu = [synthetic_batch(B, [False] * Ls, seed=77 + i, slot_ids=range(Ls)).to("cuda") for i in range(2)]
 ha = [synthetic_batch(B, [False] * Ls, seed=99 + i, slot_ids=range(Ls, 2 * Ls)).to("cuda") for i in range(2)]
 dense = torch.randn(B, 16, device="cuda")
-if "--serial-mlp" in sys.argv:
-    model.concurrent_input_mlp = False
+model.concurrent_input_mlp = "--serial-mlp" not in sys.argv
 if "--eager" in sys.argv:
     run = [lambda p=p: model(hu[p], ha[p], dense) for p in (0, 1)]
 else:
