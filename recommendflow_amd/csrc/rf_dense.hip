@@ -1025,9 +1025,12 @@ __global__ __launch_bounds__(256) void dense_head_kernel(const float* __restrict
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
     const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
-    float acc[NMAX];
+    float acc[NMAX], bv[NMAX];
 #pragma unroll
-    for (int n = 0; n < NMAX; ++n) acc[n] = 0.f;
+    for (int n = 0; n < NMAX; ++n) {
+        acc[n] = 0.f;
+        bv[n] = bias ? bias[min(n, N - 1)] : 0.f;  // loaded now: not a dependent round trip after the sums
+    }
     for (int k4 = lane; 4 * k4 < K; k4 += 64) {
         const float4 xv = xr[k4];
 #pragma unroll
@@ -1052,9 +1055,7 @@ __global__ __launch_bounds__(256) void dense_head_kernel(const float* __restrict
 #pragma unroll
     for (int n = 0; n < NMAX; ++n) {
         if (n < N) {
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) acc[n] += __shfl_xor(acc[n], o, 64);
-            acc[n] += bias ? bias[n] : 0.f;
+            acc[n] = wave_sum(acc[n]) + bv[n];
             if (act != RF_ACT_SOFTMAX) acc[n] = act_apply(act, acc[n]);
             mx = fmaxf(mx, acc[n]);
         }

@@ -158,6 +158,28 @@ int main(int argc, char** argv) {
             printf(" %.2f", ms / 200 * 1000.f);
         }
         printf("\n");
+        // the forward's order: LayerNorm (fp32 [M, 1280] -> bf16 x) writes the stats GEMM's input right before it
+        float* xf;
+        CK(hipMalloc(&xf, (size_t)M * K * 4));
+        CK(hipMemset(xf, 0, (size_t)M * K * 4));
+        fill_bf16<<<(M * (int64_t)K + 255) / 256, 256>>>(x, (int64_t)M * K, 1, 1.f);
+        auto tri = [&] {
+            rf_norm_fwd(xf, M, K, K, 0, 1e-6f, nullptr, nullptr, nullptr, nullptr, x, RF_DTYPE_BF16, K, nullptr);
+            pair();
+        };
+        for (int i = 0; i < 3; ++i) tri();
+        std::vector<float> t3;
+        for (int r = 0; r < rounds; ++r) {
+            CK(hipEventRecord(a));
+            for (int i = 0; i < 20; ++i) tri();
+            CK(hipEventRecord(e));
+            CK(hipEventSynchronize(e));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, e));
+            t3.push_back(ms / 20 * 1000.f);
+        }
+        std::sort(t3.begin(), t3.end());
+        printf("== chain LayerNorm(1280, fp32 -> bf16) + stats + lnfold: median %.2f us per triple\n", t3[t3.size() / 2]);
     }
     return 0;
 }
