@@ -376,7 +376,7 @@ def bench_esim(args):
     pooled = torch.empty((B, model.pooled_width), device="cuda")
     from recommendflow_amd.backend.layers.attention_layers import esim_soft_attention_pool
 
-    par = {"s": 0, "f": 0, "e": 0}
+    par = {"s": 0, "f": 0, "e": 0, "i": 0}
 
     def nxt(k):
         par[k] ^= 1
@@ -409,8 +409,22 @@ def bench_esim(args):
     g_att, g_in, g_mlp = CapturedGraph(att), CapturedGraph(in_mlp), CapturedGraph(mlp)
     g_full = [CapturedGraph(lambda p=p: fwd(p)) for p in (0, 1)]
 
-    _, per = _time_stages([("sparse_encoders", lambda: g_enc[nxt("s")].replay()), ("input_mlp", g_in.replay),
-                           ("esim_attention", g_att.replay), ("mlp_scorer", g_mlp.replay)], steps, 3)
+    # the forward's stages: with Esim.gather (single-valued slots, bf16 tables) the attention gathers the token
+    # rows by id and the encoders' q / a are never written: input_mlp -> token_ids -> esim_gather_attention ->
+    # mlp_scorer; the unfused stages (encoders writing q / a, then the attention) are timed beside them
+    gather = model._gather_ok(hu[0], ha[0])
+    stages = [("input_mlp", g_in.replay)]
+    if gather:
+        ids_p = [model.token_ids(hu[p], ha[p]) for p in (0, 1)]
+        g_ids = [CapturedGraph(lambda p=p: model.token_ids(hu[p], ha[p])) for p in (0, 1)]
+        g_gat = CapturedGraph(lambda: model.attention_gather(ids_p[0][0], ids_p[0][1], pooled))
+        stages += [("token_ids", lambda: g_ids[nxt("i")].replay()), ("esim_gather_attention", g_gat.replay)]
+    else:
+        stages += [("sparse_encoders", lambda: g_enc[nxt("s")].replay()), ("esim_attention", g_att.replay)]
+    stages += [("mlp_scorer", g_mlp.replay)]
+    _, per = _time_stages(stages, steps, 3)
+    _, per_u = _time_stages([("sparse_encoders", lambda: g_enc[nxt("s")].replay()), ("esim_attention", g_att.replay)],
+                            steps, 3)
     wall, _ = _time_stages([("forward", lambda: g_full[nxt("f")].replay())], steps, 3)
     att_flops = 2 * Ls * Ls * 128 * 3 * B
     mlp_flops = sum(2 * dn.in_features * dn.units for dn in model.output_mlp.denses) * B + 2 * model.dense_output.in_features * 2 * B
@@ -422,16 +436,21 @@ def bench_esim(args):
     return {"examples_per_s": round(B / wall * 1e3, 1), "ms_per_step": round(wall, 4), "launch": "hipGraph",
             "eager_ms_per_step": round(eager_wall, 4), "cpu_baseline": cpu,
             "stage_ms": {k: round(v, 4) for k, v in per.items()},
-            "encoder_GBs": round(enc_bytes / per["sparse_encoders"] / 1e6, 1),
+            "gather_path": gather,
+            "unfused_stage_ms": {k: round(v, 4) for k, v in per_u.items()},
+            "encoder_GBs": round(enc_bytes / per_u["sparse_encoders"] / 1e6, 1),
             "encoder_frac_of_measured_gather_ceiling": (
-                round(enc_bytes / per["sparse_encoders"] / 1e6 / args.probes["gather_copy_128B_GBs"], 4)
+                round(enc_bytes / per_u["sparse_encoders"] / 1e6 / args.probes["gather_copy_128B_GBs"], 4)
                 if isinstance(getattr(args, "probes", None), dict) and args.probes.get("gather_copy_128B_GBs") else None),
-            "esim_TFLOPs": round(att_flops / per["esim_attention"] / 1e9, 1),
-            "esim_mfma_frac_of_2500TF": round(att_flops / per["esim_attention"] / 1e9 / 2500, 4),
+            "esim_TFLOPs": round(att_flops / per_u["esim_attention"] / 1e9, 1),
+            "esim_mfma_frac_of_2500TF": round(att_flops / per_u["esim_attention"] / 1e9 / 2500, 4),
+            "esim_gather_TFLOPs": round(att_flops / per["esim_gather_attention"] / 1e9, 1) if gather else None,
             "mlp_TFLOPs": round(mlp_flops / per["mlp_scorer"] / 1e9, 1),
             "stages_note": "each stage is its own replayed hipGraph (graph launch included); the forward runs "
-                           "input_mlp -> encoders -> attention -> mlp_scorer on one stream; "
-                           "mlp_scorer = output MLP + Dense(2, softmax); mlp_TFLOPs over those GEMMs",
+                           "input_mlp -> token_ids -> esim_gather_attention (rows gathered by id inside the "
+                           "attention kernel) -> mlp_scorer on one stream; unfused_stage_ms = the encoders writing "
+                           "q / a and the attention reading them (encoder_GBs, esim_TFLOPs); mlp_scorer = output MLP "
+                           "+ Dense(2, softmax); mlp_TFLOPs over those GEMMs",
             "config": "200 slots (100 q + 100 a) x 1M bins/hash, D=64 bf16 (tables 51.2 GB), L=100, d=128, "
                       "input_mlp 16->256->512, output_mlp 1280->1024->512, Dense(2, softmax), bf16 MFMA"}
 

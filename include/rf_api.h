@@ -282,6 +282,24 @@ int rf_dense_head_fwd(const float* x, int64_t M, int32_t K, int64_t ldx, const v
                       int32_t N, const float* b, int32_t act, float* y, int64_t ldy, void* stream);
 
 /*
+ * The ESIM forward without the encoders' [B, L, 2D] outputs (cfg3; esim.py:78-84 over the DoubleHashingEmbedding
+ * tokens, preprocess_layers.py:82-97): rf_single_token_ids_fwd writes, for every unit u = b * n_slots + s of a
+ * batch whose slots all have batch Lmax == 1, ids[u][k] = the fused-table row of hash k of the bag's token (the
+ * index half of rf_fused_hash_embed_fwd with RF_FLAG_SINGLE_TOKEN; an empty bag: the slot's pad rows, or
+ * 0xffffffff = the zero row under RF_FLAG_MASK_PADDING; a slot whose Lmax is not 1 or that does not fit the
+ * table: 0xfffffffe = the NaN row). rf_esim_gather_fwd then runs rf_esim_soft_attention_fwd's kernel with
+ * each example's q / a images gathered from q_table / a_table (BF16 [rows][d / 2]) by those ids; spec holds the
+ * NaN row then the zero row (BF16 [2][d / 2]). Same pooled outputs as encoders + rf_esim_soft_attention_fwd
+ * (x enters the statistics through the selector MFMA, so a -0 in a table row gives the +0 the encoder writes).
+ */
+int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
+                            const int32_t* bag_off, const int32_t* lmax, int32_t batch, int64_t table_rows, uint32_t* ids,
+                            int32_t flags, void* stream);
+int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
+                       int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
+                       int64_t out_stride, int64_t out_off, void* stream);
+
+/*
  * Masked scaled-dot-product attention over heads (backend/layers/layer_utils.py:4-24, with the
  * split_heads / merge transposes of MultiHeadAttention.call, attention_layers.py:159-167, folded
  * into the addressing):

@@ -344,6 +344,14 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 __host__ __device__ constexpr size_t esim2_lds_bytes(int D, int ntt, int rs) {
     return (size_t)2 * ntt * 16 * rs * 2 + (size_t)kEsim2Waves * 3 * 2 * D * 4 + (D == 64 ? 128 * 16 : 0);
 }
+// offset of the GATHER id buffers past the statistics (and the d = 64 dummy area), from the statistics base
+__host__ __device__ constexpr size_t esim2_stats_dummy_bytes(int D) {
+    return (size_t)kEsim2Waves * 3 * 2 * D * 4 + (D == 64 ? 128 * 16 : 0);
+}
+// the GATHER kernel's LDS: the same images (row stride of the plain kernel) + two id buffers of 4 x 16 ntt dwords
+__host__ __device__ constexpr size_t esim2_gather_lds_bytes(int D, int ntt, int rs) {
+    return esim2_lds_bytes(D, ntt, rs) + (size_t)2 * 4 * 16 * ntt * 4;
+}
 __host__ __device__ constexpr int esim2_rs(int D, int ntt) {
     return esim2_lds_bytes(D, ntt, D + 16) <= 80 * 1024 ? D + 16 : D + 8;
 }
@@ -622,11 +630,25 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
     }
 }
 
-template <bool F16, int D, int NTT, int XM>
+// GATHER (rf_esim_gather_fwd): the q / a images are gathered from the two fused tables by row id (a token's
+// row = [table row of hash 0 | table row of hash 1], D / 2 elements each) instead of read from the encoders'
+// [B, L, D] outputs, which are then never written: the single-token ids (rf_single_token_ids_fwd) of example
+// e + 2G are LDS-DMA'd while e computes, and the staging of e + G reads its ids from LDS (double-buffered), so
+// no dependent global round trip sits in front of a compute phase.
+struct EsimGatherArgs {
+    const uint32_t* qid;   // [batch][L][2]
+    const uint32_t* aid;
+    const uint16_t* qtab;  // [rows][D / 2]
+    const uint16_t* atab;
+    const uint16_t* spec;  // [2][D / 2]: a NaN row (id kRowNaN), a zero row (id kRowZero)
+};
+
+template <bool F16, int D, int NTT, int XM, bool GATHER = false>
 __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
                                                                      const uint16_t* __restrict__ a, int batch, int L,
                                                                      int64_t ex_stride, int64_t ld, float* __restrict__ out,
-                                                                     int64_t out_stride, int64_t out_off) {
+                                                                     int64_t out_stride, int64_t out_off,
+                                                                     EsimGatherArgs ga = {}) {
     using M = Mfma<F16>;
     constexpr int NTH = kEsim2Waves * 64;
     constexpr int RS = esim2_rs(D, NTT);
@@ -661,6 +683,34 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     // a chunk of a row past the image (only where 16-row tiles end inside a 256-chunk group: d = 64, odd
     // tile counts) goes to this thread's slot of the dummy area past the statistics
     uint16_t* dummy = reinterpret_cast<uint16_t*>(st + kEsim2Waves * 3 * 2 * D) + (tid & 127) * 8;
+    // GATHER: two id buffers past the dummy area, each [side][row < L][hash] (4 L dwords used of IDW)
+    constexpr int IDW = 4 * L16;
+    uint32_t* idb = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(st) + esim2_stats_dummy_bytes(D));
+    auto ids_dma = [&](int64_t ee, int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < (IDW + NTH - 1) / NTH; ++j) {
+            const int w = tid + j * NTH;
+            if (w < 4 * L) {
+                const uint32_t* src = w < 2 * L ? ga.qid + ee * 2 * L + w : ga.aid + ee * 2 * L + (w - 2 * L);
+                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(idb + buf * IDW + j * NTH + wave * 64), 4, 0, 0);
+            }
+        }
+    };
+    auto prefetch_g = [&](int buf) __attribute__((always_inline)) {
+        constexpr int HC = CPR / 2;  // 16-byte chunks per table row
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int cm = tid + (i % HALF) * NTH;
+            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
+            const int side = i < HALF ? 0 : 1;
+            const uint32_t idl = idb[buf * IDW + side * 2 * L + 2 * min(r, L - 1) + (ch >= HC ? 1 : 0)];
+            const uint32_t id = r < L ? idl : kRowZero;
+            const uint16_t* tab = side ? ga.atab : ga.qtab;
+            const uint16_t* src = id >= kRowNaN ? ga.spec + (id & 1u) * (D / 2) : tab + (int64_t)id * (D / 2);
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>(src + (ch & (HC - 1)) * 8));
+        }
+    };
     int64_t e = blockIdx.x;
     uint32_t it = 0;
     // the pooled features of the previous example, stored one example late (right before the next prefetch):
@@ -692,15 +742,31 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
             }
         }
     };
+    int pbuf = 0;  // GATHER: the id buffer holding example e's ids (the other: e + G's)
     if (e < batch) {
-        prefetch(e);
+        if constexpr (GATHER) {
+            ids_dma(e, 0);
+            __syncthreads();  // (its release fence waits for the DMA) ids of e visible
+            prefetch_g(0);
+            if (e + gridDim.x < batch) ids_dma(e + gridDim.x, 1);
+        } else {
+            prefetch(e);
+        }
         stage_images();
         __syncthreads();
     }
     for (; e < batch; e += gridDim.x) {
         if (pe >= 0) flush();
         const bool more = e + gridDim.x < batch;
-        if (more) prefetch(e + gridDim.x);
+        if constexpr (GATHER) {
+            if (more) {
+                prefetch_g(pbuf ^ 1);
+                if (e + 2 * (int64_t)gridDim.x < batch) ids_dma(e + 2 * (int64_t)gridDim.x, pbuf);
+            }
+            pbuf ^= 1;
+        } else if (more) {
+            prefetch(e + gridDim.x);
+        }
 
         // v3: the stripe pairs rotate over the waves from one example to the next, so the wave left with one
         // stripe (7 tiles over 4 waves) is a different SIMD each time; statistics slots follow the stripe
@@ -898,7 +964,7 @@ int launch_esim2_nt(int grid, size_t lds, hipStream_t st, const void* q, const v
     const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, (const uint16_t*)q, (const uint16_t*)a, batch, L,
-                       ex_stride, ld, out, out_stride, out_off);
+                       ex_stride, ld, out, out_stride, out_off, EsimGatherArgs{});
     return RF_OK;
 }
 
@@ -928,6 +994,29 @@ int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, i
                        : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
     return d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
                    : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
+}
+
+// GATHER: bf16 tables, the v5 statistics, two workgroups per CU when images + id buffers fit 80 KB
+template <int D, int NTT>
+int launch_esim2g_nt(int grid, size_t lds, hipStream_t st, int batch, int L, float* out, int64_t out_stride,
+                     int64_t out_off, const EsimGatherArgs& ga) {
+    auto kern = esim2_kernel<false, D, NTT, 1, true>;
+    const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel (gather)");
+    if (rc) return rc;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, nullptr, nullptr, batch, L, (int64_t)0,
+                       (int64_t)D, out, out_stride, out_off, ga);
+    return RF_OK;
+}
+
+template <int D>
+int launch_esim2g(int nt, int grid, size_t lds, hipStream_t st, int batch, int L, float* out, int64_t out_stride,
+                  int64_t out_off, const EsimGatherArgs& ga) {
+    switch (nt) {
+#define RF_NT(N) case N: return launch_esim2g_nt<D, N>(grid, lds, st, batch, L, out, out_stride, out_off, ga);
+        RF_NT(1) RF_NT(2) RF_NT(3) RF_NT(4) RF_NT(5) RF_NT(6) RF_NT(7) RF_NT(8)
+#undef RF_NT
+        default: return rf_set_error(RF_EINVAL, "esim2 gather: bad tile count %d", nt);
+    }
 }
 
 }  // namespace
@@ -1007,4 +1096,30 @@ extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t 
     }
 #undef RF_SDPA_LAUNCH
     return rf_check_launch("sdpa_kernel");
+}
+
+extern "C" int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
+                                  int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
+                                  int64_t out_stride, int64_t out_off, void* stream) {
+    RF_REQUIRE(dtype == RF_DTYPE_BF16, "rf_esim_gather_fwd: tables must be BF16");
+    RF_REQUIRE(L >= 1 && L <= 128, "rf_esim_gather_fwd: need 1 <= L <= 128 (got %d)", L);
+    RF_REQUIRE(d == 64 || d == 128, "rf_esim_gather_fwd: d must be 64 or 128 (got %d)", d);
+    RF_REQUIRE(batch >= 0, "rf_esim_gather_fwd: batch < 0");
+    if (batch == 0) return RF_OK;
+    RF_REQUIRE(q_ids && a_ids && q_table && a_table && spec && out, "rf_esim_gather_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)q_table & 15) == 0 && ((uintptr_t)a_table & 15) == 0 && ((uintptr_t)spec & 15) == 0 &&
+                   ((uintptr_t)q_ids & 3) == 0 && ((uintptr_t)a_ids & 3) == 0,
+               "rf_esim_gather_fwd: tables / spec must be 16-byte and ids 4-byte aligned");
+    hipStream_t st = rf_stream(stream);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int nt = (L + 15) >> 4;
+    const size_t lds = esim2_gather_lds_bytes(d, nt, esim2_rs(d, nt));
+    const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+    const int grid = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
+    const EsimGatherArgs ga{q_ids, a_ids, (const uint16_t*)q_table, (const uint16_t*)a_table, (const uint16_t*)spec};
+    const int rc = d == 64 ? launch_esim2g<64>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga)
+                           : launch_esim2g<128>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga);
+    if (rc) return rc;
+    return rf_check_launch("rf_esim_gather_fwd");
 }

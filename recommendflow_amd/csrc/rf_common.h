@@ -18,6 +18,10 @@ int rf_check_launch(const char* what);  // hipGetLastError -> RF_EHIP with messa
 
 static inline hipStream_t rf_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// special row ids of the single-token id pass (rf_single_token_ids_fwd) and the ESIM gather staging: the zero row
+// (masked empty bag / rows past L) and the NaN row (a slot that does not fit the table, or whose Lmax is not 1)
+constexpr uint32_t kRowZero = 0xffffffffu, kRowNaN = 0xfffffffeu;
+
 // ---------------------------------------------------------------------------------------------
 // wave helpers
 // ---------------------------------------------------------------------------------------------

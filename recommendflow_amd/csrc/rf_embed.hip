@@ -255,6 +255,78 @@ static int fused_hash_embed_fwd_impl(uint32_t allowed_diag, const rf_slot_desc* 
                             table, table_rows, dim, out, out_stride, flags, idx_out, grid, st);
 }
 
+namespace {
+// The index half of the single-token kernel (rf_single_token_ids_fwd; the ESIM gather path, rf_attn.hip):
+// ids[u][k] = the fused-table row of hash k for unit u = b * n_slots + s (its one token; an empty bag: the
+// slot's pad rows, or kRowZero when padding is masked); a slot whose batch Lmax is not 1, or that does not fit
+// the table, gets kRowNaN (the embedding kernel writes NaN there). One wave per item (a slot x 64 bags),
+// lane j hashes bag b0 + j exactly as single_token_embed_kernel does.
+__global__ __launch_bounds__(64) void single_token_ids_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
+                                                             const uint8_t* __restrict__ tok_bytes,
+                                                             const int32_t* __restrict__ tok_off,
+                                                             const int32_t* __restrict__ bag_off,
+                                                             const int32_t* __restrict__ lmax, int64_t n_units,
+                                                             int64_t table_rows, uint32_t* __restrict__ ids, int flags) {
+    const int lane = threadIdx.x;
+    const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
+    const int batch = (int)(n_units / n_slots);
+    const int nbb = (batch + kUnits - 1) / kUnits;
+    const int64_t n_items = (int64_t)n_slots * nbb;
+    for (int64_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+        const int s = (int)(item / nbb);
+        const int b0 = (int)(item - (int64_t)s * nbb) * kUnits;
+        const int nu = min(kUnits, batch - b0);
+        if (lane >= nu) continue;
+        const rf_slot_desc* sd = slots + s;
+        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
+        const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
+        const int mask_empty = sd->mask_empty;
+        const BucketMod bmod = bucket_mod_init(nbins, mask_empty);
+        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
+        const int64_t u = (int64_t)(b0 + lane) * n_slots + s;
+        uint32_t r0 = kRowNaN, r1 = kRowNaN;
+        if (ok && lmax[s] == 1) {
+            const int t = bag_off[u];
+            if (bag_off[u + 1] > t) {
+                const int tb = tok_off[t], n = tok_off[t + 1] - tb;
+                uint64_t h0, h1;
+                siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
+                r0 = (uint32_t)(rb0 + bucket_from_hash(h0, n, bmod));
+                r1 = (uint32_t)(rb1 + bucket_from_hash(h1, n, bmod));
+            } else if (mask_pad) {
+                r0 = r1 = kRowZero;
+            } else {
+                int64_t pb0 = 0, pb1 = 0;
+                if (!mask_empty) {
+                    pb0 = (int64_t)(siphash24_dev(salt0, salt0, tok_bytes, 0) % (uint64_t)nbins);
+                    pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
+                }
+                r0 = (uint32_t)(rb0 + pb0);
+                r1 = (uint32_t)(rb1 + pb1);
+            }
+        }
+        *reinterpret_cast<uint2*>(ids + 2 * u) = make_uint2(r0, r1);
+    }
+}
+
+}  // namespace
+
+extern "C" int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                       const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
+                                       int32_t batch, int64_t table_rows, uint32_t* ids, int32_t flags, void* stream) {
+    RF_REQUIRE(n_slots >= 1 && batch >= 0, "rf_single_token_ids_fwd: need n_slots >= 1, batch >= 0");
+    RF_REQUIRE((flags & ~RF_FLAG_MASK_PADDING) == 0, "rf_single_token_ids_fwd: only RF_FLAG_MASK_PADDING is accepted");
+    RF_REQUIRE(table_rows >= 1 && table_rows < (int64_t)kRowNaN, "rf_single_token_ids_fwd: table_rows must be in [1, 2^32 - 2)");
+    const int64_t n_units = (int64_t)batch * n_slots;
+    if (n_units == 0) return RF_OK;
+    RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && lmax && ids, "rf_single_token_ids_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)ids & 7) == 0, "rf_single_token_ids_fwd: ids must be 8-byte aligned");
+    const int64_t items = (int64_t)n_slots * ((batch + kUnits - 1) / kUnits);
+    hipLaunchKernelGGL(single_token_ids_kernel, dim3(grid_for(items, 1, 256 * 32 * 2)), dim3(64), 0, rf_stream(stream),
+                       d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table_rows, ids, flags);
+    return rf_check_launch("single_token_ids_kernel");
+}
+
 extern "C" int rf_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
                                        const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
                                        int32_t batch, const void* table, int32_t table_dtype, int64_t table_rows,

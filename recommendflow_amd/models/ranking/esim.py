@@ -56,9 +56,12 @@ class Esim(torch.nn.Module):
         pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=dense.device)
         if not self.concurrent_input_mlp:
             self.input_mlp(dense, out=pooled[:, : self.d_emb])
-            q = self.enc_q(user).view(B, self.L, self.d)
-            a = self.enc_a(ad).view(B, self.L, self.d)
-            esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
+            if self._gather_ok(user, ad):
+                self._esim_gather(user, ad, pooled)
+            else:
+                q = self.enc_q(user).view(B, self.L, self.d)
+                a = self.enc_a(ad).view(B, self.L, self.d)
+                esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
             return self.dense_output(self.output_mlp(pooled))
         side = self._side_stream(dense.device)
         side.wait_stream(cur)
@@ -76,6 +79,54 @@ class Esim(torch.nn.Module):
     # forward, profiles/r03/r03b6_*): with mlp2_small v2 the serial order is faster (0.2601-0.2604 vs
     # 0.2638-0.2665 ms: the side launch slowed both encoder launches by ~2.4 us each and adds a fork/join)
     concurrent_input_mlp = False
+
+    # True: the attention gathers its q / a token rows from the tables by id (rf_single_token_ids_fwd ->
+    # rf_esim_gather_fwd) when every slot of both batches is single-valued, bf16 tables; the encoders'
+    # [B, L, 2D] outputs are then never written. Bit-identical to the encoder path
+    # (test_esim_gather_equals_encoders_plus_attention); cfg3 forward 0.2616 -> 0.1843 ms
+    # (profiles/r03/r03b7_cfg3_gather_trace.txt). False: encoders + rf_esim_soft_attention_fwd.
+    gather = True
+
+    def _gather_ok(self, user: SparseBatch, ad: SparseBatch) -> bool:
+        eq, ea = self.enc_q, self.enc_a
+        return (self.gather and isinstance(eq, FusedSparseEncoder) and isinstance(ea, FusedSparseEncoder)
+                and eq.table.dtype == torch.bfloat16 and ea.table.dtype == torch.bfloat16
+                and 2 * eq.dim == self.d and 2 * ea.dim == self.d and self.d in (64, 128) and self.L <= 128
+                and not eq.extra_flags and not ea.extra_flags
+                and eq._single_token_batch(user) and ea._single_token_batch(ad))
+
+    def token_ids(self, user: SparseBatch, ad: SparseBatch):
+        """(q_ids, a_ids) [B, L, 2] int32: each token's two fused-table rows (rf_single_token_ids_fwd)."""
+        from ...runtime import lib as L
+
+        B, dev = user.batch, self.enc_q.table.device
+        ids = []
+        for enc, b in ((self.enc_q, user), (self.enc_a, ad)):
+            if not b.is_device():
+                b = b.to(dev)
+            t = torch.empty((B, self.L, 2), dtype=torch.int32, device=dev)
+            L.call("rf_single_token_ids_fwd", L.ptr(enc.desc), len(enc.slots), L.ptr(b.tok_bytes), L.ptr(b.tok_off),
+                   L.ptr(b.bag_off), L.ptr(b.lmax), B, enc.table.shape[0], L.ptr(t),
+                   L.FLAG_MASK_PADDING if enc.mask_padding else 0, L.stream_ptr(None))
+            ids.append(t)
+        return ids[0], ids[1]
+
+    def attention_gather(self, q_ids: torch.Tensor, a_ids: torch.Tensor, pooled: torch.Tensor):
+        """The ESIM attention + pooling into pooled[:, d_emb:], its q / a images gathered by id (rf_esim_gather_fwd)."""
+        from ...runtime import lib as L
+
+        dev = pooled.device
+        spec = getattr(self, "_spec", None)
+        if spec is None or spec.device != dev:
+            spec = torch.zeros((2, self.d // 2), dtype=torch.bfloat16, device=dev)
+            spec[0] = float("nan")  # the NaN row (id 0xfffffffe), then the zero row (0xffffffff)
+            self._spec = spec
+        L.call("rf_esim_gather_fwd", L.ptr(q_ids), L.ptr(a_ids), L.ptr(self.enc_q.table), L.ptr(self.enc_a.table),
+               L.DT_BF16, q_ids.shape[0], self.L, self.d, L.ptr(spec), L.ptr(pooled), pooled.stride(0), self.d_emb,
+               L.stream_ptr(None))
+
+    def _esim_gather(self, user: SparseBatch, ad: SparseBatch, pooled: torch.Tensor):
+        self.attention_gather(*self.token_ids(user, ad), pooled)
 
     def _side_stream(self, device):
         s = getattr(self, "_side", None)

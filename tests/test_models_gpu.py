@@ -87,3 +87,41 @@ def test_esim_cfg3_shape_vs_oracle(O, cuda):
         assert torch.equal(model(du, da, dd), p_gpu)
     finally:
         model.concurrent_input_mlp = False
+
+
+@pytest.mark.parametrize("mask_padding", [False, True])
+def test_esim_gather_equals_encoders_plus_attention(cuda, mask_padding):
+    """rf_single_token_ids_fwd -> rf_esim_gather_fwd (the attention gathers its token rows by id) against the
+    encoders' [B, L, 2D] outputs -> rf_esim_soft_attention_fwd: the same pooled features and the same forward,
+    bit for bit (100 + 100 single-valued slots, some bags empty: pad rows, or the zero row when masked)."""
+    Ls, B = 100, 300
+    user = [SlotSpec(f"u{i:03d}", 20_000, (2022, 2023)) for i in range(Ls)]
+    ad = [SlotSpec(f"a{i:03d}", 20_000, (2022, 2023)) for i in range(Ls)]
+    encs = (FusedSparseEncoder(user, 64, table_dtype=torch.bfloat16, seed=4, mask_padding=mask_padding),
+            FusedSparseEncoder(ad, 64, table_dtype=torch.bfloat16, seed=5, mask_padding=mask_padding))
+    model = Esim(user, ad, n_dense=16, dim=64, seed=3, encoders=encs)
+    from recommendflow_amd.runtime.batch import from_lists
+    rng = np.random.default_rng(7)
+
+    def rows(tag):
+        return [[[] if rng.random() < 0.05 else [f"{tag}{s}_{int(rng.integers(0, 5000))}"] for s in range(Ls)]
+                for _ in range(B)]
+
+    hu, ha = from_lists(rows("u")).to("cuda"), from_lists(rows("a")).to("cuda")
+    dense = torch.randn(B, 16, generator=torch.Generator().manual_seed(9)).cuda()
+    model.gather = False
+    want = model(hu, ha, dense)
+    pw = torch.zeros((B, model.pooled_width), device="cuda")
+    q = model.enc_q(hu).view(B, Ls, 128)
+    a = model.enc_a(ha).view(B, Ls, 128)
+    from recommendflow_amd.backend.layers.attention_layers import esim_soft_attention_pool
+    esim_soft_attention_pool(q, a, out=pw, out_col=model.d_emb)
+    model.gather = True
+    assert model._gather_ok(hu, ha)
+    pg = torch.zeros_like(pw)
+    model._esim_gather(hu, ha, pg)
+    torch.cuda.synchronize()
+    assert torch.equal(pg[:, model.d_emb:], pw[:, model.d_emb:])
+    assert torch.equal(model(hu, ha, dense), want)
+    fwd = model.graphed(hu, ha, dense)
+    assert torch.equal(fwd(hu, ha, dense), want)
