@@ -69,15 +69,19 @@ class Esim(torch.nn.Module):
             self.input_mlp(dense, out=pooled[:, : self.d_emb])
         pooled.record_stream(side)
         dense.record_stream(side)
-        q = self.enc_q(user).view(B, self.L, self.d)
-        a = self.enc_a(ad).view(B, self.L, self.d)
-        esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
+        if self._gather_ok(user, ad):
+            self._esim_gather(user, ad, pooled)
+        else:
+            q = self.enc_q(user).view(B, self.L, self.d)
+            a = self.enc_a(ad).view(B, self.L, self.d)
+            esim_soft_attention_pool(q, a, out=pooled, out_col=self.d_emb)
         cur.wait_stream(side)
         return self.dense_output(self.output_mlp(pooled))
 
-    # True: the input MLP on a side stream beside the encoders. Measured (tools/cfg3_gaps.py, graph-replayed
-    # forward, profiles/r03/r03b6_*): with mlp2_small v2 the serial order is faster (0.2601-0.2604 vs
-    # 0.2638-0.2665 ms: the side launch slowed both encoder launches by ~2.4 us each and adds a fork/join)
+    # True: the input MLP on a side stream beside the encoders / the id pass. Measured (tools/cfg3_gaps.py,
+    # graph-replayed forward): serial is faster in both forms — encoders 0.2601-0.2604 vs 0.2638-0.2665 ms
+    # (profiles/r03/r03b6_*: the side launch slowed both encoder launches by ~2.4 us each), gather path
+    # 0.1802-0.1815 vs 0.1883 ms (r03b9: the id launches 12.7 -> 15.5 us beside it, plus the fork/join)
     concurrent_input_mlp = False
 
     # True: the attention gathers its q / a token rows from the tables by id (rf_single_token_ids_fwd ->
