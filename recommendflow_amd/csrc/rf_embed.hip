@@ -309,6 +309,54 @@ __global__ __launch_bounds__(64) void single_token_ids_kernel(const rf_slot_desc
     }
 }
 
+
+// The same ids, example-major (round 3): thread per unit u = b * n_slots + s, so the bag_off / tok_off reads and
+// the ids stores of a wave are consecutive (the slot-major kernel touches 64 units n_slots apart per load and
+// store); each workgroup first prepares every slot's bucket modulus into LDS (one 64-bit division per slot).
+constexpr int kIdsMaxSlots = 512;
+__global__ __launch_bounds__(256) void single_token_ids_em_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
+                                                                 const uint8_t* __restrict__ tok_bytes,
+                                                                 const int32_t* __restrict__ tok_off,
+                                                                 const int32_t* __restrict__ bag_off,
+                                                                 const int32_t* __restrict__ lmax, int64_t n_units,
+                                                                 int64_t table_rows, uint32_t* __restrict__ ids, int flags) {
+    __shared__ BucketMod sbm[kIdsMaxSlots];
+    for (int s = threadIdx.x; s < n_slots; s += blockDim.x) sbm[s] = bucket_mod_init(slots[s].num_bins, slots[s].mask_empty);
+    __syncthreads();
+    const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += (int64_t)gridDim.x * blockDim.x) {
+        const int s = (int)(u % n_slots);
+        const rf_slot_desc* sd = slots + s;
+        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
+        const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
+        const int mask_empty = sd->mask_empty;
+        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
+        uint32_t r0 = kRowNaN, r1 = kRowNaN;
+        if (ok && lmax[s] == 1) {
+            const int t = bag_off[u];
+            if (bag_off[u + 1] > t) {
+                const int tb = tok_off[t], n = tok_off[t + 1] - tb;
+                uint64_t h0, h1;
+                siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
+                const BucketMod bmod = sbm[s];
+                r0 = (uint32_t)(rb0 + bucket_from_hash(h0, n, bmod));
+                r1 = (uint32_t)(rb1 + bucket_from_hash(h1, n, bmod));
+            } else if (mask_pad) {
+                r0 = r1 = kRowZero;
+            } else {
+                int64_t pb0 = 0, pb1 = 0;
+                if (!mask_empty) {
+                    pb0 = (int64_t)(siphash24_dev(salt0, salt0, tok_bytes, 0) % (uint64_t)nbins);
+                    pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
+                }
+                r0 = (uint32_t)(rb0 + pb0);
+                r1 = (uint32_t)(rb1 + pb1);
+            }
+        }
+        *reinterpret_cast<uint2*>(ids + 2 * u) = make_uint2(r0, r1);
+    }
+}
+
 }  // namespace
 
 extern "C" int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
@@ -321,6 +369,16 @@ extern "C" int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_sl
     if (n_units == 0) return RF_OK;
     RF_REQUIRE(d_slots && tok_bytes && tok_off && bag_off && lmax && ids, "rf_single_token_ids_fwd: null pointer");
     RF_REQUIRE(((uintptr_t)ids & 7) == 0, "rf_single_token_ids_fwd: ids must be 8-byte aligned");
+    static const int slot_major = [] {  // RF_IDS_SLOT_MAJOR=1: the slot-major kernel (A/B only)
+        const char* e = getenv("RF_IDS_SLOT_MAJOR");
+        return e && e[0] == '1';
+    }();
+    if (n_slots <= kIdsMaxSlots && !slot_major) {
+        const int64_t blocks = std::min<int64_t>((n_units + 255) / 256, 256 * 32);
+        hipLaunchKernelGGL(single_token_ids_em_kernel, dim3((unsigned)blocks), dim3(256), 0, rf_stream(stream), d_slots,
+                           n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table_rows, ids, flags);
+        return rf_check_launch("single_token_ids_em_kernel");
+    }
     const int64_t items = (int64_t)n_slots * ((batch + kUnits - 1) / kUnits);
     hipLaunchKernelGGL(single_token_ids_kernel, dim3(grid_for(items, 1, 256 * 32 * 2)), dim3(64), 0, rf_stream(stream),
                        d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table_rows, ids, flags);
