@@ -1,7 +1,7 @@
 """rocprof target (diagnostics): the cfg3 ESIM forward as the bench runs it (one hipGraph per forward, two
 resident batches alternating), replayed 40 times; `rocprofv3 --kernel-trace` of this run gives every kernel's
 start/end, so tools/trace_gaps.py can split a forward into kernel time and the idle gaps between kernels.
-    python tools/cfg3_gaps.py [--eager] [--serial-mlp] [--gather]
+    python tools/cfg3_gaps.py [--eager] [--serial-mlp] [--gather] [--uniform]
 """
 import os
 import sys
@@ -20,8 +20,9 @@ B, Ls = 4096, 100
 user = [SlotSpec(f"u{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)]
 ad = [SlotSpec(f"a{i:03d}", 1_000_000, (2022, 2023)) for i in range(Ls)]
 model = Esim(user, ad, n_dense=16, dim=64, table_dtype=torch.bfloat16, seed=3)
-hu = [synthetic_batch(B, [False] * Ls, seed=77 + i, slot_ids=range(Ls)).to("cuda") for i in range(2)]
-ha = [synthetic_batch(B, [False] * Ls, seed=99 + i, slot_ids=range(Ls, 2 * Ls)).to("cuda") for i in range(2)]
+uni = "--uniform" in sys.argv  # uniform ids (no Zipf-hot rows) instead of Zipf(1.1)
+hu = [synthetic_batch(B, [False] * Ls, seed=77 + i, slot_ids=range(Ls), uniform=uni).to("cuda") for i in range(2)]
+ha = [synthetic_batch(B, [False] * Ls, seed=99 + i, slot_ids=range(Ls, 2 * Ls), uniform=uni).to("cuda") for i in range(2)]
 dense = torch.randn(B, 16, device="cuda")
 model.concurrent_input_mlp = "--serial-mlp" not in sys.argv
 model.gather = "--gather" in sys.argv
