@@ -470,7 +470,11 @@ def cpu_baseline_cfg3(model, q, a, dense, budget_s, sample=512):
     bo = model.dense_output.bias.cpu().numpy()
     cpu_model, ncpu = host_cpu()
     r = timed_runs(lambda: O.esim_scorer_f32(qs, as_, ds, pin, pout, Wo, bo), sample, budget_s / 2, warmup=2)
-    return dict(r, unit="examples/s", cores=int(os.environ.get("OMP_NUM_THREADS", ncpu)), kind="port", cpu=cpu_model,
+    usable, src = usable_cpus()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    cores = min(int(omp), usable) if omp else usable
+    return dict(r, unit="examples/s", cores=cores, cores_source=f"numpy BLAS threads: {'OMP_NUM_THREADS' if omp else 'all usable CPUs'}; {src}",
+                kind="port", cpu=cpu_model,
                 host_cpus=ncpu, sample=f"{r['runs']} x {sample} cfg3 examples through oracle.esim_scorer_f32 (SoftAttention, "
                                        f"ESIM combine/pool, input/output MLPs, Dense(2, softmax); float32 numpy/BLAS) "
                                        f"in {r['seconds']} s; the sparse encoders are not included")
@@ -1170,6 +1174,36 @@ def host_cpu():
     return model, os.cpu_count() or 1
 
 
+def usable_cpus():
+    """The CPUs this process may use: its scheduler affinity (os.sched_getaffinity), capped by a cgroup CPU quota
+    when one is set (cgroup v2 cpu.max, v1 cfs_quota / cfs_period). Returns (count, how it was derived)."""
+    import math
+
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, math.ceil(quota)))
+    src = f"os.sched_getaffinity(0) = {aff} CPUs" + ("" if quota is None else f", cgroup CPU quota {quota:g}")
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp:
+        src += f" (OMP_NUM_THREADS={omp} in the environment, not used)"
+    return n, src
+
+
 def timed_runs(fn, examples, budget_s, warmup=5, min_runs=5):
     """SURVEY §8d CPU protocol: `warmup` untimed runs, then runs until budget_s has passed (at least
     min_runs); examples/s as the total rate, the median and the p90 of the per-run rates."""
@@ -1192,12 +1226,12 @@ def cpu_baseline(enc, hb, budget_s):
     """The C oracle (OpenMP) on the same batch: examples/s, median and p90 per batch."""
     from oracle import oracle as O
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, cores_src = usable_cpus()
     model, ncpu = host_cpu()
     table = enc.table.cpu().numpy()
     r = timed_runs(lambda: O.fused_hash_embed(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, hb.batch,
                                               table, enc.dim, enc.out_width, n_threads=threads), hb.batch, budget_s)
-    return dict(r, unit="examples/s", cores=threads, kind="port", cpu=model, host_cpus=ncpu,
+    return dict(r, unit="examples/s", cores=threads, cores_source=cores_src, kind="port", cpu=model, host_cpus=ncpu,
                 sample=f"{r['runs']} x one {hb.batch}-example cfg2 batch through oracle/rf_oracle.c "
                        f"(orf_fused_hash_embed_fwd, OpenMP {threads} threads, gcc -O3) after 5 warm-up runs, "
                        f"{r['seconds']} s; median / p90 are per-batch rates")

@@ -469,12 +469,20 @@ __device__ __forceinline__ typename M::frag stripe_selector(int sp, int lr, int 
     return f;
 }
 
+// Diagnostic phase stamps (rf_diag_esim_gather_stamped only; STAMP = false compiles them out): the low 32 bits of
+// the shader clock, one vector store from lane 0 of the wave into the caller's buffer
+__device__ __forceinline__ void esim_stamp(uint32_t* p, int k, int lane) {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_s_memtime();
+    if (lane == 0) __builtin_nontemporal_store(t, p + k);
+}
+constexpr int kStampPts = 10;  // stamps per (wave, example)
+
 // KT0 = sp0 >> 1: the P @ V k-step holding stripe sp0's rows (sp1 = sp0 + 4: k-step KT0 + 2), a template
 // parameter so the selector MFMAs are placed at compile time and each half's P @ V is one basic block (a runtime
 // wave-uniform test split it into per-k-step blocks, each waiting out its own LDS reads before its MFMAs)
-template <typename M, int D, int NTT, bool TWO, int XM = 0, int KT0 = 0>
+template <typename M, int D, int NTT, bool TWO, int XM = 0, int KT0 = 0, bool STAMP = false>
 __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
-                                           int lane) {
+                                           int lane, uint32_t* stp = nullptr) {
     constexpr int nt = NTT;
     using frag = typename M::frag;
     constexpr int RS = esim2_rs(D, NTT);
@@ -517,11 +525,16 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
                 }
             }
         }
+        if constexpr (STAMP) esim_stamp(stp, 7, lane);  // scores done
         stripe_softmax3<M, NTT>(e0, L, lg, sp0 * 16 + lr < L, pa0);
         if (TWO) stripe_softmax3<M, NTT>(e1, L, lg, sp1 * 16 + lr < L, pa1);
     }
+    if constexpr (STAMP) esim_stamp(stp, 8, lane);  // softmax done
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
+        if constexpr (STAMP) {
+            if (side == 1) esim_stamp(stp, 9, lane);  // side 0 done
+        }
         const uint16_t* V = side ? as : qs;
         f4 c0[NT], c1[NT];
 #pragma unroll
@@ -641,9 +654,11 @@ struct EsimGatherArgs {
     const uint16_t* qtab;  // [rows][D / 2]
     const uint16_t* atab;
     const uint16_t* spec;  // [2][D / 2]: a NaN row (id kRowNaN), a zero row (id kRowZero)
+    uint32_t* stamps;      // STAMP only: [grid][waves][stamp_ex][kStampPts]
+    int stamp_ex;
 };
 
-template <bool F16, int D, int NTT, int XM, bool GATHER = false>
+template <bool F16, int D, int NTT, int XM, bool GATHER = false, bool STAMP = false>
 __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
                                                                      const uint16_t* __restrict__ a, int batch, int L,
                                                                      int64_t ex_stride, int64_t ld, float* __restrict__ out,
@@ -698,17 +713,32 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     };
     auto prefetch_g = [&](int buf) __attribute__((always_inline)) {
         constexpr int HC = CPR / 2;  // 16-byte chunks per table row
+        // every id read from LDS first, then the row loads: left to itself hipcc interleaves them as
+        // read -> lgkmcnt(0) -> address -> load per chunk, NCH dependent LDS round trips per example
+        uint32_t idv[NCH];
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int cm = tid + (i % HALF) * NTH;
             const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
             const int side = i < HALF ? 0 : 1;
-            const uint32_t idl = idb[buf * IDW + side * 2 * L + 2 * min(r, L - 1) + (ch >= HC ? 1 : 0)];
-            const uint32_t id = r < L ? idl : kRowZero;
+            idv[i] = idb[buf * IDW + side * 2 * L + 2 * min(r, L - 1) + (ch >= HC ? 1 : 0)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+            const int cm = tid + (i % HALF) * NTH;
+            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
+            const int side = i < HALF ? 0 : 1;
+            const uint32_t id = r < L ? idv[i] : kRowZero;
             const uint16_t* tab = side ? ga.atab : ga.qtab;
-            const uint16_t* src = id >= kRowNaN ? ga.spec + (id & 1u) * (D / 2) : tab + (int64_t)id * (D / 2);
+            // the table row or (ids kRowNaN / kRowZero) the spec row, selected branch-free: a conditional pointer
+            // makes hipcc branch (exec-mask if / else) around every chunk's address
+            const uint64_t a_tab = (uint64_t)(uintptr_t)tab + (uint64_t)id * (D / 2 * 2);
+            const uint64_t a_spec = (uint64_t)(uintptr_t)ga.spec + (uint64_t)(id & 1u) * (D / 2 * 2);
+            const uint64_t msk = 0 - (uint64_t)(id >= kRowNaN);
+            const uint64_t src = ((a_tab & ~msk) | (a_spec & msk)) + (uint64_t)(ch & (HC - 1)) * 16;
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>(src + (ch & (HC - 1)) * 8));
+            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>((uintptr_t)src));
         }
     };
     int64_t e = blockIdx.x;
@@ -756,6 +786,10 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         __syncthreads();
     }
     for (; e < batch; e += gridDim.x) {
+        if constexpr (STAMP) {
+            const int ex = (int)it;
+            esim_stamp(ga.stamps + (((int64_t)blockIdx.x * kEsim2Waves + wave) * ga.stamp_ex + min(ex, ga.stamp_ex - 1)) * kStampPts, 0, lane);
+        }
         if (pe >= 0) flush();
         const bool more = e + gridDim.x < batch;
         if constexpr (GATHER) {
@@ -772,19 +806,28 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         // stripe (7 tiles over 4 waves) is a different SIMD each time; statistics slots follow the stripe
         const int rot = (int)(it++ & 3);
         const int sp0 = (wave + rot) & 3, sp1 = sp0 + kEsim2Waves;
+        uint32_t* stp = nullptr;
+        if constexpr (STAMP) {
+            const int ex = (int)(it - 1);
+            stp = ga.stamps + (((int64_t)blockIdx.x * kEsim2Waves + wave) * ga.stamp_ex + min(ex, ga.stamp_ex - 1)) * kStampPts;
+            esim_stamp(stp, 1, lane);  // prefetch issued
+        }
         if (sp0 < nt) {
             float* wst = st + sp0 * 3 * 2 * D;
             // both-stripe / one-stripe waves are separate instantiations: no predicated MFMAs
             if (sp1 < nt) {
-                if (sp0 >> 1) esim3_wave<M, D, NTT, true, XM, 1>(qs, as, wst, sp0, sp1, L, lane);
-                else esim3_wave<M, D, NTT, true, XM, 0>(qs, as, wst, sp0, sp1, L, lane);
+                if (sp0 >> 1) esim3_wave<M, D, NTT, true, XM, 1, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
+                else esim3_wave<M, D, NTT, true, XM, 0, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
             } else {
-                if (sp0 >> 1) esim3_wave<M, D, NTT, false, XM, 1>(qs, as, wst, sp0, sp1, L, lane);
-                else esim3_wave<M, D, NTT, false, XM, 0>(qs, as, wst, sp0, sp1, L, lane);
+                if (sp0 >> 1) esim3_wave<M, D, NTT, false, XM, 1, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
+                else esim3_wave<M, D, NTT, false, XM, 0, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
             }
         }
+        if constexpr (STAMP) esim_stamp(stp, 2, lane);  // compute done
         __syncthreads();  // compute done: images free, statistics complete
+        if constexpr (STAMP) esim_stamp(stp, 3, lane);
         if (more) stage_images();
+        if constexpr (STAMP) esim_stamp(stp, 4, lane);  // next images written (prefetched rows landed)
 
         // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84)
         // every thread of the workgroup: lane l of wave w reduces side l >> 5 of the columns
@@ -820,7 +863,9 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                 pe = e;
             }
         }
+        if constexpr (STAMP) esim_stamp(stp, 5, lane);
         __syncthreads();  // next images visible; statistics reads retired
+        if constexpr (STAMP) esim_stamp(stp, 6, lane);
     }
     if (pe >= 0) flush();  // the last example's features
 }
@@ -1001,6 +1046,11 @@ template <int D, int NTT>
 int launch_esim2g_nt(int grid, size_t lds, hipStream_t st, int batch, int L, float* out, int64_t out_stride,
                      int64_t out_off, const EsimGatherArgs& ga) {
     auto kern = esim2_kernel<false, D, NTT, 1, true>;
+    if constexpr (D == 128 && NTT == 7) {  // the diagnostic stamped build: cfg3's shape only
+        if (ga.stamps) kern = esim2_kernel<false, D, NTT, 1, true, true>;
+    } else {
+        if (ga.stamps) return rf_set_error(RF_EINVAL, "stamped ESIM: only d = 128, 97 <= L <= 112");
+    }
     const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel (gather)");
     if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, nullptr, nullptr, batch, L, (int64_t)0,
@@ -1098,9 +1148,10 @@ extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t 
     return rf_check_launch("sdpa_kernel");
 }
 
-extern "C" int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
-                                  int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
-                                  int64_t out_stride, int64_t out_off, void* stream) {
+namespace {
+int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table, int32_t dtype,
+                     int32_t batch, int32_t L, int32_t d, const void* spec, float* out, int64_t out_stride, int64_t out_off,
+                     uint32_t* stamps, int32_t stamp_ex, void* stream) {
     RF_REQUIRE(dtype == RF_DTYPE_BF16, "rf_esim_gather_fwd: tables must be BF16");
     RF_REQUIRE(L >= 1 && L <= 128, "rf_esim_gather_fwd: need 1 <= L <= 128 (got %d)", L);
     RF_REQUIRE(d == 64 || d == 128, "rf_esim_gather_fwd: d must be 64 or 128 (got %d)", d);
@@ -1117,9 +1168,27 @@ extern "C" int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, 
     const size_t lds = esim2_gather_lds_bytes(d, nt, esim2_rs(d, nt));
     const int per_cu = lds <= 80 * 1024 ? 2 : 1;
     const int grid = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
-    const EsimGatherArgs ga{q_ids, a_ids, (const uint16_t*)q_table, (const uint16_t*)a_table, (const uint16_t*)spec};
+    const EsimGatherArgs ga{q_ids, a_ids, (const uint16_t*)q_table, (const uint16_t*)a_table, (const uint16_t*)spec,
+                            stamps, stamp_ex};
     const int rc = d == 64 ? launch_esim2g<64>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga)
                            : launch_esim2g<128>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga);
     if (rc) return rc;
     return rf_check_launch("rf_esim_gather_fwd");
+}
+}  // namespace
+
+extern "C" int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
+                                  int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
+                                  int64_t out_stride, int64_t out_off, void* stream) {
+    return esim_gather_impl(q_ids, a_ids, q_table, a_table, dtype, batch, L, d, spec, out, out_stride, out_off, nullptr, 0,
+                            stream);
+}
+
+extern "C" int rf_diag_esim_gather_stamped(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table,
+                                           const void* a_table, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                                           const void* spec, float* out, int64_t out_stride, int64_t out_off,
+                                           uint32_t* stamps, int32_t stamp_ex, void* stream) {
+    RF_REQUIRE(stamps && stamp_ex >= 1, "rf_diag_esim_gather_stamped: need a stamp buffer");
+    return esim_gather_impl(q_ids, a_ids, q_table, a_table, dtype, batch, L, d, spec, out, out_stride, out_off, stamps,
+                            stamp_ex, stream);
 }

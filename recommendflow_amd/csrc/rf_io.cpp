@@ -14,6 +14,7 @@
 // tf.train.Example serialisation of build_tfrecord (make_tfrecord.py:94-119).
 #include <dlfcn.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -969,9 +970,39 @@ class Reader {
             p = std::make_unique<FileProducer>(paths_[next_path_], gz_);
         }
         ++next_path_;
-        while (ahead_.size() < cycle_.size() && next_path_ + ahead_.size() < paths_.size())
-            ahead_.push_back(std::make_unique<FileProducer>(paths_[next_path_ + ahead_.size()], gz_));
+        // bounded look-ahead: a whole-file inflate holds the compressed file plus its decoded image, so the files
+        // opened ahead are capped by a host-memory budget (RF_TFR_AHEAD_MB, default 1024 MiB of on-disk bytes x 5
+        // for GZIP) as well as by the cycle length; one file always opens ahead
+        const uint64_t budget = ahead_budget();
+        uint64_t held = 0;
+        for (const auto& a : ahead_) held += a_bytes(a.get());
+        while (ahead_.size() < cycle_.size() && next_path_ + ahead_.size() < paths_.size()) {
+            const std::string& path = paths_[next_path_ + ahead_.size()];
+            const uint64_t need = est_bytes(path);
+            if (!ahead_.empty() && held + need > budget) break;
+            ahead_.push_back(std::make_unique<FileProducer>(path, gz_));
+            ahead_sz_[ahead_.back().get()] = need;
+            held += need;
+        }
+        ahead_sz_.erase(p.get());
         return p;
+    }
+    uint64_t est_bytes(const std::string& path) const {
+        struct stat sb;
+        const uint64_t disk = ::stat(path.c_str(), &sb) == 0 ? static_cast<uint64_t>(sb.st_size) : 0;
+        return gz_ ? disk * 5 : disk;
+    }
+    uint64_t a_bytes(const FileProducer* f) const {
+        auto it = ahead_sz_.find(f);
+        return it == ahead_sz_.end() ? 0 : it->second;
+    }
+    static uint64_t ahead_budget() {
+        static const uint64_t b = [] {
+            const char* e = getenv("RF_TFR_AHEAD_MB");
+            const long long mb = e ? atoll(e) : 1024;
+            return static_cast<uint64_t>(mb > 0 ? mb : 1) << 20;
+        }();
+        return b;
     }
 
     Status parse(const Schema& sc, int32_t B, rf_tfr_columns* c) {
@@ -1157,6 +1188,7 @@ class Reader {
 
     std::vector<std::string> paths_;
     std::deque<std::unique_ptr<FileProducer>> ahead_;  // opened ahead, in path order
+    std::unordered_map<const FileProducer*, uint64_t> ahead_sz_;  // their estimated host bytes
     bool gz_;
     Pool pool_;
     std::vector<std::unique_ptr<FileProducer>> cycle_;

@@ -556,7 +556,9 @@ __global__ __launch_bounds__(256) void adam_dense_kernel(float* __restrict__ w, 
 // grid beside the towers' GEMMs, so its bandwidth comes from loads in flight per wave, not from more waves
 template <int U>
 __global__ __launch_bounds__(256) void adam_untouched_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
-                                                             int64_t n4, int D4, const int32_t* __restrict__ map, AdamCoef c) {
+                                                             int64_t n4, int D4, const int32_t* __restrict__ map,
+                                                             const int32_t* __restrict__ n_uniq, AdamCoef c) {
+    if (*n_uniq < 0) return;  // invalid batch (the plan's error flag): no row takes a step
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += stride) {
         bool act[U];
@@ -747,7 +749,12 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
                        vout, seg, n_uniq, dim, out_stride, src, aux, flag);
     hipLaunchKernelGGL(classify_kernel, dim3(grid_of(max_u)), dim3(256), 0, st, seg, n_uniq, uniq_cap, long_list, long_cnt);
     }
-    if (mode == 1) return rf_check_launch("rf_fused_hash_embed_bwd_plan");
+    if (mode == 1) {
+        // the plan half reports prep's alignment flag through n_uniq too, so a consumer of the plan alone (the
+        // untouched-row Adam on the side stream) sees an invalid batch before it moves any row
+        hipLaunchKernelGGL(flag_kernel, dim3(1), dim3(64), 0, st, flag, n_uniq);
+        return rf_check_launch("rf_fused_hash_embed_bwd_plan");
+    }
     if (minmax_count) {
         RF_REQUIRE(out, "rf_fused_hash_embed_bwd: max/min pooling needs the forward output");
         hipLaunchKernelGGL(minmax_count_kernel, dim3(grid_of((int64_t)batch * n_slots * 2)), dim3(256), 0, st, d_slots,
@@ -957,7 +964,7 @@ extern "C" int rf_adam_untouched(float* table, float* m, float* v, int64_t table
         return e ? std::max(1, atoi(e)) : 256;
     }();
     hipLaunchKernelGGL(adam_untouched_kernel<4>, dim3(grid_of(table_rows * (dim / 4), gmax)), dim3(256), 0, st, table, m, v,
-                       table_rows * (dim / 4), dim / 4, map, c);
+                       table_rows * (dim / 4), dim / 4, map, n_uniq, c);
     return rf_check_launch("rf_adam_untouched");
 }
 

@@ -129,8 +129,12 @@ class TrainableDssm(torch.nn.Module):
                 planned = torch.cuda.Event()
                 planned.record(side)
                 self.sparse_opt.apply_untouched(plan.rows, plan.n_uniq, plan.cap)
-            for t in (plan.rows, plan.n_uniq, plan.ws):
-                t.record_stream(main)
+            # plan.batch is a device copy made on the side stream when `batch` was a host batch: the main stream's
+            # reduce reads it too
+            pb = plan.batch
+            for t in (plan.rows, plan.n_uniq, plan.ws, pb.tok_bytes, pb.tok_off, pb.bag_off, pb.lmax):
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(main)
             # the backward's reduce waits for the plan only: the untouched rows' update keeps running through the
             # towers' backward, the reduce and the touched rows' update (disjoint rows), and the step joins it last
             self.enc._plan, self.enc._plan_batch, self.enc._plan_stream = plan, batch, planned

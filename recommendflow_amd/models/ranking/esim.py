@@ -91,7 +91,19 @@ class Esim(torch.nn.Module):
     # (profiles/r03/r03b7_cfg3_gather_trace.txt). False: encoders + rf_esim_soft_attention_fwd.
     gather = True
 
+    def _check_batches(self, user: SparseBatch, ad: SparseBatch):
+        """The shapes both ESIM paths rely on: the gather path sizes its id buffers [B, L, 2] from these, so a
+        mismatch must raise before any launch (the encoder path raises the same errors)."""
+        if user.batch != ad.batch:
+            raise ValueError(f"user batch {user.batch} != ad batch {ad.batch}")
+        for name, b, enc in (("user", user, self.enc_q), ("ad", ad, self.enc_a)):
+            if len(enc.slots) != self.L:
+                raise ValueError(f"{name} encoder has {len(enc.slots)} slots, the attention L = {self.L}")
+            if b.n_slots != len(enc.slots):
+                raise ValueError(f"batch has {b.n_slots} slots, encoder {len(enc.slots)}")
+
     def _gather_ok(self, user: SparseBatch, ad: SparseBatch) -> bool:
+        self._check_batches(user, ad)
         eq, ea = self.enc_q, self.enc_a
         return (self.gather and isinstance(eq, FusedSparseEncoder) and isinstance(ea, FusedSparseEncoder)
                 and eq.table.dtype == torch.bfloat16 and ea.table.dtype == torch.bfloat16
@@ -103,6 +115,7 @@ class Esim(torch.nn.Module):
         """(q_ids, a_ids) [B, L, 2] int32: each token's two fused-table rows (rf_single_token_ids_fwd)."""
         from ...runtime import lib as L
 
+        self._check_batches(user, ad)
         B, dev = user.batch, self.enc_q.table.device
         ids = []
         for enc, b in ((self.enc_q, user), (self.enc_a, ad)):
@@ -119,6 +132,13 @@ class Esim(torch.nn.Module):
         """The ESIM attention + pooling into pooled[:, d_emb:], its q / a images gathered by id (rf_esim_gather_fwd)."""
         from ...runtime import lib as L
 
+        B = q_ids.shape[0]
+        if (q_ids.shape != (B, self.L, 2) or a_ids.shape != (B, self.L, 2) or q_ids.dtype != torch.int32
+                or a_ids.dtype != torch.int32 or not q_ids.is_contiguous() or not a_ids.is_contiguous()):
+            raise ValueError(f"token ids must be int32 [B, {self.L}, 2] on both sides, got {tuple(q_ids.shape)} / "
+                             f"{tuple(a_ids.shape)}")
+        if pooled.dtype != torch.float32 or pooled.dim() != 2 or pooled.shape[0] != B or pooled.shape[1] < self.d_emb + 6 * self.d or pooled.stride(1) != 1:
+            raise ValueError(f"pooled must be a row-major [{B}, >= {self.d_emb + 6 * self.d}] fp32 tensor")
         dev = pooled.device
         spec = getattr(self, "_spec", None)
         if spec is None or spec.device != dev:

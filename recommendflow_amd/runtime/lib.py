@@ -103,7 +103,8 @@ _SIGS = {
 }
 EXPORTED = tuple(_SIGS)
 # include/rf_diag.h: tools-only entry points (not the production ABI)
-_DIAG_SIGS = {"rf_diag_fused_hash_embed_fwd": _SIGS["rf_fused_hash_embed_fwd"]}
+_DIAG_SIGS = {"rf_diag_fused_hash_embed_fwd": _SIGS["rf_fused_hash_embed_fwd"],
+              "rf_diag_esim_gather_stamped": (ctypes.c_int, _SIGS["rf_esim_gather_fwd"][1][:-1] + [_vp, _i32, _vp])}
 DIAG_EXPORTED = tuple(_DIAG_SIGS)
 DIAG_ABLATIONS = 0x7000  # bits 12-14: accepted only by rf_diag_fused_hash_embed_fwd
 

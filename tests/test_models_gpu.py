@@ -125,3 +125,33 @@ def test_esim_gather_equals_encoders_plus_attention(cuda, mask_padding):
     assert torch.equal(model(hu, ha, dense), want)
     fwd = model.graphed(hu, ha, dense)
     assert torch.equal(fwd(hu, ha, dense), want)
+
+
+def test_esim_rejects_mismatched_batches(cuda):
+    """the gather path sizes its [B, L, 2] id buffers from the batches, so a user / ad batch-size
+    or slot-count mismatch (or injected encoders whose slot count differs from L) must raise before any launch,
+    as the encoder path does."""
+    Ls, B = 8, 16
+    user = [SlotSpec(f"u{i}", 5000, (2022, 2023)) for i in range(Ls)]
+    ad = [SlotSpec(f"a{i}", 5000, (2022, 2023)) for i in range(Ls)]
+    model = Esim(user, ad, n_dense=16, dim=64, seed=3)
+    dense = torch.randn(B, 16, device="cuda")
+    hu = synthetic_batch(B, [False] * Ls, seed=1).to("cuda")
+    ha = synthetic_batch(B, [False] * Ls, seed=2).to("cuda")
+    model(hu, ha, dense)  # the well-formed pair runs
+    for gather in (True, False):
+        model.gather = gather
+        with pytest.raises(ValueError):
+            model(hu, synthetic_batch(B + 4, [False] * Ls, seed=3).to("cuda"), dense)
+        with pytest.raises(ValueError):
+            model(hu, synthetic_batch(B, [False] * (Ls - 1), seed=4).to("cuda"), dense)
+    model.gather = True
+    # injected encoders whose slot count differs from L
+    short = FusedSparseEncoder(ad[:-1], 64, table_dtype=torch.bfloat16, seed=5)
+    model.enc_a = short
+    with pytest.raises(ValueError):
+        model(hu, synthetic_batch(B, [False] * (Ls - 1), seed=4).to("cuda"), dense)
+    ids = torch.zeros((B, Ls, 2), dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        model.attention_gather(ids, torch.zeros((B + 1, Ls, 2), dtype=torch.int32, device="cuda"),
+                               torch.empty((B, model.pooled_width), device="cuda"))
