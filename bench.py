@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--shard-rows", type=int, default=125_000_000, help="cfg4 weak scaling: fused-table rows per GPU")
     p.add_argument("--shard-dim", type=int, default=128)
     p.add_argument("--shard-batch", type=int, default=8192, help="cfg4: examples per GPU (65536 at P=8)")
+    p.add_argument("--sim-ranks", type=int, default=8, help="cfg4 at N=1: also time rank 0 of this many ranks "
+                                                              "(LoopbackComm; 0 = skip)")
     p.add_argument("--no-train", action="store_true", help="skip the cfg2 DSSM training-step extra")
     p.add_argument("--no-shard-train", action="store_true", help="skip the cfg4 sharded training-step extra")
     p.add_argument("--no-cascade", action="store_true", help="skip the cfg5 recall->prerank->rank extra")
@@ -634,6 +636,76 @@ def bench_sharded(args, specs, multi, rank, world):
         res["train_step"] = bench_sharded_train(args, enc, batches, out, world)
     del enc, batches, out, micro, mouts
     torch.cuda.empty_cache()
+    if world == 1 and args.sim_ranks > 1:
+        try:
+            res["simulated_p8" if args.sim_ranks == 8 else f"simulated_p{args.sim_ranks}"] = \
+                bench_sharded_sim(args, specs, multi, args.sim_ranks)
+        except Exception as e:  # noqa: BLE001 — a failed diagnostic leg must not cost the line
+            res["simulated_p8"] = f"{type(e).__name__}: {e}"[:300]
+        torch.cuda.empty_cache()
+    return res
+
+
+def bench_sharded_sim(args, specs, multi, P):
+    """cfg4's remote-row path at P ranks, timed on ONE GPU: this GPU plays rank 0 of P with a
+    LoopbackComm, so (P-1)/P of every batch's rows are remote and go route (hash-table dedup) -> id exchange ->
+    owner gather -> row exchange -> pool through the row map; the all-to-alls are device copies of the same bytes
+    (what xGMI would carry is reported beside them, not timed). Rank 0's shard is shard_rows x shard_dim fp32, the
+    logical table P times that; shard_batch examples. Pooled values of remote rows come from the wrong shard (the
+    loopback serves its own rows): timing only; the parity of this path is tests/test_sharded_gpu.py."""
+    import torch
+
+    from recommendflow_amd.backend.encoder.sharded_encoder import LoopbackComm, ShardedFusedEncoder
+    from recommendflow_amd.backend.encoder.sparse_encoder import SlotSpec
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    B, D = args.shard_batch, args.shard_dim
+    S = len(specs)
+    n_bins = args.shard_rows * P // (2 * S)
+    sp = [SlotSpec(s.name, n_bins, s.seeds, s.combiner, s.mask_empty) for s in specs]
+    comm = LoopbackComm(P)
+    enc = ShardedFusedEncoder(sp, D, 0, P, comm=comm, seed=2024)
+    batches = [synthetic_batch(B, multi, seed=4321 + i).to("cuda") for i in range(2)]
+    out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
+    names = ["route", "a2a_ids", "gather", "a2a_rows", "pool"]
+    st = {}
+
+    def step(i, ev=None):
+        b = batches[i % 2]
+        r, recv = enc.route_exchange(b, local_fast=enc.local_fast)
+        if ev: ev[1].record()
+        wanted = comm.exchange(r.local, r.counts, recv)
+        if ev: ev[2].record()
+        vec = enc.serve(wanted)
+        if ev: ev[3].record()
+        back = comm.exchange(vec, recv, r.counts)
+        if ev: ev[4].record()
+        enc.combine(b, r, back, out, local_fast=enc.local_fast)
+        if ev: ev[5].record()
+        st["req"], st["served"], st["logical"] = r.n_requests, int(wanted.shape[0]), r.n_logical
+
+    steps = max(5, args.steps // 5)
+    for i in range(3):
+        step(i)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record()
+        step(i, evs[i])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    stage = {n: round(sum(e[k].elapsed_time(e[k + 1]) for e in evs) / steps, 4) for k, n in enumerate(names)}
+    row_b = D * 4
+    res = {"ms_per_step": round(el / steps * 1e3, 4), "examples_per_s_this_rank": round(B * steps / el, 1),
+           "stage_ms": stage, "rows_read_by_pool": st["logical"], "rows_requested_after_dedup": st["req"],
+           "rows_local_in_place": st["logical"] - st["req"],
+           "dedup_ratio": round(st["req"] / max(1, st["logical"]), 4),
+           "gather_GBs": round(st["served"] * (2 * row_b + 8) / max(stage["gather"], 1e-6) / 1e6, 1),
+           "xgmi_bytes_each_way_not_timed": int(st["req"] * (8 + row_b)),
+           "config": f"rank 0 of P = {P} on one GPU (LoopbackComm: each all-to-all is a device copy of the same bytes), "
+                     f"{enc.local_rows} x {D} fp32 shard of a {enc.table_rows}-row logical table, {B} examples, cfg2 slots"}
+    del enc, batches, out
     return res
 
 
@@ -904,6 +976,26 @@ def bench_train(args, specs, multi):
         if i >= 2:
             tw += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])]
     tw /= steps
+    # the same step with the table gradient's long rows summed as a fixed-order tree (RF_FLAG_TREE_REDUCE: within
+    # SURVEY §8d's L 2^-23 sum|x| of the reference's CPU order instead of bit-exact with it)
+    enc.tree_reduce = True
+    try:
+        for i in range(2):
+            model.step(batches[i % 2], y)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            model.step(batches[i % 2], y)
+        torch.cuda.synchronize()
+        tree_ms = (time.perf_counter() - t0) / steps * 1e3
+        ev[0].record()
+        for i in range(steps):
+            g = enc.backward(batches[i % 2], dout, out=out)
+        ev[1].record()
+        torch.cuda.synchronize()
+        tree_bwd_ms = ev[0].elapsed_time(ev[1]) / steps
+    finally:
+        enc.tree_reduce = False
     tower_flops = 3 * 2 * B * sum(t.W[l].numel() for t in (model.user_tower, model.ad_tower) for l in range(len(t.units)))
     adam_bytes = enc.table.numel() * 4 * 6 + enc.table.shape[0] * 4 + n_uniq * (args.dim * 4 + 8)
     res = {"examples_per_s": round(B / step_ms * 1e3, 1), "ms_per_step": round(step_ms, 4), "loss": round(float(loss), 4),
@@ -913,6 +1005,12 @@ def bench_train(args, specs, multi):
            "tower_fwd_bwd_TFLOPs": round(tower_flops / tw[0] / 1e9, 1),
            "distinct_rows_per_step": n_uniq,
            "adam_dense_GBs": round(adam_bytes / acc[2] / 1e6, 1),
+           "tree_reduce": {"examples_per_s": round(B / tree_ms * 1e3, 1), "ms_per_step": round(tree_ms, 4),
+                           "bwd_dedup_ms": round(tree_bwd_ms, 4),
+                           "note": "FusedSparseEncoder.tree_reduce = True (RF_FLAG_TREE_REDUCE): rows with > 256 positions "
+                                   "summed as fixed-order partials + a pairwise tree, within |d| <= L 2^-23 sum|x| of the "
+                                   "reference's CPU order (tests/test_train_gpu.py::test_bwd_tree_reduce_within_bound); the "
+                                   "line's examples_per_s keeps the bit-exact CPU order"},
            "config": "cfg2 DSSM train step: 229 slots, 9999972x64 fp32 table (+ m, v), B=4096, towers [1024,512,256] "
                      "BatchNormalization(batch stats)/selu/dropout 0.3 on librf (train_mlp.TrainTower: BN folded into "
                      "the fp32 MFMA forward GEMM, SELU/dropout/BN backward kernels, library GEMMs for dW and dx), "

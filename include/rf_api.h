@@ -57,6 +57,9 @@ extern "C" {
 #define RF_FLAG_SINGLE_TOKEN 0x4 /* the caller knows every slot's batch Lmax is <= 1 (single-valued slots, e.g.
                                     cfg3): a low-register single-token kernel runs (same values); a slot whose
                                     lmax is > 1 is then written as NaN. Not with RF_FLAG_EMIT_IDX. */
+#define RF_FLAG_TREE_REDUCE 0x10  /* embedding backward only (rf_fused_hash_embed_bwd / _bwd_reduce): rows with more than
+                                    256 positions are summed as fixed-order partials + a pairwise tree (deterministic,
+                                    within SURVEY 8d's |d| <= L 2^-23 sum|x|) instead of the reference's CPU order */
 #define RF_FLAG_DIAG_XCD_ORDER 0x0800      /* A/B switch: slot-interleaved XCD item order (measured slower); results identical */
 #define RF_FLAG_DIAG_GENERAL_PHASE2 0x8000 /* A/B switch: force the general pooling path for Lmax = 1 slots; results identical */
 /* Only these two result-preserving switches are accepted here; any other bit returns RF_EINVAL. Bits 12-14
@@ -295,6 +298,25 @@ int rf_dense_head_fwd(const float* x, int64_t M, int32_t K, int64_t ldx, const v
 int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
                             const int32_t* bag_off, const int32_t* lmax, int32_t batch, int64_t table_rows, uint32_t* ids,
                             int32_t flags, void* stream);
+/*
+ * rf_single_token_ids_fwd for up to 4 batches (towers) in ONE launch (the ESIM forward's user and ad sides: both
+ * DoubleHashingEmbedding index passes, preprocess_layers.py:82-97 per tower): tasks is a HOST array of n_tasks
+ * (1..4) descriptions; each task's ids are exactly what rf_single_token_ids_fwd writes for it.
+ */
+typedef struct rf_ids_task {
+    const rf_slot_desc* slots; /* device */
+    const uint8_t* tok_bytes;
+    const int32_t* tok_off;
+    const int32_t* bag_off;
+    const int32_t* lmax;
+    uint32_t* ids;             /* [batch * n_slots][2], 8-byte aligned */
+    int64_t table_rows;
+    int32_t n_slots;
+    int32_t batch;
+    int32_t flags;             /* 0 or RF_FLAG_MASK_PADDING */
+    int32_t reserved;          /* must be 0 */
+} rf_ids_task;
+int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n_tasks, void* stream);
 int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
                        int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
                        int64_t out_stride, int64_t out_off, void* stream);

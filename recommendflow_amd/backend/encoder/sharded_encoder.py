@@ -328,6 +328,35 @@ class LocalComm:
         return [int(v)]
 
 
+class LoopbackComm:
+    """Timing stand-in for rank 0 of a P-rank job on ONE GPU (bench.py cfg4_sharded.simulated_p8): every
+    exchange is a device copy of the same bytes, and what rank 0 would receive from rank k is taken to be what it
+    sends to k (the requests of P symmetric ranks have the same statistics). The owner side then serves as many
+    rows as it would at P, from its own shard (local ids are < the shard's rows for every rank), so route -> id
+    exchange -> gather -> row exchange -> row-mapped pool run at the real sizes. The VALUES pooled for remote rows
+    come from the wrong shard: timing only, never a parity path."""
+
+    rank = 0
+
+    def __init__(self, world: int):
+        self.world = int(world)
+
+    def exchange_counts(self, counts: torch.Tensor) -> torch.Tensor:
+        return counts.clone()
+
+    def exchange(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]) -> torch.Tensor:
+        return x.clone()
+
+    def exchange_async(self, x: torch.Tensor, send_splits: List[int], recv_splits: List[int]):
+        return x.clone(), None
+
+    def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
+        return torch.cat([x] * self.world)
+
+    def all_gather_ints(self, v: int) -> List[int]:
+        return [int(v)] * self.world
+
+
 @dataclass
 class RouteState:
     counts: List[int]          # rows this rank requests from each owner

@@ -123,6 +123,9 @@ class FusedSparseEncoder(torch.nn.Module):
         self.mask_padding = bool(mask_padding)
         self.seed = int(seed)
         self.single_token = True  # RF_FLAG_SINGLE_TOKEN when a batch's host-side Lmax allows it (A/B: False)
+        # backward: rows with > 256 positions summed as fixed-order partials + a tree (RF_FLAG_TREE_REDUCE: within
+        # SURVEY §8d's L 2^-23 sum|x| of the reference's CPU order, not bit-exact with it); default: the CPU order
+        self.tree_reduce = False
         self.extra_flags = 0  # diagnostic bits (rf_api.h RF_FLAG_DIAG_*; ablations 12-14 go to rf_diag_fused_hash_embed_fwd)
         desc = np.zeros(len(self.slots), SLOT_DTYPE)
         base = int(row_base0)
@@ -221,7 +224,7 @@ class FusedSparseEncoder(torch.nn.Module):
         cnt = torch.empty(dout.shape, dtype=torch.int32, device=dev) if need_mm else None
         wsb = L.load().rf_embed_bwd_ws_bytes(n_pos, len(self.slots), self.table.shape[0])
         ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=dev)
-        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        flags = (L.FLAG_MASK_PADDING if self.mask_padding else 0) | (L.FLAG_TREE_REDUCE if self.tree_reduce else 0)
         L.call("rf_fused_hash_embed_bwd", L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes), L.ptr(batch.tok_off),
                L.ptr(batch.bag_off), L.ptr(batch.lmax), B, n_pos, L.ptr(self.table), self.table.shape[0], self.dim,
                L.ptr(out) if need_mm else None, L.ptr(dout), dout.stride(0), flags, L.ptr(cnt), L.ptr(rows), L.ptr(grad),
@@ -243,7 +246,7 @@ class FusedSparseEncoder(torch.nn.Module):
         n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
         wsb = L.load().rf_embed_bwd_ws_bytes(n_pos, len(self.slots), self.table.shape[0])
         ws = torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=dev)
-        flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
+        flags = (L.FLAG_MASK_PADDING if self.mask_padding else 0) | (L.FLAG_TREE_REDUCE if self.tree_reduce else 0)
         L.call("rf_fused_hash_embed_bwd_plan", L.ptr(self.desc), len(self.slots), L.ptr(batch.tok_bytes),
                L.ptr(batch.tok_off), L.ptr(batch.bag_off), L.ptr(batch.lmax), B, n_pos, self.table.shape[0], self.dim,
                self.out_width, flags, L.ptr(rows), cap, L.ptr(n_uniq), L.ptr(ws), ws.numel(), L.stream_ptr(stream))

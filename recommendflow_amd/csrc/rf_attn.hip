@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "rf_common.h"
 
@@ -382,6 +383,30 @@ __device__ __forceinline__ float rs4(float a, float b, float c, float d) {
     return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// v[0..N) reduced as a balanced tree (maximum3 / add pairs): dependent depth ~log instead of N
+template <int N, bool MAX>
+__device__ __forceinline__ float tree_reduce(float (&v)[8]) {
+    if constexpr (N == 1) return v[0];
+    if constexpr (MAX) {
+        if constexpr (N == 2) return fmx(v[0], v[1]);
+        if constexpr (N == 3) return fmx3(v[0], v[1], v[2]);
+        if constexpr (N == 4) return fmx3(v[0], v[1], fmx(v[2], v[3]));
+        if constexpr (N == 5) return fmx3(fmx3(v[0], v[1], v[2]), v[3], v[4]);
+        if constexpr (N == 6) return fmx(fmx3(v[0], v[1], v[2]), fmx3(v[3], v[4], v[5]));
+        if constexpr (N == 7) return fmx3(fmx3(v[0], v[1], v[2]), fmx3(v[3], v[4], v[5]), v[6]);
+        if constexpr (N == 8) return fmx3(fmx3(v[0], v[1], v[2]), fmx3(v[3], v[4], v[5]), fmx(v[6], v[7]));
+    } else {
+        if constexpr (N == 2) return v[0] + v[1];
+        if constexpr (N == 3) return (v[0] + v[1]) + v[2];
+        if constexpr (N == 4) return (v[0] + v[1]) + (v[2] + v[3]);
+        if constexpr (N == 5) return ((v[0] + v[1]) + (v[2] + v[3])) + v[4];
+        if constexpr (N == 6) return ((v[0] + v[1]) + (v[2] + v[3])) + (v[4] + v[5]);
+        if constexpr (N == 7) return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + v[6]);
+        if constexpr (N == 8) return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    }
+    return 0.f;
+}
+
 // column softmax of one E^T stripe (as stripe_softmax) with the stripe's padding rows zeroed: i = lane & 15
 template <typename M, int nt, typename frag>
 __device__ __forceinline__ void stripe_softmax3(f4 (&ev)[8], int L, int lg, bool row_ok, frag (&pa)[4]) {
@@ -392,19 +417,20 @@ __device__ __forceinline__ void stripe_softmax3(f4 (&ev)[8], int L, int lg, bool
         for (int r = 0; r < 4; ++r)
             if ((nt - 1) * 16 + lg * 4 + r >= L) ev[nt - 1][r] = -INFINITY;
     }
-    float mx = -INFINITY;
+    // the maximum and the sum as trees over the tiles (the tile-serial chains were 2 nt dependent VALU deep; the
+    // maximum is exact in any order, the sum's fp32 order is this tree's)
+    float tm[8];
 #pragma unroll
-    for (int jt = 0; jt < nt; ++jt) mx = fmx3(fmx3(mx, ev[jt][0], ev[jt][1]), ev[jt][2], ev[jt][3]);
-    mx = rows4_maximum(mx);
+    for (int jt = 0; jt < nt; ++jt) tm[jt] = fmx3(ev[jt][0], ev[jt][1], fmx(ev[jt][2], ev[jt][3]));
+    const float mx = rows4_maximum(tree_reduce<nt, true>(tm));
     const float mo = -mx * kL2E;
-    f2v sm2 = {0.f, 0.f};
 #pragma unroll
     for (int jt = 0; jt < nt; ++jt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) ev[jt][r] = __builtin_amdgcn_exp2f(fmaf(ev[jt][r], kL2E, mo));
-        sm2 += f2v{ev[jt][0], ev[jt][1]} + f2v{ev[jt][2], ev[jt][3]};
+        tm[jt] = (ev[jt][0] + ev[jt][1]) + (ev[jt][2] + ev[jt][3]);
     }
-    float inv = 1.0f / rows4_sum(sm2[0] + sm2[1]);
+    float inv = 1.0f / rows4_sum(tree_reduce<nt, false>(tm));
     inv = row_ok ? inv : 0.f;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -453,6 +479,63 @@ __device__ __forceinline__ void esim_acc4x(f4 x, f4 at, float& sx, float& sm, fl
     }
 }
 
+// maximum of v[0..N) as a tree of maximum3 (N - 1 values folded 2 per instruction, depth ~log3 N); exact in any order
+template <int N>
+__device__ __forceinline__ float max3_tree(float (&v)[N]) {
+    if constexpr (N == 1) {
+        return v[0];
+    } else if constexpr (N == 2) {
+        return fmx(v[0], v[1]);
+    } else {
+        constexpr int M = N / 3 + (N % 3 ? 1 : 0);
+        float w[M];
+#pragma unroll
+        for (int i = 0; i < N / 3; ++i) w[i] = fmx3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
+        if constexpr (N % 3 == 1) w[M - 1] = v[N - 1];
+        if constexpr (N % 3 == 2) w[M - 1] = fmx(v[N - 2], v[N - 1]);
+        return max3_tree<M>(w);
+    }
+}
+
+// the statistics of one column over the wave's 4 (one stripe) or 8 (TWO) rows as trees: sum x, sum x * att, and the
+// maximum of [x, att, x - att, x * att] (v7; the v5 chains were 8 / 8 / 16 dependent VALU deep per column)
+template <bool TWO>
+__device__ __forceinline__ void esim_stats(f4 x0, f4 a0, f4 x1, f4 a1, float& sx, float& sm, float& mx) {
+    float m[8], d[8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m[r] = x0[r] * a0[r];
+        d[r] = x0[r] - a0[r];
+        if (TWO) {
+            m[4 + r] = x1[r] * a1[r];
+            d[4 + r] = x1[r] - a1[r];
+        }
+    }
+    constexpr int NV = TWO ? 32 : 16;
+    float v[NV];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        v[4 * r] = x0[r];
+        v[4 * r + 1] = a0[r];
+        v[4 * r + 2] = d[r];
+        v[4 * r + 3] = m[r];
+        if (TWO) {
+            v[16 + 4 * r] = x1[r];
+            v[16 + 4 * r + 1] = a1[r];
+            v[16 + 4 * r + 2] = d[4 + r];
+            v[16 + 4 * r + 3] = m[4 + r];
+        }
+    }
+    mx = max3_tree<NV>(v);
+    if (TWO) {
+        sx = ((x0[0] + x0[1]) + (x0[2] + x0[3])) + ((x1[0] + x1[1]) + (x1[2] + x1[3]));
+        sm = ((m[0] + m[1]) + (m[2] + m[3])) + ((m[4] + m[5]) + (m[6] + m[7]));
+    } else {
+        sx = (x0[0] + x0[1]) + (x0[2] + x0[3]);
+        sm = (m[0] + m[1]) + (m[2] + m[3]);
+    }
+}
+
 // A operand selecting the 16 rows of stripe sp out of its 32-row P @ V k-step, in the k order of
 // stripe_softmax3's accumulator-sourced fragments (element j of lane (lr, g): k = 4g + j for j < 4,
 // 16 + 4g + j - 4 for j >= 4): row lr picks k = 16 (sp & 1) + lr, so sel @ V_kstep = x of the stripe,
@@ -476,13 +559,25 @@ __device__ __forceinline__ void esim_stamp(uint32_t* p, int k, int lane) {
     if (lane == 0) __builtin_nontemporal_store(t, p + k);
 }
 constexpr int kStampPts = 10;  // stamps per (wave, example)
+constexpr int kPfParts = 4;    // GATHER: the next example's row loads in this many parts (esim3_wave's pf hook)
+
+// the 4 values of the lower (HI = 0) or upper (HI = 1) half of a B fragment widened to fp32
+template <typename M, int HI, typename frag>
+__device__ __forceinline__ f4 frag_rows_f32(frag vf) {
+    const s8v b = __builtin_bit_cast(s8v, vf);
+    f4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = M::to_f((uint16_t)b[4 * HI + j]);
+    return r;
+}
 
 // KT0 = sp0 >> 1: the P @ V k-step holding stripe sp0's rows (sp1 = sp0 + 4: k-step KT0 + 2), a template
 // parameter so the selector MFMAs are placed at compile time and each half's P @ V is one basic block (a runtime
 // wave-uniform test split it into per-k-step blocks, each waiting out its own LDS reads before its MFMAs)
-template <typename M, int D, int NTT, bool TWO, int XM = 0, int KT0 = 0, bool STAMP = false>
+template <typename M, int D, int NTT, bool TWO, int XM = 0, int KT0 = 0, int XHI = 0, bool STAMP = false,
+          typename PF = void (*)(int)>
 __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int sp1, int L,
-                                           int lane, uint32_t* stp = nullptr) {
+                                           int lane, uint32_t* stp, PF&& pf) {
     constexpr int nt = NTT;
     using frag = typename M::frag;
     constexpr int RS = esim2_rs(D, NTT);
@@ -525,13 +620,16 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
                 }
             }
         }
+        pf(1);
         if constexpr (STAMP) esim_stamp(stp, 7, lane);  // scores done
         stripe_softmax3<M, NTT>(e0, L, lg, sp0 * 16 + lr < L, pa0);
         if (TWO) stripe_softmax3<M, NTT>(e1, L, lg, sp1 * 16 + lr < L, pa1);
     }
+    pf(2);
     if constexpr (STAMP) esim_stamp(stp, 8, lane);  // softmax done
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
+        if (side == 1) pf(3);
         if constexpr (STAMP) {
             if (side == 1) esim_stamp(stp, 9, lane);  // side 0 done
         }
@@ -595,8 +693,16 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
                                 const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, (h * NC + c) * 16, lane, hi_ok);
                                 a0[c] = M::mma(pa0[kt], vf, a0[c]);
                                 if (TWO) a1[c] = M::mma(pa1[kt], vf, a1[c]);
-                                if (kt < 2) x0[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
-                                else x1[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
+                                if constexpr (XM == 2) {
+                                    // v7: x of the stripe's rows is already in this B fragment, in the accumulator
+                                    // layout of att (element j of lane (lr, g): row 4 g + j of the k-step's lower (j < 4)
+                                    // or upper 16 rows = stripe row 4 g + j, column lr): 4 widenings, no MFMA
+                                    if (kt < 2) x0[c] = frag_rows_f32<M, XHI>(vf);
+                                    else x1[c] = frag_rows_f32<M, XHI>(vf);
+                                } else {
+                                    if (kt < 2) x0[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
+                                    else x1[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
+                                }
                             }
                         } else {
 #pragma unroll
@@ -610,13 +716,7 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
                 }
                 float hx[NC], hm[NC], hmx[NC];
 #pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    hx[c] = 0.f;
-                    hm[c] = 0.f;
-                    hmx[c] = -INFINITY;
-                    esim_acc4x(x0[c], a0[c], hx[c], hm[c], hmx[c]);
-                    if (TWO) esim_acc4x(x1[c], a1[c], hx[c], hm[c], hmx[c]);
-                }
+                for (int c = 0; c < NC; ++c) esim_stats<TWO>(x0[c], a0[c], x1[c], a1[c], hx[c], hm[c], hmx[c]);
                 // this half's reduce-scatter and stores now (nothing carried into the next half)
                 const int pk = (lg == 1) ? 2 : (lg == 2) ? 1 : lg;
                 float* w = wst + side * D + lr;
@@ -711,13 +811,18 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
             }
         }
     };
-    auto prefetch_g = [&](int buf) __attribute__((always_inline)) {
+    // the row loads of the next example in kPfParts parts: part 0 at the loop top, parts 1.. between the compute
+    // phases (esim3_wave's pf hook), so a wave never stalls issuing NCH loads in one burst behind the CU's other
+    // waves' bursts (r04 phase stamps: 2.9 K of 17.3 K cycles per example at the loop top with one burst)
+    auto prefetch_g = [&](int buf, int part) __attribute__((always_inline)) {
         constexpr int HC = CPR / 2;  // 16-byte chunks per table row
-        // every id read from LDS first, then the row loads: left to itself hipcc interleaves them as
-        // read -> lgkmcnt(0) -> address -> load per chunk, NCH dependent LDS round trips per example
+        constexpr int PC = NCH / kPfParts;
+        // every id of the part read from LDS first, then the row loads: left to itself hipcc interleaves them as
+        // read -> lgkmcnt(0) -> address -> load per chunk (dependent LDS round trips)
         uint32_t idv[NCH];
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
+            if (i / PC != part) continue;
             const int cm = tid + (i % HALF) * NTH;
             const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
             const int side = i < HALF ? 0 : 1;
@@ -726,6 +831,7 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
+            if (i / PC != part) continue;
             const int cm = tid + (i % HALF) * NTH;
             const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
             const int side = i < HALF ? 0 : 1;
@@ -733,13 +839,16 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
             const uint16_t* tab = side ? ga.atab : ga.qtab;
             // the table row or (ids kRowNaN / kRowZero) the spec row, selected branch-free: a conditional pointer
             // makes hipcc branch (exec-mask if / else) around every chunk's address
-            const uint64_t a_tab = (uint64_t)(uintptr_t)tab + (uint64_t)id * (D / 2 * 2);
-            const uint64_t a_spec = (uint64_t)(uintptr_t)ga.spec + (uint64_t)(id & 1u) * (D / 2 * 2);
-            const uint64_t msk = 0 - (uint64_t)(id >= kRowNaN);
-            const uint64_t src = ((a_tab & ~msk) | (a_spec & msk)) + (uint64_t)(ch & (HC - 1)) * 16;
+            // (an integer offset from the table pointer, so the load stays a global load: a pointer rebuilt from an
+            // integer becomes a flat load, which lgkmcnt waits for LDS reads would then also wait on)
+            const int64_t d_spec = reinterpret_cast<const char*>(ga.spec) - reinterpret_cast<const char*>(tab);
+            const int64_t o_tab = (int64_t)id * (D / 2 * 2), o_spec = d_spec + (int64_t)(id & 1u) * (D / 2 * 2);
+            const int64_t msk = -(int64_t)(id >= kRowNaN);
+            const int64_t off = ((o_tab & ~msk) | (o_spec & msk)) + (ch & (HC - 1)) * 16;
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>((uintptr_t)src));
+            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(tab) + off));
         }
+        __builtin_amdgcn_sched_barrier(0);
     };
     int64_t e = blockIdx.x;
     uint32_t it = 0;
@@ -777,7 +886,8 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         if constexpr (GATHER) {
             ids_dma(e, 0);
             __syncthreads();  // (its release fence waits for the DMA) ids of e visible
-            prefetch_g(0);
+#pragma unroll
+            for (int part = 0; part < kPfParts; ++part) prefetch_g(0, part);
             if (e + gridDim.x < batch) ids_dma(e + gridDim.x, 1);
         } else {
             prefetch(e);
@@ -792,15 +902,22 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         }
         if (pe >= 0) flush();
         const bool more = e + gridDim.x < batch;
+        const int rbuf = pbuf ^ 1;  // GATHER: the id buffer holding e + G's ids
         if constexpr (GATHER) {
             if (more) {
-                prefetch_g(pbuf ^ 1);
+                prefetch_g(rbuf, 0);
                 if (e + 2 * (int64_t)gridDim.x < batch) ids_dma(e + 2 * (int64_t)gridDim.x, pbuf);
             }
             pbuf ^= 1;
         } else if (more) {
             prefetch(e + gridDim.x);
         }
+        // the later load parts, called by esim3_wave between its phases
+        auto pf = [&](int part) __attribute__((always_inline)) {
+            if constexpr (GATHER) {
+                if (more) prefetch_g(rbuf, part);
+            }
+        };
 
         // v3: the stripe pairs rotate over the waves from one example to the next, so the wave left with one
         // stripe (7 tiles over 4 waves) is a different SIMD each time; statistics slots follow the stripe
@@ -815,13 +932,27 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         if (sp0 < nt) {
             float* wst = st + sp0 * 3 * 2 * D;
             // both-stripe / one-stripe waves are separate instantiations: no predicated MFMAs
+            // (KT0, XHI) = (sp0 >> 1, sp0 & 1) at compile time (XHI only matters for XM = 2)
+            auto run = [&](auto two, auto kt0, auto xhi) __attribute__((always_inline)) {
+                esim3_wave<M, D, NTT, decltype(two)::value, XM, decltype(kt0)::value, decltype(xhi)::value, STAMP>(
+                    qs, as, wst, sp0, sp1, L, lane, stp, pf);
+            };
+            using T_ = std::true_type;
+            using F_ = std::false_type;
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            const int xh = XM == 2 ? (sp0 & 1) : 0;
             if (sp1 < nt) {
-                if (sp0 >> 1) esim3_wave<M, D, NTT, true, XM, 1, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
-                else esim3_wave<M, D, NTT, true, XM, 0, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
+                if (sp0 >> 1) { if (xh) run(T_{}, I1{}, I1{}); else run(T_{}, I1{}, I0{}); }
+                else { if (xh) run(T_{}, I0{}, I1{}); else run(T_{}, I0{}, I0{}); }
             } else {
-                if (sp0 >> 1) esim3_wave<M, D, NTT, false, XM, 1, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
-                else esim3_wave<M, D, NTT, false, XM, 0, STAMP>(qs, as, wst, sp0, sp1, L, lane, stp);
+                if (sp0 >> 1) { if (xh) run(F_{}, I1{}, I1{}); else run(F_{}, I1{}, I0{}); }
+                else { if (xh) run(F_{}, I0{}, I1{}); else run(F_{}, I0{}, I0{}); }
             }
+        }
+        else {
+#pragma unroll
+            for (int part = 1; part < kPfParts; ++part) pf(part);
         }
         if constexpr (STAMP) esim_stamp(stp, 2, lane);  // compute done
         __syncthreads();  // compute done: images free, statistics complete
@@ -1045,9 +1176,14 @@ int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, i
 template <int D, int NTT>
 int launch_esim2g_nt(int grid, size_t lds, hipStream_t st, int batch, int L, float* out, int64_t out_stride,
                      int64_t out_off, const EsimGatherArgs& ga) {
-    auto kern = esim2_kernel<false, D, NTT, 1, true>;
+    // RF_ESIM_GXM=2: x from the P @ V B fragments (v7) instead of the selector MFMA (v5); A/B runs only
+    static const int gxm = [] {
+        const char* e = getenv("RF_ESIM_GXM");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
+    auto kern = gxm == 2 ? esim2_kernel<false, D, NTT, 2, true> : esim2_kernel<false, D, NTT, 1, true>;
     if constexpr (D == 128 && NTT == 7) {  // the diagnostic stamped build: cfg3's shape only
-        if (ga.stamps) kern = esim2_kernel<false, D, NTT, 1, true, true>;
+        if (ga.stamps) kern = gxm == 2 ? esim2_kernel<false, D, NTT, 2, true, true> : esim2_kernel<false, D, NTT, 1, true, true>;
     } else {
         if (ga.stamps) return rf_set_error(RF_EINVAL, "stamped ESIM: only d = 128, 97 <= L <= 112");
     }

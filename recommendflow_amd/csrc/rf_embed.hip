@@ -314,17 +314,17 @@ __global__ __launch_bounds__(64) void single_token_ids_kernel(const rf_slot_desc
 // the ids stores of a wave are consecutive (the slot-major kernel touches 64 units n_slots apart per load and
 // store); each workgroup first prepares every slot's bucket modulus into LDS (one 64-bit division per slot).
 constexpr int kIdsMaxSlots = 512;
-__global__ __launch_bounds__(256) void single_token_ids_em_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
-                                                                 const uint8_t* __restrict__ tok_bytes,
-                                                                 const int32_t* __restrict__ tok_off,
-                                                                 const int32_t* __restrict__ bag_off,
-                                                                 const int32_t* __restrict__ lmax, int64_t n_units,
-                                                                 int64_t table_rows, uint32_t* __restrict__ ids, int flags) {
-    __shared__ BucketMod sbm[kIdsMaxSlots];
+__device__ __forceinline__ void single_token_ids_em_body(const rf_slot_desc* __restrict__ slots, int n_slots,
+                                                        const uint8_t* __restrict__ tok_bytes,
+                                                        const int32_t* __restrict__ tok_off,
+                                                        const int32_t* __restrict__ bag_off,
+                                                        const int32_t* __restrict__ lmax, int64_t n_units,
+                                                        int64_t table_rows, uint32_t* __restrict__ ids, int flags,
+                                                        int64_t block, int64_t n_blocks, BucketMod* sbm) {
     for (int s = threadIdx.x; s < n_slots; s += blockDim.x) sbm[s] = bucket_mod_init(slots[s].num_bins, slots[s].mask_empty);
     __syncthreads();
     const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
-    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t u = block * blockDim.x + threadIdx.x; u < n_units; u += n_blocks * blockDim.x) {
         const int s = (int)(u % n_slots);
         const rf_slot_desc* sd = slots + s;
         const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
@@ -357,7 +357,61 @@ __global__ __launch_bounds__(256) void single_token_ids_em_kernel(const rf_slot_
     }
 }
 
+__global__ __launch_bounds__(256) void single_token_ids_em_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
+                                                                 const uint8_t* __restrict__ tok_bytes,
+                                                                 const int32_t* __restrict__ tok_off,
+                                                                 const int32_t* __restrict__ bag_off,
+                                                                 const int32_t* __restrict__ lmax, int64_t n_units,
+                                                                 int64_t table_rows, uint32_t* __restrict__ ids, int flags) {
+    __shared__ BucketMod sbm[kIdsMaxSlots];
+    single_token_ids_em_body(slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table_rows, ids, flags,
+                             blockIdx.x, gridDim.x, sbm);
+}
+
+// several towers in one launch (rf_single_token_ids_multi_fwd): workgroups [first[k], first[k + 1]) run task k
+struct IdsTasks {
+    rf_ids_task t[4];
+    int64_t first[5];
+    int n;
+};
+__global__ __launch_bounds__(256) void single_token_ids_multi_kernel(const IdsTasks tasks) {
+    __shared__ BucketMod sbm[kIdsMaxSlots];
+    int k = 0;
+    while (k + 1 < tasks.n && (int64_t)blockIdx.x >= tasks.first[k + 1]) ++k;
+    const rf_ids_task& t = tasks.t[k];
+    single_token_ids_em_body(t.slots, t.n_slots, t.tok_bytes, t.tok_off, t.bag_off, t.lmax, (int64_t)t.batch * t.n_slots,
+                             t.table_rows, t.ids, t.flags, (int64_t)blockIdx.x - tasks.first[k],
+                             tasks.first[k + 1] - tasks.first[k], sbm);
+}
+
 }  // namespace
+
+extern "C" int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n_tasks, void* stream) {
+    RF_REQUIRE(tasks && n_tasks >= 1 && n_tasks <= 4, "rf_single_token_ids_multi_fwd: need 1 <= n_tasks <= 4 (got %d)", n_tasks);
+    IdsTasks a{};
+    a.n = n_tasks;
+    int64_t blocks = 0;
+    for (int k = 0; k < n_tasks; ++k) {
+        const rf_ids_task& t = tasks[k];
+        RF_REQUIRE(t.n_slots >= 1 && t.n_slots <= kIdsMaxSlots && t.batch >= 0,
+                   "rf_single_token_ids_multi_fwd: task %d needs 1 <= n_slots <= %d, batch >= 0", k, kIdsMaxSlots);
+        RF_REQUIRE((t.flags & ~RF_FLAG_MASK_PADDING) == 0 && t.reserved == 0,
+                   "rf_single_token_ids_multi_fwd: task %d: only RF_FLAG_MASK_PADDING is accepted", k);
+        RF_REQUIRE(t.table_rows >= 1 && t.table_rows < (int64_t)kRowNaN,
+                   "rf_single_token_ids_multi_fwd: task %d: table_rows must be in [1, 2^32 - 2)", k);
+        const int64_t n_units = (int64_t)t.batch * t.n_slots;
+        if (n_units)
+            RF_REQUIRE(t.slots && t.tok_bytes && t.tok_off && t.bag_off && t.lmax && t.ids && ((uintptr_t)t.ids & 7) == 0,
+                       "rf_single_token_ids_multi_fwd: task %d: null pointer or ids not 8-byte aligned", k);
+        a.t[k] = t;
+        a.first[k] = blocks;
+        blocks += std::min<int64_t>((n_units + 255) / 256, 256 * 32 / n_tasks);
+    }
+    a.first[n_tasks] = blocks;
+    if (blocks == 0) return RF_OK;
+    hipLaunchKernelGGL(single_token_ids_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, rf_stream(stream), a);
+    return rf_check_launch("single_token_ids_multi_kernel");
+}
 
 extern "C" int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
                                        const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,

@@ -478,6 +478,68 @@ __global__ __launch_bounds__(1024) void reduce_long_kernel(const uint32_t* __res
     }
 }
 
+// Long segments, RF_FLAG_TREE_REDUCE (opt-in, SURVEY §8d's |d| <= L 2^-23 sum|x| bar instead of the reference's
+// CPU order): position group pi (of PT = 1024 / TPR) sums positions i0 + pi, i0 + pi + PT, ... in that order in
+// registers (8 positions' loads in flight, no LDS, no barrier per chunk), then the PT partials meet in a fixed
+// pairwise tree through LDS. The same assignment and tree for every launch: replay-deterministic.
+template <int TPR>
+__global__ __launch_bounds__(1024) void reduce_long_tree_kernel(const uint32_t* __restrict__ src,
+                                                                const uint32_t* __restrict__ aux,
+                                                                const int32_t* __restrict__ seg,
+                                                                const int32_t* __restrict__ long_list,
+                                                                const int32_t* __restrict__ long_cnt,
+                                                                const int64_t* __restrict__ uniq_rows,
+                                                                const float* __restrict__ table, int D,
+                                                                const float* __restrict__ out,
+                                                                const float* __restrict__ dout,
+                                                                const int32_t* __restrict__ cnt,
+                                                                float* __restrict__ uniq_grad) {
+    constexpr int PT = 1024 / TPR;
+    constexpr int DEPTH = 8;
+    __shared__ float4 part[PT][TPR];
+    const int t = threadIdx.x, pi = t / TPR, lane = t % TPR;
+    const bool active = lane * 4 < D;
+    const auto* dout4 = reinterpret_cast<const float4*>(dout);
+    const auto* out4 = reinterpret_cast<const float4*>(out);
+    const auto* cnt4 = reinterpret_cast<const int4*>(cnt);
+    const int nl = *long_cnt;
+    for (int j = blockIdx.x; j < nl; j += gridDim.x) {
+        const int32_t u = long_list[j];
+        const int i0 = seg[u], i1 = seg[u + 1];
+        const int64_t row = uniq_rows[u];
+        const float4 trow = (active && table) ? reinterpret_cast<const float4*>(table + row * D)[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        // this group's positions i0 + pi + PT * k, DEPTH at a time: every load of a step issued before its adds
+        for (int base = i0 + pi; base < i1; base += PT * DEPTH) {
+            uint32_t rs[DEPTH], ra[DEPTH];
+#pragma unroll
+            for (int k = 0; k < DEPTH; ++k) {
+                const int i = base + PT * k;
+                rs[k] = (i < i1 && active) ? src[i] : kZero;
+                ra[k] = (i < i1 && active) ? aux[i] : 0u;
+            }
+            float4 v[DEPTH];
+#pragma unroll
+            for (int k = 0; k < DEPTH; ++k) v[k] = pos_value(rs[k], ra[k], lane, trow, dout4, out4, cnt4);
+#pragma unroll
+            for (int k = 0; k < DEPTH; ++k) add4(acc, v[k]);
+        }
+        part[pi][lane] = acc;
+        __syncthreads();
+#pragma unroll
+        for (int s = PT / 2; s >= 1; s >>= 1) {
+            if (pi < s) {
+                float4 a = part[pi][lane];
+                add4(a, part[pi + s][lane]);
+                part[pi][lane] = a;
+            }
+            __syncthreads();
+        }
+        if (pi == 0 && active) reinterpret_cast<float4*>(uniq_grad + (int64_t)u * D)[lane] = part[0][lane];
+        __syncthreads();
+    }
+}
+
 // ---- owner-side gradient sum (sharded training) ------------------------------------------------
 __global__ __launch_bounds__(256) void ids_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t range,
                                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
@@ -695,7 +757,8 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
     RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 32) - 1, "rf_fused_hash_embed_bwd: table_rows must be in [1, 2^32 - 1)");
     RF_REQUIRE(dim >= 4 && dim <= 256 && dim % 4 == 0, "rf_fused_hash_embed_bwd: dim must be a multiple of 4 in [4, 256]");
     RF_REQUIRE(out_stride % 4 == 0 && out_stride >= 2 * (int64_t)dim, "rf_fused_hash_embed_bwd: out_stride must be a multiple of 4");
-    RF_REQUIRE((flags & ~RF_FLAG_MASK_PADDING) == 0, "rf_fused_hash_embed_bwd: only RF_FLAG_MASK_PADDING is accepted");
+    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_TREE_REDUCE)) == 0,
+               "rf_fused_hash_embed_bwd: only RF_FLAG_MASK_PADDING and RF_FLAG_TREE_REDUCE are accepted");
     RF_REQUIRE(uniq_cap >= 0 && n_uniq && ws, "rf_fused_hash_embed_bwd: null pointer");
     const BwdLayout lay = bwd_layout(n_positions, n_slots, table_rows);
     RF_REQUIRE(ws_bytes >= lay.total, "rf_fused_hash_embed_bwd: workspace too small (%zu < %zu)", ws_bytes, lay.total);
@@ -766,8 +829,12 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
         const int teams = 256 / TPR;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((max_u + teams - 1) / teams, 256 * 64));
         const int lgrid = (int)std::max<int64_t>(1, std::min<int64_t>(n / kLong + 1, 1024));
-        hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
-                           uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
+        if (flags & RF_FLAG_TREE_REDUCE)
+            hipLaunchKernelGGL(reduce_long_tree_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list,
+                               long_cnt, uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
+        else
+            hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
+                               uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
         hipLaunchKernelGGL(reduce_short_kernel<TPR>, dim3(grid), dim3(256), 0, st, src, aux, seg, n_uniq, uniq_cap,
                            uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
     };

@@ -12,6 +12,7 @@ Buffers: the ESIM kernel and the input MLP write straight into column ranges of 
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Sequence
 
 import torch
@@ -117,15 +118,19 @@ class Esim(torch.nn.Module):
 
         self._check_batches(user, ad)
         B, dev = user.batch, self.enc_q.table.device
-        ids = []
-        for enc, b in ((self.enc_q, user), (self.enc_a, ad)):
+        ids, tasks, keep = [], (L.IdsTask * 2)(), []
+        for k, (enc, b) in enumerate(((self.enc_q, user), (self.enc_a, ad))):
             if not b.is_device():
                 b = b.to(dev)
+                keep.append(b)
             t = torch.empty((B, self.L, 2), dtype=torch.int32, device=dev)
-            L.call("rf_single_token_ids_fwd", L.ptr(enc.desc), len(enc.slots), L.ptr(b.tok_bytes), L.ptr(b.tok_off),
-                   L.ptr(b.bag_off), L.ptr(b.lmax), B, enc.table.shape[0], L.ptr(t),
-                   L.FLAG_MASK_PADDING if enc.mask_padding else 0, L.stream_ptr(None))
+            tasks[k] = L.IdsTask(L.ptr(enc.desc), L.ptr(b.tok_bytes), L.ptr(b.tok_off), L.ptr(b.bag_off), L.ptr(b.lmax),
+                                 L.ptr(t), enc.table.shape[0], len(enc.slots), B,
+                                 L.FLAG_MASK_PADDING if enc.mask_padding else 0, 0)
             ids.append(t)
+        # both towers' index passes in one launch (rf_single_token_ids_multi_fwd; the host task array is read at the
+        # call, so it need not outlive it)
+        L.call("rf_single_token_ids_multi_fwd", ctypes.addressof(tasks), 2, L.stream_ptr(None))
         return ids[0], ids[1]
 
     def attention_gather(self, q_ids: torch.Tensor, a_ids: torch.Tensor, pooled: torch.Tensor):

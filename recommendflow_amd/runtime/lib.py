@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("RF_LIB") or os.path.normpath(os.path.join(_HERE, ".."
 RF_OK, RF_EINVAL, RF_EHIP, RF_EOOB = 0, -1, -2, -3
 DT_F32, DT_BF16, DT_F16 = 0, 1, 2
 COMB = {"sum": 0, "avg": 1, "max": 2, "min": 3, "first": 4, "last": 5, "null": 6, "cls": 4}
-FLAG_MASK_PADDING, FLAG_EMIT_IDX, FLAG_SINGLE_TOKEN = 0x1, 0x2, 0x4
+FLAG_MASK_PADDING, FLAG_EMIT_IDX, FLAG_SINGLE_TOKEN, FLAG_TREE_REDUCE = 0x1, 0x2, 0x4, 0x10
 ACT = {None: 0, "none": 0, "linear": 0, "gelu": 1, "relu": 2, "selu": 3, "softmax": 4}
 
 _lock = threading.Lock()
@@ -33,6 +33,7 @@ _SIGS = {
     "rf_esim_soft_attention_fwd": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
     "rf_esim_gather_fwd": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _i64, _vp]),
     "rf_single_token_ids_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i32, _vp]),
+    "rf_single_token_ids_multi_fwd": (ctypes.c_int, [_vp, _i32, _vp]),
     "rf_norm_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _vp]),
     "rf_linear_fwd": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
     "rf_dense_head_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i32, _vp, _i32, _vp, _i64, _vp]),
@@ -107,6 +108,12 @@ _DIAG_SIGS = {"rf_diag_fused_hash_embed_fwd": _SIGS["rf_fused_hash_embed_fwd"],
               "rf_diag_esim_gather_stamped": (ctypes.c_int, _SIGS["rf_esim_gather_fwd"][1][:-1] + [_vp, _i32, _vp])}
 DIAG_EXPORTED = tuple(_DIAG_SIGS)
 DIAG_ABLATIONS = 0x7000  # bits 12-14: accepted only by rf_diag_fused_hash_embed_fwd
+
+
+class IdsTask(ctypes.Structure):
+    """include/rf_api.h rf_ids_task (rf_single_token_ids_multi_fwd)."""
+    _fields_ = [("slots", _vp), ("tok_bytes", _vp), ("tok_off", _vp), ("bag_off", _vp), ("lmax", _vp), ("ids", _vp),
+                ("table_rows", _i64), ("n_slots", _i32), ("batch", _i32), ("flags", _i32), ("reserved", _i32)]
 
 
 class RFError(RuntimeError):

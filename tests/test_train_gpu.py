@@ -183,3 +183,56 @@ def test_keras_adam_multi_tensor_list(O, cuda):
         assert np.array_equal(bits(p.detach().cpu().numpy()), bits(w))
         assert np.array_equal(bits(om.cpu().numpy()), bits(m))
         assert np.array_equal(bits(ov.cpu().numpy()), bits(v))
+
+
+def _positions_per_row(O, enc, hb):
+    """Number of gradient positions of every fused-table row (the reference's padded [B, Lmax] id tensor per slot
+    and table: tokens at their bucket row, pad positions at the slot's pad row)."""
+    _, idx = O.fused_hash_embed(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, hb.batch,
+                                enc.table.cpu().numpy(), enc.dim, enc.out_width, emit_idx=True)
+    S = len(enc.slots)
+    empty = from_lists([[[b""] for _ in range(S)]])
+    _, pidx = O.fused_hash_embed(enc.host_desc, empty.tok_bytes, empty.tok_off, empty.bag_off, empty.lmax, 1,
+                                 enc.table.cpu().numpy(), enc.dim, enc.out_width, emit_idx=True)
+    rb = np.asarray(enc.host_desc["row_base"], np.int64)  # [S][2]
+    lens = np.diff(hb.bag_off).reshape(hb.batch, S)
+    slot_of_tok = np.repeat(np.tile(np.arange(S), hb.batch), lens.reshape(-1))
+    cnt = np.zeros(enc.table.shape[0], np.int64)
+    for k in range(2):
+        np.add.at(cnt, rb[slot_of_tok, k] + idx[: len(slot_of_tok), k], 1)
+        pads = (np.asarray(hb.lmax)[None, :] - lens).sum(axis=0)  # pad positions per slot
+        np.add.at(cnt, rb[:, k] + pidx[:S, k], pads)
+    return cnt
+
+
+@pytest.mark.parametrize("dim", [16, 64, 128])
+def test_bwd_tree_reduce_within_bound(O, cuda, dim):
+    """RF_FLAG_TREE_REDUCE (FusedSparseEncoder.tree_reduce): rows with more than 256 positions are summed as
+    fixed-order partials + a pairwise tree. Against the oracle's CPU-order sums every element must satisfy SURVEY
+    §8d's bar |d| <= L 2^-23 sum|x| (L = the row's positions, sum|x| = the oracle on |dout|); rows and short
+    segments are bit-exact, and the result replays bit-identically."""
+    S, B = 4, 2048
+    specs = [SlotSpec(f"f{s}", 3 + s, (2022 + s, 2023), COMBS[s % 6]) for s in range(S)]
+    enc = FusedSparseEncoder(specs, dim, seed=9)
+    enc.tree_reduce = True
+    hb = synthetic_batch(B, [True, False, True, False], seed=5, id_max=5)
+    dev = hb.to("cuda")
+    out = enc(dev)
+    dout = torch.randn(out.shape, generator=torch.Generator().manual_seed(4)).cuda()
+    sg = enc.backward(dev, dout, out=out)
+    n = sg.count()
+    gr, gg = sg.rows[:n].cpu().numpy(), sg.grad[:n].cpu().numpy()
+    sg2 = enc.backward(dev, dout, out=out)
+    assert np.array_equal(bits(sg2.grad[:n].cpu().numpy()), bits(gg))  # replay-deterministic
+    args = (enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.lmax, hb.batch, enc.table.cpu().numpy(), enc.dim,
+            out.cpu().numpy())
+    wr, wg = O.fused_hash_embed_bwd(*args, dout.cpu().numpy())
+    _, wabs = O.fused_hash_embed_bwd(*args, np.abs(dout.cpu().numpy()))
+    np.testing.assert_array_equal(gr, wr)
+    L = _positions_per_row(O, enc, hb)[gr].astype(np.float64)
+    assert L.max() > 256  # the long-segment kernel ran
+    bound = L[:, None] * 2.0 ** -23 * wabs.astype(np.float64)
+    err = np.abs(gg.astype(np.float64) - wg.astype(np.float64))
+    assert (err <= bound).all(), float((err - bound).max())
+    short = L <= 256
+    assert np.array_equal(bits(gg[short]), bits(wg[short]))

@@ -34,6 +34,13 @@ def main():
            "hbm_bytes_per_launch": int(rd + wr),
            "correction": "read = FETCH_SIZE*1024*2 (gfx950 counts 64 B per 128-B wide-read request), write = WRITE_SIZE*1024",
            "source": d}
+    # every other counter of the passes, averaged per launch (occupancy / stall / request counters)
+    names = set()
+    for f in glob.glob(f"{d}/pmc_*/run_counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if "fused_hash_embed_kernel" in r["Kernel_Name"]:
+                names.add(r["Counter_Name"])
+    res["counters_per_launch"] = {n: per_launch(d, n)[0] for n in sorted(names - {"FETCH_SIZE", "WRITE_SIZE"})}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
