@@ -67,7 +67,8 @@ def stamp_report(model, ids, pooled, B):
     from recommendflow_amd.runtime import lib as L
 
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    grid = min(B, 2 * cus)
+    split = os.environ.get("RF_ESIM_SPLIT", "1") != "0" and model.d == 128
+    grid = min(B, (3 if split else 2) * cus)
     EX, P = -(-B // grid) + 1, 10
     st = torch.zeros(grid * 4 * EX * P, dtype=torch.int32, device="cuda")
     L.call("rf_diag_esim_gather_stamped", L.ptr(ids[0]), L.ptr(ids[1]), L.ptr(model.enc_q.table), L.ptr(model.enc_a.table),
@@ -78,6 +79,11 @@ def stamp_report(model, ids, pooled, B):
     order = [0, 1, 7, 8, 9, 2, 3, 4, 5, 6]
     names = ["issue next loads", "scores (E^T)", "softmax", "P@V+stats side 0", "P@V+stats side 1", "compute barrier",
              "stage next images", "reduce pooled", "second barrier"]
+    if split:  # esim_split_kernel's points (rf_attn.hip)
+        order = [0, 1, 2, 3, 4, 5, 6, 7]
+        names = ["P1 scores over hash-0 half (+ loads issued)", "barrier, stage hash-1 half, barrier",
+                 "P2 scores over hash-1 half + softmax", "P2 P@V + stats cols 64..127", "barrier, stage hash-0, barrier",
+                 "P3 P@V + stats cols 0..63", "barrier, stage next, reduce, barrier"]
     rows = {1: [], 2: []}
     for g in range(grid):
         n_g = len(range(g, B, grid))
@@ -86,7 +92,7 @@ def stamp_report(model, ids, pooled, B):
                 sp0 = (w + k) & 3
                 v = t[g, w, k]
                 d = [(v[order[i + 1]] - v[order[i]]) % (1 << 32) for i in range(len(order) - 1)]
-                nxt = t[g, w, k + 1, 0] if k + 1 < n_g else None
+                nxt = t[g, w, k + 1, order[0]] if k + 1 < n_g else None
                 tot = (nxt - v[0]) % (1 << 32) if nxt is not None else None
                 rows[2 if sp0 + 4 < 7 else 1].append(d + [tot if tot is not None else -1])
     out = {}
