@@ -1002,313 +1002,6 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
 }
 
 // ---------------------------------------------------------------------------------------------
-// ESIM v8, GATHER at d = 128 (rf_esim_gather_fwd's default): a d = 128 token row is [hash-0 table row | hash-1 table
-// row], so the images can be staged one TABLE at a time ("half images", 64 columns): 2 x 112 x 80 bf16 = 35 KB +
-// statistics 12 KB + ids 3.5 KB = 50.5 KB per workgroup and THREE workgroups (12 waves) per CU instead of two (v6:
-// 78.5 KB, 8 waves; r04 phase stamps and counters: 41 % of wave cycles issuing, the rest waiting on dependencies,
-// LDS and barriers, so a third co-resident example hides them). Per example e:
-//   P1  E^T over the hash-0 half (k-steps 0, 1)                             [e's hash-1 rows in flight]
-//   stage the hash-1 half
-//   P2  E^T over the hash-1 half (k-steps 2, 3), softmax, P @ V and statistics for columns 64..127
-//                                                                           [e's hash-0 rows in flight again (L2)]
-//   stage the hash-0 half
-//   P3  P @ V and statistics for columns 0..63                               [e + G's hash-0 rows in flight]
-//   stage e + G's hash-0 half, reduce e's statistics
-// The MFMAs, their k order and the statistics are esim2_kernel's (its column halves are exactly these), so the
-// pooled features are bit-identical to it. Rows r >= L read the zero row (their ids are kRowZero in LDS).
-// ---------------------------------------------------------------------------------------------
-constexpr int kSplitRS = 80;  // half-image row stride (64 + 16 elements, as the d = 64 esim2 images)
-__host__ __device__ constexpr size_t esim_split_lds_bytes(int ntt) {
-    return (size_t)2 * ntt * 16 * kSplitRS * 2 + (size_t)kEsim2Waves * 3 * 2 * 128 * 4 + (size_t)2 * 4 * 16 * ntt * 4;
-}
-
-// E^T += the half image's two k-steps for the wave's stripes (esim3_wave's score loop, k-steps 2 h, 2 h + 1)
-template <typename M, int NTT, bool TWO>
-__device__ __forceinline__ void split_scores(const uint16_t* qs, const uint16_t* as, int sp0, int sp1, int lane,
-                                             f4 (&e0)[8], f4 (&e1)[8]) {
-    using frag = typename M::frag;
-    constexpr int RS = kSplitRS;
-    const int lr = lane & 15, lg = lane >> 4;
-    frag b0[2], b1[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-        b0[kk] = lds_frag<frag>(as + (sp0 * 16 + lr) * RS + kk * 32 + lg * 8);
-        b1[kk] = b0[kk];
-        if (TWO) b1[kk] = lds_frag<frag>(as + (sp1 * 16 + lr) * RS + kk * 32 + lg * 8);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int jt = 0; jt < NTT; ++jt) {
-            const frag qf = lds_frag<frag>(qs + (jt * 16 + lr) * RS + kk * 32 + lg * 8);
-            e0[jt] = M::mma(qf, b0[kk], e0[jt]);
-            if (TWO) e1[jt] = M::mma(qf, b1[kk], e1[jt]);
-        }
-    }
-}
-
-// P @ V and the ESIM statistics of the column half h (V = the half images), esim3_wave's XM branch for one h, its 4
-// column tiles in 2 passes of 2 (accumulators for 2 tiles at a time: the 168-register budget of 3 waves per SIMD)
-template <typename M, int NTT, bool TWO, int XM, int KT0, int XHI>
-__device__ __forceinline__ void split_pv(const uint16_t* qs, const uint16_t* as, float* wst, int sp0, int h, int lane,
-                                         const typename M::frag (&pa0)[4], const typename M::frag (&pa1)[4]) {
-    using frag = typename M::frag;
-    constexpr int RS = kSplitRS, D = 128, NC = 2, nt = NTT;
-    const int lr = lane & 15, lg = lane >> 4;
-    const frag sel = stripe_selector<M>(sp0, lr, lg);
-    constexpr int kt0 = KT0, kt1 = KT0 + 2;
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-        const uint16_t* V = side ? as : qs;
-        float hx[4], hm[4], hmx[4];
-#pragma unroll
-        for (int cp = 0; cp < 4; cp += NC) {
-            f4 a0[NC], a1[NC], x0[NC], x1[NC];
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                a0[c] = f4{0.f, 0.f, 0.f, 0.f};
-                a1[c] = f4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt) {
-                if (2 * kt < nt) {
-                    const bool hi_ok = 2 * kt + 1 < nt;
-                    if (kt < 2 ? kt == kt0 : (TWO && kt == kt1)) {
-#pragma unroll
-                        for (int c = 0; c < NC; ++c) {
-                            const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, (cp + c) * 16, lane, hi_ok);
-                            a0[c] = M::mma(pa0[kt], vf, a0[c]);
-                            if (TWO) a1[c] = M::mma(pa1[kt], vf, a1[c]);
-                            if constexpr (XM == 2) {
-                                if (kt < 2) x0[c] = frag_rows_f32<M, XHI>(vf);
-                                else x1[c] = frag_rows_f32<M, XHI>(vf);
-                            } else {
-                                if (kt < 2) x0[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
-                                else x1[c] = M::mma(sel, vf, f4{0.f, 0.f, 0.f, 0.f});
-                            }
-                        }
-                    } else {
-#pragma unroll
-                        for (int c = 0; c < NC; ++c) {
-                            const frag vf = v_frag_tr_acc_h<frag>(V, RS, kt * 32, (cp + c) * 16, lane, hi_ok);
-                            a0[c] = M::mma(pa0[kt], vf, a0[c]);
-                            if (TWO) a1[c] = M::mma(pa1[kt], vf, a1[c]);
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < NC; ++c) esim_stats<TWO>(x0[c], a0[c], x1[c], a1[c], hx[cp + c], hm[cp + c], hmx[cp + c]);
-        }
-        const int pk = (lg == 1) ? 2 : (lg == 2) ? 1 : lg;
-        float* w = wst + side * D + lr;
-        const int n = (h * 4 + pk) * 16;
-        w[n] = rs4<false>(hx[0], hx[1], hx[2], hx[3]);
-        w[2 * D + n] = rs4<false>(hm[0], hm[1], hm[2], hm[3]);
-        w[4 * D + n] = rs4<true>(hmx[0], hmx[1], hmx[2], hmx[3]);
-    }
-}
-
-template <int NTT, int XM, bool STAMP = false>
-__global__ __launch_bounds__(kEsim2Waves * 64, 3) void esim_split_kernel(int batch, int L, float* __restrict__ out,
-                                                                         int64_t out_stride, int64_t out_off,
-                                                                         EsimGatherArgs ga) {
-    using M = Mfma<false>;
-    using frag = typename M::frag;
-    constexpr int D = 128, NTH = kEsim2Waves * 64, RS = kSplitRS;
-    constexpr int L16 = NTT * 16, nt = NTT;
-    constexpr int CPR = 8;                               // 16-byte chunks of a half row (one 128-byte table row)
-    constexpr int NCH = (2 * L16 * CPR + NTH - 1) / NTH;  // chunks per thread per staging (= NTT)
-    constexpr int IDS = 2 * L16, IDW = 2 * IDS;           // id dwords per side / per buffer ([side][row][hash])
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    uint16_t* qs = reinterpret_cast<uint16_t*>(smem);
-    uint16_t* as = qs + L16 * RS;
-    float* st = reinterpret_cast<float*>(as + L16 * RS);  // [wave slot][stat 3][side * D + n]
-    uint32_t* idb = reinterpret_cast<uint32_t*>(st + kEsim2Waves * 3 * 2 * D);
-    const int tid = threadIdx.x, wave = tid >> 6;
-    const int64_t G = gridDim.x;
-    // the lane-dependent addresses are recomputed every example from an opaque copy of the thread index: hoisted
-    // out of the loop they outlive the 168-register budget and spill (measured: 16 dwords of scratch)
-    int tt = tid;
-
-    // the id rows L .. L16 - 1 of both buffers and sides hold the zero row, once (the DMAs write rows < L only)
-    if (L16 > L)
-    for (int w = tid; w < 2 * 2 * (L16 - L) * 2; w += NTH) {
-        const int hh = w & 1, r = L + ((w >> 1) % (L16 - L)), bs = (w >> 1) / (L16 - L);
-        idb[(bs >> 1) * IDW + (bs & 1) * IDS + 2 * r + hh] = kRowZero;
-    }
-    // ids of example ee (both sides, [L][2] each) -> buffer b, 64 dwords per wave instruction
-    auto ids_dma = [&](int64_t ee, int b) __attribute__((always_inline)) {
-        const int nc = (2 * L + 63) >> 6;
-        for (int k = wave; k < 2 * nc; k += kEsim2Waves) {
-            const int sd = k >= nc ? 1 : 0, j = k - sd * nc, w = j * 64 + (tt & 63);
-            if (w < 2 * L)
-                __builtin_amdgcn_global_load_lds((sd ? ga.aid : ga.qid) + ee * 2 * L + w,
-                                                 (__attribute__((address_space(3))) void*)(idb + b * IDW + sd * IDS + j * 64),
-                                                 4, 0, 0);
-        }
-    };
-    uint4 pre[NCH];
-    // the rows of table hh (the half hh of every token row) from id buffer b into pre: ids first (one LDS batch),
-    // then the loads; a row id kRowNaN / kRowZero reads the spec row (branch-free integer select, global loads)
-    auto prefetch_half = [&](int b, int hh) __attribute__((always_inline)) {
-        uint32_t idv[NCH];
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-            const int c = tt + i * NTH;
-            const int sd = c >= L16 * CPR ? 1 : 0, r = (c - sd * L16 * CPR) >> 3;
-            idv[i] = idb[b * IDW + sd * IDS + 2 * r + hh];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const char* base = reinterpret_cast<const char*>(ga.qtab);
-        const int64_t d_a = reinterpret_cast<const char*>(ga.atab) - base;
-        const int64_t d_spec = reinterpret_cast<const char*>(ga.spec) - base;
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-            const int c = tt + i * NTH;
-            const int sd = c >= L16 * CPR ? 1 : 0, ch = c & 7;
-            const uint32_t id = idv[i];
-            const int64_t o_tab = (sd ? d_a : 0) + (int64_t)id * 128, o_spec = d_spec + (int64_t)(id & 1u) * 128;
-            const int64_t msk = -(int64_t)(id >= kRowNaN);
-            const int64_t off = ((o_tab & ~msk) | (o_spec & msk)) + ch * 16;
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>(base + off));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto stage = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-            const int c = tt + i * NTH;
-            const int sd = c >= L16 * CPR ? 1 : 0, rem = c - sd * L16 * CPR, r = rem >> 3, ch = rem & 7;
-            *reinterpret_cast<uint4*>((sd ? as : qs) + r * RS + ch * 8) = pre[i];
-        }
-    };
-    constexpr int kOff = 1 << 30;
-    float pv[4] = {0.f, 0.f, 0.f, 0.f};
-    int po[4] = {kOff, kOff, kOff, kOff};
-    int64_t pe = -1;
-    auto flush = [&]() __attribute__((always_inline)) {
-        const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + pe * out_stride + out_off), 0, 6 * D * 4, 0x00020000);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pv[k]), ro, po[k], 0, 0);
-    };
-    int64_t e = blockIdx.x;
-    int cb = 0;  // the id buffer holding example e's ids
-    __syncthreads();  // zero id rows visible
-    if (e < batch) {
-        ids_dma(e, 0);
-        __syncthreads();  // (its fence waits for the DMA) ids of e visible
-        prefetch_half(0, 0);
-        stage();
-        __syncthreads();
-    }
-    uint32_t it = 0;
-    for (; e < batch; e += G) {
-        asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tid));
-        const int lane = tt & 63, lr = lane & 15, lg = lane >> 4;
-        const bool more = e + G < batch;
-        const int rot = (int)(it++ & 3);
-        const int sp0 = (wave + rot) & 3, sp1 = sp0 + kEsim2Waves;
-        const bool act = sp0 < nt, two = sp1 < nt;
-        uint32_t* stp = nullptr;
-        if constexpr (STAMP) {
-            stp = ga.stamps + (((int64_t)blockIdx.x * kEsim2Waves + wave) * ga.stamp_ex + min((int)(it - 1), ga.stamp_ex - 1)) * kStampPts;
-            esim_stamp(stp, 0, lane);
-        }
-        if (pe >= 0) flush();
-        if (more) ids_dma(e + G, cb ^ 1);
-        prefetch_half(cb, 1);
-        // P1: scores over the hash-0 half
-        f4 e0[8], e1[8];
-#pragma unroll
-        for (int jt = 0; jt < 8; ++jt) {
-            e0[jt] = f4{0.f, 0.f, 0.f, 0.f};
-            e1[jt] = f4{0.f, 0.f, 0.f, 0.f};
-        }
-        if (act) {
-            if (two) split_scores<M, NTT, true>(qs, as, sp0, sp1, lane, e0, e1);
-            else split_scores<M, NTT, false>(qs, as, sp0, sp1, lane, e0, e1);
-        }
-        if constexpr (STAMP) esim_stamp(stp, 1, lane);
-        __syncthreads();
-        stage();
-        __syncthreads();
-        if constexpr (STAMP) esim_stamp(stp, 2, lane);
-        prefetch_half(cb, 0);  // the hash-0 half again, for P3 (from L2: read one phase ago)
-        // P2: scores over the hash-1 half, softmax, P @ V of columns 64..127
-        float* wst = st + sp0 * 3 * 2 * D;
-        frag pa0[4], pa1[4];
-        auto pv_half = [&](int h) __attribute__((always_inline)) {
-            auto run = [&](auto tw, auto kt0, auto xhi) __attribute__((always_inline)) {
-                split_pv<M, NTT, decltype(tw)::value, XM, decltype(kt0)::value, decltype(xhi)::value>(qs, as, wst, sp0, h,
-                                                                                                      lane, pa0, pa1);
-            };
-            using T_ = std::true_type;
-            using F_ = std::false_type;
-            using I0 = std::integral_constant<int, 0>;
-            using I1 = std::integral_constant<int, 1>;
-            const int xh = XM == 2 ? (sp0 & 1) : 0;
-            if (two) {
-                if (sp0 >> 1) { if (xh) run(T_{}, I1{}, I1{}); else run(T_{}, I1{}, I0{}); }
-                else { if (xh) run(T_{}, I0{}, I1{}); else run(T_{}, I0{}, I0{}); }
-            } else {
-                if (sp0 >> 1) { if (xh) run(F_{}, I1{}, I1{}); else run(F_{}, I1{}, I0{}); }
-                else { if (xh) run(F_{}, I0{}, I1{}); else run(F_{}, I0{}, I0{}); }
-            }
-        };
-        if (act) {
-            if (two) split_scores<M, NTT, true>(qs, as, sp0, sp1, lane, e0, e1);
-            else split_scores<M, NTT, false>(qs, as, sp0, sp1, lane, e0, e1);
-            stripe_softmax3<M, NTT>(e0, L, lg, sp0 * 16 + lr < L, pa0);
-            if (two) stripe_softmax3<M, NTT>(e1, L, lg, sp1 * 16 + lr < L, pa1);
-            if constexpr (STAMP) esim_stamp(stp, 3, lane);
-            pv_half(1);
-        }
-        if constexpr (STAMP) esim_stamp(stp, 4, lane);
-        __syncthreads();
-        stage();
-        __syncthreads();
-        if constexpr (STAMP) esim_stamp(stp, 5, lane);
-        if (more) prefetch_half(cb ^ 1, 0);  // e + G's hash-0 half
-        // P3: P @ V of columns 0..63
-        if (act) pv_half(0);
-        if constexpr (STAMP) esim_stamp(stp, 6, lane);
-        __syncthreads();  // statistics complete, images free
-        if (more) stage();
-        // pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]  (esim.py:82,84), as esim2_kernel
-        {
-            constexpr int nw = nt < kEsim2Waves ? nt : kEsim2Waves;
-            const int side = lane >> 5;
-            const int n = wave * 32 + (lane & 31);
-            float sx = 0.f, smul = 0.f, m3 = -INFINITY;
-#pragma unroll
-            for (int w = 0; w < nw; ++w) {
-                const float* ws = st + w * 3 * 2 * D + side * D + n;
-                sx += ws[0];
-                smul += ws[2 * D];
-                m3 = fmx(m3, ws[4 * D]);
-            }
-            const float avg = (2.0f * sx + smul) / (float)(4 * L);
-            const float avg_o = __shfl_xor(avg, 32, 64), mx_o = __shfl_xor(m3, 32, 64);
-            pv[0] = avg;
-            pv[1] = m3;
-            pv[2] = avg - avg_o;
-            pv[3] = m3 - mx_o;
-            po[0] = (2 * side * D + n) * 4;
-            po[1] = ((2 * side + 1) * D + n) * 4;
-            po[2] = side == 0 ? (4 * D + n) * 4 : kOff;
-            po[3] = side == 0 ? (5 * D + n) * 4 : kOff;
-            pe = e;
-        }
-        __syncthreads();  // next images visible; statistics reads retired
-        if constexpr (STAMP) esim_stamp(stp, 7, lane);
-        cb ^= 1;
-    }
-    if (pe >= 0) flush();
-}
-
-// ---------------------------------------------------------------------------------------------
 // masked multi-head SDPA: one workgroup per (example, head)
 // ---------------------------------------------------------------------------------------------
 template <bool F16, int DEP>
@@ -1483,14 +1176,11 @@ int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, i
 template <int D, int NTT>
 int launch_esim2g_nt(int grid, size_t lds, hipStream_t st, int batch, int L, float* out, int64_t out_stride,
                      int64_t out_off, const EsimGatherArgs& ga) {
-    // RF_ESIM_GXM=2: x from the P @ V B fragments (v7) instead of the selector MFMA (v5); A/B runs only
-    static const int gxm = [] {
-        const char* e = getenv("RF_ESIM_GXM");
-        return e && e[0] == '2' ? 2 : 1;
-    }();
-    auto kern = gxm == 2 ? esim2_kernel<false, D, NTT, 2, true> : esim2_kernel<false, D, NTT, 1, true>;
+    // (XM = 2, x widened from the P @ V B fragments instead of the selector MFMA, measured equal: r04g3 0.0875 /
+    // 0.0869 vs 0.0872 / 0.0865 ms; the template keeps it, no launcher instantiates it)
+    auto kern = esim2_kernel<false, D, NTT, 1, true>;
     if constexpr (D == 128 && NTT == 7) {  // the diagnostic stamped build: cfg3's shape only
-        if (ga.stamps) kern = gxm == 2 ? esim2_kernel<false, D, NTT, 2, true, true> : esim2_kernel<false, D, NTT, 1, true, true>;
+        if (ga.stamps) kern = esim2_kernel<false, D, NTT, 1, true, true>;
     } else {
         if (ga.stamps) return rf_set_error(RF_EINVAL, "stamped ESIM: only d = 128, 97 <= L <= 112");
     }
@@ -1499,47 +1189,6 @@ int launch_esim2g_nt(int grid, size_t lds, hipStream_t st, int batch, int L, flo
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, nullptr, nullptr, batch, L, (int64_t)0,
                        (int64_t)D, out, out_stride, out_off, ga);
     return RF_OK;
-}
-
-// v8 (esim_split_kernel): three workgroups per CU; RF_ESIM_SPLIT=0 runs the v6 gather kernel (A/B only)
-template <int NTT>
-int launch_esim_split_nt(int cus, hipStream_t st, int batch, int L, float* out, int64_t out_stride, int64_t out_off,
-                         const EsimGatherArgs& ga) {
-    static const int gxm = [] {
-        const char* e = getenv("RF_ESIM_GXM");
-        return e && e[0] == '2' ? 2 : 1;
-    }();
-    auto kern = gxm == 2 ? esim_split_kernel<NTT, 2> : esim_split_kernel<NTT, 1>;
-    if constexpr (NTT == 7) {  // the diagnostic stamped build: cfg3's shape only
-        if (ga.stamps) kern = gxm == 2 ? esim_split_kernel<NTT, 2, true> : esim_split_kernel<NTT, 1, true>;
-    } else {
-        if (ga.stamps) return rf_set_error(RF_EINVAL, "stamped ESIM: only d = 128, 97 <= L <= 112");
-    }
-    const size_t lds = esim_split_lds_bytes(NTT);
-    const int per_cu = lds <= 53 * 1024 ? 3 : lds <= 80 * 1024 ? 2 : 1;
-    const int grid = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
-    const int rc = launch_big_lds(kern, grid, lds, st, "esim_split_kernel");
-    if (rc) return rc;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, batch, L, out, out_stride, out_off, ga);
-    return RF_OK;
-}
-
-bool esim_split_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("RF_ESIM_SPLIT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-int launch_esim_split(int nt, int cus, hipStream_t st, int batch, int L, float* out, int64_t out_stride, int64_t out_off,
-                      const EsimGatherArgs& ga) {
-    switch (nt) {
-#define RF_NT(N) case N: return launch_esim_split_nt<N>(cus, st, batch, L, out, out_stride, out_off, ga);
-        RF_NT(1) RF_NT(2) RF_NT(3) RF_NT(4) RF_NT(5) RF_NT(6) RF_NT(7) RF_NT(8)
-#undef RF_NT
-        default: return rf_set_error(RF_EINVAL, "esim split: bad tile count %d", nt);
-    }
 }
 
 template <int D>
@@ -1654,11 +1303,6 @@ int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q
     const int grid = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
     const EsimGatherArgs ga{q_ids, a_ids, (const uint16_t*)q_table, (const uint16_t*)a_table, (const uint16_t*)spec,
                             stamps, stamp_ex};
-    if (d == 128 && esim_split_enabled()) {
-        const int rc = launch_esim_split(nt, cus, st, batch, L, out, out_stride, out_off, ga);
-        if (rc) return rc;
-        return rf_check_launch("rf_esim_gather_fwd");
-    }
     const int rc = d == 64 ? launch_esim2g<64>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga)
                            : launch_esim2g<128>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga);
     if (rc) return rc;

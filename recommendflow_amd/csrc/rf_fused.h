@@ -303,14 +303,20 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         // comb_step(init, x), first/last = x; an empty bag reads the pad rows, or is zeros when masked.
         if (lean) {
             constexpr int UPT = kUnits / TEAMS;     // bags per team
+#ifdef RF_LEAN_GU
+            constexpr int GU = RF_LEAN_GU;
+#else
             constexpr int GU = CPL >= 2 ? 2 : 4;    // bags per load group
+#endif
+#ifdef RF_LEAN_PIPE
+            constexpr bool LPIPE = RF_LEAN_PIPE != 0;  // A/B build option: group q0 + GU's loads issued before q0 is consumed
+#else
+            constexpr bool LPIPE = false;
+#endif
             // the element rule is wave-uniform per item: resolved once here, not as a chain of uniform branches
             // per element (as the single-token kernel)
             auto lean_body = [&](auto rule) __attribute__((always_inline)) {
-#pragma unroll 1
-                for (int q0 = 0; q0 < UPT; q0 += GU) {
-                    uint4 v[GU][2][CPL];
-                    bool has[GU];
+                auto lean_issue = [&](uint4 (&v)[GU][2][CPL], bool (&has)[GU], int q0) __attribute__((always_inline)) {
 #pragma unroll
                     for (int g = 0; g < GU; ++g) {
                         const int jj = min(team + TEAMS * (q0 + g), nu - 1);
@@ -324,6 +330,8 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                             v[g][1][cc] = row_chunk_src<PRE>(table, local_tab, r1, dim, cidx[cc]);
                         }
                     }
+                };
+                auto lean_consume = [&](const uint4 (&v)[GU][2][CPL], const bool (&has)[GU], int q0) __attribute__((always_inline)) {
 #pragma unroll
                     for (int g = 0; g < GU; ++g) {
                         const int j = team + TEAMS * (q0 + g);
@@ -344,6 +352,27 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
                                 }
                                 if (cown[cc]) store_chunk<OT, EPV>(out + ob + (int64_t)k * dim + cidx[cc] * EPV, a);
                             }
+                    }
+                };
+                if constexpr (LPIPE) {
+                    uint4 va[GU][2][CPL], vb[GU][2][CPL];
+                    bool ha[GU], hb[GU];
+                    lean_issue(va, ha, 0);
+#pragma unroll 1
+                    for (int q0 = 0; q0 < UPT; q0 += 2 * GU) {
+                        if (q0 + GU < UPT) lean_issue(vb, hb, q0 + GU);
+                        lean_consume(va, ha, q0);
+                        if (q0 + GU >= UPT) break;
+                        if (q0 + 2 * GU < UPT) lean_issue(va, ha, q0 + 2 * GU);
+                        lean_consume(vb, hb, q0 + GU);
+                    }
+                } else {
+#pragma unroll 1
+                    for (int q0 = 0; q0 < UPT; q0 += GU) {
+                        uint4 v[GU][2][CPL];
+                        bool has[GU];
+                        lean_issue(v, has, q0);
+                        lean_consume(v, has, q0);
                     }
                 }
             };

@@ -67,7 +67,7 @@ def stamp_report(model, ids, pooled, B):
     from recommendflow_amd.runtime import lib as L
 
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    split = os.environ.get("RF_ESIM_SPLIT", "1") != "0" and model.d == 128
+    split = False  # the d-split 3-workgroup kernel (v8) was measured slower and removed (profiles/r04)
     grid = min(B, (3 if split else 2) * cus)
     EX, P = -(-B // grid) + 1, 10
     st = torch.zeros(grid * 4 * EX * P, dtype=torch.int32, device="cuda")
