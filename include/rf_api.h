@@ -60,6 +60,9 @@ extern "C" {
 #define RF_FLAG_TREE_REDUCE 0x10  /* embedding backward only (rf_fused_hash_embed_bwd / _bwd_reduce): rows with more than
                                     256 positions are summed as fixed-order partials + a pairwise tree (deterministic,
                                     within SURVEY 8d's |d| <= L 2^-23 sum|x|) instead of the reference's CPU order */
+#define RF_FLAG_SPEC_ROWS 0x20  /* rf_single_token_ids_fwd / _multi_fwd only: the NaN row is id table_rows and the zero
+                                   row table_rows + 1 (rows the caller keeps right after the table, as rf_esim_gather_fwd
+                                   reads them) instead of 0xfffffffe / 0xffffffff */
 #define RF_FLAG_DIAG_XCD_ORDER 0x0800      /* A/B switch: slot-interleaved XCD item order (measured slower); results identical */
 #define RF_FLAG_DIAG_GENERAL_PHASE2 0x8000 /* A/B switch: force the general pooling path for Lmax = 1 slots; results identical */
 /* Only these two result-preserving switches are accepted here; any other bit returns RF_EINVAL. Bits 12-14
@@ -290,10 +293,11 @@ int rf_dense_head_fwd(const float* x, int64_t M, int32_t K, int64_t ldx, const v
  * batch whose slots all have batch Lmax == 1, ids[u][k] = the fused-table row of hash k of the bag's token (the
  * index half of rf_fused_hash_embed_fwd with RF_FLAG_SINGLE_TOKEN; an empty bag: the slot's pad rows, or
  * 0xffffffff = the zero row under RF_FLAG_MASK_PADDING; a slot whose Lmax is not 1 or that does not fit the
- * table: 0xfffffffe = the NaN row). rf_esim_gather_fwd then runs rf_esim_soft_attention_fwd's kernel with
- * each example's q / a images gathered from q_table / a_table (BF16 [rows][d / 2]) by those ids; spec holds the
- * NaN row then the zero row (BF16 [2][d / 2]). Same pooled outputs as encoders + rf_esim_soft_attention_fwd
- * (x enters the statistics through the selector MFMA, so a -0 in a table row gives the +0 the encoder writes).
+ * table: 0xfffffffe = the NaN row; with RF_FLAG_SPEC_ROWS those two are table_rows + 1 and table_rows).
+ * rf_esim_gather_fwd then runs rf_esim_soft_attention_fwd's kernel with each example's q / a images gathered from
+ * q_table / a_table (BF16 [rows + 2][d / 2]: the table's q_rows / a_rows rows, then a NaN row and a zero row) by
+ * ids made with RF_FLAG_SPEC_ROWS. Same pooled outputs as encoders + rf_esim_soft_attention_fwd (x enters the
+ * statistics through the selector MFMA, so a -0 in a table row gives the +0 the encoder writes).
  */
 int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes, const int32_t* tok_off,
                             const int32_t* bag_off, const int32_t* lmax, int32_t batch, int64_t table_rows, uint32_t* ids,
@@ -313,12 +317,12 @@ typedef struct rf_ids_task {
     int64_t table_rows;
     int32_t n_slots;
     int32_t batch;
-    int32_t flags;             /* 0 or RF_FLAG_MASK_PADDING */
+    int32_t flags;             /* 0, RF_FLAG_MASK_PADDING, RF_FLAG_SPEC_ROWS */
     int32_t reserved;          /* must be 0 */
 } rf_ids_task;
 int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n_tasks, void* stream);
-int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
-                       int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
+int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows,
+                       const void* a_table, int64_t a_rows, int32_t dtype, int32_t batch, int32_t L, int32_t d, float* out,
                        int64_t out_stride, int64_t out_off, void* stream);
 
 /*

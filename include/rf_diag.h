@@ -32,9 +32,10 @@ int rf_diag_fused_hash_embed_fwd(const rf_slot_desc* d_slots, int32_t n_slots, c
  *   0 loop top, 1 next rows' loads issued, 7 scores done, 8 softmax done, 9 side 0 done, 2 compute done,
  *   3 after the compute barrier, 4 next images written, 5 pooled features reduced, 6 after the second barrier.
  * The grid is min(batch, 2 x CUs) workgroups: size stamps for that. Same results as rf_esim_gather_fwd. */
-int rf_diag_esim_gather_stamped(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
-                                int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
-                                int64_t out_stride, int64_t out_off, uint32_t* stamps, int32_t stamp_ex, void* stream);
+int rf_diag_esim_gather_stamped(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows,
+                                const void* a_table, int64_t a_rows, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                                float* out, int64_t out_stride, int64_t out_off, uint32_t* stamps, int32_t stamp_ex,
+                                void* stream);
 
 #ifdef __cplusplus
 }

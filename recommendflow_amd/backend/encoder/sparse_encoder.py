@@ -112,7 +112,7 @@ class FusedSparseEncoder(torch.nn.Module):
 
     def __init__(self, slots: Sequence[SlotSpec], dim: int, table_dtype=torch.float32, out_dtype=None,
                  seed: int = 0, mask_padding: bool = False, device="cuda", init_range=(-0.05, 0.05),
-                 table: Optional[torch.Tensor] = None, row_base0: int = 0):
+                 table: Optional[torch.Tensor] = None, row_base0: int = 0, spec_rows: bool = False):
         super().__init__()
         if not slots:
             raise ValueError("FusedSparseEncoder needs at least one slot")
@@ -151,9 +151,17 @@ class FusedSparseEncoder(torch.nn.Module):
         L.load()
         L.require_gpu()
         self.register_buffer("desc", torch.from_numpy(desc.view(np.uint8).copy()).to(device), persistent=False)
+        # spec_rows: the allocation holds two more rows right after the table, a NaN row (id table_rows) and a zero
+        # row (table_rows + 1), which the ESIM gather path's ids address directly (RF_FLAG_SPEC_ROWS); self.table
+        # stays the [table_rows, dim] view, so every other operator sees the same table
+        self.spec_rows = bool(spec_rows) and table is None
         if table is None:
-            table = torch.empty((self.table_rows, self.dim), dtype=table_dtype, device=device)
+            full = torch.empty((self.table_rows + (2 if self.spec_rows else 0), self.dim), dtype=table_dtype, device=device)
+            table = full[: self.table_rows]
             init_table(table, 0, 1, self.seed, *init_range)
+            if self.spec_rows:
+                full[self.table_rows] = float("nan")
+                full[self.table_rows + 1] = 0.0
         elif table.shape[0] < self.table_rows or table.shape[1] != self.dim:
             raise ValueError(f"shared table {tuple(table.shape)} too small for {self.table_rows} x {self.dim}")
         self.table = table

@@ -751,9 +751,9 @@ __device__ __forceinline__ void esim3_wave(const uint16_t* qs, const uint16_t* a
 struct EsimGatherArgs {
     const uint32_t* qid;   // [batch][L][2]
     const uint32_t* aid;
-    const uint16_t* qtab;  // [rows][D / 2]
+    const uint16_t* qtab;  // [rows + 2][D / 2]: rows, then the NaN row and the zero row (RF_FLAG_SPEC_ROWS ids)
     const uint16_t* atab;
-    const uint16_t* spec;  // [2][D / 2]: a NaN row (id kRowNaN), a zero row (id kRowZero)
+    uint32_t qzero, azero;  // the zero row's id in each table (rows + 1): image rows L .. L16 - 1
     uint32_t* stamps;      // STAMP only: [grid][waves][stamp_ex][kStampPts]
     int stamp_ex;
 };
@@ -798,17 +798,25 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     // a chunk of a row past the image (only where 16-row tiles end inside a 256-chunk group: d = 64, odd
     // tile counts) goes to this thread's slot of the dummy area past the statistics
     uint16_t* dummy = reinterpret_cast<uint16_t*>(st + kEsim2Waves * 3 * 2 * D) + (tid & 127) * 8;
-    // GATHER: two id buffers past the dummy area, each [side][row < L][hash] (4 L dwords used of IDW)
-    constexpr int IDW = 4 * L16;
+    // GATHER: two id buffers past the dummy area, each [side][row < L16][hash]; the DMAs write rows < L, rows L ..
+    // L16 - 1 hold the zero row's id from the kernel start on (no per-chunk row test)
+    constexpr int IDS = 2 * L16, IDW = 2 * IDS;
     uint32_t* idb = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(st) + esim2_stats_dummy_bytes(D));
+    if constexpr (GATHER) {
+        for (int w = tid; w < 2 * 2 * 2 * (L16 - L); w += NTH) {  // [buffer][side][row L ..][hash]
+            const int hh = w & 1, q = w >> 1, r = L + q % (L16 - L), bs = q / (L16 - L);
+            idb[(bs >> 1) * IDW + (bs & 1) * IDS + 2 * r + hh] = (bs & 1) ? ga.azero : ga.qzero;
+        }
+    }
+    // ids of example ee -> buffer buf, one side at a time (64 dwords per wave instruction)
     auto ids_dma = [&](int64_t ee, int buf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < (IDW + NTH - 1) / NTH; ++j) {
-            const int w = tid + j * NTH;
-            if (w < 4 * L) {
-                const uint32_t* src = w < 2 * L ? ga.qid + ee * 2 * L + w : ga.aid + ee * 2 * L + (w - 2 * L);
-                __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(idb + buf * IDW + j * NTH + wave * 64), 4, 0, 0);
-            }
+        const int nc = (2 * L + 63) >> 6;
+        for (int k = wave; k < 2 * nc; k += kEsim2Waves) {
+            const int sd = k >= nc ? 1 : 0, j = k - sd * nc, w = j * 64 + lane;
+            if (w < 2 * L)
+                __builtin_amdgcn_global_load_lds((sd ? ga.aid : ga.qid) + ee * 2 * L + w,
+                                                 (__attribute__((address_space(3))) void*)(idb + buf * IDW + sd * IDS + j * 64),
+                                                 4, 0, 0);
         }
     };
     // the row loads of the next example in kPfParts parts: part 0 at the loop top, parts 1.. between the compute
@@ -819,34 +827,29 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
         constexpr int PC = NCH / kPfParts;
         // every id of the part read from LDS first, then the row loads: left to itself hipcc interleaves them as
         // read -> lgkmcnt(0) -> address -> load per chunk (dependent LDS round trips)
+        // chunk groups wholly past the image (cfg3: 2 of 16) are neither loaded nor staged; a group that straddles
+        // the image end (d = 64) reads a valid id slot and stages into the dummy area
+        auto live = [](int i) { return i % HALF * NTH < L16 * CPR; };
+        auto straddles = [](int i) { return (i % HALF + 1) * NTH > L16 * CPR; };
         uint32_t idv[NCH];
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
-            if (i / PC != part) continue;
+            if (i / PC != part || !live(i)) continue;
             const int cm = tid + (i % HALF) * NTH;
-            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
+            const int r = straddles(i) ? min(cm >> LOG_CPR, L16 - 1) : cm >> LOG_CPR, ch = cm & (CPR - 1);
             const int side = i < HALF ? 0 : 1;
-            idv[i] = idb[buf * IDW + side * 2 * L + 2 * min(r, L - 1) + (ch >= HC ? 1 : 0)];
+            idv[i] = idb[buf * IDW + side * IDS + 2 * r + (ch >= HC ? 1 : 0)];
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
-            if (i / PC != part) continue;
-            const int cm = tid + (i % HALF) * NTH;
-            const int r = cm >> LOG_CPR, ch = cm & (CPR - 1);
-            const int side = i < HALF ? 0 : 1;
-            const uint32_t id = r < L ? idv[i] : kRowZero;
-            const uint16_t* tab = side ? ga.atab : ga.qtab;
-            // the table row or (ids kRowNaN / kRowZero) the spec row, selected branch-free: a conditional pointer
-            // makes hipcc branch (exec-mask if / else) around every chunk's address
-            // (an integer offset from the table pointer, so the load stays a global load: a pointer rebuilt from an
-            // integer becomes a flat load, which lgkmcnt waits for LDS reads would then also wait on)
-            const int64_t d_spec = reinterpret_cast<const char*>(ga.spec) - reinterpret_cast<const char*>(tab);
-            const int64_t o_tab = (int64_t)id * (D / 2 * 2), o_spec = d_spec + (int64_t)(id & 1u) * (D / 2 * 2);
-            const int64_t msk = -(int64_t)(id >= kRowNaN);
-            const int64_t off = ((o_tab & ~msk) | (o_spec & msk)) + (ch & (HC - 1)) * 16;
+            if (i / PC != part || !live(i)) continue;
+            const int ch = (tid + (i % HALF) * NTH) & (CPR - 1);
+            // every id indexes its table directly (the NaN and zero rows sit past the table's rows): one 64-bit
+            // multiply-add per chunk, the side and the chunk offset folded into the base at compile time
+            const char* tab = reinterpret_cast<const char*>(i < HALF ? ga.qtab : ga.atab) + (ch & (HC - 1)) * 16;
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(tab) + off));
+            pre[i] = __builtin_bit_cast(uint4, *reinterpret_cast<const u32x4*>(tab + (uint64_t)idv[i] * (D / 2 * 2)));
         }
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -1282,18 +1285,20 @@ extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t 
 }
 
 namespace {
-int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table, int32_t dtype,
-                     int32_t batch, int32_t L, int32_t d, const void* spec, float* out, int64_t out_stride, int64_t out_off,
-                     uint32_t* stamps, int32_t stamp_ex, void* stream) {
+int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows, const void* a_table,
+                     int64_t a_rows, int32_t dtype, int32_t batch, int32_t L, int32_t d, float* out, int64_t out_stride,
+                     int64_t out_off, uint32_t* stamps, int32_t stamp_ex, void* stream) {
     RF_REQUIRE(dtype == RF_DTYPE_BF16, "rf_esim_gather_fwd: tables must be BF16");
     RF_REQUIRE(L >= 1 && L <= 128, "rf_esim_gather_fwd: need 1 <= L <= 128 (got %d)", L);
     RF_REQUIRE(d == 64 || d == 128, "rf_esim_gather_fwd: d must be 64 or 128 (got %d)", d);
     RF_REQUIRE(batch >= 0, "rf_esim_gather_fwd: batch < 0");
     if (batch == 0) return RF_OK;
-    RF_REQUIRE(q_ids && a_ids && q_table && a_table && spec && out, "rf_esim_gather_fwd: null pointer");
-    RF_REQUIRE(((uintptr_t)q_table & 15) == 0 && ((uintptr_t)a_table & 15) == 0 && ((uintptr_t)spec & 15) == 0 &&
-                   ((uintptr_t)q_ids & 3) == 0 && ((uintptr_t)a_ids & 3) == 0,
-               "rf_esim_gather_fwd: tables / spec must be 16-byte and ids 4-byte aligned");
+    RF_REQUIRE(q_ids && a_ids && q_table && a_table && out, "rf_esim_gather_fwd: null pointer");
+    RF_REQUIRE(q_rows >= 1 && a_rows >= 1 && q_rows + 1 < (int64_t)kRowNaN && a_rows + 1 < (int64_t)kRowNaN,
+               "rf_esim_gather_fwd: table rows must be in [1, 2^32 - 3)");
+    RF_REQUIRE(((uintptr_t)q_table & 15) == 0 && ((uintptr_t)a_table & 15) == 0 && ((uintptr_t)q_ids & 3) == 0 &&
+                   ((uintptr_t)a_ids & 3) == 0,
+               "rf_esim_gather_fwd: tables must be 16-byte and ids 4-byte aligned");
     hipStream_t st = rf_stream(stream);
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1301,8 +1306,8 @@ int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q
     const size_t lds = esim2_gather_lds_bytes(d, nt, esim2_rs(d, nt));
     const int per_cu = lds <= 80 * 1024 ? 2 : 1;
     const int grid = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
-    const EsimGatherArgs ga{q_ids, a_ids, (const uint16_t*)q_table, (const uint16_t*)a_table, (const uint16_t*)spec,
-                            stamps, stamp_ex};
+    const EsimGatherArgs ga{q_ids, a_ids, (const uint16_t*)q_table, (const uint16_t*)a_table, (uint32_t)(q_rows + 1),
+                            (uint32_t)(a_rows + 1), stamps, stamp_ex};
     const int rc = d == 64 ? launch_esim2g<64>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga)
                            : launch_esim2g<128>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga);
     if (rc) return rc;
@@ -1310,18 +1315,18 @@ int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q
 }
 }  // namespace
 
-extern "C" int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, const void* a_table,
-                                  int32_t dtype, int32_t batch, int32_t L, int32_t d, const void* spec, float* out,
-                                  int64_t out_stride, int64_t out_off, void* stream) {
-    return esim_gather_impl(q_ids, a_ids, q_table, a_table, dtype, batch, L, d, spec, out, out_stride, out_off, nullptr, 0,
-                            stream);
+extern "C" int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows,
+                                  const void* a_table, int64_t a_rows, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                                  float* out, int64_t out_stride, int64_t out_off, void* stream) {
+    return esim_gather_impl(q_ids, a_ids, q_table, q_rows, a_table, a_rows, dtype, batch, L, d, out, out_stride, out_off,
+                            nullptr, 0, stream);
 }
 
 extern "C" int rf_diag_esim_gather_stamped(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table,
-                                           const void* a_table, int32_t dtype, int32_t batch, int32_t L, int32_t d,
-                                           const void* spec, float* out, int64_t out_stride, int64_t out_off,
-                                           uint32_t* stamps, int32_t stamp_ex, void* stream) {
+                                           int64_t q_rows, const void* a_table, int64_t a_rows, int32_t dtype,
+                                           int32_t batch, int32_t L, int32_t d, float* out, int64_t out_stride,
+                                           int64_t out_off, uint32_t* stamps, int32_t stamp_ex, void* stream) {
     RF_REQUIRE(stamps && stamp_ex >= 1, "rf_diag_esim_gather_stamped: need a stamp buffer");
-    return esim_gather_impl(q_ids, a_ids, q_table, a_table, dtype, batch, L, d, spec, out, out_stride, out_off, stamps,
-                            stamp_ex, stream);
+    return esim_gather_impl(q_ids, a_ids, q_table, q_rows, a_table, a_rows, dtype, batch, L, d, out, out_stride, out_off,
+                            stamps, stamp_ex, stream);
 }

@@ -305,6 +305,10 @@ __global__ __launch_bounds__(64) void single_token_ids_kernel(const rf_slot_desc
                 r1 = (uint32_t)(rb1 + pb1);
             }
         }
+        if (flags & RF_FLAG_SPEC_ROWS) {
+            r0 = r0 == kRowNaN ? (uint32_t)table_rows : r0 == kRowZero ? (uint32_t)table_rows + 1u : r0;
+            r1 = r1 == kRowNaN ? (uint32_t)table_rows : r1 == kRowZero ? (uint32_t)table_rows + 1u : r1;
+        }
         *reinterpret_cast<uint2*>(ids + 2 * u) = make_uint2(r0, r1);
     }
 }
@@ -353,6 +357,10 @@ __device__ __forceinline__ void single_token_ids_em_body(const rf_slot_desc* __r
                 r1 = (uint32_t)(rb1 + pb1);
             }
         }
+        if (flags & RF_FLAG_SPEC_ROWS) {  // the NaN / zero rows at table_rows / table_rows + 1
+            r0 = r0 == kRowNaN ? (uint32_t)table_rows : r0 == kRowZero ? (uint32_t)table_rows + 1u : r0;
+            r1 = r1 == kRowNaN ? (uint32_t)table_rows : r1 == kRowZero ? (uint32_t)table_rows + 1u : r1;
+        }
         *reinterpret_cast<uint2*>(ids + 2 * u) = make_uint2(r0, r1);
     }
 }
@@ -395,8 +403,8 @@ extern "C" int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n
         const rf_ids_task& t = tasks[k];
         RF_REQUIRE(t.n_slots >= 1 && t.n_slots <= kIdsMaxSlots && t.batch >= 0,
                    "rf_single_token_ids_multi_fwd: task %d needs 1 <= n_slots <= %d, batch >= 0", k, kIdsMaxSlots);
-        RF_REQUIRE((t.flags & ~RF_FLAG_MASK_PADDING) == 0 && t.reserved == 0,
-                   "rf_single_token_ids_multi_fwd: task %d: only RF_FLAG_MASK_PADDING is accepted", k);
+        RF_REQUIRE((t.flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_SPEC_ROWS)) == 0 && t.reserved == 0,
+                   "rf_single_token_ids_multi_fwd: task %d: only RF_FLAG_MASK_PADDING and RF_FLAG_SPEC_ROWS are accepted", k);
         RF_REQUIRE(t.table_rows >= 1 && t.table_rows < (int64_t)kRowNaN,
                    "rf_single_token_ids_multi_fwd: task %d: table_rows must be in [1, 2^32 - 2)", k);
         const int64_t n_units = (int64_t)t.batch * t.n_slots;
@@ -417,7 +425,8 @@ extern "C" int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_sl
                                        const int32_t* tok_off, const int32_t* bag_off, const int32_t* lmax,
                                        int32_t batch, int64_t table_rows, uint32_t* ids, int32_t flags, void* stream) {
     RF_REQUIRE(n_slots >= 1 && batch >= 0, "rf_single_token_ids_fwd: need n_slots >= 1, batch >= 0");
-    RF_REQUIRE((flags & ~RF_FLAG_MASK_PADDING) == 0, "rf_single_token_ids_fwd: only RF_FLAG_MASK_PADDING is accepted");
+    RF_REQUIRE((flags & ~(RF_FLAG_MASK_PADDING | RF_FLAG_SPEC_ROWS)) == 0,
+               "rf_single_token_ids_fwd: only RF_FLAG_MASK_PADDING and RF_FLAG_SPEC_ROWS are accepted");
     RF_REQUIRE(table_rows >= 1 && table_rows < (int64_t)kRowNaN, "rf_single_token_ids_fwd: table_rows must be in [1, 2^32 - 2)");
     const int64_t n_units = (int64_t)batch * n_slots;
     if (n_units == 0) return RF_OK;

@@ -5,8 +5,8 @@ Forward (reference lines in brackets):
   q, a   = user / ad sparse-slot token sequences [B, L, 2D]   (deviation D-esim-inputs: the reference takes
            BERT token sequences; here each slot is one token = its DoubleHashingEmbedding output, so the
            sequence comes straight out of one fused encoder launch per tower)
-  pooled = [d_emb, avg_q, max_q, avg_a, max_a, avg_q-avg_a, max_q-max_a]   [esim.py:78-84; one fused kernel,
-           which also applies the output MLP's first LayerNorm to the whole row and hands the GEMM bf16]
+  pooled = [d_emb, avg_q, max_q, avg_a, max_a, avg_q-avg_a, max_q-max_a]   [esim.py:78-84; one fused kernel
+           (rf_esim_gather_fwd: the q / a token rows gathered from the tables by id)]
   p      = softmax(output_mlp(pooled) W + b)                  [esim.py:85-88; Dropout = identity]
 Buffers: the ESIM kernel and the input MLP write straight into column ranges of one [B, 512 + 6d] tensor.
 """
@@ -34,8 +34,10 @@ class Esim(torch.nn.Module):
         self.L = len(user_slots)
         self.d = 2 * dim
         if encoders is None:
-            encoders = (FusedSparseEncoder(user_slots, dim, table_dtype=table_dtype, seed=seed + 1, device=device),
-                        FusedSparseEncoder(ad_slots, dim, table_dtype=table_dtype, seed=seed + 2, device=device))
+            encoders = (FusedSparseEncoder(user_slots, dim, table_dtype=table_dtype, seed=seed + 1, device=device,
+                                           spec_rows=True),
+                        FusedSparseEncoder(ad_slots, dim, table_dtype=table_dtype, seed=seed + 2, device=device,
+                                           spec_rows=True))
         self.enc_q, self.enc_a = encoders
         ln = LayerNormalization(epsilon=1e-6)
         self.input_mlp = create_mlp(list(input_units), 0.3, "gelu", ln, in_features=n_dense, dtype=mlp_dtype,
@@ -109,7 +111,7 @@ class Esim(torch.nn.Module):
         return (self.gather and isinstance(eq, FusedSparseEncoder) and isinstance(ea, FusedSparseEncoder)
                 and eq.table.dtype == torch.bfloat16 and ea.table.dtype == torch.bfloat16
                 and 2 * eq.dim == self.d and 2 * ea.dim == self.d and self.d in (64, 128) and self.L <= 128
-                and not eq.extra_flags and not ea.extra_flags
+                and not eq.extra_flags and not ea.extra_flags and eq.spec_rows and ea.spec_rows
                 and eq._single_token_batch(user) and ea._single_token_batch(ad))
 
     def token_ids(self, user: SparseBatch, ad: SparseBatch):
@@ -126,7 +128,7 @@ class Esim(torch.nn.Module):
             t = torch.empty((B, self.L, 2), dtype=torch.int32, device=dev)
             tasks[k] = L.IdsTask(L.ptr(enc.desc), L.ptr(b.tok_bytes), L.ptr(b.tok_off), L.ptr(b.bag_off), L.ptr(b.lmax),
                                  L.ptr(t), enc.table.shape[0], len(enc.slots), B,
-                                 L.FLAG_MASK_PADDING if enc.mask_padding else 0, 0)
+                                 (L.FLAG_MASK_PADDING if enc.mask_padding else 0) | L.FLAG_SPEC_ROWS, 0)
             ids.append(t)
         # both towers' index passes in one launch (rf_single_token_ids_multi_fwd; the host task array is read at the
         # call, so it need not outlive it)
@@ -144,15 +146,12 @@ class Esim(torch.nn.Module):
                              f"{tuple(a_ids.shape)}")
         if pooled.dtype != torch.float32 or pooled.dim() != 2 or pooled.shape[0] != B or pooled.shape[1] < self.d_emb + 6 * self.d or pooled.stride(1) != 1:
             raise ValueError(f"pooled must be a row-major [{B}, >= {self.d_emb + 6 * self.d}] fp32 tensor")
-        dev = pooled.device
-        spec = getattr(self, "_spec", None)
-        if spec is None or spec.device != dev:
-            spec = torch.zeros((2, self.d // 2), dtype=torch.bfloat16, device=dev)
-            spec[0] = float("nan")  # the NaN row (id 0xfffffffe), then the zero row (0xffffffff)
-            self._spec = spec
-        L.call("rf_esim_gather_fwd", L.ptr(q_ids), L.ptr(a_ids), L.ptr(self.enc_q.table), L.ptr(self.enc_a.table),
-               L.DT_BF16, q_ids.shape[0], self.L, self.d, L.ptr(spec), L.ptr(pooled), pooled.stride(0), self.d_emb,
-               L.stream_ptr(None))
+        eq, ea = self.enc_q, self.enc_a
+        if not (eq.spec_rows and ea.spec_rows):
+            raise ValueError("the gather path needs encoders built with spec_rows=True")
+        L.call("rf_esim_gather_fwd", L.ptr(q_ids), L.ptr(a_ids), L.ptr(eq.table), eq.table.shape[0], L.ptr(ea.table),
+               ea.table.shape[0], L.DT_BF16, q_ids.shape[0], self.L, self.d, L.ptr(pooled), pooled.stride(0),
+               self.d_emb, L.stream_ptr(None))
 
     def _esim_gather(self, user: SparseBatch, ad: SparseBatch, pooled: torch.Tensor):
         self.attention_gather(*self.token_ids(user, ad), pooled)

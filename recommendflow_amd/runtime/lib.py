@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("RF_LIB") or os.path.normpath(os.path.join(_HERE, ".."
 RF_OK, RF_EINVAL, RF_EHIP, RF_EOOB = 0, -1, -2, -3
 DT_F32, DT_BF16, DT_F16 = 0, 1, 2
 COMB = {"sum": 0, "avg": 1, "max": 2, "min": 3, "first": 4, "last": 5, "null": 6, "cls": 4}
-FLAG_MASK_PADDING, FLAG_EMIT_IDX, FLAG_SINGLE_TOKEN, FLAG_TREE_REDUCE = 0x1, 0x2, 0x4, 0x10
+FLAG_MASK_PADDING, FLAG_EMIT_IDX, FLAG_SINGLE_TOKEN, FLAG_TREE_REDUCE, FLAG_SPEC_ROWS = 0x1, 0x2, 0x4, 0x10, 0x20
 ACT = {None: 0, "none": 0, "linear": 0, "gelu": 1, "relu": 2, "selu": 3, "softmax": 4}
 
 _lock = threading.Lock()
@@ -31,7 +31,7 @@ _SIGS = {
     "rf_embedding_bag_fwd": (ctypes.c_int, [_vp, _i32, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _vp, _i32, _i64, _i64, _vp]),
     "rf_table_init_uniform": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _u64, _f32, _f32, _vp]),
     "rf_esim_soft_attention_fwd": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
-    "rf_esim_gather_fwd": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _i64, _vp]),
+    "rf_esim_gather_fwd": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp]),
     "rf_single_token_ids_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i32, _vp]),
     "rf_single_token_ids_multi_fwd": (ctypes.c_int, [_vp, _i32, _vp]),
     "rf_norm_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _vp]),

@@ -97,8 +97,8 @@ def test_esim_gather_equals_encoders_plus_attention(cuda, mask_padding):
     Ls, B = 100, 300
     user = [SlotSpec(f"u{i:03d}", 20_000, (2022, 2023)) for i in range(Ls)]
     ad = [SlotSpec(f"a{i:03d}", 20_000, (2022, 2023)) for i in range(Ls)]
-    encs = (FusedSparseEncoder(user, 64, table_dtype=torch.bfloat16, seed=4, mask_padding=mask_padding),
-            FusedSparseEncoder(ad, 64, table_dtype=torch.bfloat16, seed=5, mask_padding=mask_padding))
+    encs = (FusedSparseEncoder(user, 64, table_dtype=torch.bfloat16, seed=4, mask_padding=mask_padding, spec_rows=True),
+            FusedSparseEncoder(ad, 64, table_dtype=torch.bfloat16, seed=5, mask_padding=mask_padding, spec_rows=True))
     model = Esim(user, ad, n_dense=16, dim=64, seed=3, encoders=encs)
     from recommendflow_amd.runtime.batch import from_lists
     rng = np.random.default_rng(7)

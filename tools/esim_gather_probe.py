@@ -71,8 +71,9 @@ def stamp_report(model, ids, pooled, B):
     grid = min(B, (3 if split else 2) * cus)
     EX, P = -(-B // grid) + 1, 10
     st = torch.zeros(grid * 4 * EX * P, dtype=torch.int32, device="cuda")
-    L.call("rf_diag_esim_gather_stamped", L.ptr(ids[0]), L.ptr(ids[1]), L.ptr(model.enc_q.table), L.ptr(model.enc_a.table),
-           L.DT_BF16, B, model.L, model.d, L.ptr(model._spec), L.ptr(pooled), pooled.stride(0), model.d_emb, L.ptr(st), EX,
+    eq, ea = model.enc_q, model.enc_a
+    L.call("rf_diag_esim_gather_stamped", L.ptr(ids[0]), L.ptr(ids[1]), L.ptr(eq.table), eq.table.shape[0], L.ptr(ea.table),
+           ea.table.shape[0], L.DT_BF16, B, model.L, model.d, L.ptr(pooled), pooled.stride(0), model.d_emb, L.ptr(st), EX,
            L.stream_ptr(None))
     torch.cuda.synchronize()
     t = st.cpu().numpy().view(np.uint32).astype(np.int64).reshape(grid, 4, EX, P)
