@@ -86,11 +86,17 @@ class GpuShardOps:
                    L.stream_ptr(None))
         return t[:rows]
 
-    def hash_rows(self, desc, n_slots: int, batch: SparseBatch) -> torch.Tensor:
-        out = torch.empty(max(2 * batch.n_tokens, 1), dtype=torch.int64, device=self.device)
-        L.call("rf_hash_rows", L.ptr(desc), n_slots, L.ptr(batch.tok_bytes), L.ptr(batch.tok_off), L.ptr(batch.bag_off),
-               batch.batch, L.ptr(out), L.stream_ptr(None))
-        return out[: 2 * batch.n_tokens]
+    def hash_rows(self, desc, n_slots: int, batch: SparseBatch, tail: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """rf_hash_rows -> int64 [2 n_tok] (+ `tail` appended in the same buffer: the pad rows, without a cat)."""
+        n = 2 * batch.n_tokens
+        nt = 0 if tail is None else tail.numel()
+        out = torch.empty(max(n + nt, 1), dtype=torch.int64, device=self.device)
+        if nt:
+            out[n:n + nt].copy_(tail)
+        if n:
+            L.call("rf_hash_rows", L.ptr(desc), n_slots, L.ptr(batch.tok_bytes), L.ptr(batch.tok_off),
+                   L.ptr(batch.bag_off), batch.batch, L.ptr(out), L.stream_ptr(None))
+        return out[: n + nt]
 
     def bucketize(self, rows: torch.Tensor, nranks: int):
         n = rows.numel()
@@ -406,8 +412,7 @@ class ShardedFusedEncoder(torch.nn.Module):
 
     # -- the three local stages -------------------------------------------------------------------
     def _route_device(self, batch: SparseBatch):
-        rows = self.ops.hash_rows(self.desc, len(self.slots), batch)
-        req = torch.cat([rows, self.pad_rows])
+        req = self.ops.hash_rows(self.desc, len(self.slots), batch, tail=self.pad_rows)
         if self.dedup:
             counts, local, row_map = self.ops.route(req, self.nranks, self.table_rows)
         else:
@@ -429,8 +434,7 @@ class ShardedFusedEncoder(torch.nn.Module):
     def _route_hash(self, batch: SparseBatch, local_fast: bool, exchange: bool):
         """hash route: build (device counts) -> [counts all-to-all] -> ONE host read of send (+ receive) counts
         -> finish. local_fast: this rank's own rows stay out of the exchange (row_map bit 31)."""
-        rows = self.ops.hash_rows(self.desc, len(self.slots), batch)
-        req = torch.cat([rows, self.pad_rows])
+        req = self.ops.hash_rows(self.desc, len(self.slots), batch, tail=self.pad_rows)
         counts, state = self.ops.route_hash_build(req, self.nranks, self.rank if local_fast else -1, self.table_rows)
         counts = counts.to(torch.int64)
         P = counts.numel()
@@ -499,7 +503,7 @@ class ShardedFusedEncoder(torch.nn.Module):
             out = torch.empty((batch.batch, self.out_width), dtype=self.out_dtype, device=self.ops.device)
         flags = L.FLAG_MASK_PADDING if self.mask_padding else 0
         S, P = len(self.slots), self.nranks
-        rows = torch.cat([self.ops.hash_rows(self.desc, S, batch), self.pad_rows])
+        rows = self.ops.hash_rows(self.desc, S, batch, tail=self.pad_rows)
         ent, counts, seg_counts, seg_of = self.ops.pp_plan(self.desc, S, batch, rows, flags, P)
         both = torch.stack([counts, seg_counts], dim=1).to(torch.int64)           # [P, 2]: entries, segments
         recv = self.comm.exchange_counts(both.reshape(-1)).reshape(P, 2)

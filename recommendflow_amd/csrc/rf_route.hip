@@ -66,7 +66,8 @@ __global__ __launch_bounds__(256) void route_keys_kernel(const int64_t* __restri
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t g = rows[j];
         const bool ok = g >= 0 && g < table_rows;
-        keys[j] = ok ? (uint32_t)((g % P) * lp + g / P) : (uint32_t)((int64_t)P * lp);
+        const uint32_t g32 = (uint32_t)g, p32 = (uint32_t)P;  // valid rows < 2^32: 32-bit division
+        keys[j] = ok ? (g32 % p32) * (uint32_t)lp + g32 / p32 : (uint32_t)((int64_t)P * lp);
         idx[j] = (uint32_t)j;
     }
 }
@@ -89,10 +90,10 @@ __global__ __launch_bounds__(256) void route_emit_kernel(const uint32_t* __restr
         row_map[idx[i]] = uid;
         const bool head = i == 0 || k != keys[i - 1];
         if (!head) continue;
-        const int64_t owner = std::min<int64_t>((int64_t)(k / (uint64_t)lp), P - 1);  // sentinel -> last owner
+        const int64_t owner = std::min<int64_t>((int64_t)(k / (uint32_t)lp), P - 1);  // sentinel -> last owner
         const bool valid = (int64_t)k < (int64_t)P * lp;
-        local_out[uid] = valid ? (int64_t)(k % (uint64_t)lp) : (int64_t)-1;  // -1: gathered as NaN
-        const bool first = i == 0 || std::min<int64_t>((int64_t)(keys[i - 1] / (uint64_t)lp), P - 1) != owner;
+        local_out[uid] = valid ? (int64_t)(k % (uint32_t)lp) : (int64_t)-1;  // -1: gathered as NaN
+        const bool first = i == 0 || std::min<int64_t>((int64_t)(keys[i - 1] / (uint32_t)lp), P - 1) != owner;
         if (first) first_uid[owner] = uid;
     }
 }
@@ -121,17 +122,28 @@ int grid_of(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n +
 // into an open-addressing table of 32-bit keys (capacity a power of two >= 2 n); a request finds its key
 // with a plain load first and only an empty slot is claimed by atomicCAS, so a Zipf-hot row costs one
 // atomic in all. Rows this rank owns (rank >= 0) never enter the table: their row_map entry is
-// 0x80000000 | local (rf_pool_rows_fwd reads them from the local shard in place). The compacted distinct
-// keys are then sorted (radix, key bits only) so the send buffer is owner-major and, within an owner,
-// ascending by local row — the same order rf_route_rows produces.
+// 0x80000000 | local (rf_pool_rows_fwd reads them from the local shard in place). The distinct keys then
+// leave the table owner-major:
+//   P <= 64 (kOwnerMajorMaxP): rh_count (per-workgroup, per-owner live counts) -> rh_scan_owner (owner-major
+//     positions) -> rh_scatter_owner (each key straight to its position, the slot overwritten with it); finish
+//     is one launch (local ids + row map). Within an owner the rows come in table-slot order — the same set as
+//     rf_route_rows' ascending order; the exchange and the pooled output do not depend on the order within an
+//     owner (each distinct row is sent once and the row map follows it). At cfg4 P = 8 this form replaced
+//     compact + radix sort + emit (profiles/r04/route_p8_*).
+//   P > 64: rh_count -> rh_scan -> rh_scatter compact in slot order, then a radix sort (key bits only) makes the
+//     list owner-major and ascending within an owner, the order rf_route_rows produces.
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr int kChunkPerThread = 16;  // table slots per thread of the compaction (rh_count / rh_scatter)
+constexpr int kChunk = 256 * kChunkPerThread;
+constexpr int kOwnerMajorMaxP = 64;  // P <= this: owner-major scatter, no sort (rh_scan_owner / rh_scatter_owner)
 
 struct HashLayout {
     int64_t n, cap;
     int log_cap, end_bit;
     size_t sort_bytes;
-    size_t off_table, off_slot, off_kin, off_kout, off_vin, off_vout, off_cnt, off_tmp, total;
+    int64_t n_blk;
+    size_t off_table, off_slot, off_kin, off_kout, off_vin, off_vout, off_cnt, off_blk, off_blk_own, off_tmp, total;
 };
 
 HashLayout hash_layout(int64_t n, int32_t nranks, int64_t table_rows) {
@@ -153,6 +165,9 @@ HashLayout hash_layout(int64_t n, int32_t nranks, int64_t table_rows) {
     L.off_vin = o; o += v;
     L.off_vout = o; o += v;
     L.off_cnt = o; o += align256((size_t)(nranks + 2) * 4);  // counts[P] | n_uniq | reserved
+    L.n_blk = (L.cap + kChunk - 1) / kChunk;
+    L.off_blk = o; o += align256((size_t)L.n_blk * 4);
+    L.off_blk_own = o; o += nranks <= kOwnerMajorMaxP ? align256((size_t)L.n_blk * nranks * 4) : 0;
     L.off_tmp = o; o += align256(L.sort_bytes);
     L.total = o;
     return L;
@@ -162,6 +177,11 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t k, int log_cap) {
     return (uint32_t)(((uint64_t)(k * 0x9E3779B1u) * 0x85EBCA77ull) >> (32 - log_cap)) & ((1u << log_cap) - 1u);
 }
 
+// kIlp slots per thread per pass in rh_map, their loads issued together. (The same in rh_insert measured
+// slower, 144 -> 177 us at cfg4 P = 8: more requests in flight for a Zipf-hot key read its slot empty and
+// race on the CAS; its cost is the memory-side atomics, not load latency.)
+constexpr int kIlp = 4;
+
 __global__ __launch_bounds__(256) void rh_insert_kernel(const int64_t* __restrict__ rows, int64_t n, int P, int rank,
                                                         int64_t lp, int64_t table_rows, uint32_t* __restrict__ table,
                                                         int log_cap, uint32_t* __restrict__ slot,
@@ -170,13 +190,15 @@ __global__ __launch_bounds__(256) void rh_insert_kernel(const int64_t* __restric
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t g = rows[j];
         const bool ok = g >= 0 && g < table_rows;
-        const int owner = ok ? (int)(g % P) : P - 1;
+        const uint32_t g32 = (uint32_t)g, p32 = (uint32_t)P;  // valid rows < 2^32: 32-bit division
+        const uint32_t gl = g32 / p32;
+        const int owner = ok ? (int)(g32 - gl * p32) : P - 1;
         if (ok && owner == rank) {  // rank-local: read in place by the pooling, never routed
-            row_map[j] = (int32_t)(0x80000000u | (uint32_t)(g / P));
+            row_map[j] = (int32_t)(0x80000000u | gl);
             slot[j] = kEmpty;
             continue;
         }
-        const uint32_t key = ok ? (uint32_t)((int64_t)owner * lp + g / P) : (uint32_t)((int64_t)P * lp);
+        const uint32_t key = ok ? (uint32_t)owner * (uint32_t)lp + gl : (uint32_t)((int64_t)P * lp);
         uint32_t h = key_hash(key, log_cap);
         while (true) {
             uint32_t cur = table[h];
@@ -188,35 +210,297 @@ __global__ __launch_bounds__(256) void rh_insert_kernel(const int64_t* __restric
     }
 }
 
-// table slots in order -> (key, slot) pairs; per-owner counts and the distinct total by block-aggregated
-// atomics (the pairs' order is fixed by the sort that follows)
-__global__ __launch_bounds__(256) void rh_compact_kernel(const uint32_t* __restrict__ table, int64_t cap, int P,
-                                                         int64_t lp, uint32_t* __restrict__ kout,
-                                                         uint32_t* __restrict__ vout, int32_t* __restrict__ cnt) {
+// Compaction of the table's live slots into (key, slot) pairs, in slot order, in three launches with no
+// contended atomics: rh_count_kernel (each workgroup owns kChunk consecutive slots: its live count -> blk[b],
+// its per-owner counts -> blk_own[b][p] when P <= 64, else one atomic per (workgroup, owner)), rh_scan_kernel
+// (exclusive scan of blk -> workgroup bases, the distinct total, and the per-owner sums), rh_scatter_kernel
+// (the same slots again, each live one to base + its rank in slot order). The first form (one workgroup per
+// 256 slots, a global atomic per workgroup on the total and on every owner: 65,536 workgroups x 9 atomics on
+// 9 addresses for the cfg4 P = 8 table of 2^24 slots) measured 1.49 ms per call, serialised on those
+// addresses (profiles/r04/route_p8_*).
+__global__ __launch_bounds__(256) void rh_count_kernel(const uint32_t* __restrict__ table, int64_t cap, int P,
+                                                       int64_t lp, double inv_lp, int32_t* __restrict__ blk,
+                                                       int32_t* __restrict__ blk_own, int32_t* __restrict__ cnt) {
     extern __shared__ int32_t s_own[];
-    __shared__ int32_t s_base;
+    __shared__ int32_t s_wave[4];
     for (int p = threadIdx.x; p < P; p += 256) s_own[p] = 0;
-    if (threadIdx.x == 0) s_base = 0;
     __syncthreads();
-    const int64_t h = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t k = h < cap ? table[h] : kEmpty;
-    const bool live = k != kEmpty;
-    const uint64_t m = __ballot(live);
-    const int lane = threadIdx.x & 63;
-    int wbase = 0;
-    if (lane == 0 && m) wbase = atomicAdd(&s_base, __popcll(m));
-    wbase = __shfl(wbase, 0, 64);
-    if (live) atomicAdd(&s_own[min((int64_t)(k / (uint64_t)lp), (int64_t)P - 1)], 1);
+    const int64_t base = (int64_t)blockIdx.x * kChunk;
+    uint32_t k[kChunkPerThread];
+#pragma unroll
+    for (int i = 0; i < kChunkPerThread; ++i) {
+        const int64_t h = base + i * 256 + threadIdx.x;
+        k[i] = h < cap ? table[h] : kEmpty;
+    }
+    int live = 0;
+    const uint32_t lp32 = (uint32_t)lp;
+    auto owner_of = [&](uint32_t key) {  // key / lp without the 32-bit division sequence: a double product + fix-up
+        uint32_t o = (uint32_t)((double)key * inv_lp);
+        if ((uint64_t)o * lp32 > key) --o;
+        if ((uint64_t)(o + 1) * lp32 <= key) ++o;
+        return min((int)o, P - 1);
+    };
+    if (P <= 8) {  // per-thread counts packed 8 bits per owner (<= kChunkPerThread each), then a wave sum in 16-bit fields
+        uint64_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < kChunkPerThread; ++i) {
+            const bool ok = k[i] != kEmpty;
+            live += ok;
+            acc += ok ? 1ull << (8 * owner_of(k[i])) : 0ull;
+        }
+        uint64_t ev = acc & 0x00ff00ff00ff00ffull, od = (acc >> 8) & 0x00ff00ff00ff00ffull;
+        for (int off = 32; off; off >>= 1) {
+            ev += __shfl_xor(ev, off, 64);
+            od += __shfl_xor(od, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0)
+            for (int p = 0; p < P; ++p) {
+                const int c = (int)(((p & 1 ? od : ev) >> (16 * (p >> 1))) & 0xffff);
+                if (c) atomicAdd(&s_own[p], c);
+            }
+    } else if (P <= 64) {  // per-owner counts by ballot: lane p of each wave counts owner p, one LDS add per lane
+        const int lane = threadIdx.x & 63;
+        int mine = 0;
+#pragma unroll
+        for (int i = 0; i < kChunkPerThread; ++i) {
+            const bool ok = k[i] != kEmpty;
+            live += ok;
+            const int o = ok ? owner_of(k[i]) : -1;
+            for (int p = 0; p < P; ++p) {
+                const int c = __popcll(__ballot(o == p));
+                mine += lane == p ? c : 0;
+            }
+        }
+        if (lane < P && mine) atomicAdd(&s_own[lane], mine);
+    } else {
+        int run_owner = -1, run = 0;
+#pragma unroll
+        for (int i = 0; i < kChunkPerThread; ++i) {
+            if (k[i] == kEmpty) continue;
+            ++live;
+            const int o = owner_of(k[i]);
+            if (o != run_owner) {  // per-thread run-length of owners before touching LDS
+                if (run) atomicAdd(&s_own[run_owner], run);
+                run_owner = o;
+                run = 0;
+            }
+            ++run;
+        }
+        if (run) atomicAdd(&s_own[run_owner], run);
+    }
+    for (int off = 32; off; off >>= 1) live += __shfl_xor(live, off, 64);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = live;
     __syncthreads();
-    __shared__ int32_t s_gbase;
-    if (threadIdx.x == 0) s_gbase = s_base ? atomicAdd(cnt + P, s_base) : 0;
-    for (int p = threadIdx.x; p < P; p += 256)
-        if (s_own[p]) atomicAdd(cnt + p, s_own[p]);
+    if (threadIdx.x == 0) blk[blockIdx.x] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    if (P <= kOwnerMajorMaxP) {  // summed by rh_scan_(owner_)kernel: a global atomic per (workgroup, owner) serialises on P addresses
+        for (int p = threadIdx.x; p < P; p += 256) blk_own[(int64_t)blockIdx.x * P + p] = s_own[p];
+    } else {
+        for (int p = threadIdx.x; p < P; p += 256)
+            if (s_own[p]) atomicAdd(cnt + p, s_own[p]);
+    }
+}
+
+// one workgroup: blk[0..nb) -> exclusive bases in place, cnt[P] = total; P <= 64: cnt[p] = sum_b blk_own[b][p]
+__global__ __launch_bounds__(1024) void rh_scan_kernel(int32_t* __restrict__ blk, const int32_t* __restrict__ blk_own,
+                                                       int nb, int P, int32_t* __restrict__ cnt) {
+    __shared__ int32_t s_part[16];
+    __shared__ int32_t s_carry;
+    __shared__ int32_t s_own[1024];
+    if (P <= 64) {  // 1024 / P readers per owner, fixed order: deterministic
+        const int per = 1024 / P, p = threadIdx.x % P, r = threadIdx.x / P;
+        int32_t acc = 0;
+        if (r < per)
+            for (int b = r; b < nb; b += per) acc += blk_own[(int64_t)b * P + p];
+        s_own[threadIdx.x] = r < per ? acc : 0;
+        __syncthreads();
+        if (threadIdx.x < P) {
+            int32_t t = 0;
+            for (int q = 0; q < per; ++q) t += s_own[q * P + threadIdx.x];
+            cnt[threadIdx.x] = t;
+        }
+    }
+    if (threadIdx.x == 0) s_carry = 0;
     __syncthreads();
-    if (live) {
-        const int pos = s_gbase + wbase + __popcll(m & ((1ull << lane) - 1ull));
-        kout[pos] = k;
-        vout[pos] = (uint32_t)h;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int b0 = 0; b0 < nb; b0 += 1024) {
+        const int b = b0 + threadIdx.x;
+        const int32_t v = b < nb ? blk[b] : 0;
+        int32_t x = v;  // inclusive wave scan
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) s_part[wave] = x;
+        __syncthreads();
+        int32_t before = s_carry;
+        for (int w = 0; w < wave; ++w) before += s_part[w];
+        if (b < nb) blk[b] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = before + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cnt[P] = s_carry;
+}
+
+__global__ __launch_bounds__(256) void rh_scatter_kernel(const uint32_t* __restrict__ table, int64_t cap,
+                                                         const int32_t* __restrict__ blk, uint32_t* __restrict__ kout,
+                                                         uint32_t* __restrict__ vout) {
+    __shared__ int32_t s_cnt[kChunkPerThread * 4];
+    const int64_t base = (int64_t)blockIdx.x * kChunk;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t k[kChunkPerThread];
+    uint64_t m[kChunkPerThread];
+#pragma unroll
+    for (int i = 0; i < kChunkPerThread; ++i) {
+        const int64_t h = base + i * 256 + threadIdx.x;
+        k[i] = h < cap ? table[h] : kEmpty;
+        m[i] = __ballot(k[i] != kEmpty);
+        if (lane == 0) s_cnt[i * 4 + wave] = __popcll(m[i]);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the 64 (row i, wave) counts in slot order
+        const int32_t v = s_cnt[threadIdx.x];
+        int32_t x = v;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        s_cnt[threadIdx.x] = x - v;
+    }
+    __syncthreads();
+    const int32_t b0 = blk[blockIdx.x];
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int i = 0; i < kChunkPerThread; ++i) {
+        if (k[i] == kEmpty) continue;
+        const int pos = b0 + s_cnt[i * 4 + wave] + __popcll(m[i] & below);
+        kout[pos] = k[i];
+        vout[pos] = (uint32_t)(base + i * 256 + threadIdx.x);
+    }
+}
+
+// ---- owner-major compaction without the sort (P <= 64, the sharded encoder's case) ----
+// rh_scan_owner_kernel: blk_own[b][p] (live slots of owner p in workgroup b's chunk) -> in place, the position of
+// that workgroup's first owner-p key in the owner-major key list; cnt[p] = owner totals, cnt[P] = distinct total.
+// One workgroup of 1024: thread t = (r, p), p = t % P, owns blocks [r * per_r, (r + 1) * per_r) of owner p.
+__global__ __launch_bounds__(1024) void rh_scan_owner_kernel(int32_t* __restrict__ blk_own, int nb, int P,
+                                                             int32_t* __restrict__ cnt) {
+    __shared__ int32_t s_acc[1024];
+    __shared__ int32_t s_base[64];
+    const int t = threadIdx.x, p = t % P, r = t / P, R = 1024 / P;
+    const int per_r = (nb + R - 1) / R;
+    const int b0 = r < R ? r * per_r : nb, b1 = min(nb, b0 + per_r);
+    int32_t acc = 0;
+    for (int b = b0; b < b1; ++b) acc += blk_own[(int64_t)b * P + p];
+    s_acc[t] = acc;
+    __syncthreads();
+    for (int d = 1; d < R; d <<= 1) {  // inclusive scan over r for each owner (stride P in s_acc)
+        const int32_t v = (r < R && r >= d) ? s_acc[t - d * P] : 0;
+        __syncthreads();
+        if (r < R) s_acc[t] += v;
+        __syncthreads();
+    }
+    if (t == 0) {
+        int32_t run = 0;
+        for (int q = 0; q < P; ++q) {
+            const int32_t tot = s_acc[(R - 1) * P + q];
+            s_base[q] = run;
+            cnt[q] = tot;
+            run += tot;
+        }
+        cnt[P] = run;
+    }
+    __syncthreads();
+    if (r < R) {
+        int32_t run = s_base[p] + s_acc[t] - acc;
+        for (int b = b0; b < b1; ++b) {
+            const int32_t v = blk_own[(int64_t)b * P + p];
+            blk_own[(int64_t)b * P + p] = run;
+            run += v;
+        }
+    }
+}
+
+// the chunk's live keys to their owner-major positions (slot order within an owner and workgroup): keys[pos] =
+// key, and the table slot is overwritten with pos (slot -> distinct id, read by rh_finish_kernel's row map)
+__global__ __launch_bounds__(256) void rh_scatter_owner_kernel(uint32_t* table, int64_t cap, int P, int64_t lp,
+                                                               double inv_lp, const int32_t* __restrict__ off,
+                                                               uint32_t* __restrict__ keys) {
+    extern __shared__ int32_t s_c[];  // [kChunkPerThread * 4 entries (i, wave)][P] counts -> exclusive offsets
+    __shared__ int32_t s_off[64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t base = (int64_t)blockIdx.x * kChunk;
+    const uint32_t lp32 = (uint32_t)lp;
+    if (threadIdx.x < P) s_off[threadIdx.x] = off[(int64_t)blockIdx.x * P + threadIdx.x];
+    uint32_t k[kChunkPerThread];
+    int o[kChunkPerThread];
+#pragma unroll
+    for (int i = 0; i < kChunkPerThread; ++i) {
+        const int64_t h = base + i * 256 + threadIdx.x;
+        k[i] = h < cap ? table[h] : kEmpty;
+    }
+#pragma unroll
+    for (int i = 0; i < kChunkPerThread; ++i) {
+        if (k[i] == kEmpty) {
+            o[i] = -1;
+        } else {
+            uint32_t q = (uint32_t)((double)k[i] * inv_lp);
+            if ((uint64_t)q * lp32 > k[i]) --q;
+            if ((uint64_t)(q + 1) * lp32 <= k[i]) ++q;
+            o[i] = min((int)q, P - 1);
+        }
+        int mine = 0;
+        for (int p = 0; p < P; ++p) {
+            const int c = __popcll(__ballot(o[i] == p));
+            mine = lane == p ? c : mine;
+        }
+        if (lane < P) s_c[(i * 4 + wave) * P + lane] = mine;
+    }
+    __syncthreads();
+    for (int p = wave; p < P; p += 4) {  // exclusive scan over the 64 (i, wave) entries, slot order, per owner
+        const int32_t v = s_c[lane * P + p];
+        int32_t x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        s_c[lane * P + p] = x - v;
+    }
+    __syncthreads();
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int i = 0; i < kChunkPerThread; ++i) {
+        int pos = 0;
+        for (int p = 0; p < P; ++p) {
+            const uint64_t m = __ballot(o[i] == p);
+            if (o[i] == p) pos = s_off[p] + s_c[(i * 4 + wave) * P + p] + __popcll(m & below);
+        }
+        if (o[i] >= 0) {
+            keys[pos] = k[i];
+            table[base + i * 256 + threadIdx.x] = (uint32_t)pos;
+        }
+    }
+}
+
+// local_out[i] from the owner-major keys (i < u) and row_map[j] = uid of request j's slot (j < n), one launch
+__global__ __launch_bounds__(256) void rh_finish_kernel(const uint32_t* __restrict__ keys, int64_t u, int P, int64_t lp,
+                                                        int64_t* __restrict__ local_out, const uint32_t* __restrict__ slot,
+                                                        int64_t n, const uint32_t* __restrict__ uid_of_slot,
+                                                        int32_t* __restrict__ row_map) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < u; i += stride) {
+        const uint32_t k = keys[i];
+        local_out[i] = (int64_t)k < (int64_t)P * lp ? (int64_t)(k % (uint32_t)lp) : (int64_t)-1;  // -1: gathered as NaN
+    }
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n; j0 += stride * kIlp) {
+        uint32_t sl[kIlp], uid[kIlp];
+#pragma unroll
+        for (int v = 0; v < kIlp; ++v) sl[v] = j0 + v * stride < n ? slot[j0 + v * stride] : kEmpty;
+#pragma unroll
+        for (int v = 0; v < kIlp; ++v) uid[v] = sl[v] != kEmpty ? uid_of_slot[sl[v]] : 0u;
+#pragma unroll
+        for (int v = 0; v < kIlp; ++v)
+            if (sl[v] != kEmpty) row_map[j0 + v * stride] = (int32_t)uid[v];
     }
 }
 
@@ -226,16 +510,23 @@ __global__ __launch_bounds__(256) void rh_emit_kernel(const uint32_t* __restrict
                                                       uint32_t* __restrict__ uid_of_slot) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < u; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t k = keys[i];
-        local_out[i] = (int64_t)k < (int64_t)P * lp ? (int64_t)(k % (uint64_t)lp) : (int64_t)-1;  // -1: gathered as NaN
+        local_out[i] = (int64_t)k < (int64_t)P * lp ? (int64_t)(k % (uint32_t)lp) : (int64_t)-1;  // -1: gathered as NaN
         uid_of_slot[slots[i]] = (uint32_t)i;
     }
 }
 
 __global__ __launch_bounds__(256) void rh_map_kernel(const uint32_t* __restrict__ slot, int64_t n,
                                                      const uint32_t* __restrict__ uid_of_slot, int32_t* __restrict__ row_map) {
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t sl = slot[j];
-        if (sl != kEmpty) row_map[j] = (int32_t)uid_of_slot[sl];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n; j0 += stride * kIlp) {
+        uint32_t sl[kIlp], uid[kIlp];
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) sl[u] = j0 + u * stride < n ? slot[j0 + u * stride] : kEmpty;
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) uid[u] = sl[u] != kEmpty ? uid_of_slot[sl[u]] : 0u;
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u)
+            if (sl[u] != kEmpty) row_map[j0 + u * stride] = (int32_t)uid[u];
     }
 }
 
@@ -319,9 +610,21 @@ extern "C" int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nrank
         const int64_t lp = (table_rows + nranks - 1) / nranks;
         hipLaunchKernelGGL(rh_insert_kernel, dim3(grid_of(n)), dim3(256), 0, st, rows, n, nranks, rank, lp, table_rows,
                            table, lay.log_cap, reinterpret_cast<uint32_t*>(w + lay.off_slot), row_map);
-        hipLaunchKernelGGL(rh_compact_kernel, dim3((unsigned)((lay.cap + 255) / 256)), dim3(256),
-                           (size_t)nranks * sizeof(int32_t), st, table, lay.cap, nranks, lp,
-                           reinterpret_cast<uint32_t*>(w + lay.off_kin), reinterpret_cast<uint32_t*>(w + lay.off_vin), cnt);
+        auto* blk = reinterpret_cast<int32_t*>(w + lay.off_blk);
+        const dim3 gb((unsigned)lay.n_blk);
+        auto* blk_own = reinterpret_cast<int32_t*>(w + lay.off_blk_own);
+        hipLaunchKernelGGL(rh_count_kernel, gb, dim3(256), (size_t)nranks * sizeof(int32_t), st, table, lay.cap, nranks,
+                           lp, 1.0 / (double)lp, blk, blk_own, cnt);
+        if (nranks <= kOwnerMajorMaxP) {
+            hipLaunchKernelGGL(rh_scan_owner_kernel, dim3(1), dim3(1024), 0, st, blk_own, (int)lay.n_blk, nranks, cnt);
+            hipLaunchKernelGGL(rh_scatter_owner_kernel, gb, dim3(256), (size_t)kChunkPerThread * 4 * nranks * sizeof(int32_t),
+                               st, table, lay.cap, nranks, lp, 1.0 / (double)lp, blk_own,
+                               reinterpret_cast<uint32_t*>(w + lay.off_kin));
+        } else {
+            hipLaunchKernelGGL(rh_scan_kernel, dim3(1), dim3(1024), 0, st, blk, blk_own, (int)lay.n_blk, nranks, cnt);
+            hipLaunchKernelGGL(rh_scatter_kernel, gb, dim3(256), 0, st, table, lay.cap, blk,
+                               reinterpret_cast<uint32_t*>(w + lay.off_kin), reinterpret_cast<uint32_t*>(w + lay.off_vin));
+        }
     }
     if (hipMemcpyAsync(counts, cnt, sizeof(int32_t) * nranks, hipMemcpyDeviceToDevice, st) != hipSuccess)
         return rf_set_error(RF_EHIP, "rf_route_hash_build: copy failed");
@@ -343,14 +646,19 @@ extern "C" int rf_route_hash_finish(int64_t n, int32_t nranks, int64_t table_row
     auto* vin = reinterpret_cast<uint32_t*>(w + lay.off_vin);
     auto* vout = reinterpret_cast<uint32_t*>(w + lay.off_vout);
     auto* table = reinterpret_cast<uint32_t*>(w + lay.off_table);
+    const int64_t lp = (table_rows + nranks - 1) / nranks;
+    if (nranks <= kOwnerMajorMaxP) {  // keys already owner-major (rh_scatter_owner_kernel), table = slot -> uid
+        hipLaunchKernelGGL(rh_finish_kernel, dim3(grid_of((n + kIlp - 1) / kIlp)), dim3(256), 0, st, kin, n_uniq, nranks,
+                           lp, local_out, reinterpret_cast<const uint32_t*>(w + lay.off_slot), n, table, row_map);
+        return rf_check_launch("rf_route_hash_finish");
+    }
     size_t sb = lay.sort_bytes;
     if (hipcub::DeviceRadixSort::SortPairs(w + lay.off_tmp, sb, kin, kout, vin, vout, (int)n_uniq, 0, lay.end_bit, st) !=
         hipSuccess)
         return rf_set_error(RF_EHIP, "rf_route_hash_finish: radix sort failed");
-    const int64_t lp = (table_rows + nranks - 1) / nranks;
     hipLaunchKernelGGL(rh_emit_kernel, dim3(grid_of(n_uniq)), dim3(256), 0, st, kout, vout, n_uniq, nranks, lp, local_out,
                        table);
-    hipLaunchKernelGGL(rh_map_kernel, dim3(grid_of(n)), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(w + lay.off_slot),
+    hipLaunchKernelGGL(rh_map_kernel, dim3(grid_of((n + kIlp - 1) / kIlp)), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(w + lay.off_slot),
                        n, table, row_map);
     return rf_check_launch("rf_route_hash_finish");
 }

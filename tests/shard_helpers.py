@@ -27,8 +27,9 @@ class OracleShardOps:
         assert dtype == torch.float32
         return torch.from_numpy(O.table_init_uniform(rows, dim, seed=seed, row0=rank, row_stride=nranks, lo=lo, hi=hi))
 
-    def hash_rows(self, desc, n_slots, batch):
-        return torch.from_numpy(O.hash_rows(desc, batch.tok_bytes, batch.tok_off, batch.bag_off, batch.batch))
+    def hash_rows(self, desc, n_slots, batch, tail=None):
+        r = torch.from_numpy(O.hash_rows(desc, batch.tok_bytes, batch.tok_off, batch.bag_off, batch.batch))
+        return r if tail is None else torch.cat([r, tail])
 
     def bucketize(self, rows, nranks):
         c, p, l, inv = O.bucketize_owner(rows.numpy(), nranks)
