@@ -574,6 +574,7 @@ def bench_sharded(args, specs, multi, rank, world):
         enc.combine(b, r, back, out, local_fast=enc.local_fast)
         if ev: ev[5].record()
         st["req"], st["served"], st["logical"] = r.n_requests, int(wanted.shape[0]), r.n_logical
+        st["row_map"] = r.row_map
 
     steps = max(5, args.steps // 5)
     for i in range(3):
@@ -683,6 +684,7 @@ def bench_sharded_sim(args, specs, multi, P):
         enc.combine(b, r, back, out, local_fast=enc.local_fast)
         if ev: ev[5].record()
         st["req"], st["served"], st["logical"] = r.n_requests, int(wanted.shape[0]), r.n_logical
+        st["row_map"] = r.row_map
 
     steps = max(5, args.steps // 5)
     for i in range(3):
@@ -699,7 +701,8 @@ def bench_sharded_sim(args, specs, multi, P):
     row_b = D * 4
     res = {"ms_per_step": round(el / steps * 1e3, 4), "examples_per_s_this_rank": round(B * steps / el, 1),
            "stage_ms": stage, "rows_read_by_pool": st["logical"], "rows_requested_after_dedup": st["req"],
-           "rows_local_in_place": st["logical"] - st["req"],
+           "requests_local_in_place": int((st["row_map"] < 0).sum()),  # row_map bit 31: read from the own shard
+           "requests_remote": int((st["row_map"] >= 0).sum()),
            "dedup_ratio": round(st["req"] / max(1, st["logical"]), 4),
            "gather_GBs": round(st["served"] * (2 * row_b + 8) / max(stage["gather"], 1e-6) / 1e6, 1),
            "xgmi_bytes_each_way_not_timed": int(st["req"] * (8 + row_b)),

@@ -421,8 +421,8 @@ __global__ __launch_bounds__(1024) void rh_scan_owner_kernel(int32_t* __restrict
     }
 }
 
-// the chunk's live keys to their owner-major positions (slot order within an owner and workgroup): keys[pos] =
-// key, and the table slot is overwritten with pos (slot -> distinct id, read by rh_finish_kernel's row map)
+// the chunk's live keys to their owner-major positions (within an owner and workgroup: thread-major order for
+// P <= 8, slot order above): keys[pos] = key, and the table slot is overwritten with pos (slot -> distinct id, read by rh_finish_kernel's row map)
 __global__ __launch_bounds__(256) void rh_scatter_owner_kernel(uint32_t* table, int64_t cap, int P, int64_t lp,
                                                                double inv_lp, const int32_t* __restrict__ off,
                                                                uint32_t* __restrict__ keys) {
@@ -449,6 +449,39 @@ __global__ __launch_bounds__(256) void rh_scatter_owner_kernel(uint32_t* table, 
             if ((uint64_t)(q + 1) * lp32 <= k[i]) ++q;
             o[i] = min((int)q, P - 1);
         }
+    }
+    if (P <= 8) {  // thread-major order within (workgroup, owner): packed per-thread counts, one block scan
+        __shared__ uint64_t s_w[4][2];
+        uint64_t ev = 0, od = 0;  // owner p's count in the 16-bit field p >> 1 of (p & 1 ? od : ev)
+#pragma unroll
+        for (int i = 0; i < kChunkPerThread; ++i)
+            if (o[i] >= 0) {
+                const uint64_t one = 1ull << (16 * (o[i] >> 1));
+                if (o[i] & 1) od += one; else ev += one;
+            }
+        uint64_t xe = ev, xo = od;  // inclusive wave scan
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t ye = __shfl_up(xe, d, 64), yo = __shfl_up(xo, d, 64);
+            if (lane >= d) { xe += ye; xo += yo; }
+        }
+        if (lane == 63) { s_w[wave][0] = xe; s_w[wave][1] = xo; }
+        __syncthreads();
+        uint64_t re = xe - ev, ro = xo - od;  // exclusive, then plus the earlier waves
+        for (int w = 0; w < wave; ++w) { re += s_w[w][0]; ro += s_w[w][1]; }
+#pragma unroll
+        for (int i = 0; i < kChunkPerThread; ++i) {
+            if (o[i] < 0) continue;
+            const int sh = 16 * (o[i] >> 1);
+            uint64_t& r = (o[i] & 1) ? ro : re;
+            const int pos = s_off[o[i]] + (int)((r >> sh) & 0xffff);
+            r += 1ull << sh;
+            keys[pos] = k[i];
+            table[base + i * 256 + threadIdx.x] = (uint32_t)pos;
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < kChunkPerThread; ++i) {
         int mine = 0;
         for (int p = 0; p < P; ++p) {
             const int c = __popcll(__ballot(o[i] == p));
