@@ -316,52 +316,72 @@ __global__ __launch_bounds__(64) void single_token_ids_kernel(const rf_slot_desc
 
 // The same ids, example-major (round 3): thread per unit u = b * n_slots + s, so the bag_off / tok_off reads and
 // the ids stores of a wave are consecutive (the slot-major kernel touches 64 units n_slots apart per load and
-// store); each workgroup first prepares every slot's bucket modulus into LDS (one 64-bit division per slot).
+// store). Each workgroup first stages every slot's constants in LDS (salts, row bases, the bucket modulus: one
+// 64-bit division per slot), so a unit's only global reads are its CSR offsets and token bytes; u < 2^31, 32-bit
+// index arithmetic (round 4: the per-lane descriptor gathers and the 64-bit u % n_slots were a third of the
+// cfg3 id pass, profiles/r04/cfg3_*).
 constexpr int kIdsMaxSlots = 512;
+struct IdsSlot {
+    uint64_t salt0, salt1;
+    BucketMod bm;
+    int64_t rb0, rb1, nbins;
+    int32_t live;  // the slot fits the table and its batch Lmax is 1
+    int32_t mask_empty;
+};
+
 __device__ __forceinline__ void single_token_ids_em_body(const rf_slot_desc* __restrict__ slots, int n_slots,
                                                         const uint8_t* __restrict__ tok_bytes,
                                                         const int32_t* __restrict__ tok_off,
                                                         const int32_t* __restrict__ bag_off,
                                                         const int32_t* __restrict__ lmax, int64_t n_units,
                                                         int64_t table_rows, uint32_t* __restrict__ ids, int flags,
-                                                        int64_t block, int64_t n_blocks, BucketMod* sbm) {
-    for (int s = threadIdx.x; s < n_slots; s += blockDim.x) sbm[s] = bucket_mod_init(slots[s].num_bins, slots[s].mask_empty);
+                                                        int64_t block, int64_t n_blocks, IdsSlot* ssl) {
+    for (int s = threadIdx.x; s < n_slots; s += blockDim.x) {
+        const rf_slot_desc& sd = slots[s];
+        IdsSlot v;
+        v.salt0 = sd.salt[0];
+        v.salt1 = sd.salt[1];
+        v.bm = bucket_mod_init(sd.num_bins, sd.mask_empty);
+        v.rb0 = sd.row_base[0];
+        v.rb1 = sd.row_base[1];
+        v.nbins = sd.num_bins;
+        v.live = v.rb0 >= 0 && v.rb1 >= 0 && v.rb0 + v.nbins <= table_rows && v.rb1 + v.nbins <= table_rows && lmax[s] == 1;
+        v.mask_empty = sd.mask_empty;
+        ssl[s] = v;
+    }
     __syncthreads();
     const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
-    for (int64_t u = block * blockDim.x + threadIdx.x; u < n_units; u += n_blocks * blockDim.x) {
-        const int s = (int)(u % n_slots);
-        const rf_slot_desc* sd = slots + s;
-        const int64_t rb0 = sd->row_base[0], rb1 = sd->row_base[1], nbins = sd->num_bins;
-        const uint64_t salt0 = sd->salt[0], salt1 = sd->salt[1];
-        const int mask_empty = sd->mask_empty;
-        const bool ok = rb0 >= 0 && rb1 >= 0 && rb0 + nbins <= table_rows && rb1 + nbins <= table_rows;
+    const uint32_t ns = (uint32_t)n_slots, nu = (uint32_t)n_units;
+    const uint32_t stride = (uint32_t)(n_blocks * blockDim.x);
+    for (uint32_t u = (uint32_t)(block * blockDim.x) + threadIdx.x; u < nu; u += stride) {
+        const uint32_t s = u % ns;
+        const IdsSlot& sl = ssl[s];
         uint32_t r0 = kRowNaN, r1 = kRowNaN;
-        if (ok && lmax[s] == 1) {
+        if (sl.live) {
             const int t = bag_off[u];
             if (bag_off[u + 1] > t) {
                 const int tb = tok_off[t], n = tok_off[t + 1] - tb;
                 uint64_t h0, h1;
-                siphash24x2_dev(salt0, salt1, tok_bytes + tb, n, h0, h1);
-                const BucketMod bmod = sbm[s];
-                r0 = (uint32_t)(rb0 + bucket_from_hash(h0, n, bmod));
-                r1 = (uint32_t)(rb1 + bucket_from_hash(h1, n, bmod));
+                siphash24x2_dev(sl.salt0, sl.salt1, tok_bytes + tb, n, h0, h1);
+                r0 = (uint32_t)(sl.rb0 + bucket_from_hash(h0, n, sl.bm));
+                r1 = (uint32_t)(sl.rb1 + bucket_from_hash(h1, n, sl.bm));
             } else if (mask_pad) {
                 r0 = r1 = kRowZero;
             } else {
                 int64_t pb0 = 0, pb1 = 0;
-                if (!mask_empty) {
-                    pb0 = (int64_t)(siphash24_dev(salt0, salt0, tok_bytes, 0) % (uint64_t)nbins);
-                    pb1 = (int64_t)(siphash24_dev(salt1, salt1, tok_bytes, 0) % (uint64_t)nbins);
+                if (!sl.mask_empty) {
+                    pb0 = (int64_t)(siphash24_dev(sl.salt0, sl.salt0, tok_bytes, 0) % (uint64_t)sl.nbins);
+                    pb1 = (int64_t)(siphash24_dev(sl.salt1, sl.salt1, tok_bytes, 0) % (uint64_t)sl.nbins);
                 }
-                r0 = (uint32_t)(rb0 + pb0);
-                r1 = (uint32_t)(rb1 + pb1);
+                r0 = (uint32_t)(sl.rb0 + pb0);
+                r1 = (uint32_t)(sl.rb1 + pb1);
             }
         }
         if (flags & RF_FLAG_SPEC_ROWS) {  // the NaN / zero rows at table_rows / table_rows + 1
             r0 = r0 == kRowNaN ? (uint32_t)table_rows : r0 == kRowZero ? (uint32_t)table_rows + 1u : r0;
             r1 = r1 == kRowNaN ? (uint32_t)table_rows : r1 == kRowZero ? (uint32_t)table_rows + 1u : r1;
         }
-        *reinterpret_cast<uint2*>(ids + 2 * u) = make_uint2(r0, r1);
+        *reinterpret_cast<uint2*>(ids + 2 * (size_t)u) = make_uint2(r0, r1);
     }
 }
 
@@ -371,9 +391,9 @@ __global__ __launch_bounds__(256) void single_token_ids_em_kernel(const rf_slot_
                                                                  const int32_t* __restrict__ bag_off,
                                                                  const int32_t* __restrict__ lmax, int64_t n_units,
                                                                  int64_t table_rows, uint32_t* __restrict__ ids, int flags) {
-    __shared__ BucketMod sbm[kIdsMaxSlots];
+    extern __shared__ IdsSlot ssl[];
     single_token_ids_em_body(slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table_rows, ids, flags,
-                             blockIdx.x, gridDim.x, sbm);
+                             blockIdx.x, gridDim.x, ssl);
 }
 
 // several towers in one launch (rf_single_token_ids_multi_fwd): workgroups [first[k], first[k + 1]) run task k
@@ -383,13 +403,13 @@ struct IdsTasks {
     int n;
 };
 __global__ __launch_bounds__(256) void single_token_ids_multi_kernel(const IdsTasks tasks) {
-    __shared__ BucketMod sbm[kIdsMaxSlots];
+    extern __shared__ IdsSlot ssl[];
     int k = 0;
     while (k + 1 < tasks.n && (int64_t)blockIdx.x >= tasks.first[k + 1]) ++k;
     const rf_ids_task& t = tasks.t[k];
     single_token_ids_em_body(t.slots, t.n_slots, t.tok_bytes, t.tok_off, t.bag_off, t.lmax, (int64_t)t.batch * t.n_slots,
                              t.table_rows, t.ids, t.flags, (int64_t)blockIdx.x - tasks.first[k],
-                             tasks.first[k + 1] - tasks.first[k], sbm);
+                             tasks.first[k + 1] - tasks.first[k], ssl);
 }
 
 }  // namespace
@@ -408,6 +428,7 @@ extern "C" int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n
         RF_REQUIRE(t.table_rows >= 1 && t.table_rows < (int64_t)kRowNaN,
                    "rf_single_token_ids_multi_fwd: task %d: table_rows must be in [1, 2^32 - 2)", k);
         const int64_t n_units = (int64_t)t.batch * t.n_slots;
+        RF_REQUIRE(n_units < ((int64_t)1 << 31), "rf_single_token_ids_multi_fwd: task %d: batch * n_slots must be < 2^31", k);
         if (n_units)
             RF_REQUIRE(t.slots && t.tok_bytes && t.tok_off && t.bag_off && t.lmax && t.ids && ((uintptr_t)t.ids & 7) == 0,
                        "rf_single_token_ids_multi_fwd: task %d: null pointer or ids not 8-byte aligned", k);
@@ -417,7 +438,10 @@ extern "C" int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n
     }
     a.first[n_tasks] = blocks;
     if (blocks == 0) return RF_OK;
-    hipLaunchKernelGGL(single_token_ids_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, rf_stream(stream), a);
+    int max_slots = 1;
+    for (int k = 0; k < n_tasks; ++k) max_slots = std::max(max_slots, tasks[k].n_slots);
+    hipLaunchKernelGGL(single_token_ids_multi_kernel, dim3((unsigned)blocks), dim3(256), sizeof(IdsSlot) * max_slots,
+                       rf_stream(stream), a);
     return rf_check_launch("single_token_ids_multi_kernel");
 }
 
@@ -436,9 +460,10 @@ extern "C" int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_sl
         const char* e = getenv("RF_IDS_SLOT_MAJOR");
         return e && e[0] == '1';
     }();
-    if (n_slots <= kIdsMaxSlots && !slot_major) {
+    if (n_slots <= kIdsMaxSlots && !slot_major && n_units < ((int64_t)1 << 31)) {
         const int64_t blocks = std::min<int64_t>((n_units + 255) / 256, 256 * 32);
-        hipLaunchKernelGGL(single_token_ids_em_kernel, dim3((unsigned)blocks), dim3(256), 0, rf_stream(stream), d_slots,
+        hipLaunchKernelGGL(single_token_ids_em_kernel, dim3((unsigned)blocks), dim3(256), sizeof(IdsSlot) * n_slots,
+                           rf_stream(stream), d_slots,
                            n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table_rows, ids, flags);
         return rf_check_launch("single_token_ids_em_kernel");
     }
