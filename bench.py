@@ -407,6 +407,32 @@ def bench_esim(args):
         model.enc_q(hu[p], out=q)
         model.enc_a(ha[p], out=a)
 
+    # the fused scorer (Esim.fused_scorer, gather path): the input MLP and the attention write the pooled row as bf16
+    # + slice partials, the output MLP folds both LayerNorms and carries the head (no LayerNorm pass, no fp32 pooled)
+    fused = model._gather_ok(hu[0], ha[0]) and model._fused_scorer_ok(dense)
+    if fused:
+        import recommendflow_amd.runtime.lib as RL
+
+        W = model.pooled_width
+        pb = torch.empty((B, W), dtype=torch.bfloat16, device="cuda")
+        pst = torch.empty((B, W // 32, 2), device="cuda")
+
+        def in_mlp():  # noqa: F811 — the fused forward's first launch
+            model.input_mlp.forward_stats(dense, pb[:, : model.d_emb], pst, 0)
+
+        def mlp():  # noqa: F811
+            model.output_mlp.forward_prenormed_head(pb, pst, model.dense_output)
+
+        def gat(qi, ai):
+            eq, ea = model.enc_q, model.enc_a
+            RL.call("rf_esim_gather_stats_fwd", RL.ptr(qi), RL.ptr(ai), RL.ptr(eq.table), eq.table.shape[0],
+                    RL.ptr(ea.table), ea.table.shape[0], RL.DT_BF16, B, Ls, model.d, RL.ptr(pb), pb.stride(0),
+                    model.d_emb, RL.ptr(pst), W // 32, model.d_emb // 32, RL.stream_ptr(None))
+    else:
+        def gat(qi, ai):
+            model.attention_gather(qi, ai, pooled)
+    in_mlp()
+    mlp()
     g_enc = [CapturedGraph(lambda p=p: enc_p(p)) for p in (0, 1)]
     g_att, g_in, g_mlp = CapturedGraph(att), CapturedGraph(in_mlp), CapturedGraph(mlp)
     g_full = [CapturedGraph(lambda p=p: fwd(p)) for p in (0, 1)]
@@ -419,7 +445,7 @@ def bench_esim(args):
     if gather:
         ids_p = [model.token_ids(hu[p], ha[p]) for p in (0, 1)]
         g_ids = [CapturedGraph(lambda p=p: model.token_ids(hu[p], ha[p])) for p in (0, 1)]
-        g_gat = CapturedGraph(lambda: model.attention_gather(ids_p[0][0], ids_p[0][1], pooled))
+        g_gat = CapturedGraph(lambda: gat(ids_p[0][0], ids_p[0][1]))
         stages += [("token_ids", lambda: g_ids[nxt("i")].replay()), ("esim_gather_attention", g_gat.replay)]
     else:
         stages += [("sparse_encoders", lambda: g_enc[nxt("s")].replay()), ("esim_attention", g_att.replay)]
@@ -439,6 +465,7 @@ def bench_esim(args):
             "eager_ms_per_step": round(eager_wall, 4), "cpu_baseline": cpu,
             "stage_ms": {k: round(v, 4) for k, v in per.items()},
             "gather_path": gather,
+            "fused_scorer": fused,
             "unfused_stage_ms": {k: round(v, 4) for k, v in per_u.items()},
             "encoder_GBs": round(enc_bytes / per_u["sparse_encoders"] / 1e6, 1),
             "encoder_frac_of_measured_gather_ceiling": (
@@ -452,7 +479,9 @@ def bench_esim(args):
                            "input_mlp -> token_ids -> esim_gather_attention (rows gathered by id inside the "
                            "attention kernel) -> mlp_scorer on one stream; unfused_stage_ms = the encoders writing "
                            "q / a and the attention reading them (encoder_GBs, esim_TFLOPs); mlp_scorer = output MLP "
-                           "+ Dense(2, softmax); mlp_TFLOPs over those GEMMs",
+                           "+ Dense(2, softmax); mlp_TFLOPs over those GEMMs; fused_scorer: the pooled row leaves the "
+                           "input MLP and the attention as bf16 + 32-column slice partials and both output-MLP "
+                           "LayerNorms and the head are folded into its two GEMMs (no norm pass, no fp32 pooled)",
             "config": "200 slots (100 q + 100 a) x 1M bins/hash, D=64 bf16 (tables 51.2 GB), L=100, d=128, "
                       "input_mlp 16->256->512, output_mlp 1280->1024->512, Dense(2, softmax), bf16 MFMA"}
 

@@ -254,6 +254,15 @@ int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float 
                       const float* ln0_beta, const void* W0, const float* b0, int32_t H, const float* ln1_gamma,
                       const float* ln1_beta, const void* W1, const float* b1, int32_t O, int32_t act, float* out,
                       int64_t ldo, void* stream);
+/*
+ * rf_mlp2_small_fwd with out as BF16 [M][O] (row stride ldo) plus, per row and 32-column slice s of it, the pair
+ * (sum, squared deviations from the slice mean) of the fp32 values in stats[row][stats_p0 + s] (stats_P pairs per
+ * row): the producer half of an LN-folded consumer (rf_linear_lnfold_stats_fwd), as rf_linear_stats_fwd's row_stats.
+ */
+int rf_mlp2_small_stats_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float eps, const float* ln0_gamma,
+                            const float* ln0_beta, const void* W0, const float* b0, int32_t H, const float* ln1_gamma,
+                            const float* ln1_beta, const void* W1, const float* b1, int32_t O, int32_t act,
+                            void* out_bf16, int64_t ldo, float* stats, int32_t stats_P, int32_t stats_p0, void* stream);
 
 /*
  * A create_mlp layer pair with the second layer's LayerNormalization folded across the GEMMs (mlp.py:10-13:
@@ -276,6 +285,26 @@ int rf_linear_stats_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const 
 int rf_linear_lnfold_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N, const float* s,
                          const float* t, const float* row_stats, float eps, int32_t act, float* y, int64_t ldy,
                          void* stream);
+/*
+ * An LN-folded chain of create_mlp layers whose FIRST LayerNormalization is folded too (cfg3's output_mlp behind
+ * the pooled row, esim.py:84-88; mlp.py:10-13): the producers of x (rf_mlp2_small_stats_fwd, rf_esim_gather_stats_fwd)
+ * wrote it as BF16 with its slice partials, so no normalisation pass runs anywhere in the chain.
+ *   rf_linear_lnfold_stats_fwd  rf_linear_lnfold_fwd's y, written as rf_linear_stats_fwd writes its output: BF16
+ *                               y_bf16 [M][N] plus out_stats [M][4 ceil(N / 128)][2] (the next layer's input)
+ *   rf_linear_lnfold_head_fwd   rf_linear_lnfold_fwd's y (stored only when y is not NULL) and a Dense(head_n, head_act)
+ *                               head on it: out[r][h] = head_act(sum_c y[r][c] head_w[h][c] + head_b[h]), head_w
+ *                               BF16 [head_n][N], head_n = 2 (esim.py:53,88 Dense(2, 'softmax')); the per-row
+ *                               partial logits of each 128-column tile (fp32, fixed order) go through ws
+ *                               (rf_linear_lnfold_head_ws_bytes(M, N) bytes) to a per-row softmax launch.
+ */
+int rf_linear_lnfold_stats_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
+                               const float* s, const float* t, const float* row_stats, float eps, int32_t act,
+                               void* y_bf16, int64_t ldy, float* out_stats, void* stream);
+size_t rf_linear_lnfold_head_ws_bytes(int64_t M, int32_t N);
+int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
+                              const float* s, const float* t, const float* row_stats, float eps, int32_t act, float* y,
+                              int64_t ldy, const void* head_w, int32_t head_n, const float* head_b, int32_t head_act,
+                              float* out, int64_t ldo, void* ws, size_t ws_bytes, void* stream);
 
 /*
  * Small Dense head on fp32 activations  y = act(x @ W + b),  N <= 64 outputs (the ESIM scorer's
@@ -324,6 +353,16 @@ int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n_tasks, voi
 int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows,
                        const void* a_table, int64_t a_rows, int32_t dtype, int32_t batch, int32_t L, int32_t d, float* out,
                        int64_t out_stride, int64_t out_off, void* stream);
+/*
+ * rf_esim_gather_fwd with the 6 d pooled features written as BF16 (out_bf16 + row * out_stride + out_off, elements)
+ * and, per 32-column slice s of them (s = 0 .. 6 d / 32 - 1), the (sum, squared deviations from the slice mean) pair
+ * of their fp32 values in stats[row][stats_p0 + s] (stats_P pairs per row): the attention's half of the pooled row
+ * for rf_linear_lnfold_stats_fwd (cfg3: out_off = 32 stats_p0 = d_emb).
+ */
+int rf_esim_gather_stats_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows,
+                             const void* a_table, int64_t a_rows, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                             void* out_bf16, int64_t out_stride, int64_t out_off, float* stats, int32_t stats_P,
+                             int32_t stats_p0, void* stream);
 
 /*
  * Masked scaled-dot-product attention over heads (backend/layers/layer_utils.py:4-24, with the

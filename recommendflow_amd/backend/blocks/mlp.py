@@ -125,6 +125,51 @@ class MLP(torch.nn.Module):
                L.ptr(tv), L.ptr(st), n1.eps, L.ACT[self.activation], L.ptr(out), out.stride(0), L.stream_ptr(stream))
         return out
 
+    def prenormed_head_ok(self, in_features: int, head) -> bool:
+        """forward_prenormed_head applies: two bf16 layers, each behind a LayerNormalization, both folded (K >= 512,
+        K % 128 == 0 for the first: its producers' 32-column slices fill every partial slot), an elementwise
+        activation, and a bf16 Dense(2) head on the last layer's output."""
+        if not self.fold_ln or len(self.denses) != 2 or self.dtype != torch.bfloat16 or self.activation == "softmax":
+            return False
+        if any(n is None or n.mode != 0 for n in self.norms):
+            return False
+        k0, k1 = self.denses[0].in_features, self.denses[1].in_features
+        return (k0 == in_features and k0 >= 512 and k0 % 128 == 0 and k1 >= 512 and k1 % 64 == 0
+                and head is not None and head.units == 2 and head.in_features == self.denses[1].units
+                and head.weight.dtype == torch.bfloat16 and head.weight.is_contiguous())
+
+    def forward_prenormed_head(self, xb: torch.Tensor, xstats: torch.Tensor, head, out: Optional[torch.Tensor] = None,
+                               stream=None) -> torch.Tensor:
+        """head(mlp(x)) where x arrives as its producers wrote it for an LN-folded consumer: bf16 values xb [M, K]
+        and per-row, per-32-column-slice (sum, squared deviations) partials xstats [M, K / 32, 2] fp32. Layer 0:
+        LN0 folded into its GEMM, its output written as bf16 + slice partials (rf_linear_lnfold_stats_fwd); layer 1:
+        LN1 folded, the Dense(2) head's per-tile partial logits in its epilogue, then the head's softmax
+        (rf_linear_lnfold_head_fwd): no LayerNorm pass and no [M, units] fp32 round trip anywhere (mlp.py:10-13,
+        esim.py:84-88). Precision: both GEMMs multiply uncentered bf16 activations (_ln_pair's note)."""
+        d0, d1 = self.denses
+        n0, n1 = self.norms
+        M, K0 = xb.shape
+        if xb.dtype != torch.bfloat16 or xb.stride(1) != 1 or xb.stride(0) % 8 or xb.data_ptr() % 16:
+            raise ValueError("xb must be a row-major bf16 [M, K] tensor with 16-byte rows")
+        if xstats.dtype != torch.float32 or not xstats.is_contiguous() or tuple(xstats.shape) != (M, K0 // 32, 2):
+            raise ValueError(f"xstats must be contiguous fp32 [{M}, {K0 // 32}, 2]")
+        wg0, sv0, tv0 = self._ln_folded(0)
+        yb = torch.empty((M, d0.units), dtype=torch.bfloat16, device=xb.device)
+        st1 = torch.empty((M, 4 * ((d0.units + 127) // 128), 2), dtype=torch.float32, device=xb.device)
+        act = L.ACT[self.activation]
+        L.call("rf_linear_lnfold_stats_fwd", L.ptr(xb), M, K0, xb.stride(0), L.ptr(wg0), d0.units, L.ptr(sv0), L.ptr(tv0),
+               L.ptr(xstats), n0.eps, act, L.ptr(yb), yb.stride(0), L.ptr(st1), L.stream_ptr(stream))
+        wg1, sv1, tv1 = self._ln_folded(1)
+        ws_bytes = int(L.load().rf_linear_lnfold_head_ws_bytes(M, d1.units))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=xb.device)
+        if out is None:
+            out = torch.empty((M, head.units), dtype=torch.float32, device=xb.device)
+        L.call("rf_linear_lnfold_head_fwd", L.ptr(yb), M, d1.in_features, yb.stride(0), L.ptr(wg1), d1.units, L.ptr(sv1),
+               L.ptr(tv1), L.ptr(st1), n1.eps, act, None, 0, L.ptr(head.weight), head.units,
+               L.ptr(head.bias) if head.bias is not None else None, L.ACT[head.activation], L.ptr(out), out.stride(0),
+               L.ptr(ws), ws.numel(), L.stream_ptr(stream))
+        return out
+
     def _ln_folded(self, i: int):
         """(W diag(gamma) in bf16, s = its row sums, t = W beta + b) of denses[i] behind LayerNorm norms[i];
         cached until a parameter changes (replaced tensor or in-place version)."""
@@ -183,6 +228,27 @@ class MLP(torch.nn.Module):
                L.ptr(d0.weight), L.ptr(d0.bias), d0.units, L.ptr(n1.gamma), L.ptr(n1.beta), L.ptr(d1.weight),
                L.ptr(d1.bias), d1.units, L.ACT[self.activation], L.ptr(out), out.stride(0), L.stream_ptr(stream))
         return out
+
+    def forward_stats(self, x: torch.Tensor, outb: torch.Tensor, stats: torch.Tensor, p0: int, stream=None):
+        """The fused two-layer forward (rf_mlp2_small_stats_fwd) writing its output as bf16 into outb [M, O] (any row
+        stride) and its per-32-column-slice partials into stats[:, p0 : p0 + O / 32] (stats contiguous [M, P, 2]):
+        the input MLP's half of cfg3's pooled row for an LN-folded consumer (forward_prenormed_head)."""
+        if not self.denses:
+            self.build(x.shape[-1])
+        if not self._fusable(x):
+            raise ValueError("forward_stats needs the fused two-layer form (rf_mlp2_small_fwd's conditions)")
+        n0, n1 = self.norms
+        d0, d1 = self.denses
+        M = x.shape[0]
+        if outb.dtype != torch.bfloat16 or outb.shape != (M, d1.units) or outb.stride(1) != 1:
+            raise ValueError(f"outb must be bf16 [{M}, {d1.units}] with unit column stride")
+        if stats.dtype != torch.float32 or not stats.is_contiguous() or stats.dim() != 3 or stats.shape[0] != M:
+            raise ValueError("stats must be contiguous fp32 [M, P, 2]")
+        L.call("rf_mlp2_small_stats_fwd", L.ptr(x), M, d0.in_features, x.stride(0), n0.eps, L.ptr(n0.gamma), L.ptr(n0.beta),
+               L.ptr(d0.weight), L.ptr(d0.bias), d0.units, L.ptr(n1.gamma), L.ptr(n1.beta), L.ptr(d1.weight),
+               L.ptr(d1.bias), d1.units, L.ACT[self.activation], L.ptr(outb), outb.stride(0), L.ptr(stats),
+               stats.shape[1], p0, L.stream_ptr(stream))
+        return outb
 
 
 def create_mlp(hidden_units, dropout_rate, activation, normalization_layer, name=None, **kw) -> MLP:

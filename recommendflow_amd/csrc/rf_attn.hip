@@ -756,9 +756,12 @@ struct EsimGatherArgs {
     uint32_t qzero, azero;  // the zero row's id in each table (rows + 1): image rows L .. L16 - 1
     uint32_t* stamps;      // STAMP only: [grid][waves][stamp_ex][kStampPts]
     int stamp_ex;
+    uint16_t* outb;        // OB only: the pooled features as bf16 (row stride out_stride, column out_off) ...
+    float* ostats;         // ... and per 32-column slice (sum, squared deviations from the slice mean) of the fp32
+    int oP, op0;           // values: ostats[row][op0 + slice], oP pairs per row (rf_linear_lnfold_* consume them)
 };
 
-template <bool F16, int D, int NTT, int XM, bool GATHER = false, bool STAMP = false>
+template <bool F16, int D, int NTT, int XM, bool GATHER = false, bool STAMP = false, bool OB = false>
 __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16_t* __restrict__ q,
                                                                      const uint16_t* __restrict__ a, int batch, int L,
                                                                      int64_t ex_stride, int64_t ld, float* __restrict__ out,
@@ -864,9 +867,16 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     int po[4] = {kOff, kOff, kOff, kOff};
     int64_t pe = -1;
     auto flush = [&]() __attribute__((always_inline)) {
-        const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + pe * out_stride + out_off), 0, 6 * D * 4, 0x00020000);
+        if constexpr (OB) {
+            const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(ga.outb + pe * out_stride + out_off), 0, 6 * D * 2, 0x00020000);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pv[k]), ro, po[k], 0, 0);
+            for (int k = 0; k < 4; ++k)
+                __builtin_amdgcn_raw_buffer_store_b16((unsigned short)f32_to_bf16_bits(pv[k]), ro, po[k] >> 1, 0, 0);
+        } else {
+            const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + pe * out_stride + out_off), 0, 6 * D * 4, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pv[k]), ro, po[k], 0, 0);
+        }
     };
     // v6 loop: two barriers per example. The images of example e + G are written right after the barrier that
     // ends e's compute phase (nothing reads them after it; the prefetched registers landed under that compute),
@@ -995,6 +1005,28 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                 po[2] = ok0 ? (4 * D + n) * 4 : kOff;
                 po[3] = ok0 ? (5 * D + n) * 4 : kOff;
                 pe = e;
+                if constexpr (OB) {
+                    // slice statistics: the 32 lanes of this half-wave hold columns wave * 32 .. + 31 of each feature
+                    // (n0 = 0: D <= NTH / 2); stored now by the half-wave's first lane (4 per example and half)
+                    static_assert(NTH / 2 >= D && D % 32 == 0, "one 32-column slice per half-wave and feature");
+                    const int sl0 = (2 * side * D + wave * 32) / 32, sl1 = ((2 * side + 1) * D + wave * 32) / 32;
+                    const int sl2 = (4 * D + wave * 32) / 32, sl3 = (5 * D + wave * 32) / 32;
+                    const int sls[4] = {sl0, sl1, sl2, sl3};
+                    float* so = ga.ostats + ((int64_t)e * ga.oP + ga.op0) * 2;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const float v = ok ? pv[k] : 0.f;
+                        float sm = v;
+#pragma unroll
+                        for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o, 64);
+                        const float d = ok ? v - sm * (1.0f / 32.0f) : 0.f;
+                        float m2 = d * d;
+#pragma unroll
+                        for (int o = 1; o < 32; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+                        if ((lane & 31) == 0 && ok && (k < 2 || side == 0))
+                            *reinterpret_cast<float2*>(so + 2 * sls[k]) = make_float2(sm, m2);
+                    }
+                }
             }
         }
         if constexpr (STAMP) esim_stamp(stp, 5, lane);
@@ -1181,12 +1213,13 @@ int launch_esim2g_nt(int grid, size_t lds, hipStream_t st, int batch, int L, flo
                      int64_t out_off, const EsimGatherArgs& ga) {
     // (XM = 2, x widened from the P @ V B fragments instead of the selector MFMA, measured equal: r04g3 0.0875 /
     // 0.0869 vs 0.0872 / 0.0865 ms; the template keeps it, no launcher instantiates it)
-    auto kern = esim2_kernel<false, D, NTT, 1, true>;
+    auto kern = ga.outb ? esim2_kernel<false, D, NTT, 1, true, false, true> : esim2_kernel<false, D, NTT, 1, true>;
     if constexpr (D == 128 && NTT == 7) {  // the diagnostic stamped build: cfg3's shape only
         if (ga.stamps) kern = esim2_kernel<false, D, NTT, 1, true, true>;
     } else {
         if (ga.stamps) return rf_set_error(RF_EINVAL, "stamped ESIM: only d = 128, 97 <= L <= 112");
     }
+    if (ga.stamps && ga.outb) return rf_set_error(RF_EINVAL, "stamped ESIM: fp32 output only");
     const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel (gather)");
     if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, nullptr, nullptr, batch, L, (int64_t)0,
@@ -1287,13 +1320,14 @@ extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t 
 namespace {
 int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows, const void* a_table,
                      int64_t a_rows, int32_t dtype, int32_t batch, int32_t L, int32_t d, float* out, int64_t out_stride,
-                     int64_t out_off, uint32_t* stamps, int32_t stamp_ex, void* stream) {
+                     int64_t out_off, uint32_t* stamps, int32_t stamp_ex, void* stream, uint16_t* outb = nullptr,
+                     float* ostats = nullptr, int32_t oP = 0, int32_t op0 = 0) {
     RF_REQUIRE(dtype == RF_DTYPE_BF16, "rf_esim_gather_fwd: tables must be BF16");
     RF_REQUIRE(L >= 1 && L <= 128, "rf_esim_gather_fwd: need 1 <= L <= 128 (got %d)", L);
     RF_REQUIRE(d == 64 || d == 128, "rf_esim_gather_fwd: d must be 64 or 128 (got %d)", d);
     RF_REQUIRE(batch >= 0, "rf_esim_gather_fwd: batch < 0");
     if (batch == 0) return RF_OK;
-    RF_REQUIRE(q_ids && a_ids && q_table && a_table && out, "rf_esim_gather_fwd: null pointer");
+    RF_REQUIRE(q_ids && a_ids && q_table && a_table && (out || (outb && ostats)), "rf_esim_gather_fwd: null pointer");
     RF_REQUIRE(q_rows >= 1 && a_rows >= 1 && q_rows + 1 < (int64_t)kRowNaN && a_rows + 1 < (int64_t)kRowNaN,
                "rf_esim_gather_fwd: table rows must be in [1, 2^32 - 3)");
     RF_REQUIRE(((uintptr_t)q_table & 15) == 0 && ((uintptr_t)a_table & 15) == 0 && ((uintptr_t)q_ids & 3) == 0 &&
@@ -1307,7 +1341,7 @@ int esim_gather_impl(const uint32_t* q_ids, const uint32_t* a_ids, const void* q
     const int per_cu = lds <= 80 * 1024 ? 2 : 1;
     const int grid = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
     const EsimGatherArgs ga{q_ids, a_ids, (const uint16_t*)q_table, (const uint16_t*)a_table, (uint32_t)(q_rows + 1),
-                            (uint32_t)(a_rows + 1), stamps, stamp_ex};
+                            (uint32_t)(a_rows + 1), stamps, stamp_ex, outb, ostats, oP, op0};
     const int rc = d == 64 ? launch_esim2g<64>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga)
                            : launch_esim2g<128>(nt, grid, lds, st, batch, L, out, out_stride, out_off, ga);
     if (rc) return rc;
@@ -1320,6 +1354,21 @@ extern "C" int rf_esim_gather_fwd(const uint32_t* q_ids, const uint32_t* a_ids, 
                                   float* out, int64_t out_stride, int64_t out_off, void* stream) {
     return esim_gather_impl(q_ids, a_ids, q_table, q_rows, a_table, a_rows, dtype, batch, L, d, out, out_stride, out_off,
                             nullptr, 0, stream);
+}
+
+// the same attention with the pooled features written as bf16 plus per-32-column-slice (sum, squared deviations
+// from the slice mean) pairs of their fp32 values: stats[row][stats_p0 + s], s = 0 .. 6 d / 32 - 1 the slices of the
+// 6 d features (column out_off + 32 s ..), stats_P pairs per row — the producer side of rf_linear_lnfold_stats_fwd
+// (cfg3: out_off = 32 stats_p0, the slices line up with the consumer's)
+extern "C" int rf_esim_gather_stats_fwd(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table, int64_t q_rows,
+                                        const void* a_table, int64_t a_rows, int32_t dtype, int32_t batch, int32_t L,
+                                        int32_t d, void* out_bf16, int64_t out_stride, int64_t out_off, float* stats,
+                                        int32_t stats_P, int32_t stats_p0, void* stream) {
+    RF_REQUIRE(out_bf16 && stats, "rf_esim_gather_stats_fwd: null pointer");
+    RF_REQUIRE(stats_p0 >= 0 && stats_P >= stats_p0 + 6 * d / 32, "rf_esim_gather_stats_fwd: stats slots out of range");
+    RF_REQUIRE(out_off >= 0 && out_stride >= out_off + 6 * d, "rf_esim_gather_stats_fwd: bad output stride / offset");
+    return esim_gather_impl(q_ids, a_ids, q_table, q_rows, a_table, a_rows, dtype, batch, L, d, nullptr, out_stride, out_off,
+                            nullptr, 0, stream, static_cast<uint16_t*>(out_bf16), stats, stats_P, stats_p0);
 }
 
 extern "C" int rf_diag_esim_gather_stamped(const uint32_t* q_ids, const uint32_t* a_ids, const void* q_table,

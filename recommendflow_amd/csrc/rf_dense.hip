@@ -604,15 +604,26 @@ __device__ __forceinline__ void glds_stage(const void* __restrict__ xv, const vo
 //              output and W' = W diag(gamma); mu_r, rstd_r from stats over the K columns; s_c = sum_k W'[c][k],
 //              t_c = W beta + b. That is LN(x) W^T + b with the normalisation applied after the product.
 //              The workgroup first reduces its rows' P partials in a fixed order into LDS.
-enum { kEpiPlain = 0, kEpiStats = 1, kEpiLnFold = 2 };
+//   kEpiLnFoldStats  kEpiLnFold's y, then kEpiStats' bf16 store and slice partials of it (into ostats / oP): the
+//              middle layer of an LN-folded chain whose input statistics came from its producers (cfg3: the input MLP
+//              and the ESIM attention write the pooled row as bf16 + slice partials; no LayerNorm pass)
+//   kEpiLnFoldHead   kEpiLnFold's y (stored only when y is given), then the per-row partial logits of a small head
+//              Dense(NH) over this tile's columns: hpart[row][tile_n][h] = sum_c y[row][c] Wh[h][c], reduced over the
+//              tile's waves in a fixed order (head_softmax_kernel adds the tiles in order, the bias, the softmax)
+enum { kEpiPlain = 0, kEpiStats = 1, kEpiLnFold = 2, kEpiLnFoldStats = 3, kEpiLnFoldHead = 4 };
+constexpr int kHeadN = 2;  // kEpiLnFoldHead: head outputs (cfg3's Dense(2, softmax))
 
 struct EpiArgs {
-    uint16_t* yb;        // kEpiStats output
-    float* stats;        // kEpiStats: accumulated; kEpiLnFold: read
+    uint16_t* yb;        // kEpiStats / kEpiLnFoldStats output
+    float* stats;        // kEpiStats: written; kEpiLnFold*: read (the input row's slice partials)
     const float* fs;     // kEpiLnFold s_c
     const float* ft;     // kEpiLnFold t_c
     float eps;
-    int P;               // partials per row (4 per 128-column tile of the stats GEMM)
+    int P;               // partials per row of `stats` (4 per 128 columns)
+    float* ostats;       // kEpiLnFoldStats: the output's slice partials (oP per row)
+    int oP;
+    const uint16_t* hw;  // kEpiLnFoldHead: head weight [kHeadN][N] bf16
+    float* hpart;        // kEpiLnFoldHead: [M][tiles_n][kHeadN]
 };
 
 // Sum over aligned groups of G consecutive lanes (G = 1, 2, 4), the xor-butterfly order (offsets 1, 2) by DPP
@@ -704,7 +715,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
         const int col = min(n0 + wn * TN + j * 16 + lr, N - 1);
-        if constexpr (EPI == kEpiLnFold) {
+        if constexpr (EPI == kEpiLnFold || EPI == kEpiLnFoldStats || EPI == kEpiLnFoldHead) {
             pb[j] = ea.fs[col];
             pt[j] = ea.ft[col];
         } else {
@@ -724,7 +735,8 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
     const float2* rs2 = nullptr;
     float2 sp[NPR];
     bool stats_late = false;
-    if constexpr (EPI == kEpiLnFold) {
+    constexpr bool LNF = EPI == kEpiLnFold || EPI == kEpiLnFoldStats || EPI == kEpiLnFoldHead;
+    if constexpr (LNF) {
         const int64_t row = m0 + rl < M ? m0 + rl : M - 1;
         rs2 = reinterpret_cast<const float2*>(ea.stats) + row * ea.P;
         stats_late = ea.P <= NPR * TPR;
@@ -789,7 +801,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             }
         }
     }
-    if constexpr (EPI == kEpiLnFold) {
+    if constexpr (LNF) {
         if (stats_late) {
             // Chan's combine of the slices: mu = sum S_p / K, M2 = sum M2_p + (S_p - n_p mu)^2 / n_p
             float s1 = 0.f;
@@ -869,7 +881,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                     }
             }
         }
-    } else if constexpr (EPI == kEpiStats) {
+    } else if constexpr (EPI == kEpiStats || EPI == kEpiLnFoldStats) {
         // pass 1: activation, the fp32 value kept in acc (0 past N); then the bf16 stores
         with_act(act, [&](auto A) {
 #pragma unroll
@@ -879,7 +891,13 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float v = A(acc[i][j][r] + pb[j]);
+                        float v;
+                        if constexpr (EPI == kEpiStats) {
+                            v = A(acc[i][j][r] + pb[j]);
+                        } else {
+                            const int rl = wm * TM + i * 16 + lg * 4 + r;
+                            v = A(srow[2 * rl + 1] * (acc[i][j][r] - srow[2 * rl] * pb[j]) + pt[j]);
+                        }
                         acc[i][j][r] = cok ? v : 0.f;
                     }
             }
@@ -926,12 +944,14 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                     const float d1 = c0 + 16 + lr < N ? acc[i][2 * q + 1][r] - mq : 0.f;
                     const float m2 = row16_sum(d0 * d0 + d1 * d1);
                     const int64_t row = rbase + i * 16 + r;
+                    float* so = EPI == kEpiStats ? ea.stats : ea.ostats;
+                    const int sP = EPI == kEpiStats ? ea.P : ea.oP;
                     if (lr == 0 && row < M)
-                        *reinterpret_cast<float2*>(ea.stats + 2 * (row * ea.P + (n0 / kLdsBN) * 4 + wn * SPW + q)) =
+                        *reinterpret_cast<float2*>(so + 2 * (row * sP + (n0 / kLdsBN) * 4 + wn * SPW + q)) =
                             make_float2(sm, m2);
                 }
         }
-    } else {  // kEpiLnFold: the row statistics were reduced into srow before the loop
+    } else {  // kEpiLnFold / kEpiLnFoldHead: the row statistics were reduced into srow before the loop
         with_act(act, [&](auto A) {
 #pragma unroll
             for (int i = 0; i < FM; ++i)
@@ -943,29 +963,103 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                     for (int j = 0; j < FN; ++j) acc[i][j][r] = A(rstd * (acc[i][j][r] - mu * pb[j]) + pt[j]);
                 }
         });
-        if (full) {
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float* yr = y + (rbase + i * 16 + r) * ldy + cbase;
-#pragma unroll
-                    for (int j = 0; j < FN; ++j) yr[j * 16] = acc[i][j][r];
-                }
-        } else {
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int col = cbase + j * 16;
-                if (col >= N) continue;
+        if (EPI == kEpiLnFold || y) {
+            if (full) {
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int64_t row = rbase + i * 16 + r;
-                        if (row < M) y[row * ldy + col] = acc[i][j][r];
+                        float* yr = y + (rbase + i * 16 + r) * ldy + cbase;
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) yr[j * 16] = acc[i][j][r];
                     }
+            } else {
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    const int col = cbase + j * 16;
+                    if (col >= N) continue;
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int64_t row = rbase + i * 16 + r;
+                            if (row < M) y[row * ldy + col] = acc[i][j][r];
+                        }
+                }
             }
         }
+        if constexpr (EPI == kEpiLnFoldHead) {
+            // this wave's TN columns of every row it holds: sum_c y[row][c] Wh[h][c], c in fragment order, then the
+            // 16 lanes of a row (row16_sum); the WN waves of a row meet in LDS (the ring is free after a barrier)
+            float hwv[kHeadN][FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int col = cbase + j * 16;
+#pragma unroll
+                for (int h = 0; h < kHeadN; ++h)
+                    hwv[h][j] = col < N ? __uint_as_float((uint32_t)ea.hw[(int64_t)h * N + col] << 16) : 0.f;
+            }
+            float* hred = reinterpret_cast<float*>(smem_raw);  // [WN][BM][kHeadN]
+            __syncthreads();  // every wave's last fragment reads of the ring are done
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rl = wm * TM + i * 16 + lg * 4 + r;
+#pragma unroll
+                    for (int h = 0; h < kHeadN; ++h) {
+                        float v = 0.f;
+#pragma unroll
+                        for (int j = 0; j < FN; ++j) v = fmaf(acc[i][j][r], hwv[h][j], v);
+                        v = row16_sum(v);
+                        if (lr == 0) hred[(wn * BM + rl) * kHeadN + h] = v;
+                    }
+                }
+            __syncthreads();
+            const int tiles_n = (N + kLdsBN - 1) / kLdsBN;
+            for (int t = tid; t < BM * kHeadN; t += 256) {
+                const int rl = t / kHeadN, h = t % kHeadN;
+                float v = 0.f;
+#pragma unroll
+                for (int w = 0; w < WN; ++w) v += hred[(w * BM + rl) * kHeadN + h];
+                const int64_t row = m0 + rl;
+                if (row < M) ea.hpart[(row * tiles_n + n0 / kLdsBN) * kHeadN + h] = v;
+            }
+        }
+    }
+}
+
+// cfg3's head after kEpiLnFoldHead: logits[row][h] = sum over the column tiles in order of hpart + b[h]; softmax (or
+// the elementwise activation) over the kHeadN outputs; one thread per row
+__global__ __launch_bounds__(256) void head_softmax_kernel(const float* __restrict__ hpart, int tiles, int64_t M,
+                                                           const float* __restrict__ b, int act, float* __restrict__ y,
+                                                           int64_t ldy) {
+    const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (row >= M) return;
+    float z[kHeadN];
+#pragma unroll
+    for (int h = 0; h < kHeadN; ++h) {
+        float v = 0.f;
+        for (int t = 0; t < tiles; ++t) v += hpart[(row * tiles + t) * kHeadN + h];
+        z[h] = v + (b ? b[h] : 0.f);
+    }
+    if (act == RF_ACT_SOFTMAX) {
+        float m = z[0];
+#pragma unroll
+        for (int h = 1; h < kHeadN; ++h) m = fmaxf(m, z[h]);
+        float s = 0.f;
+#pragma unroll
+        for (int h = 0; h < kHeadN; ++h) {
+            z[h] = expf(z[h] - m);
+            s += z[h];
+        }
+#pragma unroll
+        for (int h = 0; h < kHeadN; ++h) y[row * ldy + h] = z[h] / s;
+    } else {
+        with_act(act, [&](auto A) {
+#pragma unroll
+            for (int h = 0; h < kHeadN; ++h) y[row * ldy + h] = A(z[h]);
+        });
     }
 }
 
@@ -1101,13 +1195,18 @@ constexpr size_t mlp2_lds_bytes() {
 
 // VEC0: K0 % 8 == 0 and H * K0 * 2 a multiple of 1 KiB, so W0 moves by LDS-DMA as it lies in memory.
 // NB: column blocks of 128 per wave pass (O <= 512 in one pass at cfg3).
-template <int H, bool VEC0>
+// OS: the output as bf16 (outb) plus, per row and 32-column slice, the (sum, squared deviations from the slice
+// mean) pair of the fp32 values into ostats[row][op0 + slice] (oP pairs per row): the producer side of an LN-folded
+// consumer GEMM (rf_linear_lnfold_*), as gemm_lds_kernel's kEpiStats
+template <int H, bool VEC0, bool OS = false>
 __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restrict__ x, int64_t M, int K0, int64_t ldx, float eps,
                                                             const float* __restrict__ g0, const float* __restrict__ be0,
                                                             const uint16_t* __restrict__ W0, const float* __restrict__ b0,
                                                             const float* __restrict__ g1, const float* __restrict__ be1,
                                                             const uint16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                            int O, int act, float* __restrict__ out, int64_t ldo) {
+                                                            int O, int act, float* __restrict__ out, int64_t ldo,
+                                                            uint16_t* __restrict__ outb, float* __restrict__ ostats, int oP,
+                                                            int op0) {
     constexpr int RS0 = 32 + 8, RSH = H + 8;  // LDS row strides (elements) of the A tiles: 16-byte row pad
     constexpr int TW = H / 64;                // layer-0 column tiles per wave (H / 4 columns)
     constexpr int KS = H / 32;                // layer-1 k steps
@@ -1294,6 +1393,40 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
         });
         // values first, stores after (see gemm_lds_kernel's epilogue)
         const int c0 = cb * kMlp2Cols;
+        if constexpr (OS) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                if (c0 + nt * 16 + lr >= O) c[nt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int n = c0 + nt * 16 + lr;
+                if (n >= O) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t row = r0 + 4 * lg + r;
+                    if (row < M) reinterpret_cast<__bf16*>(outb)[row * ldo + n] = (__bf16)c[nt][r];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NT / 2; ++q) {
+                const int cq = c0 + q * 32;
+                const int nq = min(max(O - cq, 0), 32);
+                if (nq == 0) continue;
+                const float inv_n = 1.0f / (float)nq;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float sm = row16_sum(c[2 * q][r] + c[2 * q + 1][r]);
+                    const float mq = sm * inv_n;
+                    const float d0 = cq + lr < O ? c[2 * q][r] - mq : 0.f;
+                    const float d1 = cq + 16 + lr < O ? c[2 * q + 1][r] - mq : 0.f;
+                    const float m2 = row16_sum(d0 * d0 + d1 * d1);
+                    const int64_t row = r0 + 4 * lg + r;
+                    if (lr == 0 && row < M)
+                        *reinterpret_cast<float2*>(ostats + 2 * (row * oP + op0 + cq / 32)) = make_float2(sm, m2);
+                }
+            }
+            continue;
+        }
         if (rows_full && c0 + kMlp2Cols <= O) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1338,8 +1471,35 @@ extern "C" int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t 
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return rf_set_error(RF_EHIP, "mlp2_small_kernel: %s", hipGetErrorString(e));
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, x, M, K0, ldx, eps, ln0_gamma, ln0_beta, (const uint16_t*)W0, b0,
-                       ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, out, ldo);
+                       ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, out, ldo, nullptr, nullptr, 0, 0);
     return rf_check_launch("mlp2_small_kernel");
+}
+
+extern "C" int rf_mlp2_small_stats_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float eps, const float* ln0_gamma,
+                                       const float* ln0_beta, const void* W0, const float* b0, int32_t H,
+                                       const float* ln1_gamma, const float* ln1_beta, const void* W1, const float* b1,
+                                       int32_t O, int32_t act, void* out_bf16, int64_t ldo, float* stats, int32_t stats_P,
+                                       int32_t stats_p0, void* stream) {
+    RF_REQUIRE(K0 >= 1 && K0 <= 32, "rf_mlp2_small_stats_fwd: input width must be 1..32 (got %d)", K0);
+    RF_REQUIRE(H == 128 || H == 256, "rf_mlp2_small_stats_fwd: hidden width must be 128 or 256 (got %d)", H);
+    RF_REQUIRE(O >= 1 && M >= 0 && ldx >= K0 && ldo >= O, "rf_mlp2_small_stats_fwd: bad shape");
+    RF_REQUIRE(stats_p0 >= 0 && stats_P >= stats_p0 + (O + 31) / 32, "rf_mlp2_small_stats_fwd: stats slots out of range");
+    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_mlp2_small_stats_fwd: activation must be elementwise");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && W0 && W1 && out_bf16 && stats && ln0_gamma && ln0_beta, "rf_mlp2_small_stats_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)W1 & 15) == 0 && ((uintptr_t)W0 & 15) == 0, "rf_mlp2_small_stats_fwd: W0 / W1 must be 16-byte aligned");
+    const dim3 grid((unsigned)((M + kMlp2Rows - 1) / kMlp2Rows));
+    hipStream_t st = rf_stream(stream);
+    const bool vec0 = (K0 & 7) == 0 && (H * K0 * 2) % 1024 == 0;
+    auto kern = H == 256 ? (vec0 ? mlp2_small_kernel<256, true, true> : mlp2_small_kernel<256, false, true>)
+                         : (vec0 ? mlp2_small_kernel<128, true, true> : mlp2_small_kernel<128, false, true>);
+    const size_t lds = H == 256 ? mlp2_lds_bytes<256>() : mlp2_lds_bytes<128>();
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return rf_set_error(RF_EHIP, "mlp2_small_kernel: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, x, M, K0, ldx, eps, ln0_gamma, ln0_beta, (const uint16_t*)W0, b0,
+                       ln1_gamma, ln1_beta, (const uint16_t*)W1, b1, O, act, nullptr, ldo, (uint16_t*)out_bf16, stats,
+                       stats_P, stats_p0);
+    return rf_check_launch("mlp2_small_kernel (stats)");
 }
 
 extern "C" int rf_dense_head_fwd(const float* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t w_dtype,
@@ -1487,6 +1647,62 @@ extern "C" int rf_linear_lnfold_fwd(const void* x, int64_t M, int32_t K, int64_t
     ea.eps = eps;
     ea.P = 4 * ((K + kLdsBN - 1) / kLdsBN);  // the stats call's N is this call's K
     return launch_lds_epi<kEpiLnFold>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, rf_stream(stream), "rf_linear_lnfold_fwd");
+}
+
+extern "C" int rf_linear_lnfold_stats_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
+                                          const float* s, const float* t, const float* row_stats, float eps, int32_t act,
+                                          void* y_bf16, int64_t ldy, float* out_stats, void* stream) {
+    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_linear_lnfold_stats_fwd: activation must be elementwise");
+    RF_REQUIRE(M >= 0 && N > 0 && K >= 512 && K % 64 == 0 && ldx >= K && ldx % 8 == 0 && ldy >= N,
+               "rf_linear_lnfold_stats_fwd: needs K >= 512, K %% 64 == 0, ldx %% 8 == 0");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && Wg && s && t && row_stats && y_bf16 && out_stats, "rf_linear_lnfold_stats_fwd: null pointer");
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)Wg & 15) == 0, "rf_linear_lnfold_stats_fwd: x/W must be 16-byte aligned");
+    EpiArgs ea{};
+    ea.stats = const_cast<float*>(row_stats);
+    ea.fs = s;
+    ea.ft = t;
+    ea.eps = eps;
+    ea.P = 4 * ((K + kLdsBN - 1) / kLdsBN);
+    ea.yb = static_cast<uint16_t*>(y_bf16);
+    ea.ostats = out_stats;
+    ea.oP = 4 * ((N + kLdsBN - 1) / kLdsBN);
+    return launch_lds_epi<kEpiLnFoldStats>(x, M, K, ldx, Wg, N, nullptr, act, nullptr, ldy, ea, rf_stream(stream),
+                                           "rf_linear_lnfold_stats_fwd");
+}
+
+extern "C" size_t rf_linear_lnfold_head_ws_bytes(int64_t M, int32_t N) {
+    return (size_t)std::max<int64_t>(M, 1) * ((N + kLdsBN - 1) / kLdsBN) * kHeadN * sizeof(float);
+}
+
+extern "C" int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
+                                         const float* s, const float* t, const float* row_stats, float eps, int32_t act,
+                                         float* y, int64_t ldy, const void* head_w, int32_t head_n, const float* head_b,
+                                         int32_t head_act, float* out, int64_t ldo, void* ws, size_t ws_bytes,
+                                         void* stream) {
+    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_linear_lnfold_head_fwd: activation must be elementwise");
+    RF_REQUIRE(head_n == kHeadN, "rf_linear_lnfold_head_fwd: the head must have %d outputs (got %d)", kHeadN, head_n);
+    RF_REQUIRE(head_act >= RF_ACT_NONE && head_act <= RF_ACT_SOFTMAX, "rf_linear_lnfold_head_fwd: unknown head activation");
+    RF_REQUIRE(M >= 0 && N > 0 && K >= 512 && K % 64 == 0 && ldx >= K && ldx % 8 == 0 && (!y || ldy >= N) && ldo >= head_n,
+               "rf_linear_lnfold_head_fwd: needs K >= 512, K %% 64 == 0, ldx %% 8 == 0");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(x && Wg && s && t && row_stats && head_w && out && ws, "rf_linear_lnfold_head_fwd: null pointer");
+    RF_REQUIRE(ws_bytes >= rf_linear_lnfold_head_ws_bytes(M, N), "rf_linear_lnfold_head_fwd: workspace too small");
+    RF_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)Wg & 15) == 0, "rf_linear_lnfold_head_fwd: x/W must be 16-byte aligned");
+    EpiArgs ea{};
+    ea.stats = const_cast<float*>(row_stats);
+    ea.fs = s;
+    ea.ft = t;
+    ea.eps = eps;
+    ea.P = 4 * ((K + kLdsBN - 1) / kLdsBN);
+    ea.hw = static_cast<const uint16_t*>(head_w);
+    ea.hpart = static_cast<float*>(ws);
+    hipStream_t st = rf_stream(stream);
+    const int rc = launch_lds_epi<kEpiLnFoldHead>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, st, "rf_linear_lnfold_head_fwd");
+    if (rc != RF_OK) return rc;
+    hipLaunchKernelGGL(head_softmax_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, (const float*)ws,
+                       (N + kLdsBN - 1) / kLdsBN, M, head_b, head_act, out, ldo);
+    return rf_check_launch("head_softmax_kernel");
 }
 
 extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,

@@ -58,6 +58,8 @@ class Esim(torch.nn.Module):
         cur = torch.cuda.current_stream(dense.device)
         pooled = torch.empty((B, self.pooled_width), dtype=torch.float32, device=dense.device)
         if not self.concurrent_input_mlp:
+            if self._gather_ok(user, ad) and self._fused_scorer_ok(dense):
+                return self._forward_fused_scorer(user, ad, dense)
             self.input_mlp(dense, out=pooled[:, : self.d_emb])
             if self._gather_ok(user, ad):
                 self._esim_gather(user, ad, pooled)
@@ -93,6 +95,34 @@ class Esim(torch.nn.Module):
     # (test_esim_gather_equals_encoders_plus_attention); cfg3 forward 0.2616 -> 0.1843 ms
     # (profiles/r03/r03b7_cfg3_gather_trace.txt). False: encoders + rf_esim_soft_attention_fwd.
     gather = True
+
+    # True (gather path): the pooled row is never normalised by its own pass nor stored as fp32 — the input MLP and
+    # the attention write it as bf16 with per-32-column-slice partials, the output MLP folds both LayerNorms into
+    # its GEMMs and the Dense(2, softmax) head's partial logits ride the last GEMM's epilogue.
+    # False: pooled fp32 -> rf_norm_fwd -> stats GEMM -> LN-fold GEMM -> rf_dense_head_fwd.
+    fused_scorer = True
+
+    def _fused_scorer_ok(self, dense: torch.Tensor) -> bool:
+        return (self.fused_scorer and self.d_emb % 32 == 0 and (6 * self.d) % 32 == 0
+                and self.input_mlp.denses and self.input_mlp._fusable(dense)
+                and self.output_mlp.prenormed_head_ok(self.pooled_width, self.dense_output))
+
+    def _forward_fused_scorer(self, user: SparseBatch, ad: SparseBatch, dense: torch.Tensor) -> torch.Tensor:
+        """input MLP -> pooled[:, :d_emb] (bf16 + slice partials, rf_mlp2_small_stats_fwd); id pass; attention ->
+        pooled[:, d_emb:] (rf_esim_gather_stats_fwd); output MLP + head on the folded chain (forward_prenormed_head)."""
+        from ...runtime import lib as L
+
+        B, W = user.batch, self.pooled_width
+        pb = torch.empty((B, W), dtype=torch.bfloat16, device=dense.device)
+        pst = torch.empty((B, W // 32, 2), dtype=torch.float32, device=dense.device)
+        self.input_mlp.forward_stats(dense, pb[:, : self.d_emb], pst, 0)
+        q_ids, a_ids = self.token_ids(user, ad)
+        self._check_ids(q_ids, a_ids)
+        eq, ea = self.enc_q, self.enc_a
+        L.call("rf_esim_gather_stats_fwd", L.ptr(q_ids), L.ptr(a_ids), L.ptr(eq.table), eq.table.shape[0], L.ptr(ea.table),
+               ea.table.shape[0], L.DT_BF16, B, self.L, self.d, L.ptr(pb), pb.stride(0), self.d_emb, L.ptr(pst), W // 32,
+               self.d_emb // 32, L.stream_ptr(None))
+        return self.output_mlp.forward_prenormed_head(pb, pst, self.dense_output)
 
     def _check_batches(self, user: SparseBatch, ad: SparseBatch):
         """The shapes both ESIM paths rely on: the gather path sizes its id buffers [B, L, 2] from these, so a
@@ -135,15 +165,19 @@ class Esim(torch.nn.Module):
         L.call("rf_single_token_ids_multi_fwd", ctypes.addressof(tasks), 2, L.stream_ptr(None))
         return ids[0], ids[1]
 
-    def attention_gather(self, q_ids: torch.Tensor, a_ids: torch.Tensor, pooled: torch.Tensor):
-        """The ESIM attention + pooling into pooled[:, d_emb:], its q / a images gathered by id (rf_esim_gather_fwd)."""
-        from ...runtime import lib as L
-
+    def _check_ids(self, q_ids: torch.Tensor, a_ids: torch.Tensor):
         B = q_ids.shape[0]
         if (q_ids.shape != (B, self.L, 2) or a_ids.shape != (B, self.L, 2) or q_ids.dtype != torch.int32
                 or a_ids.dtype != torch.int32 or not q_ids.is_contiguous() or not a_ids.is_contiguous()):
             raise ValueError(f"token ids must be int32 [B, {self.L}, 2] on both sides, got {tuple(q_ids.shape)} / "
                              f"{tuple(a_ids.shape)}")
+
+    def attention_gather(self, q_ids: torch.Tensor, a_ids: torch.Tensor, pooled: torch.Tensor):
+        """The ESIM attention + pooling into pooled[:, d_emb:], its q / a images gathered by id (rf_esim_gather_fwd)."""
+        from ...runtime import lib as L
+
+        B = q_ids.shape[0]
+        self._check_ids(q_ids, a_ids)
         if pooled.dtype != torch.float32 or pooled.dim() != 2 or pooled.shape[0] != B or pooled.shape[1] < self.d_emb + 6 * self.d or pooled.stride(1) != 1:
             raise ValueError(f"pooled must be a row-major [{B}, >= {self.d_emb + 6 * self.d}] fp32 tensor")
         eq, ea = self.enc_q, self.enc_a

@@ -42,6 +42,15 @@ _SIGS = {
                                             _vp]),
     "rf_mlp2_small_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i32,
                                          _i32, _vp, _i64, _vp]),
+    "rf_mlp2_small_stats_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
+                                               _i32, _i32, _vp, _i64, _vp, _i32, _i32, _vp]),
+    "rf_linear_lnfold_stats_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _f32, _i32, _vp, _i64,
+                                                  _vp, _vp]),
+    "rf_linear_lnfold_head_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
+    "rf_linear_lnfold_head_fwd": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _vp, _vp, _vp, _f32, _i32, _vp, _i64,
+                                                 _vp, _i32, _vp, _i32, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "rf_esim_gather_stats_fwd": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _i64, _i64,
+                                                _vp, _i32, _i32, _vp]),
     "rf_sdpa_fwd": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "rf_bucketize_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
     "rf_bucketize_owner": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),

@@ -322,3 +322,68 @@ def test_mlp_layernorm_folded_across_gemms(O, cuda, M):
     np.testing.assert_allclose(y, want, rtol=2e-2, atol=2e-2)
     np.testing.assert_allclose(y, y_unfused, rtol=2e-2, atol=2e-2)
     assert err_fold <= 2 * err_unfused + 1e-3, (err_fold, err_unfused)
+
+
+def _slice_stats(y: np.ndarray) -> np.ndarray:
+    """[M, K] fp32 -> [M, K / 32, 2]: per 32-column slice its sum and squared deviations from the slice mean."""
+    M, K = y.shape
+    s = y.reshape(M, K // 32, 32).astype(np.float64)
+    S = s.sum(2)
+    M2 = ((s - S[..., None] / 32) ** 2).sum(2)
+    return np.stack([S, M2], axis=2)
+
+
+def _bf16_bits(t: torch.Tensor) -> np.ndarray:
+    return t.contiguous().view(torch.int16).cpu().numpy()
+
+
+@pytest.mark.parametrize("M", [100, 4096])
+def test_mlp2_small_stats_output(cuda, M):
+    """rf_mlp2_small_stats_fwd: the same values as rf_mlp2_small_fwd, stored as bf16 (round-to-nearest-even of the
+    fp32 output, bit for bit), and per 32-column slice the (sum, squared deviations) pair of those fp32 values
+    at columns [p0, p0 + O / 32) of a wider stats row."""
+    mlp = create_mlp([256, 512], 0.3, "gelu", LayerNormalization(epsilon=1e-6), in_features=16, dtype=torch.bfloat16,
+                     seed=3)
+    x = torch.randn(M, 16, generator=torch.Generator().manual_seed(M)).cuda()
+    y = mlp(x)
+    pb = torch.zeros((M, 1280), dtype=torch.bfloat16, device="cuda")
+    st = torch.full((M, 40, 2), -7.0, device="cuda")
+    mlp.forward_stats(x, pb[:, :512], st, 0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_bf16_bits(pb[:, :512]), _bf16_bits(y.to(torch.bfloat16)))
+    got = st.cpu().numpy()
+    np.testing.assert_allclose(got[:, :16], _slice_stats(y.cpu().numpy()), rtol=1e-5, atol=1e-4)
+    assert (got[:, 16:] == -7.0).all()  # slots past the producer's columns untouched
+
+
+@pytest.mark.parametrize("M", [300, 4096])
+def test_mlp_prenormed_head(O, cuda, M):
+    """forward_prenormed_head (LN0 folded from producer partials -> rf_linear_lnfold_stats_fwd -> LN1 folded with the
+    Dense(2, softmax) head in the epilogue -> rf_linear_lnfold_head_fwd) against float64 LN -> Dense(gelu) x 2 ->
+    Dense(2, softmax) of the same parameters (cfg3's output MLP + head shapes); x is given to it as bf16 values +
+    slice partials of the fp32 row, as the input MLP and the attention write them."""
+    mlp = create_mlp([1024, 512], 0.3, "gelu", LayerNormalization(epsilon=1e-6), in_features=1280, dtype=torch.bfloat16,
+                     seed=9)
+    head = Dense(512, 2, activation="softmax", dtype=torch.bfloat16, seed=31)
+    g = torch.Generator().manual_seed(M + 1)
+    for nm in mlp.norms:
+        nm.gamma.copy_(torch.rand(nm.width, generator=g) + 0.5)
+        nm.beta.copy_(torch.randn(nm.width, generator=g) * 0.2)
+    for dn in mlp.denses:
+        dn.bias.copy_(torch.randn(dn.units, generator=g) * 0.1)
+    head.bias.copy_(torch.randn(2, generator=g) * 0.1)
+    x = torch.randn(M, 1280, generator=g) * 1.5 + 0.3
+    xb = x.to(torch.bfloat16).cuda()
+    xs = torch.from_numpy(_slice_stats(x.numpy()).astype(np.float32)).cuda()
+    assert mlp.prenormed_head_ok(1280, head)
+    p = mlp.forward_prenormed_head(xb, xs, head).cpu().numpy()
+    params = [{"W": dn.weight.float().cpu().numpy().T, "b": dn.bias.cpu().numpy(), "gamma": nm.gamma.cpu().numpy(),
+               "beta": nm.beta.cpu().numpy()} for nm, dn in zip(mlp.norms, mlp.denses)]
+    h = O.mlp(x.numpy(), params, "gelu", "ln")
+    want = O.activation(h @ head.weight.float().cpu().numpy().T.astype(np.float64) + head.bias.cpu().numpy(), "softmax")
+    assert np.abs(p - want).max() <= 1e-2
+    assert (p.argmax(1) == want.argmax(1)).mean() >= 0.999
+    np.testing.assert_allclose(p.sum(1), 1.0, atol=1e-5)
+    # the unfused chain of the same module (fp32 x -> LN pass -> stats GEMM -> LN-fold GEMM -> head kernel)
+    p_unfused = head(mlp(x.cuda())).cpu().numpy()
+    assert np.abs(p - p_unfused).max() <= 1e-2

@@ -81,12 +81,17 @@ def test_esim_cfg3_shape_vs_oracle(O, cuda):
     assert (p.argmax(1) == want.argmax(1)).mean() >= 0.999
     fwd = model.graphed(du, da, dd)
     assert torch.equal(fwd(du, da, dd), p_gpu)
-    # the input MLP on a side stream beside the encoders (the A/B switch) gives the same bits
-    model.concurrent_input_mlp = True
+    # the unfused scorer (pooled fp32 -> LayerNorm pass -> GEMMs -> head) at the same bar, and the input MLP on a
+    # side stream beside the encoders (the A/B switch, unfused scorer) gives its bits
+    model.fused_scorer = False
     try:
-        assert torch.equal(model(du, da, dd), p_gpu)
+        p_unf = model(du, da, dd)
+        assert np.abs(p_unf.cpu().numpy() - want).max() <= 1e-2
+        model.concurrent_input_mlp = True
+        assert torch.equal(model(du, da, dd), p_unf)
     finally:
         model.concurrent_input_mlp = False
+        model.fused_scorer = True
 
 
 @pytest.mark.parametrize("mask_padding", [False, True])
@@ -109,6 +114,7 @@ def test_esim_gather_equals_encoders_plus_attention(cuda, mask_padding):
 
     hu, ha = from_lists(rows("u")).to("cuda"), from_lists(rows("a")).to("cuda")
     dense = torch.randn(B, 16, generator=torch.Generator().manual_seed(9)).cuda()
+    model.fused_scorer = False  # bit-equality of the two attention paths under the same (unfused) scorer
     model.gather = False
     want = model(hu, ha, dense)
     pw = torch.zeros((B, model.pooled_width), device="cuda")
@@ -125,6 +131,11 @@ def test_esim_gather_equals_encoders_plus_attention(cuda, mask_padding):
     assert torch.equal(model(hu, ha, dense), want)
     fwd = model.graphed(hu, ha, dense)
     assert torch.equal(fwd(hu, ha, dense), want)
+    # the fused scorer on the gather path: the same probabilities within the §8d bar
+    model.fused_scorer = True
+    pf = model(hu, ha, dense).cpu().numpy()
+    assert np.abs(pf - want.cpu().numpy()).max() <= 1e-2
+    assert (pf.argmax(1) == want.cpu().numpy().argmax(1)).mean() >= 0.99
 
 
 def test_esim_rejects_mismatched_batches(cuda):
@@ -212,3 +223,37 @@ def test_esim_cfg3_full_shape_sampled(O, cuda):
     want = O.activation(x @ W.T.astype(np.float64) + model.dense_output.bias.cpu().numpy(), "softmax")
     assert np.abs(p[idx] - want).max() <= 1e-2
     assert (p[idx].argmax(1) == want.argmax(1)).all()
+
+
+def test_esim_gather_stats_output(cuda):
+    """rf_esim_gather_stats_fwd: the pooled features of rf_esim_gather_fwd stored as bf16 (RNE of the same fp32
+    values, bit for bit) and the (sum, squared deviations) pairs of each 32-column slice of those fp32 values."""
+    import recommendflow_amd.runtime.lib as L
+
+    Ls, B = 100, 300
+    user = [SlotSpec(f"u{i:03d}", 20_000, (2022, 2023)) for i in range(Ls)]
+    ad = [SlotSpec(f"a{i:03d}", 20_000, (2022, 2023)) for i in range(Ls)]
+    model = Esim(user, ad, n_dense=16, dim=64, seed=3)
+    hu = synthetic_batch(B, [False] * Ls, seed=7, slot_ids=range(Ls)).to("cuda")
+    ha = synthetic_batch(B, [False] * Ls, seed=8, slot_ids=range(Ls, 2 * Ls)).to("cuda")
+    qi, ai = model.token_ids(hu, ha)
+    W = model.pooled_width
+    pooled = torch.zeros((B, W), device="cuda")
+    model.attention_gather(qi, ai, pooled)
+    pb = torch.zeros((B, W), dtype=torch.bfloat16, device="cuda")
+    st = torch.full((B, W // 32, 2), -7.0, device="cuda")
+    eq, ea = model.enc_q, model.enc_a
+    L.call("rf_esim_gather_stats_fwd", L.ptr(qi), L.ptr(ai), L.ptr(eq.table), eq.table.shape[0], L.ptr(ea.table),
+           ea.table.shape[0], L.DT_BF16, B, Ls, 128, L.ptr(pb), pb.stride(0), model.d_emb, L.ptr(st), W // 32,
+           model.d_emb // 32, L.stream_ptr(None))
+    torch.cuda.synchronize()
+    feat = pooled[:, model.d_emb:]
+    np.testing.assert_array_equal(pb[:, model.d_emb:].contiguous().view(torch.int16).cpu().numpy(),
+                                  feat.to(torch.bfloat16).contiguous().view(torch.int16).cpu().numpy())
+    f = feat.cpu().numpy().astype(np.float64).reshape(B, -1, 32)
+    S = f.sum(2)
+    M2 = ((f - S[..., None] / 32) ** 2).sum(2)
+    got = st.cpu().numpy()
+    np.testing.assert_allclose(got[:, model.d_emb // 32:, 0], S, rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(got[:, model.d_emb // 32:, 1], M2, rtol=1e-4, atol=1e-4)
+    assert (got[:, : model.d_emb // 32] == -7.0).all()
