@@ -383,6 +383,22 @@ __device__ __forceinline__ float rs4(float a, float b, float c, float d) {
     return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// Sum over each 32-lane half of the wave, in every lane of the half, without LDS: the 16-lane rows by DPP (quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror), then rows 0 + 1 and 2 + 3 by one v_permlane16_swap
+// (a' = [r0, r0, r2, r2], b' = [r1, r1, r3, r3] for a = b = v)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float half32_sum(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    v += dpp_f<0x141>(v);
+    v += dpp_f<0x140>(v);
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+
 // v[0..N) reduced as a balanced tree (maximum3 / add pairs): dependent depth ~log instead of N
 template <int N, bool MAX>
 __device__ __forceinline__ float tree_reduce(float (&v)[8]) {
@@ -1013,19 +1029,28 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                     const int sl2 = (4 * D + wave * 32) / 32, sl3 = (5 * D + wave * 32) / 32;
                     const int sls[4] = {sl0, sl1, sl2, sl3};
                     float* so = ga.ostats + ((int64_t)e * ga.oP + ga.op0) * 2;
+                    // one pass around a pivot (the half's first value): S = sum d + 32 p, M2 = sum d^2 - (sum d)^2 / 32
+                    // with d = v - p; the 8 reductions are independent DPP chains (no LDS round trips)
+                    float sd[4], sq[4], pvt[4];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        const float v = ok ? pv[k] : 0.f;
-                        float sm = v;
-#pragma unroll
-                        for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o, 64);
-                        const float d = ok ? v - sm * (1.0f / 32.0f) : 0.f;
-                        float m2 = d * d;
-#pragma unroll
-                        for (int o = 1; o < 32; o <<= 1) m2 += __shfl_xor(m2, o, 64);
-                        if ((lane & 31) == 0 && ok && (k < 2 || side == 0))
-                            *reinterpret_cast<float2*>(so + 2 * sls[k]) = make_float2(sm, m2);
+                        const float p0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv[k]), 0));
+                        const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv[k]), 32));
+                        pvt[k] = side ? p1 : p0;
+                        const float d = ok ? pv[k] - pvt[k] : 0.f;
+                        sd[k] = d;
+                        sq[k] = d * d;
                     }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        sd[k] = half32_sum(sd[k]);
+                        sq[k] = half32_sum(sq[k]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if ((lane & 31) == 0 && ok && (k < 2 || side == 0))
+                            *reinterpret_cast<float2*>(so + 2 * sls[k]) =
+                                make_float2(sd[k] + 32.0f * pvt[k], fmaxf(sq[k] - sd[k] * sd[k] * (1.0f / 32.0f), 0.f));
                 }
             }
         }

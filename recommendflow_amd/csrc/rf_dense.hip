@@ -712,8 +712,16 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
     // The epilogue's per-column parameters (bias, or the LN fold's s_c / t_c) are loaded now, under the first
     // stage's copies, instead of as dependent loads after the last MFMA (one HBM round trip off the tail).
     float pb[FN], pt[FN];
+    // kEpiLnFoldHead: the head weights of this lane's columns, loaded here for the same reason (0 past N)
+    float hwv[EPI == kEpiLnFoldHead ? kHeadN : 1][FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
+        if constexpr (EPI == kEpiLnFoldHead) {
+            const int c = n0 + wn * TN + j * 16 + lr;
+#pragma unroll
+            for (int h = 0; h < kHeadN; ++h)
+                hwv[h][j] = c < N ? __uint_as_float((uint32_t)ea.hw[(int64_t)h * N + c] << 16) : 0.f;
+        }
         const int col = min(n0 + wn * TN + j * 16 + lr, N - 1);
         if constexpr (EPI == kEpiLnFold || EPI == kEpiLnFoldStats || EPI == kEpiLnFoldHead) {
             pb[j] = ea.fs[col];
@@ -991,14 +999,6 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
         if constexpr (EPI == kEpiLnFoldHead) {
             // this wave's TN columns of every row it holds: sum_c y[row][c] Wh[h][c], c in fragment order, then the
             // 16 lanes of a row (row16_sum); the WN waves of a row meet in LDS (the ring is free after a barrier)
-            float hwv[kHeadN][FN];
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                const int col = cbase + j * 16;
-#pragma unroll
-                for (int h = 0; h < kHeadN; ++h)
-                    hwv[h][j] = col < N ? __uint_as_float((uint32_t)ea.hw[(int64_t)h * N + col] << 16) : 0.f;
-            }
             float* hred = reinterpret_cast<float*>(smem_raw);  // [WN][BM][kHeadN]
             __syncthreads();  // every wave's last fragment reads of the ring are done
 #pragma unroll
@@ -1397,14 +1397,23 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
                 if (c0 + nt * 16 + lr >= O) c[nt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const int n = c0 + nt * 16 + lr;
-                if (n >= O) continue;
+            if (rows_full && c0 + kMlp2Cols <= O) {  // interior block: unguarded stores (see gemm_lds_kernel's epilogue)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int64_t row = r0 + 4 * lg + r;
-                    if (row < M) reinterpret_cast<__bf16*>(outb)[row * ldo + n] = (__bf16)c[nt][r];
+                    __bf16* yr = reinterpret_cast<__bf16*>(outb) + (r0 + 4 * lg + r) * ldo + c0 + lr;
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) yr[nt * 16] = (__bf16)c[nt][r];
+                }
+            } else {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int n = c0 + nt * 16 + lr;
+                    if (n >= O) continue;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int64_t row = r0 + 4 * lg + r;
+                        if (row < M) reinterpret_cast<__bf16*>(outb)[row * ldo + n] = (__bf16)c[nt][r];
+                    }
                 }
             }
 #pragma unroll
