@@ -63,7 +63,41 @@ def cosent_loss(y_true, query, doc, scale=20):
     return _Cosent.apply((query * doc).sum(dim=1), y_true.reshape(-1), scale)
 
 
+def _mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x [M, K] @ w[N, K]^T in fp32 on librf (rf_linear_fwd: exact-fp32 MFMA, LDS-DMA ring when K % 32 == 0 and
+    K >= 256). Shapes whose rows are not 16-byte multiples (K % 4 != 0: odd in-batch sizes in the backward) stay on
+    torch's GPU GEMM."""
+    x, w = x.float().contiguous(), w.float().contiguous()
+    M, K = x.shape
+    N = w.shape[0]
+    if K % 4 or x.data_ptr() % 16 or w.data_ptr() % 16 or M == 0:
+        return x @ w.t()
+    y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    L.call("rf_linear_fwd", L.ptr(x), L.DT_F32, M, K, x.stride(0), L.ptr(w), N, None, 0, L.ptr(y), y.stride(0),
+           L.stream_ptr())
+    return y
+
+
+class _InBatchLogits(torch.autograd.Function):
+    """logits = query @ doc^T (match_losses.py:160, tf.matmul(query, doc, transpose_b=True)) and its two backward
+    products on librf: dq = g @ doc, dd = g^T @ query (each as x @ w^T with w the transposed operand)."""
+
+    @staticmethod
+    def forward(ctx, q, d):
+        q, d = q.float().contiguous(), d.float().contiguous()
+        ctx.save_for_backward(q, d)
+        return _mm_nt(q, d)
+
+    @staticmethod
+    def backward(ctx, g):
+        q, d = ctx.saved_tensors
+        g = g.float().contiguous()
+        dq = _mm_nt(g, d.t()) if ctx.needs_input_grad[0] else None
+        dd = _mm_nt(g.t(), q.t()) if ctx.needs_input_grad[1] else None
+        return dq, dd
+
+
 def batch_neg_sample_scaled_multi_class_ce_loss(y_true, query, doc, scale=20):
     """mean_i(-log(exp(s<q_i,d_i>) / sum_j exp(s<q_i,d_j>)) * y_i) (match_losses.py:150-165)."""
     L.require_gpu()
-    return _InBatchCE.apply(query @ doc.t(), y_true.reshape(-1), scale)
+    return _InBatchCE.apply(_InBatchLogits.apply(query, doc), y_true.reshape(-1), scale)
