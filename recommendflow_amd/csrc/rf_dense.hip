@@ -1198,8 +1198,11 @@ constexpr size_t mlp2_lds_bytes() {
 // OS: the output as bf16 (outb) plus, per row and 32-column slice, the (sum, squared deviations from the slice
 // mean) pair of the fp32 values into ostats[row][op0 + slice] (oP pairs per row): the producer side of an LN-folded
 // consumer GEMM (rf_linear_lnfold_*), as gemm_lds_kernel's kEpiStats
-template <int H, bool VEC0, bool OS = false>
-__global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restrict__ x, int64_t M, int K0, int64_t ldx, float eps,
+// CW: layer-1 columns per wave block (128, or 64 with gridDim.y = 2 column halves: the W1 fragments then take 128
+// instead of 256 VGPRs, so two workgroups share a CU and cover each other's load and barrier waits; the two halves
+// recompute layer 0 and LN1 of their 16 rows, which is cheap)
+template <int H, bool VEC0, bool OS = false, int CW = kMlp2Cols>
+__global__ __launch_bounds__(256, CW == 64 ? 2 : 1) void mlp2_small_kernel(const float* __restrict__ x, int64_t M, int K0, int64_t ldx, float eps,
                                                             const float* __restrict__ g0, const float* __restrict__ be0,
                                                             const uint16_t* __restrict__ W0, const float* __restrict__ b0,
                                                             const float* __restrict__ g1, const float* __restrict__ be1,
@@ -1210,7 +1213,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
     constexpr int RS0 = 32 + 8, RSH = H + 8;  // LDS row strides (elements) of the A tiles: 16-byte row pad
     constexpr int TW = H / 64;                // layer-0 column tiles per wave (H / 4 columns)
     constexpr int KS = H / 32;                // layer-1 k steps
-    constexpr int NT = kMlp2Cols / 16;        // layer-1 column tiles per block
+    constexpr int NT = CW / 16;               // layer-1 column tiles per block
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem_raw);
     uint16_t* w0s = xs + kMlp2Rows * RS0;
@@ -1221,7 +1224,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
     float* red = pbe1 + H;  // [2][4 waves][16 rows]
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int64_t r0 = (int64_t)blockIdx.x * kMlp2Rows;
-    const int nblk = (O + kMlp2Cols - 1) / kMlp2Cols;
+    const int nblk = (O + CW - 1) / CW;
     // Issue order: wave 0's LN0 inputs, W0 and the per-column parameters by LDS-DMA, then this wave's first
     // layer-1 block of W1 fragments and bias into registers (16 B per lane per MFMA, from L2): everything is
     // in flight together and lands in about one memory latency (a wave stalls issuing past 63 outstanding
@@ -1258,13 +1261,13 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
             if (be1) dma4(be1 + tid, pbe1 + wave * 64); else pbe1[tid] = 0.f;
         }
     }
-    const int cb0 = wave;  // layer-1 column blocks wave, wave + 4, ...
+    const int cb0 = wave + 4 * (int)blockIdx.y;  // layer-1 column blocks cb0, cb0 + 4 gridDim.y, ...
     bf16x8 wf[NT][KS];
     float bb1[NT];
     auto load_w1 = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-            const int col = min(cb * kMlp2Cols + nt * 16 + lr, O - 1);  // columns past O: never stored
+            const int col = min(cb * CW + nt * 16 + lr, O - 1);  // columns past O: never stored
 #pragma unroll
             for (int kk = 0; kk < KS; ++kk)
                 wf[nt][kk] = *reinterpret_cast<const bf16x8*>(W1 + (int64_t)col * H + kk * 32 + lg * 8);
@@ -1374,7 +1377,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) ha[kk] = *reinterpret_cast<const bf16x8*>(hs + lr * RSH + kk * 32 + lg * 8);
     const bool rows_full = r0 + kMlp2Rows <= M;
-    for (int cb = cb0; cb < nblk; cb += 4) {
+    for (int cb = cb0; cb < nblk; cb += 4 * (int)gridDim.y) {
         if (cb != cb0) {
             load_w1(cb);
         }
@@ -1392,12 +1395,12 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
                 for (int r = 0; r < 4; ++r) c[nt][r] = A(c[nt][r] + bb1[nt]);
         });
         // values first, stores after (see gemm_lds_kernel's epilogue)
-        const int c0 = cb * kMlp2Cols;
+        const int c0 = cb * CW;
         if constexpr (OS) {
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
                 if (c0 + nt * 16 + lr >= O) c[nt] = f4{0.f, 0.f, 0.f, 0.f};
-            if (rows_full && c0 + kMlp2Cols <= O) {  // interior block: unguarded stores (see gemm_lds_kernel's epilogue)
+            if (rows_full && c0 + CW <= O) {  // interior block: unguarded stores (see gemm_lds_kernel's epilogue)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     __bf16* yr = reinterpret_cast<__bf16*>(outb) + (r0 + 4 * lg + r) * ldo + c0 + lr;
@@ -1436,7 +1439,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
             }
             continue;
         }
-        if (rows_full && c0 + kMlp2Cols <= O) {
+        if (rows_full && c0 + CW <= O) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float* yr = out + (r0 + 4 * lg + r) * ldo + c0 + lr;
@@ -1460,6 +1463,23 @@ __global__ __launch_bounds__(256, 1) void mlp2_small_kernel(const float* __restr
 
 }  // namespace
 
+namespace {
+// the mlp2 kernel for (H, VEC0, OS) at 64-column wave blocks, and its grid: two column halves once the output has
+// more than four 64-column blocks (cfg3: O = 512 -> 512 workgroups, two per CU)
+using Mlp2Kern = void (*)(const float*, int64_t, int, int64_t, float, const float*, const float*, const uint16_t*,
+                          const float*, const float*, const float*, const uint16_t*, const float*, int, int, float*, int64_t,
+                          uint16_t*, float*, int, int);
+template <bool OS>
+Mlp2Kern mlp2_pick(int H, bool vec0) {
+    if (H == 256) return vec0 ? mlp2_small_kernel<256, true, OS, 64> : mlp2_small_kernel<256, false, OS, 64>;
+    return vec0 ? mlp2_small_kernel<128, true, OS, 64> : mlp2_small_kernel<128, false, OS, 64>;
+}
+dim3 mlp2_grid(int64_t M, int O) {
+    const int nblk = (O + 63) / 64;
+    return dim3((unsigned)((M + kMlp2Rows - 1) / kMlp2Rows), nblk > 4 ? 2u : 1u);
+}
+}  // namespace
+
 extern "C" int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t ldx, float eps, const float* ln0_gamma,
                                  const float* ln0_beta, const void* W0, const float* b0, int32_t H, const float* ln1_gamma,
                                  const float* ln1_beta, const void* W1, const float* b1, int32_t O, int32_t act, float* out,
@@ -1471,11 +1491,10 @@ extern "C" int rf_mlp2_small_fwd(const float* x, int64_t M, int32_t K0, int64_t 
     if (M == 0) return RF_OK;
     RF_REQUIRE(x && W0 && W1 && out && ln0_gamma && ln0_beta, "rf_mlp2_small_fwd: null pointer");
     RF_REQUIRE(((uintptr_t)W1 & 15) == 0 && ((uintptr_t)W0 & 15) == 0, "rf_mlp2_small_fwd: W0 / W1 must be 16-byte aligned");
-    const dim3 grid((unsigned)((M + kMlp2Rows - 1) / kMlp2Rows));
+    const dim3 grid = mlp2_grid(M, O);
     hipStream_t st = rf_stream(stream);
     const bool vec0 = (K0 & 7) == 0 && (H * K0 * 2) % 1024 == 0;
-    auto kern = H == 256 ? (vec0 ? mlp2_small_kernel<256, true> : mlp2_small_kernel<256, false>)
-                         : (vec0 ? mlp2_small_kernel<128, true> : mlp2_small_kernel<128, false>);
+    auto kern = mlp2_pick<false>(H, vec0);
     const size_t lds = H == 256 ? mlp2_lds_bytes<256>() : mlp2_lds_bytes<128>();
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return rf_set_error(RF_EHIP, "mlp2_small_kernel: %s", hipGetErrorString(e));
@@ -1497,11 +1516,10 @@ extern "C" int rf_mlp2_small_stats_fwd(const float* x, int64_t M, int32_t K0, in
     if (M == 0) return RF_OK;
     RF_REQUIRE(x && W0 && W1 && out_bf16 && stats && ln0_gamma && ln0_beta, "rf_mlp2_small_stats_fwd: null pointer");
     RF_REQUIRE(((uintptr_t)W1 & 15) == 0 && ((uintptr_t)W0 & 15) == 0, "rf_mlp2_small_stats_fwd: W0 / W1 must be 16-byte aligned");
-    const dim3 grid((unsigned)((M + kMlp2Rows - 1) / kMlp2Rows));
+    const dim3 grid = mlp2_grid(M, O);
     hipStream_t st = rf_stream(stream);
     const bool vec0 = (K0 & 7) == 0 && (H * K0 * 2) % 1024 == 0;
-    auto kern = H == 256 ? (vec0 ? mlp2_small_kernel<256, true, true> : mlp2_small_kernel<256, false, true>)
-                         : (vec0 ? mlp2_small_kernel<128, true, true> : mlp2_small_kernel<128, false, true>);
+    auto kern = mlp2_pick<true>(H, vec0);
     const size_t lds = H == 256 ? mlp2_lds_bytes<256>() : mlp2_lds_bytes<128>();
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return rf_set_error(RF_EHIP, "mlp2_small_kernel: %s", hipGetErrorString(e));
