@@ -624,7 +624,34 @@ struct EpiArgs {
     int oP;
     const uint16_t* hw;  // kEpiLnFoldHead: head weight [kHeadN][N] bf16
     float* hpart;        // kEpiLnFoldHead: [M][tiles_n][kHeadN]
+    int* hcnt;           // kEpiLnFoldHead: one counter per row block (zero between launches), or null: separate softmax
+    const float* hb;     // head bias [kHeadN] or null
+    int hact;            // head activation
+    float* hout;         // [M][kHeadN] probabilities, row stride hldo
+    int64_t hldo;
 };
+
+// the head's outputs of one row from its logits: softmax over the kHeadN values, or an elementwise activation
+__device__ __forceinline__ void head_finish(float (&z)[kHeadN], int act, float* __restrict__ y) {
+    if (act == RF_ACT_SOFTMAX) {
+        float m = z[0];
+#pragma unroll
+        for (int h = 1; h < kHeadN; ++h) m = fmaxf(m, z[h]);
+        float s = 0.f;
+#pragma unroll
+        for (int h = 0; h < kHeadN; ++h) {
+            z[h] = expf(z[h] - m);
+            s += z[h];
+        }
+#pragma unroll
+        for (int h = 0; h < kHeadN; ++h) y[h] = z[h] / s;
+    } else {
+        with_act(act, [&](auto A) {
+#pragma unroll
+            for (int h = 0; h < kHeadN; ++h) y[h] = A(z[h]);
+        });
+    }
+}
 
 // Sum over aligned groups of G consecutive lanes (G = 1, 2, 4), the xor-butterfly order (offsets 1, 2) by DPP
 template <int G>
@@ -1023,7 +1050,42 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
 #pragma unroll
                 for (int w = 0; w < WN; ++w) v += hred[(w * BM + rl) * kHeadN + h];
                 const int64_t row = m0 + rl;
-                if (row < M) ea.hpart[(row * tiles_n + n0 / kLdsBN) * kHeadN + h] = v;
+                float* dst = ea.hpart + (row * tiles_n + n0 / kLdsBN) * kHeadN + h;
+                if (row < M) {
+                    if (ea.hcnt) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: L2-served
+                    else *dst = v;
+                }
+            }
+            if (ea.hcnt) {
+                // the row block's last tile to finish finishes the head (MI355X_MICROARCH's hand-off row 1: every
+                // storing wave waits for its sc1 stores, a barrier, ONE agent-scope add per workgroup on the row
+                // block's counter; the workgroup whose add returned tiles_n - 1 reads every tile's partials with sc1
+                // loads, adds them in tile order (as head_softmax_kernel) and resets the counter for the next launch)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                int* s_last = reinterpret_cast<int*>(smem_raw);
+                if (tid == 0) {
+                    const int old = __hip_atomic_fetch_add(ea.hcnt + tile / tiles_n, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_last[0] = old == tiles_n - 1;
+                }
+                __syncthreads();
+                if (s_last[0]) {
+                    if (tid == 0) __hip_atomic_store(ea.hcnt + tile / tiles_n, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (int rl = tid; rl < BM; rl += 256) {
+                        const int64_t row = m0 + rl;
+                        if (row >= M) continue;
+                        float z[kHeadN];
+#pragma unroll
+                        for (int h = 0; h < kHeadN; ++h) {
+                            float v = 0.f;
+                            for (int t = 0; t < tiles_n; ++t)
+                                v += __hip_atomic_load(ea.hpart + (row * tiles_n + t) * kHeadN + h, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                            z[h] = v + (ea.hb ? ea.hb[h] : 0.f);
+                        }
+                        head_finish(z, ea.hact, ea.hout + row * ea.hldo);
+                    }
+                }
             }
         }
     }
@@ -1043,24 +1105,7 @@ __global__ __launch_bounds__(256) void head_softmax_kernel(const float* __restri
         for (int t = 0; t < tiles; ++t) v += hpart[(row * tiles + t) * kHeadN + h];
         z[h] = v + (b ? b[h] : 0.f);
     }
-    if (act == RF_ACT_SOFTMAX) {
-        float m = z[0];
-#pragma unroll
-        for (int h = 1; h < kHeadN; ++h) m = fmaxf(m, z[h]);
-        float s = 0.f;
-#pragma unroll
-        for (int h = 0; h < kHeadN; ++h) {
-            z[h] = expf(z[h] - m);
-            s += z[h];
-        }
-#pragma unroll
-        for (int h = 0; h < kHeadN; ++h) y[row * ldy + h] = z[h] / s;
-    } else {
-        with_act(act, [&](auto A) {
-#pragma unroll
-            for (int h = 0; h < kHeadN; ++h) y[row * ldy + h] = A(z[h]);
-        });
-    }
+    head_finish(z, act, y + row * ldy);
 }
 
 template <int BM>
@@ -1698,8 +1743,16 @@ extern "C" int rf_linear_lnfold_stats_fwd(const void* x, int64_t M, int32_t K, i
                                            "rf_linear_lnfold_stats_fwd");
 }
 
+// ws = the per-tile partial logits [M][tiles][kHeadN] fp32, then one int32 counter per 64-row block (the LAST
+// tile of a row block to finish runs the softmax; the counters must be zero before the first launch on this ws
+// and every launch leaves them zero)
+namespace {
+size_t head_part_bytes(int64_t M, int32_t N) {
+    return (((size_t)std::max<int64_t>(M, 1) * ((N + kLdsBN - 1) / kLdsBN) * kHeadN * sizeof(float)) + 255) & ~(size_t)255;
+}
+}  // namespace
 extern "C" size_t rf_linear_lnfold_head_ws_bytes(int64_t M, int32_t N) {
-    return (size_t)std::max<int64_t>(M, 1) * ((N + kLdsBN - 1) / kLdsBN) * kHeadN * sizeof(float);
+    return head_part_bytes(M, N) + (size_t)((std::max<int64_t>(M, 1) + 63) / 64) * sizeof(int32_t);
 }
 
 extern "C" int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
@@ -1724,9 +1777,22 @@ extern "C" int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, in
     ea.P = 4 * ((K + kLdsBN - 1) / kLdsBN);
     ea.hw = static_cast<const uint16_t*>(head_w);
     ea.hpart = static_cast<float*>(ws);
+    ea.hb = head_b;
+    ea.hact = head_act;
+    ea.hout = out;
+    ea.hldo = ldo;
     hipStream_t st = rf_stream(stream);
+    // the in-kernel finish needs 64-row tiles (one counter per 64 rows) and is the default; RF_HEAD_SEPARATE=1 runs
+    // the softmax as its own launch (A/B)
+    static const bool separate = [] {
+        const char* e = getenv("RF_HEAD_SEPARATE");
+        return e && e[0] == '1';
+    }();
+    const int64_t t128 = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
+    const bool fused = !separate && t128 < 512;  // launch_lds_epi's choice: 64-row tiles below 512 128-row tiles
+    ea.hcnt = fused ? reinterpret_cast<int*>(static_cast<char*>(ws) + head_part_bytes(M, N)) : nullptr;
     const int rc = launch_lds_epi<kEpiLnFoldHead>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, st, "rf_linear_lnfold_head_fwd");
-    if (rc != RF_OK) return rc;
+    if (rc != RF_OK || fused) return rc;
     hipLaunchKernelGGL(head_softmax_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, (const float*)ws,
                        (N + kLdsBN - 1) / kLdsBN, M, head_b, head_act, out, ldo);
     return rf_check_launch("head_softmax_kernel");

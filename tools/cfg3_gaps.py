@@ -1,7 +1,7 @@
 """rocprof target (diagnostics): the cfg3 ESIM forward as the bench runs it (one hipGraph per forward, two
 resident batches alternating), replayed 40 times; `rocprofv3 --kernel-trace` of this run gives every kernel's
 start/end, so tools/trace_gaps.py can split a forward into kernel time and the idle gaps between kernels.
-    python tools/cfg3_gaps.py [--eager] [--serial-mlp] [--gather] [--uniform]
+    python tools/cfg3_gaps.py [--eager] [--serial-mlp] [--gather] [--uniform] [--unfused]
 """
 import os
 import sys
@@ -26,6 +26,7 @@ ha = [synthetic_batch(B, [False] * Ls, seed=99 + i, slot_ids=range(Ls, 2 * Ls), 
 dense = torch.randn(B, 16, device="cuda")
 model.concurrent_input_mlp = "--serial-mlp" not in sys.argv
 model.gather = "--gather" in sys.argv
+model.fused_scorer = "--unfused" not in sys.argv  # A/B: pooled fp32 -> LayerNorm pass -> GEMMs -> head
 if "--eager" in sys.argv:
     run = [lambda p=p: model(hu[p], ha[p], dense) for p in (0, 1)]
 else:
