@@ -888,6 +888,39 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 __builtin_amdgcn_raw_buffer_store_b16((unsigned short)f32_to_bf16_bits(pv[k]), ro, po[k] >> 1, 0, 0);
+            // slice statistics of the previous example's features, here (after the barrier, beside this example's
+            // prefetch and compute) rather than inside the barrier-bounded reduction: the 32 lanes of a half-wave
+            // hold columns wave * 32 .. + 31 of each feature (D <= NTH / 2); one pass around a pivot (the half's
+            // first value): S = sum d + 32 p, M2 = sum d^2 - (sum d)^2 / 32, d = v - p, 8 independent DPP chains
+            static_assert(NTH / 2 >= D && D % 32 == 0, "one 32-column slice per half-wave and feature");
+            const int side = lane >> 5;
+            const bool ok = po[0] != kOff;  // column wave * 32 + (lane & 31) < D
+            float sd[4], sq[4], pvt[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float p0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv[k]), 0));
+                const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv[k]), 32));
+                pvt[k] = side ? p1 : p0;
+                const float d = ok ? pv[k] - pvt[k] : 0.f;
+                sd[k] = d;
+                sq[k] = d * d;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                sd[k] = half32_sum(sd[k]);
+                sq[k] = half32_sum(sq[k]);
+            }
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(ga.ostats + (pe * ga.oP + ga.op0) * 2), 0, 6 * D / 32 * 8,
+                                                              0x00020000);
+            const bool lead = (lane & 31) == 0 && ok;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int sl = ((k < 2 ? (2 * side + k) * D : (4 + k - 2) * D) + wave * 32) / 32;
+                const int off = lead && (k < 2 || side == 0) ? sl * 8 : kOff;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sd[k] + 32.0f * pvt[k]), rs, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaxf(sq[k] - sd[k] * sd[k] * (1.0f / 32.0f), 0.f)),
+                                                      rs, off + 4, 0, 0);
+            }
         } else {
             const auto ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + pe * out_stride + out_off), 0, 6 * D * 4, 0x00020000);
 #pragma unroll
@@ -1021,37 +1054,6 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                 po[2] = ok0 ? (4 * D + n) * 4 : kOff;
                 po[3] = ok0 ? (5 * D + n) * 4 : kOff;
                 pe = e;
-                if constexpr (OB) {
-                    // slice statistics: the 32 lanes of this half-wave hold columns wave * 32 .. + 31 of each feature
-                    // (n0 = 0: D <= NTH / 2); stored now by the half-wave's first lane (4 per example and half)
-                    static_assert(NTH / 2 >= D && D % 32 == 0, "one 32-column slice per half-wave and feature");
-                    const int sl0 = (2 * side * D + wave * 32) / 32, sl1 = ((2 * side + 1) * D + wave * 32) / 32;
-                    const int sl2 = (4 * D + wave * 32) / 32, sl3 = (5 * D + wave * 32) / 32;
-                    const int sls[4] = {sl0, sl1, sl2, sl3};
-                    float* so = ga.ostats + ((int64_t)e * ga.oP + ga.op0) * 2;
-                    // one pass around a pivot (the half's first value): S = sum d + 32 p, M2 = sum d^2 - (sum d)^2 / 32
-                    // with d = v - p; the 8 reductions are independent DPP chains (no LDS round trips)
-                    float sd[4], sq[4], pvt[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const float p0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv[k]), 0));
-                        const float p1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pv[k]), 32));
-                        pvt[k] = side ? p1 : p0;
-                        const float d = ok ? pv[k] - pvt[k] : 0.f;
-                        sd[k] = d;
-                        sq[k] = d * d;
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        sd[k] = half32_sum(sd[k]);
-                        sq[k] = half32_sum(sq[k]);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if ((lane & 31) == 0 && ok && (k < 2 || side == 0))
-                            *reinterpret_cast<float2*>(so + 2 * sls[k]) =
-                                make_float2(sd[k] + 32.0f * pvt[k], fmaxf(sq[k] - sd[k] * sd[k] * (1.0f / 32.0f), 0.f));
-                }
             }
         }
         if constexpr (STAMP) esim_stamp(stp, 5, lane);
