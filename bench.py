@@ -965,6 +965,9 @@ def bench_train(args, specs, multi):
     dout = torch.randn((B, enc.out_width), device="cuda")
     out = torch.empty((B, enc.out_width), device="cuda")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    from recommendflow_amd.backend.optim import SparseAdam
+
+    dense_opt = SparseAdam(enc.table, learning_rate=1e-3)  # the one-launch dense step, timed as a stage
     acc = np.zeros(4)
     for i in range(steps):
         ev[0].record()
@@ -972,13 +975,26 @@ def bench_train(args, specs, multi):
         ev[1].record()
         g = enc.backward(batches[i % 2], dout, out=out)
         ev[2].record()
-        model.sparse_opt.apply(g)
+        dense_opt.apply(g)
         ev[3].record()
+        model.sparse_opt.apply(g)  # deferred: replay of the gradient's rows + their update
+        ev[4].record()
         torch.cuda.synchronize()
-        acc += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3]), 0]
+        acc += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3]), ev[3].elapsed_time(ev[4])]
     acc /= steps
     n_uniq = g.count()
-    from recommendflow_amd.backend.optim import SparseAdam
+    del dense_opt
+    # the r04 schedule for A/B: the whole-table untouched update on a side stream beside the towers
+    split = TrainableDssm(enc, n_user, learning_rate=1e-3, seed=7, deferred_adam=False)
+    for i in range(2):
+        split.step(batches[i % 2], y)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        split.step(batches[i % 2], y)
+    torch.cuda.synchronize()
+    split_ms = (time.perf_counter() - t0) / steps * 1e3
+    del split
 
     lazy = SparseAdam(enc.table, lazy=True)
     for i in range(2):
@@ -1032,7 +1048,12 @@ def bench_train(args, specs, multi):
     adam_bytes = enc.table.numel() * 4 * 6 + enc.table.shape[0] * 4 + n_uniq * (args.dim * 4 + 8)
     res = {"examples_per_s": round(B / step_ms * 1e3, 1), "ms_per_step": round(step_ms, 4), "loss": round(float(loss), 4),
            "sparse_stage_ms": {"fwd": round(acc[0], 4), "bwd_dedup": round(acc[1], 4), "adam_dense": round(acc[2], 4),
-                               "adam_lazy": round(lazy_ms, 4)},
+                               "adam_deferred": round(acc[3], 4), "adam_lazy": round(lazy_ms, 4)},
+           "table_adam": "deferred (SparseAdam(deferred=True): exact dense Keras Adam, a row's missed untouched steps "
+                         "replayed when it is next read; tests/test_train_step_gpu.py::test_deferred_table_adam_equals_dense)",
+           "split_dense_adam": {"examples_per_s": round(B / split_ms * 1e3, 1), "ms_per_step": round(split_ms, 4),
+                                "note": "the same exact step with the whole-table untouched update on a side stream "
+                                        "beside the towers (rf_adam_untouched, the r04 schedule)"},
            "tower_stage_ms": {"fwd_bwd": round(tw[0], 4), "adam": round(tw[1], 4)},
            "tower_fwd_bwd_TFLOPs": round(tower_flops / tw[0] / 1e9, 1),
            "distinct_rows_per_step": n_uniq,
@@ -1046,7 +1067,7 @@ def bench_train(args, specs, multi):
            "config": "cfg2 DSSM train step: 229 slots, 9999972x64 fp32 table (+ m, v), B=4096, towers [1024,512,256] "
                      "BatchNormalization(batch stats)/selu/dropout 0.3 on librf (train_mlp.TrainTower: BN folded into "
                      "the fp32 MFMA forward GEMM, SELU/dropout/BN backward kernels, library GEMMs for dW and dx), "
-                     "cosent_loss (HIP), Keras Adam (dense, exact) on the table, Adam on the towers"}
+                     "cosent_loss (HIP), Keras Adam (dense semantics, exact; deferred per row) on the table, Adam on the towers"}
     del model, enc, batches
     torch.cuda.empty_cache()
     return res

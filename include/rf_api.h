@@ -579,6 +579,20 @@ int rf_adam_untouched(float* table, float* m, float* v, int64_t table_rows, int3
 int rf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
                   const float* uniq_grad, const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1,
                   float beta2, float epsilon, int32_t lazy, void* ws, size_t ws_bytes, void* stream);
+/*
+ * The dense step deferred, exactly: last[r] (int32, one per row) = the step through which row r's var / m / v
+ * are current. rf_adam_replay brings every row of uniq_rows[:n_uniq] (all rows when uniq_rows is NULL) from
+ * last[r] to t_now by applying the untouched-row update of each step s in last[r] + 1 .. t_now with lr_log[s]
+ * (f32, the step's bias-corrected lr, index = step), then sets last[r] = t_set (t_now, or t_now + 1 when the
+ * caller's rf_adam_apply(lazy = 1) for step t_now + 1 follows on the same stream). The same fp32 expressions in
+ * the same order as rf_adam_untouched step by step: bit-identical var / m / v whenever a row is read. The DSSM
+ * train step replays the batch's rows (rf_fused_hash_embed_bwd_plan) before its forward and the gradient's rows
+ * before the touched update; a full replay (materialize) precedes any other read of the table. n_uniq < 0 (the
+ * plan's invalid-batch flag): nothing moves. Same Keras reference as rf_adam_apply.
+ */
+int rf_adam_replay(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                   const int32_t* n_uniq, int64_t uniq_cap, int32_t* last, int32_t t_now, int32_t t_set,
+                   const float* lr_log, float beta1, float beta2, float epsilon, void* stream);
 
 /* ---- two-tower training losses (rf_loss.hip), forward + gradient ---------------- */
 /* Workspace of both loss entry points (bytes). */

@@ -6,6 +6,11 @@ defaults beta_1 = 0.9, beta_2 = 0.999, epsilon = 1e-7. For an Embedding variable
 Adam._resource_apply_sparse to the deduplicated IndexedSlices gradient: m and v decay over the whole
 variable, the scaled gradient is scatter-added, and every row moves (dense semantics). ``lazy=True``
 touches only the rows in the gradient (TF-Addons LazyAdam; deviation D-lazy-adam, opt-in).
+``deferred=True`` keeps the dense semantics but moves an untouched row only when it is next listed: each row
+carries the step it is current through, and rf_adam_replay applies the missed steps' untouched updates (same
+fp32 expressions, same order, each step's own lr) before a forward reads the row or its gradient update runs.
+Every row read is bit-identical to the dense step's; ``materialize()`` brings the whole table current before
+anything else reads it (evaluation, checkpoints, tests).
 
 Dense variables (the towers) take Keras' Adam._resource_apply_dense (TF ResourceApplyAdam) through
 ``KerasAdam`` (rf_adam_dense, one launch per variable).
@@ -23,24 +28,63 @@ class SparseAdam:
     """tf.keras.optimizers.Adam for an fp32 fused embedding table, driven by SparseGrad (rf_adam_apply)."""
 
     def __init__(self, table: torch.Tensor, learning_rate: float = 0.001, beta_1: float = 0.9, beta_2: float = 0.999,
-                 epsilon: float = 1e-7, lazy: bool = False):
+                 epsilon: float = 1e-7, lazy: bool = False, deferred: bool = False):
         if table.dtype != torch.float32 or table.dim() != 2 or not table.is_contiguous():
             raise ValueError("SparseAdam needs a contiguous fp32 [rows, dim] table")
+        if lazy and deferred:
+            raise ValueError("SparseAdam: lazy and deferred are exclusive (deferred keeps the dense semantics)")
         self.table = table
         self.learning_rate, self.beta_1, self.beta_2, self.epsilon = learning_rate, beta_1, beta_2, epsilon
         self.lazy = bool(lazy)
+        self.deferred = bool(deferred)
         self.m = torch.zeros_like(table)
         self.v = torch.zeros_like(table)
         self.iterations = 0
-        wsb = int(L.load().rf_adam_ws_bytes(table.shape[0], int(self.lazy)))
+        wsb = int(L.load().rf_adam_ws_bytes(table.shape[0], int(self.lazy or self.deferred)))
         self._ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=table.device)
+        if self.deferred:
+            self.last = torch.zeros(table.shape[0], dtype=torch.int32, device=table.device)
+            self._lr_host = np.zeros(1, np.float32)  # index = step (entry 0 unused)
+            self._lr_dev = None
+
+    def _lr_at(self, t: int) -> np.float32:
+        f = np.float32
+        tt = f(t)
+        b1p, b2p = np.power(f(self.beta_1), tt), np.power(f(self.beta_2), tt)
+        return f(self.learning_rate) * (np.sqrt(f(1) - b2p) / (f(1) - b1p))
 
     def step_lr(self) -> float:
         """lr_t * sqrt(1 - beta_2^t) / (1 - beta_1^t) in float32, t = iterations + 1 (Keras local_step)."""
-        f = np.float32
-        t = f(self.iterations + 1)
-        b1p, b2p = np.power(f(self.beta_1), t), np.power(f(self.beta_2), t)
-        return float(f(self.learning_rate) * (np.sqrt(f(1) - b2p) / (f(1) - b1p)))
+        return float(self._lr_at(self.iterations + 1))
+
+    def _lr_log(self, t: int) -> torch.Tensor:
+        """Device f32 [>= t + 1]: entry s = step s's lr (the scalar step_lr() computes, element by element)."""
+        if self._lr_dev is None or len(self._lr_host) <= t:
+            n = max(4096, 2 * len(self._lr_host), t + 1)
+            host = np.zeros(n, np.float32)
+            host[: len(self._lr_host)] = self._lr_host
+            for s in range(max(1, len(self._lr_host)), n):
+                host[s] = self._lr_at(s)
+            self._lr_host = host
+            self._lr_dev = torch.from_numpy(host).to(self.table.device)
+        return self._lr_dev
+
+    def _replay(self, rows, n_uniq, cap: int, t_set: int, stream=None):
+        t = self.iterations
+        L.call("rf_adam_replay", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0],
+               self.table.shape[1], L.ptr(rows) if rows is not None else None, L.ptr(n_uniq) if rows is not None else None,
+               cap, L.ptr(self.last), t, t_set, L.ptr(self._lr_log(t)), self.beta_1, self.beta_2, self.epsilon,
+               L.stream_ptr(stream))
+
+    def prepare(self, rows: torch.Tensor, n_uniq: torch.Tensor, cap: int, stream=None):
+        """deferred: bring rows[:n_uniq] current through the last completed step before a forward reads them."""
+        if self.deferred:
+            self._replay(rows, n_uniq, cap, self.iterations, stream)
+
+    def materialize(self, stream=None):
+        """deferred: every row current (the table, m and v then equal the dense step's, bit for bit)."""
+        if self.deferred:
+            self._replay(None, None, 0, self.iterations, stream)
 
     def apply_untouched(self, rows: torch.Tensor, n_uniq: torch.Tensor, cap: int, stream=None):
         """The first half of this iteration's dense step: every row not in rows[:n_uniq] (rf_adam_untouched). The
@@ -57,6 +101,15 @@ class SparseAdam:
         self.iterations += 1
 
     def apply(self, g: SparseGrad, stream=None):
+        if self.deferred:
+            # the gradient's rows current through the last step (a no-op for rows prepare() already moved), marked
+            # current through this one, then their touched update
+            self._replay(g.rows, g.n_uniq, g.cap, self.iterations + 1, stream)
+            L.call("rf_adam_apply", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0],
+                   self.table.shape[1], L.ptr(g.rows), L.ptr(g.grad), L.ptr(g.n_uniq), g.cap, self.step_lr(), self.beta_1,
+                   self.beta_2, self.epsilon, 1, L.ptr(self._ws), self._ws.numel(), L.stream_ptr(stream))
+            self.iterations += 1
+            return
         L.call("rf_adam_apply", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0], self.table.shape[1],
                L.ptr(g.rows), L.ptr(g.grad), L.ptr(g.n_uniq), g.cap, self.step_lr(), self.beta_1, self.beta_2,
                self.epsilon, int(self.lazy), L.ptr(self._ws), self._ws.numel(), L.stream_ptr(stream))

@@ -540,6 +540,169 @@ __global__ __launch_bounds__(1024) void reduce_long_tree_kernel(const uint32_t* 
     }
 }
 
+// Long segments, exact CPU order, streamed (D <= 128): the serial adds are the whole critical path of a Zipf-hot
+// or padding row (a cfg2 padding row has ~57 K positions), so nothing else waits on them. Wave 0 only adds; the
+// other kStreamWaves - 1 waves produce. Producer wave w takes chunks w - 1, w - 1 + NP, ... of Q positions: one
+// index load per lane, then all Q row loads of the chunk in flight at once (lane = KD adjacent columns, one load
+// per position), the mean / max / min transform, a wait for its ring slot to be free, the chunk written column-
+// major into the slot, and the slot's ready mark (release). Wave 0 waits for a slot's mark (acquire), reads 4
+// positions of each of its columns per ds_read_b128, adds them in order and marks the slot consumed. The marks are
+// LDS words at workgroup scope; no block barrier per chunk. Same value per position (pos_value's arithmetic) and
+// the same order as reduce_long_kernel: bit-identical results.
+constexpr int kStreamWaves = 16;
+
+template <int KD>
+__global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
+    const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux, const int32_t* __restrict__ seg,
+    const int32_t* __restrict__ long_list, const int32_t* __restrict__ long_cnt, const int64_t* __restrict__ uniq_rows,
+    const float* __restrict__ table, int D, const float* __restrict__ out, const float* __restrict__ dout,
+    const int32_t* __restrict__ cnt, float* __restrict__ uniq_grad) {
+    constexpr int Q = 64 / KD;       // positions per chunk (Q * KD values per producer lane)
+    constexpr int PS = Q + 4;        // column stride: 16-byte aligned columns, banks spread
+    constexpr int SLOT = 64 * KD * PS;
+    constexpr int R = 8;             // ring slots (KD 1: 139 KB, KD 2: 147 KB of LDS)
+    constexpr int NP = kStreamWaves - 1;
+    __shared__ __attribute__((aligned(16))) float ring[R * SLOT];
+    __shared__ int ready[R];
+    __shared__ int consumed;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nl = *long_cnt;
+    for (int j = blockIdx.x; j < nl; j += gridDim.x) {
+        if (threadIdx.x < R) ready[threadIdx.x] = 0;
+        if (threadIdx.x == 0) consumed = 0;
+        __syncthreads();
+        const int32_t u = long_list[j];
+        const int i0 = seg[u], i1 = seg[u + 1];
+        const int nch = (i1 - i0 + Q - 1) / Q;
+        if (wave == 0) {
+            float acc[KD];
+#pragma unroll
+            for (int k = 0; k < KD; ++k) acc[k] = 0.f;
+            for (int c = 0; c < nch; ++c) {
+                const int sl = c % R;
+                while (__hip_atomic_load(&ready[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != c + 1) {
+                }
+                const float* b = ring + sl * SLOT + lane * KD * PS;
+                const int np = min(Q, i1 - i0 - c * Q);
+                if (np == Q) {
+                    float4 v[Q / 4][KD];
+#pragma unroll
+                    for (int r = 0; r < Q / 4; ++r)
+#pragma unroll
+                        for (int k = 0; k < KD; ++k) v[r][k] = *reinterpret_cast<const float4*>(b + k * PS + 4 * r);
+#pragma unroll
+                    for (int r = 0; r < Q / 4; ++r)
+#pragma unroll
+                        for (int k = 0; k < KD; ++k) {
+                            acc[k] += v[r][k].x;
+                            acc[k] += v[r][k].y;
+                            acc[k] += v[r][k].z;
+                            acc[k] += v[r][k].w;
+                        }
+                } else {
+                    for (int q = 0; q < np; ++q)
+#pragma unroll
+                        for (int k = 0; k < KD; ++k) acc[k] += b[k * PS + q];
+                }
+                if (lane == 0) __hip_atomic_store(&consumed, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int k = 0; k < KD; ++k)
+                if (lane * KD + k < D) uniq_grad[(int64_t)u * D + lane * KD + k] = acc[k];
+        } else {
+            const int64_t row = uniq_rows[u];
+            float tr[KD];
+#pragma unroll
+            for (int k = 0; k < KD; ++k) tr[k] = (table && lane * KD + k < D) ? table[row * D + lane * KD + k] : 0.f;
+            const bool full = lane * KD + KD <= D;  // all KD columns of this lane exist
+            for (int c = wave - 1; c < nch; c += NP) {
+                const int ib = i0 + c * Q;
+                const int np = min(Q, i1 - ib);
+                const uint32_t ms = lane < np ? src[ib + lane] : kZero;
+                const uint32_t ma = lane < np ? aux[ib + lane] : 0u;
+                float v[Q][KD];
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const uint32_t s4 = (uint32_t)__builtin_amdgcn_readlane((int)ms, q);
+                    const float* g = dout + (int64_t)s4 * 4 + lane * KD;
+                    if (s4 == kZero) {
+#pragma unroll
+                        for (int k = 0; k < KD; ++k) v[q][k] = 0.f;
+                    } else if (KD == 2 && full) {
+                        const float2 x = *reinterpret_cast<const float2*>(g);
+                        v[q][0] = x.x;
+                        v[q][KD - 1] = x.y;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < KD; ++k) v[q][k] = lane * KD + k < D ? g[k] : 0.f;
+                    }
+                }
+                // mean / max / min (block-uniform test: any such position in the chunk)
+                const int comb_any = __builtin_amdgcn_readfirstlane(
+                    (int)(__ballot((lane < np) && ((ma >> 24) == RF_COMB_AVG || (ma >> 24) == RF_COMB_MAX ||
+                                                   (ma >> 24) == RF_COMB_MIN)) != 0));
+                if (comb_any) {
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+                        const uint32_t s4 = (uint32_t)__builtin_amdgcn_readlane((int)ms, q);
+                        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)ma, q);
+                        if (s4 == kZero) continue;
+                        const int comb = (int)(a >> 24);
+                        if (comb == RF_COMB_AVG) {
+                            const float L = (float)(a & 0xffffffu);
+#pragma unroll
+                            for (int k = 0; k < KD; ++k) v[q][k] = v[q][k] / L;
+                        } else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) {
+#pragma unroll
+                            for (int k = 0; k < KD; ++k) {
+                                const int64_t e = (int64_t)s4 * 4 + lane * KD + k;
+                                if (lane * KD + k < D)
+                                    v[q][k] = ((tr[k] == out[e] ? 1.f : 0.f) / (float)cnt[e]) * v[q][k];
+                            }
+                        }
+                    }
+                }
+                while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c + 1 - R)
+                    __builtin_amdgcn_s_sleep(1);
+                float* b = ring + (c % R) * SLOT + lane * KD * PS;
+#pragma unroll
+                for (int k = 0; k < KD; ++k)
+#pragma unroll
+                    for (int r = 0; r < Q / 4; ++r)
+                        *reinterpret_cast<float4*>(b + k * PS + 4 * r) =
+                            make_float4(v[4 * r][k], v[4 * r + 1][k], v[4 * r + 2][k], v[4 * r + 3][k]);
+                if (lane == 0) __hip_atomic_store(&ready[c % R], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// exact-order long segments: the streamed kernel for D <= 128 (RF_BWD_LONG_LEGACY=1 keeps the barrier-per-chunk one
+// for A/B), reduce_long_kernel beyond
+bool long_legacy() {
+    static const bool v = [] {
+        const char* e = std::getenv("RF_BWD_LONG_LEGACY");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+template <int TPR>
+void launch_long_exact(int lgrid, hipStream_t st, const uint32_t* src, const uint32_t* aux, const int32_t* seg,
+                       const int32_t* long_list, const int32_t* long_cnt, const int64_t* rows, const float* table, int dim,
+                       const float* out, const float* dout, const int32_t* cnt, float* grad) {
+    if (dim <= 64 && !long_legacy())
+        hipLaunchKernelGGL(reduce_long_stream_kernel<1>, dim3(lgrid), dim3(64 * kStreamWaves), 0, st, src, aux, seg,
+                           long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
+    else if (dim <= 128 && !long_legacy())
+        hipLaunchKernelGGL(reduce_long_stream_kernel<2>, dim3(lgrid), dim3(64 * kStreamWaves), 0, st, src, aux, seg,
+                           long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
+    else
+        hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
+                           rows, table, dim, out, dout, cnt, grad);
+}
+
 // ---- owner-side gradient sum (sharded training) ------------------------------------------------
 __global__ __launch_bounds__(256) void ids_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t range,
                                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
@@ -650,6 +813,51 @@ __global__ __launch_bounds__(256) void adam_untouched_kernel(float* __restrict__
                 reinterpret_cast<float4*>(m)[i] = mv[u];
                 reinterpret_cast<float4*>(v)[i] = vv[u];
             }
+    }
+}
+
+// Deferred dense step (exact): a row's untouched Keras steps l + 1 .. t_now are applied when the row is next
+// listed (before a forward reads it, or before its touched update), one step at a time with that step's lr
+// (lr_log[s]) through adam_elem's untouched branch — the fp32 expressions adam_untouched_kernel would have run
+// step by step, in the same order, so the row's bits are the same. A team of TPR lanes per row (one wave holds a
+// whole team: every lane reads last[r] before lane 0 writes it). uniq_rows == nullptr: every row (materialize).
+template <int TPR>
+__global__ __launch_bounds__(256) void adam_replay_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                                          int64_t table_rows, int D4, const int64_t* __restrict__ uniq_rows,
+                                                          const int32_t* __restrict__ n_uniq_p, int64_t cap,
+                                                          int32_t* __restrict__ last, int t_now, int t_set,
+                                                          const float* __restrict__ lr_log, AdamCoef c) {
+    constexpr int TEAMS = 256 / TPR;
+    const int team = threadIdx.x / TPR, lane = threadIdx.x % TPR;
+    int64_t nu = table_rows;
+    if (uniq_rows) {
+        const int32_t n = *n_uniq_p;
+        if (n < 0) return;  // invalid batch (the plan's error flag): no row moves
+        nu = min<int64_t>(n, cap);
+    }
+    for (int64_t u = (int64_t)blockIdx.x * TEAMS + team; u < nu; u += (int64_t)gridDim.x * TEAMS) {
+        const int64_t r = uniq_rows ? uniq_rows[u] : u;
+        const int l = last[r];
+        if (l < t_now) {
+            for (int j = lane; j < D4; j += TPR) {
+                const int64_t i = r * D4 + j;
+                float4 wv = reinterpret_cast<float4*>(w)[i];
+                float4 mv = reinterpret_cast<float4*>(m)[i];
+                float4 vv = reinterpret_cast<float4*>(v)[i];
+                AdamCoef cs = c;
+                for (int s = l + 1; s <= t_now; ++s) {
+                    cs.lr = lr_log[s];
+                    adam_elem(wv.x, mv.x, vv.x, false, 0.f, cs);
+                    adam_elem(wv.y, mv.y, vv.y, false, 0.f, cs);
+                    adam_elem(wv.z, mv.z, vv.z, false, 0.f, cs);
+                    adam_elem(wv.w, mv.w, vv.w, false, 0.f, cs);
+                }
+                reinterpret_cast<float4*>(w)[i] = wv;
+                reinterpret_cast<float4*>(m)[i] = mv;
+                reinterpret_cast<float4*>(v)[i] = vv;
+            }
+        }
+        if (lane == 0 && l != t_set) last[r] = t_set;
     }
 }
 
@@ -833,8 +1041,8 @@ int embed_bwd_impl(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* 
             hipLaunchKernelGGL(reduce_long_tree_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list,
                                long_cnt, uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
         else
-            hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
-                               uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
+            launch_long_exact<TPR>(lgrid, st, src, aux, seg, long_list, long_cnt, uniq_rows, table, dim, out, dout,
+                                   minmax_count, uniq_grad);
         hipLaunchKernelGGL(reduce_short_kernel<TPR>, dim3(grid), dim3(256), 0, st, src, aux, seg, n_uniq, uniq_cap,
                            uniq_rows, table, dim, out, dout, minmax_count, uniq_grad);
     };
@@ -951,8 +1159,8 @@ extern "C" int rf_segment_sum_rows(const int64_t* ids, const float* vals, int64_
         hipLaunchKernelGGL(reduce_short_kernel<TPR>, dim3(grid), dim3(256), 0, st, src, aux, seg, n_uniq, uniq_cap,
                            uniq_ids, nullptr, dim, nullptr, vals, nullptr, uniq_vals);
         const int lgrid = (int)std::max<int64_t>(1, std::min<int64_t>(n / kLong + 1, 1024));
-        hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
-                           uniq_ids, nullptr, dim, nullptr, vals, nullptr, uniq_vals);
+        launch_long_exact<TPR>(lgrid, st, src, aux, seg, long_list, long_cnt, uniq_ids, nullptr, dim, nullptr, vals,
+                               nullptr, uniq_vals);
     };
     const int d4 = dim / 4;
     if (d4 <= 1) launch(std::integral_constant<int, 1>{});
@@ -1033,6 +1241,40 @@ extern "C" int rf_adam_untouched(float* table, float* m, float* v, int64_t table
     hipLaunchKernelGGL(adam_untouched_kernel<4>, dim3(grid_of(table_rows * (dim / 4), gmax)), dim3(256), 0, st, table, m, v,
                        table_rows * (dim / 4), dim / 4, map, n_uniq, c);
     return rf_check_launch("rf_adam_untouched");
+}
+
+extern "C" int rf_adam_replay(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                              const int32_t* n_uniq, int64_t uniq_cap, int32_t* last, int32_t t_now, int32_t t_set,
+                              const float* lr_log, float beta1, float beta2, float epsilon, void* stream) {
+    RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 31), "rf_adam_replay: table_rows must be in [1, 2^31)");
+    RF_REQUIRE(dim >= 4 && dim % 4 == 0, "rf_adam_replay: dim must be a multiple of 4");
+    RF_REQUIRE(t_now >= 0 && (t_set == t_now || t_set == t_now + 1), "rf_adam_replay: t_set must be t_now or t_now + 1");
+    RF_REQUIRE(table && m && v && last && (t_now == 0 || lr_log), "rf_adam_replay: null pointer");
+    RF_REQUIRE(!uniq_rows || (n_uniq && uniq_cap >= 0), "rf_adam_replay: uniq_rows needs n_uniq and uniq_cap");
+    RF_REQUIRE((((uintptr_t)table | (uintptr_t)m | (uintptr_t)v) & 15) == 0, "rf_adam_replay: buffers must be 16-byte aligned");
+    hipStream_t st = rf_stream(stream);
+    const int64_t nu = uniq_rows ? uniq_cap : table_rows;
+    if (nu == 0) return RF_OK;
+    AdamCoef c;
+    c.lr = 0.f;
+    c.b1 = beta1;
+    c.b2 = beta2;
+    c.omb1 = 1.0f - beta1;
+    c.omb2 = 1.0f - beta2;
+    c.eps = epsilon;
+    const int D4 = dim / 4;
+    auto launch = [&](auto tpr) {
+        constexpr int TPR = decltype(tpr)::value;
+        const int64_t teams = 256 / TPR;
+        hipLaunchKernelGGL(adam_replay_kernel<TPR>, dim3(grid_of((nu + teams - 1) / teams * 256, 256 * 64)), dim3(256), 0, st,
+                           table, m, v, table_rows, D4, uniq_rows, n_uniq, uniq_cap, last, t_now, t_set, lr_log, c);
+    };
+    if (D4 <= 4) launch(std::integral_constant<int, 4>{});
+    else if (D4 <= 8) launch(std::integral_constant<int, 8>{});
+    else if (D4 <= 16) launch(std::integral_constant<int, 16>{});
+    else if (D4 <= 32) launch(std::integral_constant<int, 32>{});
+    else launch(std::integral_constant<int, 64>{});
+    return rf_check_launch("rf_adam_replay");
 }
 
 extern "C" int rf_adam_dense(float* w, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,

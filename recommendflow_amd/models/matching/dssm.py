@@ -64,7 +64,7 @@ class TrainableDssm(torch.nn.Module):
     on the towers (rf_adam_dense), Keras defaults (lr 1e-3, 0.9, 0.999, 1e-7)."""
 
     def __init__(self, encoder: FusedSparseEncoder, n_user_slots: int, units=(1024, 512, 256), dropout=0.3,
-                 learning_rate=1e-3, loss="cosent", lazy_adam=False, seed=0):
+                 learning_rate=1e-3, loss="cosent", lazy_adam=False, seed=0, deferred_adam=None):
         super().__init__()
         from ...backend.blocks.train_mlp import TrainTower
         from ...backend.losses import match_losses
@@ -79,11 +79,20 @@ class TrainableDssm(torch.nn.Module):
         self.ad_tower = TrainTower(self.wa, units, rate=dropout, eps=1e-6, seed=2 * seed + 2, generator=g, device=dev)
         self.loss_fn = {"cosent": match_losses.cosent_loss,
                         "inbatch_ce": match_losses.batch_neg_sample_scaled_multi_class_ce_loss}[loss]
-        self.sparse_opt = SparseAdam(encoder.table, learning_rate=learning_rate, lazy=lazy_adam)
+        if deferred_adam is None:
+            deferred_adam = self.deferred_table_adam and not lazy_adam
+        self.sparse_opt = SparseAdam(encoder.table, learning_rate=learning_rate, lazy=lazy_adam, deferred=deferred_adam)
         self.dense_opt = KerasAdam(list(self.user_tower.parameters()) + list(self.ad_tower.parameters()),
                                    learning_rate=learning_rate)
 
     overlap_table_adam = True  # False: the table's dense Adam runs after the backward in one launch (A/B)
+    # True: the table's dense Adam is deferred per row (SparseAdam(deferred=True): a row's missed untouched steps are
+    # replayed when the row is next read; bit-identical rows, no whole-table pass per step). Default for new models.
+    deferred_table_adam = True
+
+    def materialize(self):
+        """Bring every table row current (deferred Adam) before anything outside step() reads the table."""
+        self.sparse_opt.materialize()
 
     def _side_stream(self):
         s = getattr(self, "_side", None)
@@ -95,6 +104,8 @@ class TrainableDssm(torch.nn.Module):
         from ...backend.blocks.train_mlp import towers_forward
         from ...runtime.train import embed
 
+        if not self.training:
+            self.sparse_opt.materialize()
         x = embed(self.enc, batch)
         if after_embed is not None:
             after_embed()
@@ -118,7 +129,13 @@ class TrainableDssm(torch.nn.Module):
         # single replica, dense (exact Keras) Adam: the table rows NOT in this batch's gradient take their update
         # on a side stream while the towers run (their Keras step needs no gradient); the gradient's rows get
         # theirs after the backward (SparseAdam.apply_untouched / apply_touched == apply, bit for bit)
-        split = dp is None and not self.sparse_opt.lazy and self.overlap_table_adam
+        deferred = self.sparse_opt.deferred
+        split = dp is None and not self.sparse_opt.lazy and not deferred and self.overlap_table_adam
+        if deferred:
+            # the batch's rows current before the forward reads them; the backward's reduce reuses the plan
+            plan = self.enc.backward_plan(batch)
+            self.sparse_opt.prepare(plan.rows, plan.n_uniq, plan.cap)
+            self.enc._plan, self.enc._plan_batch, self.enc._plan_stream = plan, batch, None
 
         def launch_untouched():
             main = torch.cuda.current_stream()

@@ -236,3 +236,37 @@ def test_bwd_tree_reduce_within_bound(O, cuda, dim):
     assert (err <= bound).all(), float((err - bound).max())
     short = L <= 256
     assert np.array_equal(bits(gg[short]), bits(wg[short]))
+
+
+@pytest.mark.parametrize("dim", [4, 40, 64, 128])
+def test_adam_deferred_replay_matches_dense(cuda, dim):
+    """SparseAdam(deferred=True) against the one-launch dense Adam over seven steps whose row sets differ (rows
+    untouched for up to six steps): after prepare() the listed rows equal the dense table's rows; after
+    materialize() table, m and v are bit-identical; an invalid batch (n_uniq < 0) moves nothing."""
+    from recommendflow_amd.backend.encoder.sparse_encoder import SparseGrad
+
+    R = 3000
+    g0 = torch.Generator().manual_seed(dim)
+    base = torch.randn((R, dim), generator=g0).cuda()
+    dense = SparseAdam(base.clone(), learning_rate=0.01)
+    defer = SparseAdam(base.clone(), learning_rate=0.01, deferred=True)
+    for k in range(7):
+        n = [900, 40, 2500, 7, 1200, 300, 2999][k]
+        rows = torch.sort(torch.randperm(R, generator=g0)[:n]).values.cuda()
+        grad = torch.randn((n, dim), generator=g0).cuda()
+        nu = torch.tensor([n], dtype=torch.int32, device="cuda")
+        g = SparseGrad(rows, grad, nu, n)
+        defer.prepare(rows, nu, n)
+        assert torch.equal(defer.table[rows], dense.table[rows])
+        dense.apply(g)
+        defer.apply(g)
+        assert torch.equal(defer.table[rows], dense.table[rows])
+    bad = torch.tensor([-1], dtype=torch.int32, device="cuda")
+    before = defer.table.clone()
+    defer.prepare(rows, bad, n)
+    assert torch.equal(before, defer.table)
+    defer.materialize()
+    torch.cuda.synchronize()
+    for a, b in ((defer.table, dense.table), (defer.m, dense.m), (defer.v, dense.v)):
+        assert np.array_equal(bits(a.cpu().numpy()), bits(b.cpu().numpy()))
+    assert int(defer.last.min()) == defer.iterations == 7

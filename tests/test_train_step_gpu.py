@@ -12,11 +12,12 @@ from recommendflow_amd.runtime.train import embed
 pytestmark = pytest.mark.gpu
 
 
-def _model(loss="cosent", lazy=False):
+def _model(loss="cosent", lazy=False, deferred=None):
     S = 16
     specs = [SlotSpec(f"f{s}", 500, (2022, 2023), ["sum", "avg"][s % 2]) for s in range(S)]
     enc = FusedSparseEncoder(specs, 16, seed=4)
-    return TrainableDssm(enc, 6, units=(64, 32), dropout=0.0, learning_rate=0.01, loss=loss, lazy_adam=lazy, seed=1), S
+    return TrainableDssm(enc, 6, units=(64, 32), dropout=0.0, learning_rate=0.01, loss=loss, lazy_adam=lazy, seed=1,
+                         deferred_adam=deferred), S
 
 
 def test_sparse_grad_through_autograd_matches_oracle(O, cuda):
@@ -107,7 +108,7 @@ def test_overlapped_table_adam_equals_dense(cuda):
     S = 16
     hb = synthetic_batch(128, [s % 4 == 0 for s in range(S)], seed=21, id_max=400).to("cuda")
     y = (torch.arange(128, device="cuda") % 2).float()
-    models = [_model()[0] for _ in range(2)]
+    models = [_model(deferred=False)[0] for _ in range(2)]
     models[1].overlap_table_adam = False
     for _ in range(3):
         for m in models:
@@ -118,3 +119,32 @@ def test_overlapped_table_adam_equals_dense(cuda):
     assert torch.equal(a.sparse_opt.m, b.sparse_opt.m) and torch.equal(a.sparse_opt.v, b.sparse_opt.v)
     for p, q in zip(a.parameters(), b.parameters()):
         assert torch.equal(p, q)
+
+
+def test_deferred_table_adam_equals_dense(cuda):
+    """TrainableDssm's default table Adam (SparseAdam(deferred=True): a row's missed untouched steps are replayed
+    when the row is next read) against the split and the one-launch dense Adam, over batches whose row sets differ
+    (rows skip one or two steps, then are read again): bit-identical losses at every step, and after materialize()
+    bit-identical tables, Adam moments and towers."""
+    S = 16
+    hbs = [synthetic_batch(128, [s % 4 == 0 for s in range(S)], seed=40 + i, id_max=300 + 200 * i).to("cuda")
+           for i in range(3)]
+    y = (torch.arange(128, device="cuda") % 2).float()
+    models = [_model(deferred=d)[0] for d in (False, False, True)]
+    models[1].overlap_table_adam = False
+    assert models[2].sparse_opt.deferred and not models[0].sparse_opt.deferred
+    losses = [[], [], []]
+    for k in (0, 1, 2, 0, 2, 1):
+        for i, m in enumerate(models):
+            losses[i].append(m.step(hbs[k], y).cpu().numpy().view(np.uint32).item())
+    assert losses[0] == losses[1] == losses[2], losses
+    last = models[2].sparse_opt.last
+    assert int((last < models[2].sparse_opt.iterations).sum()) > 0  # some rows are still behind before materialize
+    models[2].materialize()
+    torch.cuda.synchronize()
+    for a in models[:2]:
+        b = models[2]
+        assert torch.equal(a.enc.table, b.enc.table)
+        assert torch.equal(a.sparse_opt.m, b.sparse_opt.m) and torch.equal(a.sparse_opt.v, b.sparse_opt.v)
+        for p, q in zip(a.parameters(), b.parameters()):
+            assert torch.equal(p, q)

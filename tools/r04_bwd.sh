@@ -1,0 +1,26 @@
+#!/bin/bash
+# GPU: streamed exact long-segment reduce — parity (train + sharded GPU tests), train-step A/B vs the
+# barrier-per-chunk kernel (RF_BWD_LONG_LEGACY=1), and the kernel stats of the new one.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$PWD
+OUT=gpurun_out/${TAG:-r04bwd}
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_train_gpu.py tests/test_sharded_gpu.py > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
+tail -2 "$OUT/pytest.log"
+for k in new legacy new legacy; do
+  if [ $k = legacy ]; then export RF_BWD_LONG_LEGACY=1; else unset RF_BWD_LONG_LEGACY; fi
+  timeout -k 10 300 python tools/train_step_probe.py --steps 30 > "$OUT/probe_$k.json" 2>&1 || { tail -5 "$OUT/probe_$k.json"; exit 1; }
+  echo "$k $(tail -1 "$OUT/probe_$k.json" | cut -c1-300)"
+done
+unset RF_BWD_LONG_LEGACY
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o run -- python3 "$ROOT/tools/train_step_probe.py" --steps 8 > "$ROOT/$OUT/prof.log" 2>&1 || { tail -5 "$ROOT/$OUT/prof.log"; exit 1; }
+f=$(find "$ROOT/$OUT/prof" -name "*kernel_stats.csv" | head -1)
+python3 - "$f" <<'PY'
+import csv,sys
+rows=list(csv.DictReader(open(sys.argv[1])))
+tot=sum(float(r['TotalDurationNs']) for r in rows)
+for r in sorted(rows,key=lambda r:-float(r['TotalDurationNs']))[:25]:
+    print(f"{float(r['TotalDurationNs'])/1e6:9.3f} ms {int(r['Calls']):5d} {float(r['AverageNs'])/1e3:9.1f} us {100*float(r['TotalDurationNs'])/tot:5.1f}%  {r['Name'][:100]}")
+PY
