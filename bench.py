@@ -744,7 +744,7 @@ def bench_sharded_sim(args, specs, multi, P):
 def bench_sharded_train(args, enc, batches, out, world):
     """cfg4 training step: forward_train (route, ids/rows all-to-all, pool) ->
     backward (rf_pool_rows_bwd on the requester, reverse all-to-all of (local id, grad) pairs,
-    rf_segment_sum_rows on the owner) -> lazy Keras Adam on the shard (rf_adam_apply, touched rows).
+    rf_segment_sum_rows on the owner) -> Keras Adam on the shard (dense semantics, deferred per row).
     Bit-exact vs the oracle (tests/test_sharded_gpu.py::test_simulated_backward_and_adam)."""
     import torch
     import torch.distributed as dist
@@ -752,7 +752,10 @@ def bench_sharded_train(args, enc, batches, out, world):
     from recommendflow_amd.backend.optim import SparseAdam
 
     B = batches[0].batch
-    opt = SparseAdam(enc.shard, learning_rate=1e-4, lazy=True)
+    # Keras' dense Adam on the shard, deferred per row: the rows this shard serves are replayed current before the
+    # forward reads them (serve_hook), the gradient's rows before their update
+    opt = SparseAdam(enc.shard, learning_rate=1e-4, deferred=True)
+    enc.serve_hook = opt.prepare_ids
     g = torch.Generator(device="cuda").manual_seed(5 + enc.rank)
     dout = torch.randn((B, enc.out_width), generator=g, device="cuda") * 1e-3
     names = ["forward", "backward", "adam"]
@@ -788,11 +791,13 @@ def bench_sharded_train(args, enc, batches, out, world):
     el = float(t.item())
     stage = {n: round(sum(e[k].elapsed_time(e[k + 1]) for e in evs) / steps, 4) for k, n in enumerate(names)}
     n_rows = int(opt.m.shape[0])
+    enc.serve_hook = None
     del opt
     torch.cuda.empty_cache()
     return {"examples_per_s": round(B * enc.nranks * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 4),
             "stage_ms_rank0": stage, "shard_rows": n_rows,
-            "optimizer": "Keras Adam, lazy (touched rows only; DESIGN D-lazy-adam)"}
+            "optimizer": "Keras Adam, dense semantics deferred per row (SparseAdam(deferred=True) + serve_hook; "
+                         "tests/test_sharded_gpu.py::test_sharded_deferred_adam_equals_dense)"}
 
 
 def bench_cascade(args, enc):

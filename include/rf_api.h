@@ -584,7 +584,9 @@ int rf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t 
  * are current. rf_adam_replay brings every row of uniq_rows[:n_uniq] (all rows when uniq_rows is NULL) from
  * last[r] to t_now by applying the untouched-row update of each step s in last[r] + 1 .. t_now with lr_log[s]
  * (f32, the step's bias-corrected lr, index = step), then sets last[r] = t_set (t_now, or t_now + 1 when the
- * caller's rf_adam_apply(lazy = 1) for step t_now + 1 follows on the same stream). The same fp32 expressions in
+ * caller's rf_adam_apply(lazy = 1) for step t_now + 1 follows on the same stream). n_uniq NULL: all uniq_cap
+ * listed rows. A row may be listed more than once (it is replayed once: the first team to swap last[r] owns it);
+ * rows outside [0, table_rows) are skipped. The same fp32 expressions in
  * the same order as rf_adam_untouched step by step: bit-identical var / m / v whenever a row is read. The DSSM
  * train step replays the batch's rows (rf_fused_hash_embed_bwd_plan) before its forward and the gradient's rows
  * before the touched update; a full replay (materialize) precedes any other read of the table. n_uniq < 0 (the

@@ -411,6 +411,8 @@ class ShardedFusedEncoder(torch.nn.Module):
         self.pad_rows = self.ops.hash_rows(self.desc, S, empty)
 
     # -- the three local stages -------------------------------------------------------------------
+    serve_hook = None  # forward_train calls serve_hook(local ids) before serving them from the shard
+
     def _route_device(self, batch: SparseBatch):
         req = self.ops.hash_rows(self.desc, len(self.slots), batch, tail=self.pad_rows)
         if self.dedup:
@@ -567,6 +569,8 @@ def _shard_training_methods():
         batch = self.ops.prepare_batch(batch)
         st, recv_counts = self.route_exchange(batch)
         wanted = self.comm.exchange(st.local, st.counts, recv_counts)
+        if self.serve_hook is not None:  # e.g. SparseAdam(deferred=True).prepare_ids: the rows current before read
+            self.serve_hook(wanted)
         back = self.comm.exchange(self.serve(wanted), recv_counts, st.counts)
         out = self.combine(batch, st, back, out)
         return TrainCtx(batch, st, wanted, recv_counts, back, out)

@@ -72,9 +72,17 @@ class SparseAdam:
     def _replay(self, rows, n_uniq, cap: int, t_set: int, stream=None):
         t = self.iterations
         L.call("rf_adam_replay", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0],
-               self.table.shape[1], L.ptr(rows) if rows is not None else None, L.ptr(n_uniq) if rows is not None else None,
+               self.table.shape[1], L.ptr(rows) if rows is not None else None, L.ptr(n_uniq) if n_uniq is not None else None,
                cap, L.ptr(self.last), t, t_set, L.ptr(self._lr_log(t)), self.beta_1, self.beta_2, self.epsilon,
                L.stream_ptr(stream))
+
+    def prepare_ids(self, ids: torch.Tensor, stream=None):
+        """deferred: prepare() for a plain int64 id list that may repeat ids (the rows a shard serves to every
+        requester; each listed row is replayed once, ids outside the table are skipped)."""
+        if self.deferred and ids.numel():
+            if ids.dtype != torch.int64 or not ids.is_contiguous():
+                ids = ids.to(torch.int64).contiguous()
+            self._replay(ids, None, ids.numel(), self.iterations, stream)
 
     def prepare(self, rows: torch.Tensor, n_uniq: torch.Tensor, cap: int, stream=None):
         """deferred: bring rows[:n_uniq] current through the last completed step before a forward reads them."""

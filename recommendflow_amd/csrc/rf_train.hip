@@ -820,7 +820,9 @@ __global__ __launch_bounds__(256) void adam_untouched_kernel(float* __restrict__
 // listed (before a forward reads it, or before its touched update), one step at a time with that step's lr
 // (lr_log[s]) through adam_elem's untouched branch — the fp32 expressions adam_untouched_kernel would have run
 // step by step, in the same order, so the row's bits are the same. A team of TPR lanes per row (one wave holds a
-// whole team: every lane reads last[r] before lane 0 writes it). uniq_rows == nullptr: every row (materialize).
+// whole team); lane 0 claims the row by swapping last[r] from the value it read to t_set (compare-and-swap), so a
+// row listed twice (the ids several ranks requested from one shard) is replayed once. uniq_rows == nullptr: every
+// row (materialize); n_uniq_p == nullptr: all cap listed rows; rows outside [0, table_rows) are skipped.
 template <int TPR>
 __global__ __launch_bounds__(256) void adam_replay_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                                                           int64_t table_rows, int D4, const int64_t* __restrict__ uniq_rows,
@@ -831,13 +833,25 @@ __global__ __launch_bounds__(256) void adam_replay_kernel(float* __restrict__ w,
     const int team = threadIdx.x / TPR, lane = threadIdx.x % TPR;
     int64_t nu = table_rows;
     if (uniq_rows) {
-        const int32_t n = *n_uniq_p;
+        const int32_t n = n_uniq_p ? *n_uniq_p : 0;
         if (n < 0) return;  // invalid batch (the plan's error flag): no row moves
-        nu = min<int64_t>(n, cap);
+        nu = n_uniq_p ? min<int64_t>(n, cap) : cap;
     }
+    const int base = (threadIdx.x & 63) - lane;  // the team's first lane in the wave
     for (int64_t u = (int64_t)blockIdx.x * TEAMS + team; u < nu; u += (int64_t)gridDim.x * TEAMS) {
         const int64_t r = uniq_rows ? uniq_rows[u] : u;
-        const int l = last[r];
+        if (r < 0 || r >= table_rows) continue;  // team-uniform
+        int l = 0;
+        if (lane == 0) {
+            l = __hip_atomic_load(&last[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (l < t_set) {
+                int e = l;
+                if (!__hip_atomic_compare_exchange_strong(&last[r], &e, t_set, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT))
+                    l = t_set;  // another team holds this row
+            }
+        }
+        l = __shfl(l, base, 64);
         if (l < t_now) {
             for (int j = lane; j < D4; j += TPR) {
                 const int64_t i = r * D4 + j;
@@ -857,7 +871,6 @@ __global__ __launch_bounds__(256) void adam_replay_kernel(float* __restrict__ w,
                 reinterpret_cast<float4*>(v)[i] = vv;
             }
         }
-        if (lane == 0 && l != t_set) last[r] = t_set;
     }
 }
 
@@ -1250,7 +1263,7 @@ extern "C" int rf_adam_replay(float* table, float* m, float* v, int64_t table_ro
     RF_REQUIRE(dim >= 4 && dim % 4 == 0, "rf_adam_replay: dim must be a multiple of 4");
     RF_REQUIRE(t_now >= 0 && (t_set == t_now || t_set == t_now + 1), "rf_adam_replay: t_set must be t_now or t_now + 1");
     RF_REQUIRE(table && m && v && last && (t_now == 0 || lr_log), "rf_adam_replay: null pointer");
-    RF_REQUIRE(!uniq_rows || (n_uniq && uniq_cap >= 0), "rf_adam_replay: uniq_rows needs n_uniq and uniq_cap");
+    RF_REQUIRE(uniq_cap >= 0, "rf_adam_replay: uniq_cap must be >= 0");
     RF_REQUIRE((((uintptr_t)table | (uintptr_t)m | (uintptr_t)v) & 15) == 0, "rf_adam_replay: buffers must be 16-byte aligned");
     hipStream_t st = rf_stream(stream);
     const int64_t nu = uniq_rows ? uniq_cap : table_rows;

@@ -280,3 +280,33 @@ def test_simulated_backward_and_adam(O, cuda, P, mask_padding):
     order = np.argsort(rows)
     O.adam_apply(t, m, v, rows[order], gr[order], O.keras_adam_lr(0.01, 0.9, 0.999, 1), 0.9, 0.999, 1e-7)
     assert np.array_equal(full_table(encs).view(np.uint32), t.view(np.uint32))
+
+
+def test_sharded_deferred_adam_equals_dense(cuda):
+    """The cfg4 training step's optimizer: SparseAdam(deferred=True) on the shard with serve_hook replaying the
+    served rows (ids repeat: the forward_train path serves every request) against the dense Keras Adam on a twin
+    encoder, four steps over batches with different row sets: the pooled outputs of every step and, after
+    materialize(), the shard, m and v bit-identical."""
+    from recommendflow_amd.backend.encoder.sharded_encoder import LocalComm
+    from recommendflow_amd.backend.optim import SparseAdam
+
+    sp = slots(14, seed=31)
+    encs = [ShardedFusedEncoder(sp, 32, 0, 1, comm=LocalComm(), seed=6) for _ in range(2)]
+    dense = SparseAdam(encs[0].shard, learning_rate=0.01)
+    defer = SparseAdam(encs[1].shard, learning_rate=0.01, deferred=True)
+    encs[1].serve_hook = defer.prepare_ids
+    hbs = [synthetic_batch(96, [i % 3 == 0 for i in range(len(sp))], seed=90 + k, id_max=150 + 100 * k).to("cuda")
+           for k in range(3)]
+    g = torch.Generator().manual_seed(3)
+    for k in (0, 1, 2, 0):
+        dout = torch.randn((96, encs[0].out_width), generator=g).cuda()
+        outs = []
+        for e, opt in zip(encs, (dense, defer)):
+            ctx = e.forward_train(hbs[k])
+            outs.append(ctx.out.clone())
+            opt.apply(e.backward(ctx, dout))
+        assert torch.equal(outs[0], outs[1])
+    defer.materialize()
+    torch.cuda.synchronize()
+    for a, b in ((dense.table, defer.table), (dense.m, defer.m), (dense.v, defer.v)):
+        assert np.array_equal(bits(a), bits(b))

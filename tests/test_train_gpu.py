@@ -241,7 +241,8 @@ def test_bwd_tree_reduce_within_bound(O, cuda, dim):
 @pytest.mark.parametrize("dim", [4, 40, 64, 128])
 def test_adam_deferred_replay_matches_dense(cuda, dim):
     """SparseAdam(deferred=True) against the one-launch dense Adam over seven steps whose row sets differ (rows
-    untouched for up to six steps): after prepare() the listed rows equal the dense table's rows; after
+    untouched for up to six steps): after prepare() / prepare_ids() (repeated and out-of-table ids) the listed
+    rows equal the dense table's rows; after
     materialize() table, m and v are bit-identical; an invalid batch (n_uniq < 0) moves nothing."""
     from recommendflow_amd.backend.encoder.sparse_encoder import SparseGrad
 
@@ -256,7 +257,11 @@ def test_adam_deferred_replay_matches_dense(cuda, dim):
         grad = torch.randn((n, dim), generator=g0).cuda()
         nu = torch.tensor([n], dtype=torch.int32, device="cuda")
         g = SparseGrad(rows, grad, nu, n)
-        defer.prepare(rows, nu, n)
+        if k % 2:  # an id list with repeats and out-of-table ids (a shard's served requests): each row replayed once
+            ids = torch.cat([rows, torch.tensor([-1, R, R + 5], device="cuda"), rows.flip(0)])
+            defer.prepare_ids(ids)
+        else:
+            defer.prepare(rows, nu, n)
         assert torch.equal(defer.table[rows], dense.table[rows])
         dense.apply(g)
         defer.apply(g)
