@@ -15,6 +15,7 @@ the moving statistics fold into the weights (no dropout).
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -41,6 +42,41 @@ def _linear_f32(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int, out
     else:
         L.call("rf_linear_fwd", L.ptr(x), L.DT_F32, M, K, x.stride(0), L.ptr(W), N, L.ptr(b), act, L.ptr(out),
                out.stride(0), stream)
+
+
+# Input-layer weight gradient on a side stream (opt-in, overlap_input_wgrad()): the widest GEMM of the backward
+# (G = dpre^T x over the 8704 / 20480-wide tower inputs) is not on the path to the input gradient, so it can run
+# beside what follows it on the main stream — the other tower's backward, the sparse table's reduce and Adam.
+# join_input_wgrad() makes a stream wait for it before anything reads those gradients.
+_WGRAD = {"on": False, "side": {}, "events": []}
+
+
+class overlap_input_wgrad:
+    # off by default: measured slower (cfg2 step 9.56-9.59 vs 9.75-9.78 ms same box, profiles/r04/wgrad_overlap_ab.txt):
+    # the side GEMM slows the BN backward and the sparse reduce it runs beside more than it saves
+    enabled = os.environ.get("RF_WGRAD_OVERLAP", "0") == "1"
+
+    def __enter__(self):
+        _WGRAD["on"] = self.enabled
+        return self
+
+    def __exit__(self, *exc):
+        _WGRAD["on"] = False
+        return False
+
+
+def join_input_wgrad(stream=None):
+    cur = torch.cuda.current_stream() if stream is None else stream
+    for ev in _WGRAD["events"]:
+        cur.wait_event(ev)
+    _WGRAD["events"].clear()
+
+
+def _side_stream(dev) -> torch.cuda.Stream:
+    s = _WGRAD["side"].get(dev)
+    if s is None:
+        s = _WGRAD["side"][dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def _ws(M: int, K: int, device) -> torch.Tensor:
@@ -100,12 +136,28 @@ def _tower_backward(tower: "TrainTower", step: int, x: torch.Tensor, params, out
         db = torch.empty(N, dtype=torch.float32, device=dev)
         L.call("rf_selu_dropout_bwd", L.ptr(dh), dh.stride(0), L.ptr(outs[l]), N, M, N, tower.rate,
                layer_seed(tower.seed, step, l), L.ptr(dpre), N, L.ptr(db), L.ptr(ws), ws.numel(), st)
-        G = torch.mm(dpre.t(), h_in)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
         dW = torch.empty_like(W)
-        L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]), L.ptr(vars_[l]),
-               tower.eps, L.ptr(dW), st)
-        del G
-        dz = torch.mm(dpre, W)  # [M][K] (library GEMM)
+        if l == 0 and _WGRAD["on"]:
+            dz = torch.mm(dpre, W)  # the input gradient's GEMM first, on the main stream
+            main = torch.cuda.current_stream()
+            side = _side_stream(dev)
+            side.wait_stream(main)  # after dz: the weight gradient runs beside the BN backward and what follows
+            with torch.cuda.stream(side):
+                G = torch.mm(dpre.t(), h_in)
+                L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
+                       L.ptr(vars_[l]), tower.eps, L.ptr(dW), L.stream_ptr(side))
+                done = torch.cuda.Event()
+                done.record(side)
+            for t in (dpre, h_in, db, g, be, means[l], vars_[l], dW, W):  # read / written on the side stream
+                t.record_stream(side)
+            _WGRAD["events"].append(done)
+            del G
+        else:
+            G = torch.mm(dpre.t(), h_in)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
+            L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
+                   L.ptr(vars_[l]), tower.eps, L.ptr(dW), st)
+            del G
+            dz = torch.mm(dpre, W)  # [M][K] (library GEMM)
         dx = dx_out if l == 0 else torch.empty((M, K), dtype=torch.float32, device=dev)
         dgamma = torch.empty(K, dtype=torch.float32, device=dev)
         dbeta = torch.empty(K, dtype=torch.float32, device=dev)

@@ -158,15 +158,20 @@ class TrainableDssm(torch.nn.Module):
 
         u, v = self(batch, after_embed=launch_untouched if split else None)
         loss = self.loss_fn(labels, u, v)
-        (loss * dp.loss_scale() if dp is not None else loss).backward()
+        from ...backend.blocks.train_mlp import join_input_wgrad, overlap_input_wgrad
+
+        with overlap_input_wgrad():  # the towers' input-layer weight gradients run beside the sparse reduce / Adam
+            (loss * dp.loss_scale() if dp is not None else loss).backward()
         sg = self.enc.grad
         if dp is not None:
+            join_input_wgrad()
             dp.allreduce_dense(list(self.user_tower.parameters()) + list(self.ad_tower.parameters()))
             sg = dp.allgather_sparse(sg, self.enc.table_rows)
         if split:
             self.sparse_opt.apply_touched(sg)
         else:
             self.sparse_opt.apply(sg)
+        join_input_wgrad()
         self.dense_opt.step()
         if split:  # the next step's lookup reads every row
             torch.cuda.current_stream().wait_stream(self._side_stream())
