@@ -597,6 +597,18 @@ int rf_adam_replay(float* table, float* m, float* v, int64_t table_rows, int32_t
                    const float* lr_log, float beta1, float beta2, float epsilon, void* stream);
 
 /* ---- two-tower training losses (rf_loss.hip), forward + gradient ---------------- */
+/*
+ * The DSSM score ahead of cosent_loss (dssm.py:35-36 K.l2_normalize of both towers, match_losses.py:46 row dot):
+ * score[i] = <a_i / max(|a_i|, eps), b_i / max(|b_i|, eps)> for a, b [batch, n] fp32 (row strides lda / ldb);
+ * norms[2i], norms[2i+1] = |a_i|, |b_i| (unclamped, for the backward). The backward writes
+ * da_i = g ds_i (v_i - s_i u_i) / |a_i| (v_i / eps where |a_i| <= eps) and db likewise, g = *gscale (device
+ * scalar, NULL = 1): the upstream gradient of the loss folded in, so the cosent dscore feeds it directly.
+ */
+int rf_cosine_rows_fwd(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t batch, int32_t n, float eps,
+                       float* score, float* norms, void* stream);
+int rf_cosine_rows_bwd(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t batch, int32_t n, float eps,
+                       const float* score, const float* norms, const float* dscore, const float* gscale, float* da,
+                       int64_t ldda, float* db, int64_t lddb, void* stream);
 /* Workspace of both loss entry points (bytes). */
 size_t rf_loss_ws_bytes(int32_t batch);
 /*

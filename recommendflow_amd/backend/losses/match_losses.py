@@ -57,6 +57,50 @@ class _InBatchCE(torch.autograd.Function):
         return dl * g, None, None
 
 
+class _CosineCosent(torch.autograd.Function):
+    """cosent_loss(y, l2norm(a), l2norm(b)) from the raw tower outputs a, b in 2 + 4 launches: rf_cosine_rows_fwd
+    (both normalisations and the row dot product), rf_cosent_loss (loss and dscore), and one backward launch
+    (rf_cosine_rows_bwd: the normalisations' Jacobians with dscore and the upstream gradient folded in)."""
+
+    @staticmethod
+    def forward(ctx, a, b, label, scale, eps):
+        a, b = a.float(), b.float()
+        if a.stride(1) != 1 or b.stride(1) != 1:
+            a, b = a.contiguous(), b.contiguous()
+        B, N = a.shape
+        s = torch.empty(B, dtype=torch.float32, device=a.device)
+        nrm = torch.empty(2 * B, dtype=torch.float32, device=a.device)
+        L.call("rf_cosine_rows_fwd", L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), B, N, float(eps), L.ptr(s), L.ptr(nrm),
+               L.stream_ptr())
+        label = label.float().contiguous()
+        loss = torch.empty((), dtype=torch.float32, device=a.device)
+        ds = torch.empty_like(s)
+        ws = _ws(B, a.device)
+        L.call("rf_cosent_loss", L.ptr(s), L.ptr(label), B, float(scale), L.ptr(loss), L.ptr(ds), L.ptr(ws), ws.numel(),
+               L.stream_ptr())
+        ctx.save_for_backward(a, b, s, nrm, ds)
+        ctx.eps = float(eps)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, s, nrm, ds = ctx.saved_tensors
+        B, N = a.shape
+        g = g.float().contiguous()
+        da = torch.empty((B, N), dtype=torch.float32, device=a.device)
+        db = torch.empty((B, N), dtype=torch.float32, device=a.device)
+        L.call("rf_cosine_rows_bwd", L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), B, N, ctx.eps, L.ptr(s), L.ptr(nrm),
+               L.ptr(ds), L.ptr(g), L.ptr(da), N, L.ptr(db), N, L.stream_ptr())
+        return da, db, None, None, None
+
+
+def cosine_cosent_loss(y_true, a, b, scale=20, eps=1e-6):
+    """cosent_loss(y_true, normalize(a), normalize(b)) (the DSSM training loss, dssm.py:35-36 + match_losses.py:42-56)
+    on the towers' raw outputs, fused (_CosineCosent)."""
+    L.require_gpu()
+    return _CosineCosent.apply(a, b, y_true.reshape(-1), scale, eps)
+
+
 def cosent_loss(y_true, query, doc, scale=20):
     """logsumexp([0] ++ [scale*(s_i - s_j) : y_i < y_j]), s = <query_i, doc_i> (match_losses.py:42-56)."""
     L.require_gpu()

@@ -178,7 +178,84 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ v,
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// ---- l2-normalised row cosine (the DSSM score ahead of cosent_loss) ------------------------------------------
+// s_i = <a_i / max(|a_i|, eps), b_i / max(|b_i|, eps)>: K.l2_normalize of both towers (dssm.py:35-36) then the
+// row dot product of match_losses.py:46. One wave per row; each lane walks columns lane, lane + 64, ... and the
+// three sums meet in a fixed butterfly (deterministic). nrm[2i], nrm[2i+1] = the unclamped |a_i|, |b_i|.
+__global__ __launch_bounds__(256) void cosine_rows_fwd_kernel(const float* __restrict__ a, int64_t lda,
+                                                              const float* __restrict__ b, int64_t ldb, int B, int N,
+                                                              float eps, float* __restrict__ s, float* __restrict__ nrm) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= B) return;
+    const float* ai = a + (int64_t)i * lda;
+    const float* bi = b + (int64_t)i * ldb;
+    float aa = 0.f, bb = 0.f, ab = 0.f;
+    for (int j = lane; j < N; j += 64) {
+        const float x = ai[j], y = bi[j];
+        aa += x * x;
+        bb += y * y;
+        ab += x * y;
+    }
+    aa = wave_sum(aa);
+    bb = wave_sum(bb);
+    ab = wave_sum(ab);
+    if (lane == 0) {
+        const float ra = sqrtf(aa), rb = sqrtf(bb);
+        s[i] = ab / (fmaxf(ra, eps) * fmaxf(rb, eps));
+        nrm[2 * i] = ra;
+        nrm[2 * i + 1] = rb;
+    }
+}
+
+// d s_i / d a_i = (v_i - s_i u_i) / |a_i| while |a_i| > eps (the normalisation's Jacobian (I - u u^T) / |a|), and
+// v_i / eps where the norm is clamped (u = a / eps is linear in a); likewise for b. da_i = g * ds_i * that, with ds
+// the loss's per-score gradient and g the upstream scalar (*gscale, device) — the cosent backward fused in.
+__global__ __launch_bounds__(256) void cosine_rows_bwd_kernel(const float* __restrict__ a, int64_t lda,
+                                                              const float* __restrict__ b, int64_t ldb, int B, int N,
+                                                              float eps, const float* __restrict__ s,
+                                                              const float* __restrict__ nrm, const float* __restrict__ ds,
+                                                              const float* __restrict__ gscale, float* __restrict__ da,
+                                                              int64_t ldda, float* __restrict__ db, int64_t lddb) {
+    const int lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= B) return;
+    const float ra = nrm[2 * i], rb = nrm[2 * i + 1];
+    const float na = fmaxf(ra, eps), nb = fmaxf(rb, eps);
+    const float si = s[i];
+    const float g = ds[i] * (gscale ? *gscale : 1.f);
+    const bool ca = ra > eps, cb = rb > eps;  // unclamped
+    const float* ai = a + (int64_t)i * lda;
+    const float* bi = b + (int64_t)i * ldb;
+    for (int j = lane; j < N; j += 64) {
+        const float u = ai[j] / na, v = bi[j] / nb;
+        da[(int64_t)i * ldda + j] = g * (ca ? (v - si * u) / na : v / eps);
+        db[(int64_t)i * lddb + j] = g * (cb ? (u - si * v) / nb : u / eps);
+    }
+}
+
 }  // namespace
+
+extern "C" int rf_cosine_rows_fwd(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t batch, int32_t n,
+                                  float eps, float* score, float* norms, void* stream) {
+    RF_REQUIRE(batch >= 0 && n >= 1 && lda >= n && ldb >= n, "rf_cosine_rows_fwd: bad shape");
+    if (batch == 0) return RF_OK;
+    RF_REQUIRE(a && b && score && norms, "rf_cosine_rows_fwd: null pointer");
+    hipLaunchKernelGGL(cosine_rows_fwd_kernel, dim3((batch + 3) / 4), dim3(256), 0, rf_stream(stream), a, lda, b, ldb,
+                       batch, n, eps, score, norms);
+    return rf_check_launch("rf_cosine_rows_fwd");
+}
+
+extern "C" int rf_cosine_rows_bwd(const float* a, int64_t lda, const float* b, int64_t ldb, int32_t batch, int32_t n,
+                                  float eps, const float* score, const float* norms, const float* dscore,
+                                  const float* gscale, float* da, int64_t ldda, float* db, int64_t lddb, void* stream) {
+    RF_REQUIRE(batch >= 0 && n >= 1 && lda >= n && ldb >= n && ldda >= n && lddb >= n, "rf_cosine_rows_bwd: bad shape");
+    if (batch == 0) return RF_OK;
+    RF_REQUIRE(a && b && score && norms && dscore && da && db, "rf_cosine_rows_bwd: null pointer");
+    hipLaunchKernelGGL(cosine_rows_bwd_kernel, dim3((batch + 3) / 4), dim3(256), 0, rf_stream(stream), a, lda, b, ldb,
+                       batch, n, eps, score, norms, dscore, gscale, da, ldda, db, lddb);
+    return rf_check_launch("rf_cosine_rows_bwd");
+}
 
 // tile maxima (ni x nj) | Rp, Cp (nj x B each) | D (B) | row-block sums (ni); also the in-batch CE's row losses
 extern "C" size_t rf_loss_ws_bytes(int32_t batch) {

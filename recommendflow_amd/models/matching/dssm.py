@@ -9,6 +9,7 @@ dtype) on the exact-fp32 MFMA path; the sparse part is one fused encoder launch 
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -79,6 +80,8 @@ class TrainableDssm(torch.nn.Module):
         self.ad_tower = TrainTower(self.wa, units, rate=dropout, eps=1e-6, seed=2 * seed + 2, generator=g, device=dev)
         self.loss_fn = {"cosent": match_losses.cosent_loss,
                         "inbatch_ce": match_losses.batch_neg_sample_scaled_multi_class_ce_loss}[loss]
+        # cosent on the raw tower outputs: normalisation, row dot, loss and their backward in 3 + 4 launches
+        self._fused_loss = match_losses.cosine_cosent_loss if loss == "cosent" else None
         if deferred_adam is None:
             deferred_adam = self.deferred_table_adam and not lazy_adam
         self.sparse_opt = SparseAdam(encoder.table, learning_rate=learning_rate, lazy=lazy_adam, deferred=deferred_adam)
@@ -89,6 +92,7 @@ class TrainableDssm(torch.nn.Module):
     # True: the table's dense Adam is deferred per row (SparseAdam(deferred=True): a row's missed untouched steps are
     # replayed when the row is next read; bit-identical rows, no whole-table pass per step). Default for new models.
     deferred_table_adam = True
+    fused_loss = os.environ.get("RF_FUSED_LOSS", "1") != "0"  # cosent: match_losses.cosine_cosent_loss on the raw tower outputs (False: torch normalize + loss)
 
     def materialize(self):
         """Bring every table row current (deferred Adam) before anything outside step() reads the table."""
@@ -100,7 +104,7 @@ class TrainableDssm(torch.nn.Module):
             s = self._side = torch.cuda.Stream(device=self.enc.table.device)
         return s
 
-    def forward(self, batch: SparseBatch, after_embed=None):
+    def forward(self, batch: SparseBatch, after_embed=None, raw: bool = False):
         from ...backend.blocks.train_mlp import towers_forward
         from ...runtime.train import embed
 
@@ -115,6 +119,8 @@ class TrainableDssm(torch.nn.Module):
             tu, ta = towers_forward(x, [(self.user_tower, 0, self.wu), (self.ad_tower, self.wu, self.wa)])
         else:
             tu, ta = self.user_tower(x[:, : self.wu]), self.ad_tower(x[:, self.wu:])
+        if raw:
+            return tu, ta
         u = torch.nn.functional.normalize(tu, dim=-1, eps=1e-6)
         v = torch.nn.functional.normalize(ta, dim=-1, eps=1e-6)
         return u, v
@@ -156,8 +162,9 @@ class TrainableDssm(torch.nn.Module):
             # towers' backward, the reduce and the touched rows' update (disjoint rows), and the step joins it last
             self.enc._plan, self.enc._plan_batch, self.enc._plan_stream = plan, batch, planned
 
-        u, v = self(batch, after_embed=launch_untouched if split else None)
-        loss = self.loss_fn(labels, u, v)
+        fused = self._fused_loss is not None and self.fused_loss
+        u, v = self(batch, after_embed=launch_untouched if split else None, raw=fused)
+        loss = self._fused_loss(labels, u, v, eps=1e-6) if fused else self.loss_fn(labels, u, v)
         from ...backend.blocks.train_mlp import join_input_wgrad, overlap_input_wgrad
 
         with overlap_input_wgrad():  # the towers' input-layer weight gradients run beside the sparse reduce / Adam

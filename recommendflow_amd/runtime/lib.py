@@ -78,6 +78,9 @@ _SIGS = {
     "rf_adam_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
     "rf_adam_apply": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _i32, _vp,
                                      ctypes.c_size_t, _vp]),
+    "rf_cosine_rows_fwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _f32, _vp, _vp, _vp]),
+    "rf_cosine_rows_bwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                          _i64, _vp]),
     "rf_loss_ws_bytes": (ctypes.c_size_t, [_i32]),
     "rf_cosent_loss": (ctypes.c_int, [_vp, _vp, _i32, _f32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_inbatch_ce_loss": (ctypes.c_int, [_vp, _i64, _vp, _i32, _f32, _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),

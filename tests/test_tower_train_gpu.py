@@ -65,10 +65,12 @@ def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate, off):
         close(t.moving_var[l].cpu().numpy(), 0.99 + 0.01 * cache[l]["var"], rtol=1e-4)
 
 
-def test_two_tower_loss_and_gradients_vs_oracle(O, cuda):
+@pytest.mark.parametrize("fused", [False, True])
+def test_two_tower_loss_and_gradients_vs_oracle(O, cuda, fused):
     """The DSSM training graph on two towers: u, v = l2norm(tower(x)), cosent loss on <u, v> (match_losses.py
-    :42-56); loss and the gradients reaching the towers' inputs and parameters vs float64 at rtol 1e-4."""
-    from recommendflow_amd.backend.losses.match_losses import cosent_loss
+    :42-56); loss and the gradients reaching the towers' inputs and parameters vs float64 at rtol 1e-4. fused: the
+    train step's form (cosine_cosent_loss on the raw tower outputs: rf_cosine_rows_fwd / _bwd around cosent)."""
+    from recommendflow_amd.backend.losses.match_losses import cosent_loss, cosine_cosent_loss
 
     M, ku, ka, units, rate = 256, 320, 448, (96, 48), 0.3
     tu, ta = _tower(ku, units, rate, seed=7), _tower(ka, units, rate, seed=8)
@@ -77,9 +79,12 @@ def test_two_tower_loss_and_gradients_vs_oracle(O, cuda):
     xa = (torch.randn(M, ka, generator=g) * 0.05).cuda().requires_grad_(True)
     y = (torch.arange(M) % 3 == 0).float().cuda()
     su, sa = tu.steps, ta.steps
-    u = torch.nn.functional.normalize(tu(xu), dim=-1, eps=1e-6)
-    v = torch.nn.functional.normalize(ta(xa), dim=-1, eps=1e-6)
-    loss = cosent_loss(y, u, v)
+    if fused:
+        loss = cosine_cosent_loss(y, tu(xu), ta(xa), eps=1e-6)
+    else:
+        u = torch.nn.functional.normalize(tu(xu), dim=-1, eps=1e-6)
+        v = torch.nn.functional.normalize(ta(xa), dim=-1, eps=1e-6)
+        loss = cosent_loss(y, u, v)
     loss.backward()
 
     lu, la = _oracle_layers(tu), _oracle_layers(ta)
@@ -179,3 +184,39 @@ def test_eval_mode_folds_moving_statistics(O, cuda):
                                1e-6)
         h = O.selu(h @ p["W"].T + p["b"])
     close(got, h)
+
+
+def test_cosine_rows_vs_float64(cuda):
+    """rf_cosine_rows_fwd / _bwd: the score and both input gradients vs float64 (rtol 1e-5 / 1e-4), including a
+    zero row (clamped norm: u = a / eps), a row below eps, strided inputs, and the upstream scale folded in."""
+    from recommendflow_amd.runtime import lib as L
+
+    B, N, eps = 37, 200, 1e-6
+    g = torch.Generator().manual_seed(5)
+    base = torch.randn(B, N + 8, generator=g, dtype=torch.float64)
+    base[3] = 0.0
+    base[7] *= 1e-9
+    b64 = torch.randn(B, N, generator=g, dtype=torch.float64)
+    a = base.float().cuda()[:, :N]  # row stride N + 8
+    b = b64.float().cuda()
+    s = torch.empty(B, device="cuda")
+    nrm = torch.empty(2 * B, device="cuda")
+    L.call("rf_cosine_rows_fwd", L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), B, N, eps, L.ptr(s), L.ptr(nrm),
+           L.stream_ptr())
+    A, Bm = a.double().cpu(), b.double().cpu()
+    na = A.norm(dim=1, keepdim=True).clamp_min(eps)
+    nb = Bm.norm(dim=1, keepdim=True).clamp_min(eps)
+    want = ((A / na) * (Bm / nb)).sum(1)
+    np.testing.assert_allclose(s.double().cpu().numpy(), want.numpy(), rtol=1e-5, atol=1e-6)
+    ds = torch.randn(B, generator=g).cuda()
+    gs = torch.tensor(0.25, device="cuda")
+    da = torch.empty(B, N, device="cuda")
+    db = torch.empty(B, N, device="cuda")
+    L.call("rf_cosine_rows_bwd", L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), B, N, eps, L.ptr(s), L.ptr(nrm), L.ptr(ds),
+           L.ptr(gs), L.ptr(da), N, L.ptr(db), N, L.stream_ptr())
+    Ar = A.clone().requires_grad_(True)
+    Br = Bm.clone().requires_grad_(True)
+    sc = ((Ar / Ar.norm(dim=1, keepdim=True).clamp_min(eps)) * (Br / Br.norm(dim=1, keepdim=True).clamp_min(eps))).sum(1)
+    (sc * ds.double().cpu() * 0.25).sum().backward()
+    np.testing.assert_allclose(da.double().cpu().numpy(), Ar.grad.numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(db.double().cpu().numpy(), Br.grad.numpy(), rtol=1e-4, atol=1e-6)
