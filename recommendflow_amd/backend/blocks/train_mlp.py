@@ -79,6 +79,23 @@ def _side_stream(dev) -> torch.cuda.Stream:
     return s
 
 
+# The small layers' backward GEMMs (K, N <= 1024) are host-bound: hipBLASLt's per-call algorithm query costs more
+# host time than their kernels take. RF_SMALL_MM_ROCBLAS=1 routes them to rocBLAS (A/B; the large input-layer
+# GEMMs stay on hipBLASLt).
+_SMALL_MM_ROCBLAS = os.environ.get("RF_SMALL_MM_ROCBLAS", "0") == "1"
+
+
+def _mm(a: torch.Tensor, b: torch.Tensor, small: bool) -> torch.Tensor:
+    if not (small and _SMALL_MM_ROCBLAS):
+        return torch.mm(a, b)
+    prev = torch.backends.cuda.preferred_blas_library()
+    torch.backends.cuda.preferred_blas_library("cublas")
+    try:
+        return torch.mm(a, b)
+    finally:
+        torch.backends.cuda.preferred_blas_library(prev)
+
+
 def _ws(M: int, K: int, device) -> torch.Tensor:
     return torch.empty(max(int(L.load().rf_tower_ws_bytes(M, K)), 4), dtype=torch.uint8, device=device)
 
@@ -153,11 +170,12 @@ def _tower_backward(tower: "TrainTower", step: int, x: torch.Tensor, params, out
             _WGRAD["events"].append(done)
             del G
         else:
-            G = torch.mm(dpre.t(), h_in)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
+            small = K <= 1024 and N <= 1024
+            G = _mm(dpre.t(), h_in, small)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
             L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
                    L.ptr(vars_[l]), tower.eps, L.ptr(dW), st)
             del G
-            dz = torch.mm(dpre, W)  # [M][K] (library GEMM)
+            dz = _mm(dpre, W, small)  # [M][K] (library GEMM)
         dx = dx_out if l == 0 else torch.empty((M, K), dtype=torch.float32, device=dev)
         dgamma = torch.empty(K, dtype=torch.float32, device=dev)
         dbeta = torch.empty(K, dtype=torch.float32, device=dev)

@@ -71,7 +71,7 @@ def test_cosent_kernel(cuda, B):
     loss = _Cosent.apply(st, torch.tensor(y, device="cuda"), 20.0)
     loss.backward()
     want, wds = O.cosent_loss(y, s)
-    assert abs(float(loss) - want) <= 1e-5 * max(1.0, abs(want))
+    assert abs(float(loss.detach()) - want) <= 1e-5 * max(1.0, abs(want))
     np.testing.assert_allclose(st.grad.cpu().numpy(), wds, rtol=1e-4, atol=1e-6)
 
 
