@@ -98,6 +98,10 @@ class TrainableDssm(torch.nn.Module):
         """Bring every table row current (deferred Adam) before anything outside step() reads the table."""
         self.sparse_opt.materialize()
 
+    def state_dict(self, *args, **kwargs):
+        self.materialize()  # a checkpoint holds the dense step's table, m and v
+        return super().state_dict(*args, **kwargs)
+
     def _side_stream(self):
         s = getattr(self, "_side", None)
         if s is None:

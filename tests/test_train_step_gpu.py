@@ -148,3 +148,25 @@ def test_deferred_table_adam_equals_dense(cuda):
         assert torch.equal(a.sparse_opt.m, b.sparse_opt.m) and torch.equal(a.sparse_opt.v, b.sparse_opt.v)
         for p, q in zip(a.parameters(), b.parameters()):
             assert torch.equal(p, q)
+
+
+def test_deferred_adam_eval_forward_reads_current_rows(cuda):
+    """After deferred-Adam training steps, the eval-mode forward (which materializes first) returns the dense
+    model's scores bit for bit, and state_dict() holds the dense step's table."""
+    S = 16
+    hbs = [synthetic_batch(128, [s % 4 == 0 for s in range(S)], seed=60 + i, id_max=300 + 250 * i).to("cuda")
+           for i in range(2)]
+    y = (torch.arange(128, device="cuda") % 2).float()
+    dense, defer = _model(deferred=False)[0], _model(deferred=True)[0]
+    for k in (0, 1, 0):
+        dense.step(hbs[k], y)
+        defer.step(hbs[k], y)
+    dense.eval()
+    defer.eval()
+    with torch.no_grad():
+        for hb in hbs:
+            ud, vd = dense(hb)
+            uf, vf = defer(hb)
+            assert torch.equal(ud, uf) and torch.equal(vd, vf)
+    assert torch.equal(dense.enc.table, defer.enc.table)
+    assert int(defer.sparse_opt.last.min()) == defer.sparse_opt.iterations
