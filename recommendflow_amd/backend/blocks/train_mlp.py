@@ -31,9 +31,19 @@ def layer_seed(base: int, step: int, layer: int) -> int:
     return x
 
 
+# The two wide input layers (K = 8704 / 20480 at cfg2): hipBLASLt's fp32 kernel runs them at 146-151 TF/s against
+# 123-130 for rf_linear_splitk_fwd, so the forward takes the library GEMM with its bias epilogue there
+# (then SELU in place); RF_TOWER_BLASLT_WIDE=0 keeps librf's split-K kernel (A/B).
+_BLASLT_WIDE = os.environ.get("RF_TOWER_BLASLT_WIDE", "1") == "1"
+
+
 def _linear_f32(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int, out: torch.Tensor, stream: int):
     M, K = x.shape
     N = W.shape[0]
+    if _BLASLT_WIDE and K >= 4096 and act == L.ACT["selu"] and out.is_contiguous():
+        torch.addmm(b, x, W.t(), out=out)
+        torch.selu_(out)
+        return
     ws_bytes = int(L.load().rf_linear_splitk_ws_bytes(L.DT_F32, M, K, N))
     if ws_bytes:
         ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device)
