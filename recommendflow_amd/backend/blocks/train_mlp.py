@@ -35,12 +35,13 @@ def layer_seed(base: int, step: int, layer: int) -> int:
 # 123-130 for rf_linear_splitk_fwd, so the forward takes the library GEMM with its bias epilogue there
 # (then SELU in place); RF_TOWER_BLASLT_WIDE=0 keeps librf's split-K kernel (A/B).
 _BLASLT_WIDE = os.environ.get("RF_TOWER_BLASLT_WIDE", "1") == "1"
+_BLASLT_MIN_K = int(os.environ.get("RF_TOWER_BLASLT_MIN_K", "4096"))
 
 
 def _linear_f32(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int, out: torch.Tensor, stream: int):
     M, K = x.shape
     N = W.shape[0]
-    if _BLASLT_WIDE and K >= 4096 and act == L.ACT["selu"] and out.is_contiguous():
+    if _BLASLT_WIDE and K >= _BLASLT_MIN_K and act == L.ACT["selu"] and out.is_contiguous():
         torch.addmm(b, x, W.t(), out=out)
         torch.selu_(out)
         return

@@ -32,6 +32,7 @@ def act_name(activation) -> Optional[str]:
 
 # RF_TOWER_BLASLT_WIDE=0: fp32 layers with K >= 4096 stay on librf's split-K kernel (A/B)
 _BLASLT_WIDE = os.environ.get("RF_TOWER_BLASLT_WIDE", "1") == "1"
+_BLASLT_MIN_K = int(os.environ.get("RF_TOWER_BLASLT_MIN_K", "4096"))
 
 
 class _nullctx:
@@ -83,7 +84,7 @@ class Dense(torch.nn.Module):
         most one 128-tile per CU: rf_linear_splitk_ws_bytes > 0); the partial-sum workspace comes from the
         caching allocator on the launch stream."""
         M, dt = x.shape[0], L.torch_dtype_code(self.dtype)
-        if (_BLASLT_WIDE and self.dtype == torch.float32 and self.in_features >= 4096 and out.is_contiguous()
+        if (_BLASLT_WIDE and self.dtype == torch.float32 and self.in_features >= _BLASLT_MIN_K and out.is_contiguous()
                 and self.activation in (None, "none", "linear", "relu", "selu")):
             # fp32 deep-K layers (the DSSM towers' 8704 / 20480-wide inputs): hipBLASLt's kernel with its bias
             # epilogue runs them at 146-151 TF/s against 123-130 for rf_linear_splitk_fwd (DESIGN §4.4)
