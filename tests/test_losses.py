@@ -92,7 +92,7 @@ def test_inbatch_ce_kernel(cuda, B, K):
     loss.backward()
     P = (q.detach().double() @ d.detach().double().t()).cpu().numpy()
     want, dP = O.inbatch_ce_loss(y.cpu().numpy(), P)
-    assert abs(float(loss) - want) <= 1e-5 * max(1.0, abs(want))
+    assert abs(float(loss.detach()) - want) <= 1e-5 * max(1.0, abs(want))
     np.testing.assert_allclose(q.grad.cpu().numpy(), dP @ d.detach().cpu().numpy(), rtol=1e-4, atol=1e-6)
     # the logits' backward products run on librf (rf_linear_fwd) where the rows allow it: dd = dP^T q
     np.testing.assert_allclose(d.grad.cpu().numpy(), dP.T @ q.detach().cpu().numpy(), rtol=1e-4, atol=1e-6)
