@@ -543,7 +543,7 @@ __global__ __launch_bounds__(1024) void reduce_long_tree_kernel(const uint32_t* 
 // Long segments, exact CPU order, streamed (D <= 128): the serial adds are the whole critical path of a Zipf-hot
 // or padding row (a cfg2 padding row has ~57 K positions), so nothing else waits on them. Wave 0 only adds; the
 // other kStreamWaves - 1 waves produce. Producer wave w takes chunks w - 1, w - 1 + NP, ... of Q positions: one
-// index load per lane, then all Q row loads of the chunk in flight at once (lane = KD adjacent columns, one load
+// index load per lane, then all Q row loads of the chunk in flight at once (lane l = columns l, l + 64, ...; one load
 // per position), the mean / max / min transform, a wait for its ring slot to be free, the chunk written column-
 // major into the slot, and the slot's ready mark (release). Wave 0 waits for a slot's mark (acquire), reads 4
 // positions of each of its columns per ds_read_b128, adds them in order and marks the slot consumed. The marks are
@@ -558,7 +558,8 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
     const float* __restrict__ table, int D, const float* __restrict__ out, const float* __restrict__ dout,
     const int32_t* __restrict__ cnt, float* __restrict__ uniq_grad) {
     constexpr int Q = 64 / KD;       // positions per chunk (Q * KD values per producer lane)
-    constexpr int PS = Q + 4;        // column stride: 16-byte aligned columns, banks spread
+    constexpr int PS = Q + 4;        // column stride: 16-byte aligned, and lane l's column at 4 l (mod 64) banks for
+                                     // 16 lanes (PS = 68 or 36), so each 16-lane pass of a ds_read_b128 is conflict-free
     constexpr int SLOT = 64 * KD * PS;
     constexpr int R = 8;             // ring slots (KD 1: 139 KB, KD 2: 147 KB of LDS)
     constexpr int NP = kStreamWaves - 1;
@@ -582,14 +583,14 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
                 const int sl = c % R;
                 while (__hip_atomic_load(&ready[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != c + 1) {
                 }
-                const float* b = ring + sl * SLOT + lane * KD * PS;
+                const float* b = ring + sl * SLOT + lane * PS;  // this lane's columns c * 64 + lane
                 const int np = min(Q, i1 - i0 - c * Q);
                 if (np == Q) {
                     float4 v[Q / 4][KD];
 #pragma unroll
                     for (int r = 0; r < Q / 4; ++r)
 #pragma unroll
-                        for (int k = 0; k < KD; ++k) v[r][k] = *reinterpret_cast<const float4*>(b + k * PS + 4 * r);
+                        for (int k = 0; k < KD; ++k) v[r][k] = *reinterpret_cast<const float4*>(b + k * 64 * PS + 4 * r);
 #pragma unroll
                     for (int r = 0; r < Q / 4; ++r)
 #pragma unroll
@@ -602,19 +603,18 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
                 } else {
                     for (int q = 0; q < np; ++q)
 #pragma unroll
-                        for (int k = 0; k < KD; ++k) acc[k] += b[k * PS + q];
+                        for (int k = 0; k < KD; ++k) acc[k] += b[k * 64 * PS + q];
                 }
                 if (lane == 0) __hip_atomic_store(&consumed, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
 #pragma unroll
             for (int k = 0; k < KD; ++k)
-                if (lane * KD + k < D) uniq_grad[(int64_t)u * D + lane * KD + k] = acc[k];
+                if (k * 64 + lane < D) uniq_grad[(int64_t)u * D + k * 64 + lane] = acc[k];
         } else {
             const int64_t row = uniq_rows[u];
             float tr[KD];
 #pragma unroll
-            for (int k = 0; k < KD; ++k) tr[k] = (table && lane * KD + k < D) ? table[row * D + lane * KD + k] : 0.f;
-            const bool full = lane * KD + KD <= D;  // all KD columns of this lane exist
+            for (int k = 0; k < KD; ++k) tr[k] = (table && k * 64 + lane < D) ? table[row * D + k * 64 + lane] : 0.f;
             for (int c = wave - 1; c < nch; c += NP) {
                 const int ib = i0 + c * Q;
                 const int np = min(Q, i1 - ib);
@@ -624,17 +624,13 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const uint32_t s4 = (uint32_t)__builtin_amdgcn_readlane((int)ms, q);
-                    const float* g = dout + (int64_t)s4 * 4 + lane * KD;
+                    const float* g = dout + (int64_t)s4 * 4 + lane;
                     if (s4 == kZero) {
 #pragma unroll
                         for (int k = 0; k < KD; ++k) v[q][k] = 0.f;
-                    } else if (KD == 2 && full) {
-                        const float2 x = *reinterpret_cast<const float2*>(g);
-                        v[q][0] = x.x;
-                        v[q][KD - 1] = x.y;
                     } else {
 #pragma unroll
-                        for (int k = 0; k < KD; ++k) v[q][k] = lane * KD + k < D ? g[k] : 0.f;
+                        for (int k = 0; k < KD; ++k) v[q][k] = k * 64 + lane < D ? g[k * 64] : 0.f;
                     }
                 }
                 // mean / max / min (block-uniform test: any such position in the chunk)
@@ -655,8 +651,8 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
                         } else if (comb == RF_COMB_MAX || comb == RF_COMB_MIN) {
 #pragma unroll
                             for (int k = 0; k < KD; ++k) {
-                                const int64_t e = (int64_t)s4 * 4 + lane * KD + k;
-                                if (lane * KD + k < D)
+                                const int64_t e = (int64_t)s4 * 4 + k * 64 + lane;
+                                if (k * 64 + lane < D)
                                     v[q][k] = ((tr[k] == out[e] ? 1.f : 0.f) / (float)cnt[e]) * v[q][k];
                             }
                         }
@@ -664,12 +660,12 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
                 }
                 while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c + 1 - R)
                     __builtin_amdgcn_s_sleep(1);
-                float* b = ring + (c % R) * SLOT + lane * KD * PS;
+                float* b = ring + (c % R) * SLOT + lane * PS;
 #pragma unroll
                 for (int k = 0; k < KD; ++k)
 #pragma unroll
                     for (int r = 0; r < Q / 4; ++r)
-                        *reinterpret_cast<float4*>(b + k * PS + 4 * r) =
+                        *reinterpret_cast<float4*>(b + k * 64 * PS + 4 * r) =
                             make_float4(v[4 * r][k], v[4 * r + 1][k], v[4 * r + 2][k], v[4 * r + 3][k]);
                 if (lane == 0) __hip_atomic_store(&ready[c % R], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
