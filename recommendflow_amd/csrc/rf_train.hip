@@ -615,11 +615,21 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
             float tr[KD];
 #pragma unroll
             for (int k = 0; k < KD; ++k) tr[k] = (table && k * 64 + lane < D) ? table[row * D + k * 64 + lane] : 0.f;
+            // this producer's next chunk's (src, aux) are loaded while the current chunk's rows are in flight, so a
+            // chunk costs one memory round trip (its rows), not two (indices, then rows)
+            auto idx_load = [&](int c, uint32_t& ms, uint32_t& ma) {
+                const int ib = i0 + c * Q;
+                const int np = c < nch ? min(Q, i1 - ib) : 0;
+                ms = lane < np ? src[ib + lane] : kZero;
+                ma = lane < np ? aux[ib + lane] : 0u;
+            };
+            uint32_t ms_next, ma_next;
+            idx_load(wave - 1, ms_next, ma_next);
             for (int c = wave - 1; c < nch; c += NP) {
                 const int ib = i0 + c * Q;
                 const int np = min(Q, i1 - ib);
-                const uint32_t ms = lane < np ? src[ib + lane] : kZero;
-                const uint32_t ma = lane < np ? aux[ib + lane] : 0u;
+                const uint32_t ms = ms_next;
+                const uint32_t ma = ma_next;
                 float v[Q][KD];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
@@ -633,6 +643,7 @@ __global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
                         for (int k = 0; k < KD; ++k) v[q][k] = k * 64 + lane < D ? g[k * 64] : 0.f;
                     }
                 }
+                idx_load(c + NP, ms_next, ma_next);
                 // mean / max / min (block-uniform test: any such position in the chunk)
                 const int comb_any = __builtin_amdgcn_readfirstlane(
                     (int)(__ballot((lane < np) && ((ma >> 24) == RF_COMB_AVG || (ma >> 24) == RF_COMB_MAX ||
