@@ -542,27 +542,27 @@ __global__ __launch_bounds__(1024) void reduce_long_tree_kernel(const uint32_t* 
 
 // Long segments, exact CPU order, streamed (D <= 128): the serial adds are the whole critical path of a Zipf-hot
 // or padding row (a cfg2 padding row has ~57 K positions), so nothing else waits on them. Wave 0 only adds; the
-// other kStreamWaves - 1 waves produce. Producer wave w takes chunks w - 1, w - 1 + NP, ... of Q positions: one
+// other NW - 1 waves produce. Producer wave w takes chunks w - 1, w - 1 + NP, ... of Q positions: one
 // index load per lane, then all Q row loads of the chunk in flight at once (lane l = columns l, l + 64, ...; one load
 // per position), the mean / max / min transform, a wait for its ring slot to be free, the chunk written column-
 // major into the slot, and the slot's ready mark (release). Wave 0 waits for a slot's mark (acquire), reads 4
 // positions of each of its columns per ds_read_b128, adds them in order and marks the slot consumed. The marks are
 // LDS words at workgroup scope; no block barrier per chunk. Same value per position (pos_value's arithmetic) and
 // the same order as reduce_long_kernel: bit-identical results.
-constexpr int kStreamWaves = 16;
-
-template <int KD>
-__global__ __launch_bounds__(64 * kStreamWaves) void reduce_long_stream_kernel(
+// NW waves, Q positions per chunk: <KD 1: 16 waves, Q 64> (15 producers x 64 values), <KD 2: 8 waves, Q 64> (7 producers
+// x 128 values, two waves per SIMD for the registers; RF_BWD_LONG_KD2_NARROW=1: 16 waves, Q 32 for A/B)
+template <int KD, int NW, int Q>
+__global__ __launch_bounds__(64 * NW) void reduce_long_stream_kernel(
     const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ long_list, const int32_t* __restrict__ long_cnt, const int64_t* __restrict__ uniq_rows,
     const float* __restrict__ table, int D, const float* __restrict__ out, const float* __restrict__ dout,
     const int32_t* __restrict__ cnt, float* __restrict__ uniq_grad) {
-    constexpr int Q = 64 / KD;       // positions per chunk (Q * KD values per producer lane)
+    static_assert(Q % 4 == 0 && Q <= 64, "Q: 4 .. 64 positions per chunk");
     constexpr int PS = Q + 4;        // column stride: 16-byte aligned, and lane l's column at 4 l (mod 64) banks for
                                      // 16 lanes (PS = 68 or 36), so each 16-lane pass of a ds_read_b128 is conflict-free
     constexpr int SLOT = 64 * KD * PS;
-    constexpr int R = 8;             // ring slots (KD 1: 139 KB, KD 2: 147 KB of LDS)
-    constexpr int NP = kStreamWaves - 1;
+    constexpr int R = KD * Q <= 64 ? 8 : 4;  // ring slots: 139 KB (KD 1, Q 64), 147 KB (KD 2, Q 32), 139 KB (KD 2, Q 64)
+    constexpr int NP = NW - 1;
     __shared__ __attribute__((aligned(16))) float ring[R * SLOT];
     __shared__ int ready[R];
     __shared__ int consumed;
@@ -695,16 +695,28 @@ bool long_legacy() {
     return v;
 }
 
+bool kd2_narrow() {
+    static const bool v = [] {
+        const char* e = std::getenv("RF_BWD_LONG_KD2_NARROW");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 template <int TPR>
 void launch_long_exact(int lgrid, hipStream_t st, const uint32_t* src, const uint32_t* aux, const int32_t* seg,
                        const int32_t* long_list, const int32_t* long_cnt, const int64_t* rows, const float* table, int dim,
                        const float* out, const float* dout, const int32_t* cnt, float* grad) {
     if (dim <= 64 && !long_legacy())
-        hipLaunchKernelGGL(reduce_long_stream_kernel<1>, dim3(lgrid), dim3(64 * kStreamWaves), 0, st, src, aux, seg,
+        hipLaunchKernelGGL((reduce_long_stream_kernel<1, 16, 64>), dim3(lgrid), dim3(64 * 16), 0, st, src, aux, seg,
                            long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
     else if (dim <= 128 && !long_legacy())
-        hipLaunchKernelGGL(reduce_long_stream_kernel<2>, dim3(lgrid), dim3(64 * kStreamWaves), 0, st, src, aux, seg,
-                           long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
+        if (kd2_narrow())
+            hipLaunchKernelGGL((reduce_long_stream_kernel<2, 16, 32>), dim3(lgrid), dim3(64 * 16), 0, st, src, aux, seg,
+                               long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
+        else
+            hipLaunchKernelGGL((reduce_long_stream_kernel<2, 8, 64>), dim3(lgrid), dim3(64 * 8), 0, st, src, aux, seg,
+                               long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
     else
         hipLaunchKernelGGL(reduce_long_kernel<TPR>, dim3(lgrid), dim3(1024), 0, st, src, aux, seg, long_list, long_cnt,
                            rows, table, dim, out, dout, cnt, grad);
