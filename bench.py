@@ -766,7 +766,7 @@ def bench_sharded_train(args, enc, batches, out, world):
         if ev: ev[1].record()
         sg = enc.backward(ctx, dout)
         if ev: ev[2].record()
-        opt.apply(sg)
+        opt.apply(sg, rows_current=True)  # every gradient row was served, so replayed, this step
         if ev: ev[3].record()
         st["rows"] = sg.cap
 

@@ -595,6 +595,14 @@ int rf_adam_apply(float* table, float* m, float* v, int64_t table_rows, int32_t 
 int rf_adam_replay(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
                    const int32_t* n_uniq, int64_t uniq_cap, int32_t* last, int32_t t_now, int32_t t_set,
                    const float* lr_log, float beta1, float beta2, float epsilon, void* stream);
+/*
+ * The touched half of the deferred step when every listed row is already current through t_set - 1 (the caller
+ * replayed exactly these rows for this step, e.g. the DSSM step's plan rows): rf_adam_apply(lazy = 1) on
+ * uniq_rows[:n_uniq] plus last[r] = t_set, in one pass (no separate marking replay). Rows must be distinct.
+ */
+int rf_adam_apply_current(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,
+                          const float* uniq_grad, const int32_t* n_uniq, int64_t uniq_cap, float lr, float beta1,
+                          float beta2, float epsilon, int32_t* last, int32_t t_set, void* stream);
 
 /* ---- two-tower training losses (rf_loss.hip), forward + gradient ---------------- */
 /*

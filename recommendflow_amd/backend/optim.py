@@ -88,6 +88,7 @@ class SparseAdam:
         """deferred: bring rows[:n_uniq] current through the last completed step before a forward reads them."""
         if self.deferred:
             self._replay(rows, n_uniq, cap, self.iterations, stream)
+            self._prepared = (rows, n_uniq, self.iterations)
 
     def materialize(self, stream=None):
         """deferred: every row current (the table, m and v then equal the dense step's, bit for bit)."""
@@ -108,8 +109,22 @@ class SparseAdam:
                self.epsilon, 1, L.ptr(self._ws), self._ws.numel(), L.stream_ptr(stream))
         self.iterations += 1
 
-    def apply(self, g: SparseGrad, stream=None):
+    def apply(self, g: SparseGrad, stream=None, rows_current: bool = False):
+        """One Keras Adam step with g. rows_current (deferred only): the caller guarantees every row of g was
+        replayed for this step (prepare / prepare_ids), so the marking rides on the touched update."""
         if self.deferred:
+            prep = getattr(self, "_prepared", None)
+            self._prepared = None
+            if (rows_current or (prep is not None and prep[0] is g.rows and prep[1] is g.n_uniq
+                                 and prep[2] == self.iterations)):
+                # every gradient row was replayed for this step (the plan's own rows, or the caller says so): the
+                # touched update marks them in the same pass
+                L.call("rf_adam_apply_current", L.ptr(self.table), L.ptr(self.m), L.ptr(self.v), self.table.shape[0],
+                       self.table.shape[1], L.ptr(g.rows), L.ptr(g.grad), L.ptr(g.n_uniq), g.cap, self.step_lr(),
+                       self.beta_1, self.beta_2, self.epsilon, L.ptr(self.last), self.iterations + 1,
+                       L.stream_ptr(stream))
+                self.iterations += 1
+                return
             # the gradient's rows current through the last step (a no-op for rows prepare() already moved), marked
             # current through this one, then their touched update
             self._replay(g.rows, g.n_uniq, g.cap, self.iterations + 1, stream)

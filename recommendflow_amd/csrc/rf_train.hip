@@ -894,15 +894,18 @@ __global__ __launch_bounds__(256) void adam_replay_kernel(float* __restrict__ w,
 }
 
 // lazy: touched rows only
+// last != nullptr (the deferred step, rows already current): also marks each row current through t_set
 __global__ __launch_bounds__(256) void adam_lazy_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                                                         int D4, const int64_t* __restrict__ uniq_rows,
                                                         const int32_t* __restrict__ n_uniq_p, int64_t cap,
-                                                        const float* __restrict__ grad, AdamCoef c) {
+                                                        const float* __restrict__ grad, AdamCoef c,
+                                                        int32_t* __restrict__ last = nullptr, int t_set = 0) {
     const int64_t nu = min<int64_t>(*n_uniq_p, cap);
     const int64_t n4 = nu * D4;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t u = i / D4;
         const int j = (int)(i - u * D4);
+        if (last && j == 0) last[uniq_rows[u]] = t_set;
         const int64_t e = uniq_rows[u] * D4 + j;
         float4 wv = reinterpret_cast<float4*>(w)[e];
         float4 mv = reinterpret_cast<float4*>(m)[e];
@@ -1231,7 +1234,7 @@ extern "C" int rf_adam_apply(float* table, float* m, float* v, int64_t table_row
     if (lazy) {
         if (uniq_cap > 0)
             hipLaunchKernelGGL(adam_lazy_kernel, dim3(grid_of(uniq_cap * D4)), dim3(256), 0, st, table, m, v, D4, uniq_rows,
-                               n_uniq, uniq_cap, uniq_grad, c);
+                               n_uniq, uniq_cap, uniq_grad, c, (int32_t*)nullptr, 0);
         return rf_check_launch("adam_lazy_kernel");
     }
     auto* map = static_cast<int32_t*>(ws);
@@ -1273,6 +1276,30 @@ extern "C" int rf_adam_untouched(float* table, float* m, float* v, int64_t table
     hipLaunchKernelGGL(adam_untouched_kernel<4>, dim3(grid_of(table_rows * (dim / 4), gmax)), dim3(256), 0, st, table, m, v,
                        table_rows * (dim / 4), dim / 4, map, n_uniq, c);
     return rf_check_launch("rf_adam_untouched");
+}
+
+extern "C" int rf_adam_apply_current(float* table, float* m, float* v, int64_t table_rows, int32_t dim,
+                                     const int64_t* uniq_rows, const float* uniq_grad, const int32_t* n_uniq,
+                                     int64_t uniq_cap, float lr, float beta1, float beta2, float epsilon, int32_t* last,
+                                     int32_t t_set, void* stream) {
+    RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 31), "rf_adam_apply_current: table_rows must be in [1, 2^31)");
+    RF_REQUIRE(dim >= 4 && dim % 4 == 0, "rf_adam_apply_current: dim must be a multiple of 4");
+    RF_REQUIRE(table && m && v && n_uniq && last && uniq_cap >= 0 && (uniq_cap == 0 || (uniq_rows && uniq_grad)),
+               "rf_adam_apply_current: null pointer");
+    RF_REQUIRE((((uintptr_t)table | (uintptr_t)m | (uintptr_t)v | (uintptr_t)uniq_grad) & 15) == 0,
+               "rf_adam_apply_current: buffers must be 16-byte aligned");
+    if (uniq_cap == 0) return RF_OK;
+    AdamCoef c;
+    c.lr = lr;
+    c.b1 = beta1;
+    c.b2 = beta2;
+    c.omb1 = 1.0f - beta1;
+    c.omb2 = 1.0f - beta2;
+    c.eps = epsilon;
+    const int D4 = dim / 4;
+    hipLaunchKernelGGL(adam_lazy_kernel, dim3(grid_of(uniq_cap * D4)), dim3(256), 0, rf_stream(stream), table, m, v, D4,
+                       uniq_rows, n_uniq, uniq_cap, uniq_grad, c, last, t_set);
+    return rf_check_launch("rf_adam_apply_current");
 }
 
 extern "C" int rf_adam_replay(float* table, float* m, float* v, int64_t table_rows, int32_t dim, const int64_t* uniq_rows,

@@ -99,6 +99,8 @@ _SIGS = {
                                                       _vp]),
     "rf_adam_dense": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp]),
     "rf_adam_dense_multi": (_i32, [_vp, _i32, _i64, _f32, _f32, _f32, _f32, _vp]),
+    "rf_adam_apply_current": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp,
+                                             _i32, _vp]),
     "rf_adam_replay": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _vp, _i32, _i32, _vp, _f32, _f32, _f32,
                                       _vp]),
     "rf_adam_untouched": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp,
