@@ -695,6 +695,14 @@ bool long_legacy() {
     return v;
 }
 
+bool kd1_eight() {  // RF_BWD_LONG_KD1_8W=1: D <= 64 with 8 waves (A/B)
+    static const bool v = [] {
+        const char* e = std::getenv("RF_BWD_LONG_KD1_8W");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 bool kd2_narrow() {
     static const bool v = [] {
         const char* e = std::getenv("RF_BWD_LONG_KD2_NARROW");
@@ -708,8 +716,12 @@ void launch_long_exact(int lgrid, hipStream_t st, const uint32_t* src, const uin
                        const int32_t* long_list, const int32_t* long_cnt, const int64_t* rows, const float* table, int dim,
                        const float* out, const float* dout, const int32_t* cnt, float* grad) {
     if (dim <= 64 && !long_legacy())
-        hipLaunchKernelGGL((reduce_long_stream_kernel<1, 16, 64>), dim3(lgrid), dim3(64 * 16), 0, st, src, aux, seg,
-                           long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
+        if (kd1_eight())
+            hipLaunchKernelGGL((reduce_long_stream_kernel<1, 8, 64>), dim3(lgrid), dim3(64 * 8), 0, st, src, aux, seg,
+                               long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
+        else
+            hipLaunchKernelGGL((reduce_long_stream_kernel<1, 16, 64>), dim3(lgrid), dim3(64 * 16), 0, st, src, aux, seg,
+                               long_list, long_cnt, rows, table, dim, out, dout, cnt, grad);
     else if (dim <= 128 && !long_legacy())
         if (kd2_narrow())
             hipLaunchKernelGGL((reduce_long_stream_kernel<2, 16, 32>), dim3(lgrid), dim3(64 * 16), 0, st, src, aux, seg,
