@@ -296,9 +296,11 @@ int rf_linear_lnfold_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const
  *                               BF16 [head_n][N], head_n = 2 (esim.py:53,88 Dense(2, 'softmax')); the per-row
  *                               partial logits of each 128-column tile (fp32, fixed order) go through ws
  *                               (rf_linear_lnfold_head_ws_bytes(M, N) bytes); the last tile of each 64-row block
- *                               to finish adds them in tile order and writes the softmax. ws ends in one counter
- *                               per 64-row block: it must be ZERO before the first call on a ws, and every call
- *                               leaves it zero (reuse the same ws; one stream at a time).
+ *                               to finish adds them in tile order and writes the softmax. ws STARTS with one
+ *                               counter per 64-row block (the partials sit at its far end): the counters must be
+ *                               ZERO before the first call on a ws, and every call leaves them zero. One zeroed ws
+ *                               serves calls of any M <= the M it was sized for, with the same N (one stream at a
+ *                               time).
  */
 int rf_linear_lnfold_stats_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
                                const float* s, const float* t, const float* row_stats, float eps, int32_t act,

@@ -160,8 +160,10 @@ class MLP(torch.nn.Module):
         L.call("rf_linear_lnfold_stats_fwd", L.ptr(xb), M, K0, xb.stride(0), L.ptr(wg0), d0.units, L.ptr(sv0), L.ptr(tv0),
                L.ptr(xstats), n0.eps, act, L.ptr(yb), yb.stride(0), L.ptr(st1), L.stream_ptr(stream))
         wg1, sv1, tv1 = self._ln_folded(1)
-        # the workspace ends in one counter per 64-row block that the launch needs zero and leaves zero (the row
-        # block's last tile runs the softmax): allocated zeroed once and reused (one stream at a time per module)
+        # the workspace starts with one counter per 64-row block that the launch needs zero and leaves zero (the
+        # row block's last tile runs the softmax) and keeps the partial logits at its far end, so one zeroed ws
+        # serves every M up to the one it was sized for (N = d1.units is fixed per module): allocated zeroed when
+        # too small and reused (one stream at a time per module)
         ws_bytes = int(L.load().rf_linear_lnfold_head_ws_bytes(M, d1.units))
         ws = getattr(self, "_head_ws", None)
         if ws is None or ws.numel() < ws_bytes or ws.device != xb.device:

@@ -95,6 +95,24 @@ class SparseAdam:
         if self.deferred:
             self._replay(None, None, 0, self.iterations, stream)
 
+    def state(self) -> dict:
+        """The table, m, v and the step count, every row current (materialize() first): what a checkpoint holds."""
+        self.materialize()
+        return {"table": self.table, "m": self.m, "v": self.v, "iterations": int(self.iterations)}
+
+    def load_state(self, table: torch.Tensor, m: torch.Tensor, v: torch.Tensor, iterations: int, stream=None):
+        """Overwrite the table, m and v in place with a checkpoint's values taken after `iterations` steps. Every row
+        is then current through that step (deferred: `last` is reset, so no missed step is replayed onto the loaded
+        values)."""
+        for dst, src, nm in ((self.table, table, "table"), (self.m, m, "m"), (self.v, v, "v")):
+            if tuple(src.shape) != tuple(dst.shape):
+                raise ValueError(f"SparseAdam.load_state: {nm} shape {tuple(src.shape)} != {tuple(dst.shape)}")
+            dst.copy_(src)
+        self.iterations = int(iterations)
+        self._prepared = None
+        if self.deferred:
+            self.last.fill_(self.iterations)
+
     def apply_untouched(self, rows: torch.Tensor, n_uniq: torch.Tensor, cap: int, stream=None):
         """The first half of this iteration's dense step: every row not in rows[:n_uniq] (rf_adam_untouched). The
         second half is apply_touched() with the gradient over exactly those rows; together they equal apply()."""

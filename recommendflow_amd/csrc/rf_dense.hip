@@ -1065,11 +1065,14 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                 __syncthreads();
                 int* s_last = reinterpret_cast<int*>(smem_raw);
                 if (tid == 0) {
-                    const int old = __hip_atomic_fetch_add(ea.hcnt + tile / tiles_n, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // release: this workgroup's partial stores (ordered before it by the barrier) happen-before the
+                    // add; acquire: the finisher sees every other tile's released partials
+                    const int old = __hip_atomic_fetch_add(ea.hcnt + tile / tiles_n, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
                     s_last[0] = old == tiles_n - 1;
                 }
                 __syncthreads();
                 if (s_last[0]) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread of the finisher, after tid 0's acquire
                     if (tid == 0) __hip_atomic_store(ea.hcnt + tile / tiles_n, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     for (int rl = tid; rl < BM; rl += 256) {
                         const int64_t row = m0 + rl;
@@ -1743,16 +1746,19 @@ extern "C" int rf_linear_lnfold_stats_fwd(const void* x, int64_t M, int32_t K, i
                                            "rf_linear_lnfold_stats_fwd");
 }
 
-// ws = the per-tile partial logits [M][tiles][kHeadN] fp32, then one int32 counter per 64-row block (the LAST
-// tile of a row block to finish runs the softmax; the counters must be zero before the first launch on this ws
-// and every launch leaves them zero)
+// ws = one int32 counter per 64-row block at the START of ws (the LAST tile of a row block to finish runs the
+// softmax; the counters must be zero before the first launch on this ws and every launch leaves them zero), and
+// the per-tile partial logits [M][tiles][kHeadN] fp32 at the END of ws (256-byte aligned down). Counters at a
+// fixed offset and partials at the far end keep one zeroed ws reusable across calls of any M with the same N:
+// a smaller call's partials never land on a larger call's counters (ws_bytes >= counters(M) + partials(M))
 namespace {
 size_t head_part_bytes(int64_t M, int32_t N) {
     return (((size_t)std::max<int64_t>(M, 1) * ((N + kLdsBN - 1) / kLdsBN) * kHeadN * sizeof(float)) + 255) & ~(size_t)255;
 }
 }  // namespace
 extern "C" size_t rf_linear_lnfold_head_ws_bytes(int64_t M, int32_t N) {
-    return head_part_bytes(M, N) + (size_t)((std::max<int64_t>(M, 1) + 63) / 64) * sizeof(int32_t);
+    // counters rounded up to 256 B so that the partials, aligned down from the end, never reach them
+    return head_part_bytes(M, N) + ((((size_t)((std::max<int64_t>(M, 1) + 63) / 64) * sizeof(int32_t)) + 255) & ~(size_t)255);
 }
 
 extern "C" int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, int64_t ldx, const void* Wg, int32_t N,
@@ -1776,7 +1782,8 @@ extern "C" int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, in
     ea.eps = eps;
     ea.P = 4 * ((K + kLdsBN - 1) / kLdsBN);
     ea.hw = static_cast<const uint16_t*>(head_w);
-    ea.hpart = static_cast<float*>(ws);
+    const size_t part_off = (ws_bytes - head_part_bytes(M, N)) & ~(size_t)255;
+    ea.hpart = reinterpret_cast<float*>(static_cast<char*>(ws) + part_off);
     ea.hb = head_b;
     ea.hact = head_act;
     ea.hout = out;
@@ -1790,10 +1797,10 @@ extern "C" int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, in
     }();
     const int64_t t128 = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
     const bool fused = !separate && t128 < 512;  // launch_lds_epi's choice: 64-row tiles below 512 128-row tiles
-    ea.hcnt = fused ? reinterpret_cast<int*>(static_cast<char*>(ws) + head_part_bytes(M, N)) : nullptr;
+    ea.hcnt = fused ? static_cast<int*>(ws) : nullptr;
     const int rc = launch_lds_epi<kEpiLnFoldHead>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, st, "rf_linear_lnfold_head_fwd");
     if (rc != RF_OK || fused) return rc;
-    hipLaunchKernelGGL(head_softmax_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, (const float*)ws,
+    hipLaunchKernelGGL(head_softmax_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, (const float*)ea.hpart,
                        (N + kLdsBN - 1) / kLdsBN, M, head_b, head_act, out, ldo);
     return rf_check_launch("head_softmax_kernel");
 }

@@ -814,7 +814,9 @@ template <int U>
 __global__ __launch_bounds__(256) void adam_untouched_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                                                              int64_t n4, int D4, const int32_t* __restrict__ map,
                                                              const int32_t* __restrict__ n_uniq, AdamCoef c) {
-    if (*n_uniq < 0) return;  // invalid batch (the plan's error flag): no row takes a step
+    // an invalid batch (the plan's error flag, n_uniq < 0) lists no row: its step still counts and every row takes
+    // the untouched update, as adam_dense_kernel and the deferred replay of that step do (one rule for all modes)
+    (void)n_uniq;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; base < n4; base += stride) {
         bool act[U];

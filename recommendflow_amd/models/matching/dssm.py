@@ -98,9 +98,34 @@ class TrainableDssm(torch.nn.Module):
         """Bring every table row current (deferred Adam) before anything outside step() reads the table."""
         self.sparse_opt.materialize()
 
-    def state_dict(self, *args, **kwargs):
-        self.materialize()  # a checkpoint holds the dense step's table, m and v
-        return super().state_dict(*args, **kwargs)
+    def embedding_table(self) -> torch.Tensor:
+        """The fused table with every row current: the accessor for readers outside step() / the eval forward
+        (export, search index builds). enc.table itself may hold rows behind by deferred steps."""
+        self.materialize()
+        return self.enc.table
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        # the fused table is a plain attribute of the encoder, not a parameter: a checkpoint gets it here, with the
+        # table optimizer's m, v and step count, every row current (the dense step's values bit for bit)
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        st = self.sparse_opt.state()
+        for k in ("table", "m", "v"):
+            t = st[k]
+            destination[prefix + "sparse_" + k] = t if keep_vars else t.detach()
+        destination[prefix + "sparse_iterations"] = torch.tensor(st["iterations"], dtype=torch.int64)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        keys = [prefix + "sparse_" + k for k in ("table", "m", "v", "iterations")]
+        present = [k in state_dict for k in keys]
+        if all(present):
+            t, m, v, it = (state_dict[k] for k in keys)
+            # rows loaded are current through the checkpoint's step: the deferred replay starts from there
+            self.sparse_opt.load_state(t, m, v, int(it))
+        elif strict:
+            missing_keys.extend(k for k, p in zip(keys, present) if not p)
+        rest = {k: v for k, v in state_dict.items() if k not in keys}
+        super()._load_from_state_dict(rest, prefix, local_metadata, strict, missing_keys, unexpected_keys, error_msgs)
 
     def _side_stream(self):
         s = getattr(self, "_side", None)

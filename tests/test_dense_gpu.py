@@ -395,3 +395,21 @@ def test_mlp_prenormed_head(O, cuda, M):
     assert err_f <= 2 * err_u + 2e-3, (err_f, err_u, flips_f, flips_u)
     # arg-max: random head weights leave many rows near p = 0.5, where any rounding flips it
     assert flips_f <= max(2 * flips_u, 0.002 * M), (err_f, err_u, flips_f, flips_u)
+
+
+def test_mlp_prenormed_head_varying_batch(cuda):
+    """One module called at M = 4096, then a tail batch M = 300, then 4096 again: the head's workspace
+    keeps its per-64-row counters at a fixed offset and its partial logits at the far end, so the smaller call's
+    partials never land on counters a later call reads. Every row must come out as the full-batch call gives it."""
+    mlp = create_mlp([1024, 512], 0.3, "gelu", LayerNormalization(epsilon=1e-6), in_features=1280, dtype=torch.bfloat16,
+                     seed=9)
+    head = Dense(512, 2, activation="softmax", dtype=torch.bfloat16, seed=31)
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(4096, 1280, generator=g) * 1.5 + 0.3
+    xb = x.to(torch.bfloat16).cuda()
+    xs = torch.from_numpy(_slice_stats(x.numpy()).astype(np.float32)).cuda()
+    full = mlp.forward_prenormed_head(xb, xs, head).clone()
+    for m in (300, 64, 4000, 1):
+        tail = mlp.forward_prenormed_head(xb[:m].contiguous(), xs[:m].contiguous(), head)
+        torch.testing.assert_close(tail, full[:m], rtol=0, atol=1e-6)
+    torch.testing.assert_close(mlp.forward_prenormed_head(xb, xs, head), full, rtol=0, atol=0)

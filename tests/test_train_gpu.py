@@ -275,3 +275,36 @@ def test_adam_deferred_replay_matches_dense(cuda, dim):
     for a, b in ((defer.table, dense.table), (defer.m, dense.m), (defer.v, dense.v)):
         assert np.array_equal(bits(a.cpu().numpy()), bits(b.cpu().numpy()))
     assert int(defer.last.min()) == defer.iterations == 7
+
+
+def test_adam_invalid_batch_same_rule_every_mode(cuda):
+    """one rule for an invalid batch (n_uniq < 0, the backward plan's error flag) in every table-Adam mode:
+    the step counts, no row takes a gradient, every row takes that step's untouched update. The one-launch dense
+    Adam, the split form (untouched rows, then the listed rows) and the deferred form (replayed at materialize) stay
+    bit-identical over valid, invalid, valid steps."""
+    from recommendflow_amd.backend.encoder.sparse_encoder import SparseGrad
+
+    R, dim = 2000, 32
+    g0 = torch.Generator().manual_seed(5)
+    base = torch.randn((R, dim), generator=g0).cuda()
+    dense = SparseAdam(base.clone(), learning_rate=0.01)
+    split = SparseAdam(base.clone(), learning_rate=0.01)
+    defer = SparseAdam(base.clone(), learning_rate=0.01, deferred=True)
+    for k, valid in enumerate((True, False, True)):
+        n = 700
+        rows = torch.sort(torch.randperm(R, generator=g0)[:n]).values.cuda()
+        grad = torch.randn((n, dim), generator=g0).cuda()
+        nu = torch.tensor([n if valid else -4], dtype=torch.int32, device="cuda")
+        g = SparseGrad(rows, grad, nu, n)
+        dense.apply(g)
+        split.apply_untouched(rows, nu, n)
+        split.apply_touched(g)
+        defer.prepare(rows, nu, n)
+        defer.apply(g)
+    defer.materialize()
+    torch.cuda.synchronize()
+    assert dense.iterations == split.iterations == defer.iterations == 3
+    for x in (split, defer):
+        for a, b in ((x.table, dense.table), (x.m, dense.m), (x.v, dense.v)):
+            assert np.array_equal(bits(a.cpu().numpy()), bits(b.cpu().numpy()))
+    assert not torch.equal(dense.table, base)

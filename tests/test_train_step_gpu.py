@@ -170,3 +170,35 @@ def test_deferred_adam_eval_forward_reads_current_rows(cuda):
             assert torch.equal(ud, uf) and torch.equal(vd, vf)
     assert torch.equal(dense.enc.table, defer.enc.table)
     assert int(defer.sparse_opt.last.min()) == defer.sparse_opt.iterations
+
+
+def test_deferred_adam_checkpoint_round_trip(cuda):
+    """state_dict() of a deferred-Adam model carries the fused table, m, v and the step count with every
+    row current (the dense model's values bit for bit), and load_state_dict() into a model with different table
+    contents resets the deferred bookkeeping, so training continues exactly as the dense model does (no missed step
+    is replayed onto the loaded rows)."""
+    S = 16
+    hbs = [synthetic_batch(128, [s % 4 == 0 for s in range(S)], seed=80 + i, id_max=300 + 250 * i).to("cuda")
+           for i in range(2)]
+    y = (torch.arange(128, device="cuda") % 2).float()
+    dense, defer = _model(deferred=False)[0], _model(deferred=True)[0]
+    for k in (0, 1, 0):
+        dense.step(hbs[k], y)
+        defer.step(hbs[k], y)
+    sd = defer.state_dict()
+    assert torch.equal(sd["sparse_table"], dense.enc.table)
+    assert torch.equal(sd["sparse_m"], dense.sparse_opt.m) and torch.equal(sd["sparse_v"], dense.sparse_opt.v)
+    assert int(sd["sparse_iterations"]) == 3
+    sd = {k: v.clone() for k, v in sd.items()}
+    fresh = _model(deferred=True)[0]
+    fresh.step(hbs[1], y)  # one step of its own: rows behind by one, iterations 1
+    fresh.load_state_dict(sd)
+    assert fresh.sparse_opt.iterations == 3 and int(fresh.sparse_opt.last.min()) == 3
+    fresh.dense_opt.m = [m.clone() for m in dense.dense_opt.m]
+    fresh.dense_opt.v = [v.clone() for v in dense.dense_opt.v]
+    fresh.dense_opt.iterations = dense.dense_opt.iterations
+    for k in (1, 0):
+        ld = dense.step(hbs[k], y)
+        lf = fresh.step(hbs[k], y)
+        assert torch.equal(ld, lf)
+    assert torch.equal(fresh.embedding_table(), dense.enc.table)
