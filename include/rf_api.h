@@ -168,6 +168,27 @@ int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int3
                                int64_t out_off, float* att_out, void* stream);
 
 /*
+ * Exact-fp32 GEMM of the DSSM towers, forward and training step (models/matching/dssm.py:25-26 create_mlp(...,
+ * "selu", BatchNormalization) -> backend/blocks/mlp.py:4-15 Dense; its gradients under model.fit,
+ * example/ranking_search/train.py:96-104): C[m][n] = act(sum_k A(m, k) B(k, n) + bias[n]), f32 products and f32
+ * accumulation (v_mfma_f32_16x16x4_f32), every operand layout the towers need:
+ *   a_kc = 1: A(m, k) = A[m lda + k] (k contiguous)      a_kc = 0: A(m, k) = A[k lda + m]
+ *   b_kc = 1: B(k, n) = B[n ldb + k] (k contiguous)      b_kc = 0: B(k, n) = B[k ldb + n]
+ * forward y = x W^T: (a_kc, b_kc) = (1, 1); weight gradient G = dpre^T h: (0, 0); input gradient dz = dpre W: (1, 0).
+ * bias may be NULL; act an elementwise RF_ACT_*. Requirements: K, lda, ldb multiples of 4, A and B 16-byte
+ * aligned, a k-contiguous operand's 128-row block and an m/n-contiguous operand's K + 64 rows below 2 GiB.
+ * Stream-K over one persistent workgroup per CU: a 128 x 128 tile cut between workgroups is summed by the last to
+ * finish in k order, so the result is the same bits every launch. ws: rf_gemm_f32_ws_bytes(M, N, K) bytes; its
+ * first 4 ceil(M / 128) ceil(N / 128) bytes (rounded up to 256) are per-tile counters that must be ZERO before the
+ * first call on a ws; every call leaves them zero. One zeroed ws serves calls of every shape it is large enough for
+ * (the partial tiles sit at its far end); one stream at a time. Replaces the tower Dense's MatMul / BiasAdd / Selu
+ * and the two MatMuls of its gradient.
+ */
+size_t rf_gemm_f32_ws_bytes(int64_t M, int64_t N, int64_t K);
+int rf_gemm_f32(const float* A, int64_t lda, int32_t a_kc, const float* B, int64_t ldb, int32_t b_kc, int64_t M, int64_t N,
+                int64_t K, const float* bias, int32_t act, float* C, int64_t ldc, void* ws, size_t ws_bytes, void* stream);
+
+/*
  * DSSM tower training (models/matching/dssm.py:25-26: create_mlp([1024, 512, 256], 0.3, "selu",
  * BatchNormalization(1e-6)) per tower, trained by model.fit, example/ranking_search/train.py:96-104). All F32.
  * A layer's BatchNormalization in training mode (batch statistics; Keras tf.nn.moments, biased variance) folds

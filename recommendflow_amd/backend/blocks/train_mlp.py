@@ -5,11 +5,11 @@ example/ranking_search/train.py:96-104) on librf.so, replacing torch.nn.BatchNor
 Per layer, forward (training):
   mean, var = rf_col_stats(h)                          batch statistics (Keras tf.nn.moments: biased variance)
   W', b'    = rf_bn_fold(W, b, gamma, beta, mean, var) BatchNormalization folded into the Dense
-  y         = selu(h W'^T + b')                        rf_linear_splitk_fwd / rf_linear_fwd, fp32 MFMA
+  y         = selu(h W'^T + b')                        rf_gemm_f32, exact-fp32 MFMA, bias + SELU in its epilogue
   h_next    = rf_dropout_fwd(y)                        Keras Dropout(rate): kept / (1 - rate), counter-hash mask
 and the moving statistics move as Keras does (moving = moving * momentum + batch * (1 - momentum), momentum
 0.99, the biased batch variance). Backward: rf_selu_dropout_bwd (dpre and the bias gradient), the Dense weight
-gradient G = dpre^T h (library GEMM) through rf_bn_fold_grad, dz = dpre W (library GEMM), rf_bn_bwd. In eval mode
+gradient G = dpre^T h (rf_gemm_f32) through rf_bn_fold_grad, dz = dpre W (rf_gemm_f32), rf_bn_bwd. In eval mode
 the moving statistics fold into the weights (no dropout).
 """
 from __future__ import annotations
@@ -20,7 +20,10 @@ from typing import List, Optional, Sequence
 
 import torch
 
+from ...runtime import gemm as GM
 from ...runtime import lib as L
+
+_ACT_NAME = {0: "none", 1: "gelu", 2: "relu", 3: "selu"}
 
 _SEED_MIX = 0x9E3779B97F4A7C15
 
@@ -31,11 +34,12 @@ def layer_seed(base: int, step: int, layer: int) -> int:
     return x
 
 
-# The two wide input layers (K = 8704 / 20480 at cfg2): hipBLASLt's fp32 kernel runs them at 146-151 TF/s against
-# 123-130 for rf_linear_splitk_fwd, so the forward takes the library GEMM with its bias epilogue there
-# (then SELU in place); RF_TOWER_BLASLT_WIDE=0 keeps librf's split-K kernel (A/B).
-_BLASLT_WIDE = os.environ.get("RF_TOWER_BLASLT_WIDE", "1") == "1"
+# Every GEMM of the towers (forward, weight gradient, input gradient) runs on rf_gemm_f32 (librf: stream-K
+# exact-fp32 MFMA). A/B switches only: RF_TOWER_BLASLT_WIDE=1 sends the forward of layers with K >= 4096 to
+# hipBLASLt (torch.addmm + an in-place SELU); RF_TOWER_BWD_BLAS=1 sends the backward products to torch.mm.
+_BLASLT_WIDE = os.environ.get("RF_TOWER_BLASLT_WIDE", "0") == "1"
 _BLASLT_MIN_K = int(os.environ.get("RF_TOWER_BLASLT_MIN_K", "4096"))
+_BWD_BLAS = os.environ.get("RF_TOWER_BWD_BLAS", "0") == "1"
 
 
 def _linear_f32(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int, out: torch.Tensor, stream: int):
@@ -44,6 +48,9 @@ def _linear_f32(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int, out
     if _BLASLT_WIDE and K >= _BLASLT_MIN_K and act == L.ACT["selu"] and out.is_contiguous():
         torch.addmm(b, x, W.t(), out=out)
         torch.selu_(out)
+        return
+    if GM.supported(x, W, out):
+        GM.gemm_f32(x, W, trans_b=True, bias=b, act=_ACT_NAME[act], out=out, stream=stream)
         return
     ws_bytes = int(L.load().rf_linear_splitk_ws_bytes(L.DT_F32, M, K, N))
     if ws_bytes:
@@ -166,27 +173,36 @@ def _tower_backward(tower: "TrainTower", step: int, x: torch.Tensor, params, out
                layer_seed(tower.seed, step, l), L.ptr(dpre), N, L.ptr(db), L.ptr(ws), ws.numel(), st)
         dW = torch.empty_like(W)
         if l == 0 and _WGRAD["on"]:
-            dz = torch.mm(dpre, W)  # the input gradient's GEMM first, on the main stream
+            # the input gradient's GEMM first, on the main stream
+            dz = GM.gemm_f32(dpre, W, stream=st) if GM.supported(dpre, W) else torch.mm(dpre, W)
             main = torch.cuda.current_stream()
             side = _side_stream(dev)
             side.wait_stream(main)  # after dz: the weight gradient runs beside the BN backward and what follows
             with torch.cuda.stream(side):
-                G = torch.mm(dpre.t(), h_in)
-                L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
+                Gw = GM.gemm_f32(dpre, h_in, trans_a=True, stream=side) if GM.supported(dpre, h_in) \
+                    else torch.mm(dpre.t(), h_in)
+                L.call("rf_bn_fold_grad", L.ptr(Gw), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
                        L.ptr(vars_[l]), tower.eps, L.ptr(dW), L.stream_ptr(side))
                 done = torch.cuda.Event()
                 done.record(side)
             for t in (dpre, h_in, db, g, be, means[l], vars_[l], dW, W):  # read / written on the side stream
                 t.record_stream(side)
             _WGRAD["events"].append(done)
-            del G
-        else:
+            del Gw
+        elif _BWD_BLAS or not GM.supported(dpre, h_in, W):
             small = K <= 1024 and N <= 1024
-            G = _mm(dpre.t(), h_in, small)  # [N][K]: the Dense weight's gradient before the fold (library GEMM)
-            L.call("rf_bn_fold_grad", L.ptr(G), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
+            Gw = _mm(dpre.t(), h_in, small)  # [N][K]: the Dense weight's gradient before the fold (A/B: torch.mm)
+            L.call("rf_bn_fold_grad", L.ptr(Gw), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
                    L.ptr(vars_[l]), tower.eps, L.ptr(dW), st)
-            del G
-            dz = _mm(dpre, W, small)  # [M][K] (library GEMM)
+            del Gw
+            dz = _mm(dpre, W, small)  # [M][K]
+        else:
+            # G = dpre^T h [N][K] (the Dense weight's gradient before the fold) and dz = dpre W [M][K]: rf_gemm_f32
+            Gw = GM.gemm_f32(dpre, h_in, trans_a=True, stream=st)
+            L.call("rf_bn_fold_grad", L.ptr(Gw), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
+                   L.ptr(vars_[l]), tower.eps, L.ptr(dW), st)
+            del Gw
+            dz = GM.gemm_f32(dpre, W, stream=st)
         dx = dx_out if l == 0 else torch.empty((M, K), dtype=torch.float32, device=dev)
         dgamma = torch.empty(K, dtype=torch.float32, device=dev)
         dbeta = torch.empty(K, dtype=torch.float32, device=dev)

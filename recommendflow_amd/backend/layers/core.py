@@ -14,6 +14,7 @@ from typing import Optional
 
 import torch
 
+from ...runtime import gemm as G
 from ...runtime import lib as L
 
 
@@ -30,8 +31,9 @@ def act_name(activation) -> Optional[str]:
 
 
 
-# RF_TOWER_BLASLT_WIDE=0: fp32 layers with K >= 4096 stay on librf's split-K kernel (A/B)
-_BLASLT_WIDE = os.environ.get("RF_TOWER_BLASLT_WIDE", "1") == "1"
+# fp32 layers run on rf_gemm_f32 (librf). RF_TOWER_BLASLT_WIDE=1 is an A/B switch only: fp32 layers with K >= 4096
+# then take hipBLASLt (torch.addmm) instead
+_BLASLT_WIDE = os.environ.get("RF_TOWER_BLASLT_WIDE", "0") == "1"
 _BLASLT_MIN_K = int(os.environ.get("RF_TOWER_BLASLT_MIN_K", "4096"))
 
 
@@ -84,8 +86,14 @@ class Dense(torch.nn.Module):
         most one 128-tile per CU: rf_linear_splitk_ws_bytes > 0); the partial-sum workspace comes from the
         caching allocator on the launch stream."""
         M, dt = x.shape[0], L.torch_dtype_code(self.dtype)
-        if (_BLASLT_WIDE and self.dtype == torch.float32 and self.in_features >= _BLASLT_MIN_K and out.is_contiguous()
-                and self.activation in (None, "none", "linear", "relu", "selu")):
+        blaslt = (_BLASLT_WIDE and self.dtype == torch.float32 and self.in_features >= _BLASLT_MIN_K
+                  and out.is_contiguous() and self.activation in (None, "none", "linear", "relu", "selu"))
+        if self.dtype == torch.float32 and not blaslt and self.activation != "softmax" and G.supported(x, weight, out):
+            # fp32 layers (the DSSM towers, dssm.py:25-26): rf_gemm_f32, stream-K exact-fp32 MFMA with the bias
+            # and activation in its epilogue
+            return G.gemm_f32(x, weight, trans_b=True, bias=bias, act=self.activation or "none", out=out,
+                              stream=stream)
+        if blaslt:
             # fp32 deep-K layers (the DSSM towers' 8704 / 20480-wide inputs): hipBLASLt's kernel with its bias
             # epilogue runs them at 146-151 TF/s against 123-130 for rf_linear_splitk_fwd (DESIGN §4.4)
             with torch.cuda.stream(stream) if isinstance(stream, torch.cuda.Stream) else _nullctx():

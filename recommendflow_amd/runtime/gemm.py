@@ -1,0 +1,71 @@
+"""Exact-fp32 GEMM of the DSSM towers on librf.so (rf_gemm_f32, include/rf_api.h).
+
+Reference: every fp32 Dense of the towers (models/matching/dssm.py:25-26, create_mlp -> backend/blocks/mlp.py:4-15)
+and, under model.fit (example/ranking_search/train.py:96-104), the two MatMuls of its gradient. One entry point
+covers the three layouts:
+    forward        y  = act(x W^T + b)   gemm_f32(x, W, trans_b=True)      A k-contiguous, B k-contiguous
+    weight grad    G  = dpre^T h         gemm_f32(dpre, h, trans_a=True)   A m-contiguous, B n-contiguous
+    input grad     dz = dpre W           gemm_f32(dpre, W)                 A k-contiguous, B n-contiguous
+The workspace (per-tile counters that every launch leaves zero, then the stream-K partial tiles) is allocated
+zeroed once per (device, stream) and grown as needed; calls on one stream share it.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import lib as L
+
+_WS = {}
+_RETIRED = []
+calls = 0  # launches since import (tests assert the tower paths run here)
+
+
+def _workspace(dev: torch.device, stream_handle: int, need: int) -> torch.Tensor:
+    key = (dev.index, stream_handle)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < need:
+        # a grown ws starts zeroed (its counters); the old one may still be read by launches queued on this stream,
+        # so it is never released (growth happens a handful of times per process)
+        if ws is not None:
+            _RETIRED.append(ws)
+        ws = _WS[key] = torch.zeros(max(need, 256), dtype=torch.uint8, device=dev)
+    return ws
+
+
+def _op(t: torch.Tensor, kc: bool):
+    """(pointer source, leading dimension) of an operand given as a 2-D view: kc = its rows are the contraction
+    index's neighbours (unit column stride either way)."""
+    if t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.float32:
+        raise ValueError("rf_gemm_f32 operands are 2-D fp32 views with unit column stride")
+    return t, t.stride(0)
+
+
+def supported(*ts: torch.Tensor) -> bool:
+    """Operand views rf_gemm_f32 accepts: fp32, unit column stride, leading dimension % 4 == 0, 16-byte aligned."""
+    return all(t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 4 == 0
+               and t.data_ptr() % 16 == 0 for t in ts)
+
+
+def gemm_f32(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+             bias: Optional[torch.Tensor] = None, act: str = "none", out: Optional[torch.Tensor] = None,
+             stream=None) -> torch.Tensor:
+    """out[M][N] = act(op(a) op(b) + bias) with op(a) = a^T if trans_a (a stored [K][M]) else a ([M][K]) and
+    op(b) = b^T if trans_b (b stored [N][K]) else b ([K][N]); fp32 products and accumulation (exact MFMA)."""
+    global calls
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[0], b.shape[1]) if trans_b else (b.shape[1], b.shape[0])
+    if Kb != K:
+        raise ValueError(f"rf_gemm_f32: inner dimensions differ ({K} vs {Kb})")
+    A, lda = _op(a, not trans_a)
+    B, ldb = _op(b, trans_b)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    st = stream if isinstance(stream, int) else L.stream_ptr(stream)
+    need = int(L.load().rf_gemm_f32_ws_bytes(M, N, K))
+    ws = _workspace(a.device, st, need)
+    L.call("rf_gemm_f32", L.ptr(A), lda, int(not trans_a), L.ptr(B), ldb, int(trans_b), M, N, K, L.ptr(bias),
+           L.ACT[act], L.ptr(out), out.stride(0), L.ptr(ws), ws.numel(), st)
+    calls += 1
+    return out

@@ -105,6 +105,9 @@ _SIGS = {
                                       _vp]),
     "rf_adam_untouched": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp,
                                          ctypes.c_size_t, _vp]),
+    "rf_gemm_f32_ws_bytes": (ctypes.c_size_t, [_i64, _i64, _i64]),
+    "rf_gemm_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i32, _i64, _i64, _i64, _vp, _i32, _vp, _i64, _vp,
+                                   ctypes.c_size_t, _vp]),
     "rf_tower_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
     "rf_col_stats": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_bn_fold": (ctypes.c_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp]),

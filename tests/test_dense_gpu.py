@@ -118,17 +118,26 @@ def test_dense_head_fp32_activations(O, cuda, M, K, N, act, wdt):
 
 
 @pytest.mark.parametrize("M,K,N", [(100, 32, 64), (257, 8704, 1024), (64, 20480, 256), (4096, 8704, 1024),
-                                   (300, 2052, 100)])
-def test_dense_fp32_exact_mfma(O, cuda, M, K, N):
-    """cfg2 towers run in fp32 (the reference's dtype): rtol 1e-5 / atol 1e-6 vs float64.
-    The deep-K shapes take the split-K form (rf_linear_splitk_fwd: 8 / 2 splits; 2052 a K tail per split)."""
-    import recommendflow_amd.runtime.lib as L
+                                   (4096, 20480, 1024), (300, 2052, 100)])
+@pytest.mark.parametrize("route", ["librf", "blaslt"])
+def test_dense_fp32_exact_mfma(O, cuda, M, K, N, route, monkeypatch):
+    """cfg2 towers run in fp32 (the reference's dtype): rtol 1e-5 / atol 1e-6 vs float64. route
+    "librf" (the default): every shape runs rf_gemm_f32 (asserted: its launch counter moves, torch.addmm / mm are
+    never called); "blaslt": the A/B switch (RF_TOWER_BLASLT_WIDE=1) sends K >= 4096 to hipBLASLt."""
+    from recommendflow_amd.backend.layers import core
+    from recommendflow_amd.runtime import gemm as G
 
+    monkeypatch.setattr(core, "_BLASLT_WIDE", route == "blaslt")
+    if route == "librf":
+        def refuse(*a, **k):
+            raise AssertionError("a vendor GEMM ran on the librf route")
+        monkeypatch.setattr(torch, "addmm", refuse)
+        monkeypatch.setattr(torch, "mm", refuse)
     x = rnd((M, K), K, 0.5, torch.float32)
     dense = Dense(K, N, activation="selu", dtype=torch.float32, seed=1, bias=torch.linspace(-0.3, 0.3, N))
-    split = L.load().rf_linear_splitk_ws_bytes(L.DT_F32, M, K, N) > 0
-    assert split == (K >= 2048), (M, K, N)
+    n0 = G.calls
     y = dense(x.cuda()).cpu().numpy()
+    assert (G.calls - n0 == 1) == (route == "librf" or K < 4096), (route, G.calls - n0)
     W = dense.weight.cpu().numpy().astype(np.float64)
     want = O.activation(x.numpy().astype(np.float64) @ W.T + dense.bias.cpu().numpy(), "selu")
     np.testing.assert_allclose(y, want, rtol=1e-5, atol=1e-6 * np.sqrt(K))

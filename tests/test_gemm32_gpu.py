@@ -1,0 +1,102 @@
+"""GPU: rf_gemm_f32 (recommendflow_amd/csrc/rf_gemm32.hip), the exact-fp32 stream-K GEMM of the DSSM towers'
+forward and training step (models/matching/dssm.py:25-26; example/ranking_search/train.py:96-104), against a float64
+torch GEMM of the same operands. It is a floating-point kernel, so the oracle is a float64 product: the bound is on
+|C - ref| / (|A| |B| + |bias|) elementwise, 2e-6 (fp32 products and K-term fp32 accumulation; K <= 20480), and the
+result must be the same bits on every launch (tiles cut between workgroups are summed in k order)."""
+import pytest
+import torch
+
+from recommendflow_amd.runtime import gemm as G
+
+pytestmark = pytest.mark.gpu
+
+ACT = {"none": lambda t: t, "selu": torch.selu, "relu": torch.relu, "gelu": torch.nn.functional.gelu}
+
+
+def _operands(M, N, K, ta, tb, seed, bias=True):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    a = torch.randn((K, M) if ta else (M, K), device="cuda", generator=g)
+    b = torch.randn((N, K) if tb else (K, N), device="cuda", generator=g)
+    bi = torch.randn(N, device="cuda", generator=g) if bias else None
+    return a, b, bi
+
+
+def _check(c, a, b, ta, tb, bias, act):
+    A = (a.t() if ta else a).double()
+    B = (b.t() if tb else b).double()
+    ref = A @ B
+    scale = A.abs() @ B.abs()
+    if bias is not None:
+        ref = ref + bias.double()
+        scale = scale + bias.double().abs()
+    ref = ACT[act](ref)
+    err = ((c.double() - ref).abs() / (scale + 1e-30)).max().item() if c.numel() else 0.0
+    assert not torch.isnan(c).any()
+    assert err < 2e-6, err
+
+
+# the cfg2 towers' GEMMs at full size: forward (x W^T, 8704 / 20480 wide inputs), weight gradient (dpre^T h),
+# input gradient (dpre W)
+TOWER = [("fwd_user", 4096, 1024, 8704, False, True, "selu"), ("fwd_ad", 4096, 1024, 20480, False, True, "selu"),
+         ("fwd_l2", 4096, 512, 1024, False, True, "selu"), ("fwd_l3", 4096, 256, 512, False, True, "selu"),
+         ("dw_user", 1024, 8704, 4096, True, False, "none"), ("dw_ad", 1024, 20480, 4096, True, False, "none"),
+         ("dw_l2", 512, 1024, 4096, True, False, "none"), ("dz_user", 4096, 8704, 1024, False, False, "none"),
+         ("dz_ad", 4096, 20480, 1024, False, False, "none"), ("dz_l3", 4096, 512, 256, False, False, "none")]
+
+
+@pytest.mark.parametrize("name,M,N,K,ta,tb,act", TOWER, ids=[t[0] for t in TOWER])
+def test_tower_shapes_vs_float64(cuda, name, M, N, K, ta, tb, act):
+    a, b, bias = _operands(M, N, K, ta, tb, seed=M + N + K, bias=act != "none")
+    c = G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act=act)
+    _check(c, a, b, ta, tb, bias, act)
+    c2 = G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act=act)
+    assert torch.equal(c, c2)  # fixed combine order: replays are bit-identical
+
+
+EDGE = [(300, 200, 100), (132, 260, 36), (257, 132, 1028), (132, 127, 68), (1000, 700, 4100), (1, 4, 4), (129, 1, 132),
+        (64, 64, 0), (4096, 300, 12)]
+
+
+@pytest.mark.parametrize("M,N,K", EDGE)
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False), (True, True)])
+def test_ragged_shapes_every_layout(cuda, M, N, K, ta, tb):
+    """Ragged M / N (partial tiles), K tails (K % 32 != 0), K = 0 (bias + activation only), tiny grids, every
+    operand layout; the m/n-contiguous layouts need their leading dimension % 4 == 0, so M and N are padded in
+    storage there (the operand is a column slice of a wider tensor)."""
+    g = torch.Generator(device="cuda").manual_seed(M * 31 + N * 7 + K)
+    pad = lambda n: (n + 3) // 4 * 4
+    a_full = torch.randn((K, pad(M)) if ta else (M, pad(K)), device="cuda", generator=g)
+    b_full = torch.randn((N, pad(K)) if tb else (K, pad(N)), device="cuda", generator=g)
+    a = a_full[:, :M] if ta else a_full[:, :K]
+    b = b_full[:, :K] if tb else b_full[:, :N]
+    bias = torch.randn(N, device="cuda", generator=g)
+    c = torch.full((M, N), float("nan"), device="cuda")
+    G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act="relu", out=c)
+    _check(c, a, b, ta, tb, bias, "relu")
+
+
+def test_workspace_shared_across_shapes(cuda):
+    """One zeroed workspace per stream serves every shape: a small call after a large one, a large one after a small
+    one (the per-tile counters sit at the start, the partial tiles at the far end), the results unchanged."""
+    shapes = [(4096, 1024, 8704, False, True), (256, 512, 4096, True, False), (4096, 8704, 1024, False, False),
+              (300, 200, 100, False, True), (1024, 20480, 4096, True, False)]
+    first = []
+    for i, (M, N, K, ta, tb) in enumerate(shapes):
+        a, b, _ = _operands(M, N, K, ta, tb, seed=i, bias=False)
+        first.append((a, b, ta, tb, G.gemm_f32(a, b, trans_a=ta, trans_b=tb)))
+    for a, b, ta, tb, c in reversed(first):
+        assert torch.equal(G.gemm_f32(a, b, trans_a=ta, trans_b=tb), c)
+    for a, b, ta, tb, c in first:
+        _check(c, a, b, ta, tb, None, "none")
+
+
+def test_output_row_stride_and_views(cuda):
+    """Operands and output as column blocks of wider tensors (the towers read their blocks of the fused encoder
+    output in place): leading dimensions larger than the logical widths."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(512, 8704 + 20480, device="cuda", generator=g)
+    W = torch.randn(1024, 20480, device="cuda", generator=g) * 0.01
+    out = torch.full((512, 2048), float("nan"), device="cuda")
+    G.gemm_f32(x[:, 8704:], W, trans_b=True, out=out[:, 1024:])
+    _check(out[:, 1024:], x[:, 8704:], W, False, True, None, "none")
+    assert torch.isnan(out[:, :1024]).all()  # nothing written outside the view

@@ -36,10 +36,25 @@ def _oracle_layers(t):
 
 
 @pytest.mark.parametrize("M,in_f,units,rate,off", [(512, 384, (128, 64, 32), 0.3, 4), (300, 2048, (256, 64), 0.0, 4),
-                                                   (1024, 8704, (1024, 512, 256), 0.3, 4)])
-def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate, off):
-    """Output, input gradient and every parameter gradient vs float64; the last shape is cfg2's user tower
-    (K = 8704: the split-K forward)."""
+                                                   (1024, 8704, (1024, 512, 256), 0.3, 4),
+                                                   (512, 20480, (1024, 512, 256), 0.3, 8)])
+@pytest.mark.parametrize("route", ["librf", "blas"])
+def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate, off, route, monkeypatch):
+    """Output, input gradient and every parameter gradient vs float64; the last shapes are cfg2's user and ad towers
+    (K = 8704 / 20480). route "librf" (the default): every forward and backward GEMM runs rf_gemm_f32 (asserted:
+    3 launches per layer, torch.mm / addmm never called); "blas": the A/B switches (hipBLASLt forward for K >= 4096,
+    torch.mm backward)."""
+    from recommendflow_amd.backend.blocks import train_mlp
+    from recommendflow_amd.runtime import gemm as G
+
+    monkeypatch.setattr(train_mlp, "_BLASLT_WIDE", route == "blas")
+    monkeypatch.setattr(train_mlp, "_BWD_BLAS", route == "blas")
+    if route == "librf":
+        def refuse(*a, **k):
+            raise AssertionError("a vendor GEMM ran on the librf route")
+        monkeypatch.setattr(torch, "addmm", refuse)
+        monkeypatch.setattr(torch, "mm", refuse)
+    n0 = G.calls
     t = _tower(in_f, units, rate)
     g = torch.Generator().manual_seed(M + in_f)
     xfull = (torch.randn(M, in_f + 8, generator=g) * 0.05 + 0.01).cuda()
@@ -48,6 +63,8 @@ def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate, off):
     out = t(x)
     dout = torch.randn(out.shape, generator=g).cuda()
     out.backward(dout)
+    if route == "librf":
+        assert G.calls - n0 == 3 * len(units), G.calls - n0
     layers = _oracle_layers(t)
     seeds = [layer_seed(t.seed, step, l) for l in range(len(units))]
     want, cache = O.tower_train_fwd(x.detach().cpu().numpy(), layers, rate, seeds)

@@ -1,0 +1,452 @@
+// rf_gemm32.hip — the exact-fp32 GEMMs of the DSSM towers (models/matching/dssm.py:25-26:
+// create_mlp([1024, 512, 256], 0.3, "selu", BatchNormalization(1e-6)), backend/blocks/mlp.py:4-15), forward and
+// training step (example/ranking_search/train.py:96-104, model.fit with Adam):
+//   forward        y  = act(x W'^T + b')   A = x    [M][K]    (k contiguous),   B = W'  [N][K] (k contiguous)
+//   weight grad    G  = dpre^T h           A = dpre [K][M]    (m contiguous),   B = h   [K][N] (n contiguous)
+//   input grad     dz = dpre W             A = dpre [M][K]    (k contiguous),   B = W   [K][N] (n contiguous)
+// C[m][n] = sum_k A(m, k) B(k, n) on v_mfma_f32_16x16x4_f32 (f32 products, f32 accumulation; gfx950 has no xf32).
+//
+// Schedule (one 128 x 128 output tile per workgroup at a time, 4 waves of 64 x 64, two workgroups per CU):
+//   * stream-K: the (tile, 32-k step) iterations of the whole GEMM are cut into G equal ranges, one per persistent
+//     workgroup (G = 2 per CU), so every workgroup does the same MFMA work whatever the tile count; ranges are
+//     laid out XCD-major (the workgroups of one XCD take consecutive tiles: their A rows / B columns share its L2);
+//   * a tile cut between workgroups: each stores its raw partial tile (write-through sc1 stores), one agent-scope
+//     ticket per workgroup, and the LAST to arrive adds every segment in k order (fixed: the result does not depend
+//     on arrival order) and runs the epilogue (MI355X_MICROARCH.md, inter-workgroup hand-off: sc1 payload,
+//     vmcnt(0), barrier, one relaxed agent-scope add whose return value names the last arriver, sc1 loads);
+//   * per 32-k step: the next step's 32 KB are loaded into registers (buffer loads, 4 x 16 B per thread and
+//     operand) one step ahead and written to the other half of a double-buffered LDS ring under this step's
+//     MFMAs; fragments of half 1 are read under half 0's MFMAs, and the next step's half 0 under half 1's:
+//     one barrier per step;
+//   * LDS formats: a k-contiguous operand keeps 128-byte rows (32 k), 16-byte chunk c of row r at c ^ ((r >> 1) & 7)
+//     (the 16 rows of one ds_read_b128 quarter-wave hit 16 distinct bank groups); an m/n-contiguous operand keeps
+//     32 k-rows of 512 bytes, chunk c of k-row kk at c ^ (((kk >> 2) & 3) << 2) (the four lane groups of an MFMA
+//     read four k-rows: distinct banks), read as ds_read_b32 (pairs of k-rows 512 B apart: ds_read2_b32);
+//   * both layouts feed the MFMA in one permuted k order: in half h, MFMA e takes k = 16 h + 4 lg + e in lane
+//     group lg.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "../../recommendflow_amd/csrc/rf_act.h"
+#include "../../recommendflow_amd/csrc/rf_common.h"
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 128, kBN = 128, kBK = 64, kThreads = 256;
+constexpr int kStage = (kBM + kBN) * kBK;  // floats per LDS stage (64 KB)
+constexpr int kSlot = kBM * kBN;           // floats per partial tile (64 KB)
+constexpr int kMinIters = 8;               // 32-k steps per workgroup at least (small GEMMs take fewer workgroups)
+constexpr int kWgPerCu = 1;                // one 4-wave workgroup per CU: one wave per SIMD, registers to spare
+constexpr uint32_t kOOB = 0x80000000u;            // a buffer offset past every extent: the load returns zeros
+constexpr int kLdsBytes = 2 * kStage * 4 + 16;     // two stages + the last-arriver flag
+
+struct GemmArgs {
+    const float* A;
+    const float* B;
+    float* C;
+    const float* bias;
+    int64_t lda, ldb, ldc;
+    int M, N, K;
+    int act;
+    int tiles_n, nk;
+    int64_t units;  // tiles * nk
+    int* cnt;       // one arrival counter per tile (zero between launches)
+    int one;        // 1 (a branch condition the compiler cannot fold)
+    float* slots;   // 2 G partial tiles
+};
+
+__device__ __forceinline__ int64_t seg_lo(int64_t v, int64_t U, int G) { return v * U / G; }
+
+// the workgroup (virtual index) whose range holds iteration x
+__device__ __forceinline__ int seg_owner(int64_t x, int64_t U, int G) {
+    int v = (int)(x * G / U);
+    while (v + 1 < G && seg_lo(v + 1, U, G) <= x) ++v;
+    while (v > 0 && seg_lo(v, U, G) > x) --v;
+    return v;
+}
+
+__device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// extents are < 2^31 (rf_gemm_f32 checks): kOOB is past every one
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, bytes <= 0 ? 0u : (uint32_t)bytes, 0x00020000);
+}
+
+// One operand of the tile: where this thread's four 16-byte chunks per 32-k step come from and go to. KC: k-contiguous
+// rows (tile dim = rows); else k-rows with the tile dim contiguous. One buffer resource per segment whose extent ends
+// at the matrix's last byte (k-rows past K and the last row's k tail read zeros); the step's k offset rides in the
+// per-lane offset (the range check covers it).
+template <bool KC>
+struct Operand {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t voff[8];  // per chunk, at k = 0
+    uint32_t kstep;    // bytes per 64-k step
+    int kcol;          // KC: this thread's k offset in a step (the K tail masks it)
+    uint32_t loff[8];  // LDS float offsets of the chunks
+
+    __device__ __forceinline__ void init(const float* p, int64_t ld, int rows, int row0, int K, int tid) {
+        if constexpr (KC) {
+            // 256-byte rows (64 k) = 16 chunks; 16 threads per row; chunk c of row r at c ^ (r & 15)
+            const int ch = tid & 15;
+            kcol = ch * 4;
+            const int last = rows - 1 - row0;
+            rs = rsrc(p + (int64_t)row0 * ld, (int64_t)last * ld * 4 + (int64_t)K * 4);
+            kstep = kBK * 4;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int r = (tid >> 4) + 16 * c;
+                voff[c] = (uint32_t)(((int64_t)min(r, last) * ld + ch * 4) * 4);
+                loff[c] = r * 64 + ((ch ^ (r & 15)) << 2);
+            }
+        } else {
+            const int c32 = tid & 31;
+            kcol = 0;
+            rs = rsrc(p + row0, ((int64_t)(K - 1) * ld + (ld - row0)) * 4);
+            kstep = (uint32_t)(kBK * ld * 4);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int kk = (tid >> 5) + 8 * c;
+                voff[c] = (uint32_t)(((int64_t)kk * ld + c32 * 4) * 4);
+                loff[c] = kk * 128 + ((c32 ^ (((kk >> 2) & 3) << 2)) << 2);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void load1(f4& r, int c, int kt, int K) const {
+        const uint32_t ko = (uint32_t)kt * kstep;
+        if constexpr (KC) {
+            const bool ok = kt * kBK + kcol < K;
+            r = bload(rs, ok ? voff[c] + ko : kOOB);
+        } else {
+            r = bload(rs, voff[c] + ko);
+        }
+    }
+    __device__ __forceinline__ void store1(const f4& r, int c, float* st) const {
+        *reinterpret_cast<f4*>(st + loff[c]) = r;
+    }
+};
+
+// fragments of k-chunk q (16 k): f[i][e] = X(k = 16 q + 4 lg + e, tile index t0 + 16 i + lr)
+template <bool KC>
+__device__ __forceinline__ void read_frag(f4 (&f)[4], const float* st, int t0, int q, int lr, int lg) {
+    if constexpr (KC) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            f[i] = *reinterpret_cast<const f4*>(st + (t0 + 16 * i + lr) * 64 + (((4 * q + lg) ^ lr) << 2));
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int col = t0 + 16 * i + lr;
+            const float* p = st + (((col >> 2) ^ (lg << 2)) << 2) + (col & 3) + (16 * q + 4 * lg) * 128;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f[i][e] = p[e * 128];
+        }
+    }
+}
+
+__device__ __forceinline__ void mfma_half(f4 (&acc)[4][4], const f4 (&a)[4], const f4 (&b)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+}
+
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
+    // DS read instructions per half-step for both operands: 4 ds_read_b128 (k-contiguous) or 8 ds_read2_b32 (else)
+    constexpr int kFragReads = (AKC ? 4 : 8) + (BKC ? 4 : 8);
+    extern __shared__ __attribute__((aligned(16))) float lds[];  // 2 stages + the last-arriver flag
+    int& s_last = *reinterpret_cast<int*>(lds + 2 * kStage);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int G = gridDim.x;
+    // XCD-major virtual index (block b runs on XCD b % 8): one XCD's workgroups take consecutive ranges
+    const int q8 = G / 8, r8 = G % 8, xcd = blockIdx.x % 8;
+    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
+    const int64_t U = g.units;
+    const int64_t lo = seg_lo(v, U, G), hi = seg_lo(v + 1, U, G);
+    const int K = g.K;
+
+    for (int64_t u = lo; u < hi;) {
+        const int tile = (int)(u / g.nk);
+        const int k_lo = (int)(u - (int64_t)tile * g.nk);
+        const int k_hi = (int)min<int64_t>(g.nk, hi - (int64_t)tile * g.nk);
+        u = (int64_t)tile * g.nk + k_hi;
+        const int m0 = (tile / g.tiles_n) * kBM, n0 = (tile % g.tiles_n) * kBN;
+
+        Operand<AKC> oa;
+        Operand<BKC> ob;
+        oa.init(g.A, g.lda, g.M, m0, K, tid);
+        ob.init(g.B, g.ldb, g.N, n0, K, tid);
+        float bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[j] = g.bias ? g.bias[min(n0 + wn * 64 + 16 * j + lr, g.N - 1)] : 0.f;
+
+        f4 acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+        __syncthreads();  // the previous segment's LDS reads and s_last are done
+        // one register set: step kt's data is loaded during step kt - 2 ... written during step kt - 1
+        f4 ra[8], rb[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { oa.load1(ra[c], c, k_lo, K); ob.load1(rb[c], c, k_lo, K); }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { oa.store1(ra[c], c, lds); ob.store1(rb[c], c, lds + kBM * kBK); }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { oa.load1(ra[c], c, k_lo + 1, K); ob.load1(rb[c], c, k_lo + 1, K); }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        f4 fa[2][4], fb[2][4];
+        read_frag<AKC>(fa[0], lds, wm * 64, 0, lr, lg);
+        read_frag<BKC>(fb[0], lds + kBM * kBK, wn * 64, 0, lr, lg);
+
+        constexpr int G1 = kFragReads >= 16 ? 1 : 24 / kFragReads;  // reads G1 MFMAs apart
+        constexpr int GR = 64 / kFragReads;                          // reads spread over the whole quarter
+        // One step (64 k) in four quarters of 64 MFMAs, each in a block of its own (behind branches the compiler
+        // cannot fold: MFMAs carry no chain, instruction selection would order them past the barrier):
+        //   Q0: MFMAs of chunk 0 | reads of chunk 1 | copies 0..7 of the next tile (A), loads of the tile after
+        //   Q1: MFMAs of chunk 1 | reads of chunk 2 | copies 0..7 (B), loads
+        //   Q2: MFMAs of chunk 2 | reads of chunk 3            then barrier (the next tile written, this read)
+        //   Q3: MFMAs of chunk 3 | reads of the next tile's chunk 0
+        auto step = [&](int kt, const float* cur, float* nxt) {
+            read_frag<AKC>(fa[1], cur, wm * 64, 1, lr, lg);
+            read_frag<BKC>(fb[1], cur + kBM * kBK, wn * 64, 1, lr, lg);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) { oa.store1(ra[c], c, nxt); oa.load1(ra[c], c, kt + 2, K); }
+            mfma_half(acc, fa[0], fb[0]);
+#pragma unroll
+            for (int q = 0; q < kFragReads; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, G1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, (64 - G1 * kFragReads) / 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, (64 - G1 * kFragReads) / 8 - (64 - G1 * kFragReads) / 16, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (g.one) asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            read_frag<AKC>(fa[0], cur, wm * 64, 2, lr, lg);
+            read_frag<BKC>(fb[0], cur + kBM * kBK, wn * 64, 2, lr, lg);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) { ob.store1(rb[c], c, nxt + kBM * kBK); ob.load1(rb[c], c, kt + 2, K); }
+            mfma_half(acc, fa[1], fb[1]);
+#pragma unroll
+            for (int q = 0; q < kFragReads; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, G1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x008, (64 - G1 * kFragReads) / 16, 1);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x008, (64 - G1 * kFragReads) / 8 - (64 - G1 * kFragReads) / 16, 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (g.one) asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            read_frag<AKC>(fa[1], cur, wm * 64, 3, lr, lg);
+            read_frag<BKC>(fb[1], cur + kBM * kBK, wn * 64, 3, lr, lg);
+            mfma_half(acc, fa[0], fb[0]);
+#pragma unroll
+            for (int q = 0; q < kFragReads; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, GR, 2);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (g.one) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();  // the next tile is written; every wave is done reading this one
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            read_frag<AKC>(fa[0], nxt, wm * 64, 0, lr, lg);
+            read_frag<BKC>(fb[0], nxt + kBM * kBK, wn * 64, 0, lr, lg);
+            mfma_half(acc, fa[1], fb[1]);
+#pragma unroll
+            for (int q = 0; q < kFragReads; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, G1, 3);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 3);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 64 - G1 * kFragReads, 3);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        int kt = k_lo;
+        for (; kt + 1 < k_hi; kt += 2) {
+            step(kt, lds, lds + kStage);
+            step(kt + 1, lds + kStage, lds);
+        }
+        if (kt < k_hi) step(kt, lds, lds + kStage);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+        const bool full = k_lo == 0 && k_hi == g.nk;
+        if (!full) {
+            // a cut tile: this segment's raw partial into its slot, one ticket; the last arriver combines in k order
+            const int slot_id = (tile == (int)(lo / g.nk)) ? 2 * v : 2 * v + 1;
+            float* slot = g.slots + (size_t)slot_id * kSlot;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        __hip_atomic_store(slot + ((wave * 64 + (i * 4 + j) * 4 + r) * 64 + lane), acc[i][j][r],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const int v_first = seg_owner((int64_t)tile * g.nk, U, G);
+            const int v_last = seg_owner((int64_t)tile * g.nk + g.nk - 1, U, G);
+            if (tid == 0) {
+                const int old = __hip_atomic_fetch_add(g.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_last = old == v_last - v_first;
+            }
+            __syncthreads();
+            if (!s_last) continue;
+            if (tid == 0) __hip_atomic_store(g.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int w = v_first; w <= v_last; ++w) {
+                const int sid = (tile == (int)(seg_lo(w, U, G) / g.nk)) ? 2 * w : 2 * w + 1;
+                const float* p = g.slots + (size_t)sid * kSlot;
+                float t[4][4][4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            t[i][j][r] = __hip_atomic_load(p + ((wave * 64 + (i * 4 + j) * 4 + r) * 64 + lane),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) acc[i][j][r] = w == v_first ? t[i][j][r] : acc[i][j][r] + t[i][j][r];
+            }
+        }
+        // epilogue: bias + activation, values first, stores after (unguarded on interior tiles)
+        rf_act::with_act(g.act, [&](auto F) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] = F(acc[i][j][r] + bv[j]);
+        });
+        const int rbase = m0 + wm * 64 + lg * 4, cbase = n0 + wn * 64 + lr;
+        if (m0 + kBM <= g.M && n0 + kBN <= g.N) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float* yr = g.C + (int64_t)(rbase + 16 * i + r) * g.ldc + cbase;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) yr[16 * j] = acc[i][j][r];
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = rbase + 16 * i + r;
+                    if (row >= g.M) continue;
+                    float* yr = g.C + (int64_t)row * g.ldc + cbase;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (cbase + 16 * j < g.N) yr[16 * j] = acc[i][j][r];
+                }
+        }
+    }
+}
+
+int cu_count() {
+    static const int n = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return cus > 0 ? cus : 256;
+    }();
+    return n;
+}
+
+int64_t tiles_of(int64_t M, int64_t N) { return ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN); }
+size_t slot_bytes() { return (size_t)2 * kWgPerCu * cu_count() * kSlot * sizeof(float); }  // 2 slots per workgroup
+size_t cnt_bytes(int64_t tiles) { return (((size_t)std::max<int64_t>(tiles, 1) * 4) + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" size_t rf_gemm_f32_ws_bytes(int64_t M, int64_t N, int64_t K) {
+    (void)K;
+    return cnt_bytes(tiles_of(M, N)) + slot_bytes();
+}
+
+extern "C" int rf_gemm_f32(const float* A, int64_t lda, int32_t a_kc, const float* B, int64_t ldb, int32_t b_kc,
+                           int64_t M, int64_t N, int64_t K, const float* bias, int32_t act, float* C, int64_t ldc,
+                           void* ws, size_t ws_bytes, void* stream) {
+    RF_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30),
+               "rf_gemm_f32: bad shape");
+    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_gemm_f32: activation must be elementwise");
+    if (M == 0 || N == 0) return RF_OK;
+    RF_REQUIRE((K == 0 || (A && B)) && C && ws, "rf_gemm_f32: null pointer");
+    RF_REQUIRE(K == 0 || (K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0),
+               "rf_gemm_f32: K, lda, ldb must be multiples of 4 and A, B 16-byte aligned");
+    RF_REQUIRE(K == 0 || ((a_kc ? lda >= K : lda >= M) && (b_kc ? ldb >= K : ldb >= N)), "rf_gemm_f32: leading dimension too small");
+    RF_REQUIRE(ldc >= N,
+               "rf_gemm_f32: leading dimension too small");
+    // 32-bit buffer offsets: a k-contiguous operand's 128-row tile block, an m/n-contiguous operand's whole K rows
+    RF_REQUIRE((a_kc ? 128 * (__int128)lda : (K + 64) * (__int128)lda) * 4 < ((__int128)1 << 31) &&
+                   (b_kc ? 128 * (__int128)ldb : (K + 64) * (__int128)ldb) * 4 < ((__int128)1 << 31),
+               "rf_gemm_f32: operand block exceeds 2 GiB (32-bit buffer offsets)");
+    const int64_t tiles = tiles_of(M, N);
+    RF_REQUIRE(ws_bytes >= rf_gemm_f32_ws_bytes(M, N, K), "rf_gemm_f32: workspace too small");
+    GemmArgs g{};
+    g.A = A;
+    g.B = B;
+    g.C = C;
+    g.bias = bias;
+    g.lda = lda;
+    g.ldb = ldb;
+    g.ldc = ldc;
+    g.M = (int)M;
+    g.N = (int)N;
+    g.K = (int)K;
+    g.act = act;
+    g.tiles_n = (int)((N + kBN - 1) / kBN);
+    g.nk = (int)std::max<int64_t>((K + kBK - 1) / kBK, 1);
+    g.units = tiles * g.nk;
+    g.one = 1;
+    // counters at the start, partial slots at the far end: one zeroed ws serves calls of any shape it is large
+    // enough for (a smaller call's slots never land on a larger call's counters)
+    g.cnt = static_cast<int*>(ws);
+    g.slots = reinterpret_cast<float*>(static_cast<char*>(ws) + ((ws_bytes - slot_bytes()) & ~(size_t)255));
+    const int64_t gmax = (int64_t)kWgPerCu * cu_count();
+    int G = (int)std::max<int64_t>(1, std::min<int64_t>(gmax, g.units / kMinIters));
+#ifdef RF_G32_LAB
+    if (const char* e = getenv("RF_G32_GRID")) G = std::max(1, std::min(atoi(e), (int)gmax));
+#endif
+    hipStream_t st = rf_stream(stream);
+    const int which = (a_kc ? 2 : 0) + (b_kc ? 1 : 0);
+    static void (*const kerns[4])(GemmArgs) = {gemm32_kernel<false, false>, gemm32_kernel<false, true>,
+                                               gemm32_kernel<true, false>, gemm32_kernel<true, true>};
+    static bool attr_set[4] = {false, false, false, false};
+    if (!attr_set[which]) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kerns[which]),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm32_kernel: %s", hipGetErrorString(e));
+        attr_set[which] = true;
+    }
+    hipLaunchKernelGGL(kerns[which], dim3(G), dim3(kThreads), kLdsBytes, st, g);
+    return rf_check_launch("gemm32_kernel");
+}
