@@ -168,6 +168,22 @@ def main():
     def step(i):
         enc(dev[i % len(dev)], out=out)
 
+    # The peak the roofline divides by is measured first (STREAM copy, random-row gather ceilings): it also leaves
+    # the GPU at its loaded clock. Measured cause of the headline's first-launch slope (tools/settle_probe.py,
+    # profiles/r05/settle_probe.txt): launches 5-24 after 2 s idle take 271 us, after any 0.3 s of unrelated GPU
+    # work 256 us (the settled value); a full pass over the table's pages does not remove the slope: it is the
+    # clock ramp, not cache or TLB warm-up.
+    probes = None
+    if not args.no_probes:
+        try:
+            probes = bench_probes(args)
+        except Exception as e:  # noqa: BLE001
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            probes = {"error": f"{type(e).__name__}: {e}"[:300]}
+    args.probes = probes
+    torch.cuda.synchronize()
+
     for i in range(args.warmup):
         step(i)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -200,15 +216,6 @@ def main():
             uniform_leg = bench_uniform(args, enc, multi, rank, out)
         except Exception as e:  # noqa: BLE001 — the headline line must still print
             uniform_leg = {"error": f"{type(e).__name__}: {e}"[:300]}
-    probes = None
-    if not args.no_probes:
-        try:
-            probes = bench_probes(args)
-        except Exception as e:  # noqa: BLE001
-            torch.cuda.synchronize()
-            torch.cuda.empty_cache()
-            probes = {"error": f"{type(e).__name__}: {e}"[:300]}
-    args.probes = probes
 
     sharded = None
     if not args.no_sharded:
@@ -335,14 +342,43 @@ def main():
             pass
 
 
-def _time_stages(stages, steps, warmup):
+def _warm(fn, warm_s: float = 0.25, min_iters: int = 2):
+    """Untimed repetitions of fn until about warm_s seconds of GPU work have run (see _time_stages)."""
+    import torch
+
+    for _ in range(min_iters):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < warm_s and n < 10000:
+        fn()
+        n += 1
+        if n % 8 == 0:  # bounded queue: thousands of unsynchronised graph launches slow later ones on the host
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+
+
+def _time_stages(stages, steps, warmup, warm_s: float = 0.25):
     """stages: list of (name, fn). HIP events around every stage on the current stream; returns
-    (ms per step, {stage: ms})."""
+    (ms per step, {stage: ms}). The untimed warm-up runs `warmup` steps and then more until about warm_s seconds of
+    the same work have run: a leg starts after host-side setup (graph capture, allocation) with the GPU idle, and the
+    clock takes tens of ms of load to come back (tools/gemm32_insitu_probe.py: the towers' 20480-wide GEMM 1.19 ms
+    back to back, 1.24 after 1 ms idle, 1.40 after 50 ms idle; tools/settle_probe.py for the encoder)."""
     import torch
 
     for _ in range(warmup):
         for _, fn in stages:
             fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < warm_s and n < 10000:
+        for _, fn in stages:
+            fn()
+        n += 1
+        if n % 8 == 0:  # bounded queue: thousands of unsynchronised graph launches slow later ones on the host
+            torch.cuda.synchronize()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(stages) + 1)] for _ in range(steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -542,8 +578,7 @@ def bench_dssm(args, enc, host):
         ea(ha, out=xa)
 
     def towers():
-        u = torch.nn.functional.normalize(model.user_dense(xu), dim=-1, eps=1e-6)
-        v = torch.nn.functional.normalize(model.ad_dense(xa), dim=-1, eps=1e-6)
+        u, v = model.towers(xu, xa)
         (u * v).sum(-1)
 
     steps = max(5, args.steps // 5)
@@ -958,9 +993,13 @@ def bench_train(args, specs, multi):
     batches = [synthetic_batch(B, multi, seed=555 + i).to("cuda") for i in range(2)]
     y = (torch.rand(B, generator=torch.Generator().manual_seed(0)) < 0.3).float().cuda()
     steps = max(5, args.steps // 5)
-    for i in range(2):
-        model.step(batches[i % 2], y)
-    torch.cuda.synchronize()
+    wi = [0]
+
+    def warm_step():
+        model.step(batches[wi[0] % 2], y)
+        wi[0] += 1
+
+    _warm(warm_step)  # the clock back at load after the previous leg's host-side setup (_time_stages)
     t0 = time.perf_counter()
     for i in range(steps):
         loss = model.step(batches[i % 2], y)
@@ -991,9 +1030,8 @@ def bench_train(args, specs, multi):
     del dense_opt
     # the r04 schedule for A/B: the whole-table untouched update on a side stream beside the towers
     split = TrainableDssm(enc, n_user, learning_rate=1e-3, seed=7, deferred_adam=False)
-    for i in range(2):
-        split.step(batches[i % 2], y)
-    torch.cuda.synchronize()
+    wi[0] = 0
+    _warm(lambda: (split.step(batches[wi[0] % 2], y), wi.__setitem__(0, wi[0] + 1)))
     t0 = time.perf_counter()
     for i in range(steps):
         split.step(batches[i % 2], y)
@@ -1015,12 +1053,21 @@ def bench_train(args, specs, multi):
     xin = torch.randn((B, enc.out_width), generator=torch.Generator().manual_seed(3)).cuda() * 0.05
     model.train()
     tw = np.zeros(2)
+    from recommendflow_amd.backend.blocks.train_mlp import towers_forward
+
+    def tower_fb(xg):
+        # the step's tower path: both towers layer by layer over column blocks of one input (towers_forward)
+        tu, ta = towers_forward(xg, [(model.user_tower, 0, model.wu), (model.ad_tower, model.wu, model.wa)])
+        uu = torch.nn.functional.normalize(tu, dim=-1, eps=1e-6)
+        vv = torch.nn.functional.normalize(ta, dim=-1, eps=1e-6)
+        model.loss_fn(y, uu, vv).backward()
+
+    _warm(lambda: tower_fb(xin.detach().requires_grad_(True)), min_iters=1)
+    model.dense_opt.zero_grad(set_to_none=True)
     for i in range(steps + 2):
         xg = xin.detach().requires_grad_(True)
         ev[0].record()
-        uu = torch.nn.functional.normalize(model.user_tower(xg[:, : model.wu]), dim=-1, eps=1e-6)
-        vv = torch.nn.functional.normalize(model.ad_tower(xg[:, model.wu:]), dim=-1, eps=1e-6)
-        model.loss_fn(y, uu, vv).backward()
+        tower_fb(xg)
         ev[1].record()
         model.dense_opt.step()
         ev[2].record()

@@ -187,6 +187,24 @@ int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int3
 size_t rf_gemm_f32_ws_bytes(int64_t M, int64_t N, int64_t K);
 int rf_gemm_f32(const float* A, int64_t lda, int32_t a_kc, const float* B, int64_t ldb, int32_t b_kc, int64_t M, int64_t N,
                 int64_t K, const float* bias, int32_t act, float* C, int64_t ldc, void* ws, size_t ws_bytes, void* stream);
+/* rf_gemm_f32_grouped: 1..4 independent GEMMs of one operand layout in ONE launch (the same layer of both DSSM
+ * towers: their tiles share the stream-K grid, so two small GEMMs fill the chip that one would leave idle). probs is
+ * a HOST array; per problem the rf_gemm_f32 fields and requirements; ws: rf_gemm_f32_grouped_ws_bytes(probs, n). */
+typedef struct rf_gemm_f32_problem {
+    const float* A;
+    int64_t lda;
+    const float* B;
+    int64_t ldb;
+    float* C;
+    int64_t ldc;
+    const float* bias;
+    int64_t M, N, K;
+    int32_t act;
+    int32_t reserved; /* 0 */
+} rf_gemm_f32_problem;
+size_t rf_gemm_f32_grouped_ws_bytes(const rf_gemm_f32_problem* probs, int32_t n);
+int rf_gemm_f32_grouped(const rf_gemm_f32_problem* probs, int32_t n, int32_t a_kc, int32_t b_kc, void* ws, size_t ws_bytes,
+                        void* stream);
 
 /*
  * DSSM tower training (models/matching/dssm.py:25-26: create_mlp([1024, 512, 256], 0.3, "selu",

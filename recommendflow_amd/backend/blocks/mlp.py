@@ -257,5 +257,32 @@ class MLP(torch.nn.Module):
         return outb
 
 
+def forward_towers(mlps: Sequence[MLP], xs: Sequence[torch.Tensor], stream=None) -> List[torch.Tensor]:
+    """The forward of several fp32 BatchNormalization MLPs of equal depth (the DSSM user and ad towers,
+    dssm.py:25-26) layer by layer: each layer's GEMMs of every tower through runtime.gemm.gemm_f32_layer (ONE
+    rf_gemm_f32_grouped launch for the small layers, whose tiles then fill the chip together; one launch each for
+    layers with a tile per CU), BatchNormalization folded into the weights (MLP._bn_folded), bias + activation in the
+    epilogue. Any other MLP mix runs each MLP on its own."""
+    from ...runtime import gemm as G
+
+    for m, x in zip(mlps, xs):
+        if not m.denses:
+            m.build(x.shape[-1])
+    depth = {len(m.denses) for m in mlps}
+    ok = (len(depth) == 1 and all(m.dtype == torch.float32 and m.activation not in ("softmax",)
+                                  and all(n is not None and n.mode == 1 for n in m.norms) for m in mlps)
+          and all(x.dtype == torch.float32 and G.supported(x) for x in xs))
+    if not ok:
+        return [m(x, stream=stream) for m, x in zip(mlps, xs)]
+    hs = list(xs)
+    for i in range(depth.pop()):
+        probs = []
+        for m, h in zip(mlps, hs):
+            w, b = m._bn_folded(i)
+            probs.append((h, w, b, m.activation or "none", None))
+        hs = G.gemm_f32_layer(probs, trans_b=True, stream=stream)
+    return hs
+
+
 def create_mlp(hidden_units, dropout_rate, activation, normalization_layer, name=None, **kw) -> MLP:
     return MLP(hidden_units, dropout_rate, activation, normalization_layer, name=name, **kw)

@@ -118,121 +118,190 @@ def _ws(M: int, K: int, device) -> torch.Tensor:
     return torch.empty(max(int(L.load().rf_tower_ws_bytes(M, K)), 4), dtype=torch.uint8, device=device)
 
 
-def _tower_forward(tower: "TrainTower", x: torch.Tensor, params):
-    """The training forward of one tower on x (a 2-D fp32 view with unit column stride; any row stride).
-    Returns (outputs per layer, batch means, batch variances, the step number that seeded the masks)."""
-    if x.dim() != 2 or x.stride(1) != 1 or x.dtype != torch.float32:
-        raise ValueError("TrainTower input must be a 2-D fp32 tensor with unit column stride")
-    M = x.shape[0]
-    dev, st = x.device, L.stream_ptr(None)
-    step = tower.steps
-    tower.steps += 1
-    h = x
-    outs, means, vars_ = [], [], []
-    for l in range(len(tower.units)):
-        W, b, g, be = params[4 * l: 4 * l + 4]
-        N, K = W.shape
-        mean = torch.empty(K, dtype=torch.float32, device=dev)
-        var = torch.empty(K, dtype=torch.float32, device=dev)
-        ws = _ws(M, K, dev)
-        L.call("rf_col_stats", L.ptr(h), M, K, h.stride(0), L.ptr(mean), L.ptr(var), L.ptr(ws), ws.numel(), st)
-        Wf = torch.empty_like(W)
-        bf = torch.empty(N, dtype=torch.float32, device=dev)
-        L.call("rf_bn_fold", L.ptr(W), N, K, L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(mean), L.ptr(var), tower.eps,
-               L.ptr(Wf), L.ptr(bf), st)
-        y = torch.empty((M, N), dtype=torch.float32, device=dev)
-        _linear_f32(h, Wf, bf, L.ACT["selu"], y, st)
-        L.call("rf_dropout_fwd", L.ptr(y), M, N, N, tower.rate, layer_seed(tower.seed, step, l), L.ptr(y), N, st)
-        with torch.no_grad():
-            tower.moving_mean[l].mul_(tower.momentum).add_(mean, alpha=1.0 - tower.momentum)
-            tower.moving_var[l].mul_(tower.momentum).add_(var, alpha=1.0 - tower.momentum)
-        outs.append(y)
-        means.append(mean)
-        vars_.append(var)
-        h = y
-    return outs, means, vars_, step
+def _gemm_layer(probs, trans_a: bool, trans_b: bool, stream):
+    """One layer's GEMMs of every tower: probs = [(a, b, bias, act name, out)]. librf (rf_gemm_f32, grouped into one
+    launch where runtime.gemm.group_pays) when every operand qualifies; otherwise torch one by one."""
+    if all(GM.supported(a, b) and (o is None or GM.supported(o)) for a, b, _, _, o in probs):
+        return GM.gemm_f32_layer(probs, trans_a=trans_a, trans_b=trans_b, stream=stream)
+    outs = []
+    for a, b, bias, act, o in probs:
+        A = a.t() if trans_a else a
+        B = b.t() if trans_b else b
+        r = torch.mm(A, B) if bias is None else torch.addmm(bias, A, B)
+        r = {"selu": torch.selu, "relu": torch.relu, "none": lambda t: t}[act](r)
+        if o is not None:
+            o.copy_(r)
+            r = o
+        outs.append(r)
+    return outs
 
 
-def _tower_backward(tower: "TrainTower", step: int, x: torch.Tensor, params, outs, means, vars_, dout: torch.Tensor,
-                    dx_out: torch.Tensor):
-    """Backward of _tower_forward: parameter gradients (W, b, gamma, beta per layer) returned, the input gradient
-    written into dx_out (a view of x's shape; any row stride)."""
-    n = len(tower.units)
-    dev, st = x.device, L.stream_ptr(None)
-    M = x.shape[0]
-    dh = dout if dout.stride(1) == 1 else dout.contiguous()
-    grads: List[Optional[torch.Tensor]] = [None] * (4 * n)
+def _towers_forward(towers, xs, params_list):
+    """The training forward of several towers of equal depth on their inputs xs (2-D fp32 views with unit column
+    stride; any row stride), layer by layer: per tower the batch statistics and the BatchNormalization fold, then ONE
+    grouped GEMM (bias + SELU epilogue) for the layer of every tower, then per tower the dropout.
+    Returns per tower (outputs per layer, batch means, batch variances, the step number that seeded the masks)."""
+    for x in xs:
+        if x.dim() != 2 or x.stride(1) != 1 or x.dtype != torch.float32:
+            raise ValueError("TrainTower input must be a 2-D fp32 tensor with unit column stride")
+    n = len(towers[0].units)
+    if any(len(t.units) != n for t in towers):
+        raise ValueError("towers of one grouped forward need equal depth")
+    dev, st = xs[0].device, L.stream_ptr(None)
+    steps = []
+    for t in towers:
+        steps.append(t.steps)
+        t.steps += 1
+    hs = list(xs)
+    res = [([], [], []) for _ in towers]
+    for l in range(n):
+        probs, folded = [], []
+        for ti, (tower, h, params) in enumerate(zip(towers, hs, params_list)):
+            W, b, g, be = params[4 * l: 4 * l + 4]
+            N, K = W.shape
+            M = h.shape[0]
+            mean = torch.empty(K, dtype=torch.float32, device=dev)
+            var = torch.empty(K, dtype=torch.float32, device=dev)
+            ws = _ws(M, K, dev)
+            L.call("rf_col_stats", L.ptr(h), M, K, h.stride(0), L.ptr(mean), L.ptr(var), L.ptr(ws), ws.numel(), st)
+            Wf = torch.empty_like(W)
+            bf = torch.empty(N, dtype=torch.float32, device=dev)
+            L.call("rf_bn_fold", L.ptr(W), N, K, L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(mean), L.ptr(var), tower.eps,
+                   L.ptr(Wf), L.ptr(bf), st)
+            y = torch.empty((M, N), dtype=torch.float32, device=dev)
+            res[ti][1].append(mean)
+            res[ti][2].append(var)
+            folded.append(Wf)
+            probs.append((h, Wf, bf, "selu", y))
+        if _BLASLT_WIDE and any(p[0].shape[1] >= _BLASLT_MIN_K for p in probs):
+            for (h, Wf, bf, _, y) in probs:  # A/B: the forward GEMMs on hipBLASLt / librf one by one
+                _linear_f32(h, Wf, bf, L.ACT["selu"], y, st)
+            ys = [p[4] for p in probs]
+        else:
+            ys = _gemm_layer(probs, False, True, st)
+        for ti, (tower, y) in enumerate(zip(towers, ys)):
+            M, N = y.shape
+            L.call("rf_dropout_fwd", L.ptr(y), M, N, N, tower.rate, layer_seed(tower.seed, steps[ti], l), L.ptr(y), N, st)
+            with torch.no_grad():
+                tower.moving_mean[l].mul_(tower.momentum).add_(res[ti][1][l], alpha=1.0 - tower.momentum)
+                tower.moving_var[l].mul_(tower.momentum).add_(res[ti][2][l], alpha=1.0 - tower.momentum)
+            res[ti][0].append(y)
+        hs = ys
+    return [(o, m, v, stp) for (o, m, v), stp in zip(res, steps)]
+
+
+def _towers_backward(towers, steps, xs, params_list, outs_l, means_l, vars_l, douts, dx_outs):
+    """Backward of _towers_forward: per tower the parameter gradients (W, b, gamma, beta per layer) returned, the
+    input gradients written into dx_outs (views of the xs' shapes; any row stride). Per layer, last to first: per tower
+    the SELU / dropout backward (dpre, the bias gradient); ONE grouped GEMM for every tower's Dense weight gradient
+    G = dpre^T h, per tower its fold (rf_bn_fold_grad); ONE grouped GEMM for dz = dpre W; per tower the
+    BatchNormalization backward."""
+    n = len(towers[0].units)
+    dev, st = xs[0].device, L.stream_ptr(None)
+    dhs = [d if d.stride(1) == 1 else d.contiguous() for d in douts]
+    grads = [[None] * (4 * n) for _ in towers]
     for l in reversed(range(n)):
-        W, b, g, be = params[4 * l: 4 * l + 4]
-        N, K = W.shape
-        h_in = x if l == 0 else outs[l - 1]
-        ws = _ws(M, max(K, N), dev)
-        dpre = torch.empty((M, N), dtype=torch.float32, device=dev)
-        db = torch.empty(N, dtype=torch.float32, device=dev)
-        L.call("rf_selu_dropout_bwd", L.ptr(dh), dh.stride(0), L.ptr(outs[l]), N, M, N, tower.rate,
-               layer_seed(tower.seed, step, l), L.ptr(dpre), N, L.ptr(db), L.ptr(ws), ws.numel(), st)
-        dW = torch.empty_like(W)
+        dpres, dbs, wss, hins = [], [], [], []
+        for ti, tower in enumerate(towers):
+            W = params_list[ti][4 * l]
+            N, K = W.shape
+            h_in = xs[ti] if l == 0 else outs_l[ti][l - 1]
+            M = h_in.shape[0]
+            ws = _ws(M, max(K, N), dev)
+            dpre = torch.empty((M, N), dtype=torch.float32, device=dev)
+            db = torch.empty(N, dtype=torch.float32, device=dev)
+            dh = dhs[ti]
+            L.call("rf_selu_dropout_bwd", L.ptr(dh), dh.stride(0), L.ptr(outs_l[ti][l]), N, M, N, tower.rate,
+                   layer_seed(tower.seed, steps[ti], l), L.ptr(dpre), N, L.ptr(db), L.ptr(ws), ws.numel(), st)
+            dpres.append(dpre)
+            dbs.append(db)
+            wss.append(ws)
+            hins.append(h_in)
+        dWs = [torch.empty_like(params_list[ti][4 * l]) for ti in range(len(towers))]
+
+        def wgrad(stream, stream_ptr):
+            if _BWD_BLAS:
+                Gs = [_mm(dp.t(), h, h.shape[1] <= 1024 and dp.shape[1] <= 1024) for dp, h in zip(dpres, hins)]
+            else:
+                Gs = _gemm_layer([(dp, h, None, "none", None) for dp, h in zip(dpres, hins)], True, False, stream_ptr)
+            for ti, tower in enumerate(towers):
+                W, b, g, be = params_list[ti][4 * l: 4 * l + 4]
+                N, K = W.shape
+                L.call("rf_bn_fold_grad", L.ptr(Gs[ti]), N, K, L.ptr(dbs[ti]), L.ptr(g), L.ptr(be),
+                       L.ptr(means_l[ti][l]), L.ptr(vars_l[ti][l]), tower.eps, L.ptr(dWs[ti]), stream_ptr)
+
+        def igrad(stream_ptr):
+            if _BWD_BLAS:
+                return [_mm(dp, params_list[ti][4 * l], True) for ti, dp in enumerate(dpres)]
+            return _gemm_layer([(dp, params_list[ti][4 * l], None, "none", None) for ti, dp in enumerate(dpres)],
+                               False, False, stream_ptr)
+
         if l == 0 and _WGRAD["on"]:
-            # the input gradient's GEMM first, on the main stream
-            dz = GM.gemm_f32(dpre, W, stream=st) if GM.supported(dpre, W) else torch.mm(dpre, W)
+            dzs = igrad(st)  # the input gradient's GEMM first, on the main stream
             main = torch.cuda.current_stream()
             side = _side_stream(dev)
             side.wait_stream(main)  # after dz: the weight gradient runs beside the BN backward and what follows
             with torch.cuda.stream(side):
-                Gw = GM.gemm_f32(dpre, h_in, trans_a=True, stream=side) if GM.supported(dpre, h_in) \
-                    else torch.mm(dpre.t(), h_in)
-                L.call("rf_bn_fold_grad", L.ptr(Gw), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
-                       L.ptr(vars_[l]), tower.eps, L.ptr(dW), L.stream_ptr(side))
+                wgrad(side, L.stream_ptr(side))
                 done = torch.cuda.Event()
                 done.record(side)
-            for t in (dpre, h_in, db, g, be, means[l], vars_[l], dW, W):  # read / written on the side stream
-                t.record_stream(side)
+            for ti in range(len(towers)):  # read / written on the side stream
+                for t in (dpres[ti], hins[ti], dbs[ti], means_l[ti][l], vars_l[ti][l], dWs[ti], *params_list[ti][4 * l: 4 * l + 4]):
+                    t.record_stream(side)
             _WGRAD["events"].append(done)
-            del Gw
-        elif _BWD_BLAS or not GM.supported(dpre, h_in, W):
-            small = K <= 1024 and N <= 1024
-            Gw = _mm(dpre.t(), h_in, small)  # [N][K]: the Dense weight's gradient before the fold (A/B: torch.mm)
-            L.call("rf_bn_fold_grad", L.ptr(Gw), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
-                   L.ptr(vars_[l]), tower.eps, L.ptr(dW), st)
-            del Gw
-            dz = _mm(dpre, W, small)  # [M][K]
         else:
-            # G = dpre^T h [N][K] (the Dense weight's gradient before the fold) and dz = dpre W [M][K]: rf_gemm_f32
-            Gw = GM.gemm_f32(dpre, h_in, trans_a=True, stream=st)
-            L.call("rf_bn_fold_grad", L.ptr(Gw), N, K, L.ptr(db), L.ptr(g), L.ptr(be), L.ptr(means[l]),
-                   L.ptr(vars_[l]), tower.eps, L.ptr(dW), st)
-            del Gw
-            dz = GM.gemm_f32(dpre, W, stream=st)
-        dx = dx_out if l == 0 else torch.empty((M, K), dtype=torch.float32, device=dev)
-        dgamma = torch.empty(K, dtype=torch.float32, device=dev)
-        dbeta = torch.empty(K, dtype=torch.float32, device=dev)
-        L.call("rf_bn_bwd", L.ptr(dz), K, L.ptr(h_in), h_in.stride(0), M, K, L.ptr(means[l]), L.ptr(vars_[l]), L.ptr(g),
-               tower.eps, L.ptr(dx), dx.stride(0), L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), ws.numel(), st)
-        grads[4 * l: 4 * l + 4] = [dW, db, dgamma, dbeta]
-        dh = dx
+            wgrad(None, st)
+            dzs = igrad(st)
+        for ti, tower in enumerate(towers):
+            W, b, g, be = params_list[ti][4 * l: 4 * l + 4]
+            N, K = W.shape
+            h_in = hins[ti]
+            M = h_in.shape[0]
+            dx = dx_outs[ti] if l == 0 else torch.empty((M, K), dtype=torch.float32, device=dev)
+            dgamma = torch.empty(K, dtype=torch.float32, device=dev)
+            dbeta = torch.empty(K, dtype=torch.float32, device=dev)
+            dz = dzs[ti]
+            L.call("rf_bn_bwd", L.ptr(dz), dz.stride(0), L.ptr(h_in), h_in.stride(0), M, K, L.ptr(means_l[ti][l]),
+                   L.ptr(vars_l[ti][l]), L.ptr(g), tower.eps, L.ptr(dx), dx.stride(0), L.ptr(dgamma), L.ptr(dbeta),
+                   L.ptr(wss[ti]), wss[ti].numel(), st)
+            grads[ti][4 * l: 4 * l + 4] = [dWs[ti], dbs[ti], dgamma, dbeta]
+            dhs[ti] = dx
     return grads
 
 
 class _TowersFn(torch.autograd.Function):
     """Towers over column blocks of ONE input (the DSSM user and ad blocks of the fused encoder's output):
     the backward writes every tower's input gradient into its block of one full-width gradient, so autograd
-    never materialises zero-filled slice gradients and adds them."""
+    never materialises zero-filled slice gradients and adds them. Towers of equal depth run layer by layer
+    together (one grouped GEMM per layer and pass)."""
 
     @staticmethod
     def forward(ctx, x, blocks, *params):
-        outs_all, saved, meta = [], [], []
+        towers = [t for t, _, _ in blocks]
+        plist, p0 = [], 0
+        for t in towers:
+            np_ = 4 * len(t.units)
+            plist.append(params[p0: p0 + np_])
+            p0 += np_
+        xs = [x[:, off: off + width] for _, off, width in blocks]
+        groups = [[i] for i in range(len(towers))]
+        if len({len(t.units) for t in towers}) == 1:
+            groups = [list(range(len(towers)))]
+        res = [None] * len(towers)
+        for grp in groups:
+            for i, r in zip(grp, _towers_forward([towers[i] for i in grp], [xs[i] for i in grp], [plist[i] for i in grp])):
+                res[i] = r
+        saved, meta = [], []
         p0 = 0
-        for tower, off, width in blocks:
+        for (tower, off, width), (outs, means, vars_, step) in zip(blocks, res):
             np_ = 4 * len(tower.units)
-            ps = params[p0: p0 + np_]
-            outs, means, vars_, step = _tower_forward(tower, x[:, off: off + width], ps)
             meta.append((tower, off, width, step, p0, np_, len(saved)))
             saved += [*outs, *means, *vars_]
-            outs_all.append(outs[-1])
             p0 += np_
         ctx.meta = meta
+        ctx.groups = groups
         ctx.save_for_backward(x, *params, *saved)
-        return tuple(outs_all)
+        return tuple(r[0][-1] for r in res)
 
     @staticmethod
     def backward(ctx, *douts):
@@ -242,13 +311,21 @@ class _TowersFn(torch.autograd.Function):
         saved = ctx.saved_tensors[1 + nparams:]
         dx = torch.zeros_like(x) if sum(m[2] for m in ctx.meta) != x.shape[1] else torch.empty_like(x)
         grads: List[Optional[torch.Tensor]] = [None] * nparams
+        per = []
         for (tower, off, width, step, p0, np_, s0), dout in zip(ctx.meta, douts):
             n = len(tower.units)
             outs, means, vars_ = saved[s0: s0 + n], saved[s0 + n: s0 + 2 * n], saved[s0 + 2 * n: s0 + 3 * n]
             if dout is None:
                 dout = torch.zeros_like(outs[-1])
-            grads[p0: p0 + np_] = _tower_backward(tower, step, x[:, off: off + width], params[p0: p0 + np_], outs, means,
-                                                  vars_, dout, dx[:, off: off + width])
+            per.append((tower, step, x[:, off: off + width], params[p0: p0 + np_], outs, means, vars_, dout,
+                        dx[:, off: off + width], p0, np_))
+        for grp in ctx.groups:
+            sel = [per[i] for i in grp]
+            gs = _towers_backward([p[0] for p in sel], [p[1] for p in sel], [p[2] for p in sel], [p[3] for p in sel],
+                                  [p[4] for p in sel], [p[5] for p in sel], [p[6] for p in sel], [p[7] for p in sel],
+                                  [p[8] for p in sel])
+            for p, g in zip(sel, gs):
+                grads[p[9]: p[9] + p[10]] = g
         return (dx, None, *grads)
 
 

@@ -6,23 +6,25 @@
 //   input grad     dz = dpre W             A = dpre [M][K]    (k contiguous),   B = W   [K][N] (n contiguous)
 // C[m][n] = sum_k A(m, k) B(k, n) on v_mfma_f32_16x16x4_f32 (f32 products, f32 accumulation; gfx950 has no xf32).
 //
-// Schedule (one 128 x 128 output tile per workgroup at a time, 4 waves of 64 x 64, two workgroups per CU):
-//   * stream-K: the (tile, 32-k step) iterations of the whole GEMM are cut into G equal ranges, one per persistent
-//     workgroup (G = 2 per CU), so every workgroup does the same MFMA work whatever the tile count; ranges are
+// Schedule (one 128 x 128 output tile per workgroup at a time, 4 waves of 64 x 64, one workgroup per CU):
+//   * stream-K: the (tile, 64-k step) iterations of the whole GEMM are cut into G equal ranges, one per persistent
+//     workgroup (G = the CU count), so every workgroup does the same MFMA work whatever the tile count; ranges are
 //     laid out XCD-major (the workgroups of one XCD take consecutive tiles: their A rows / B columns share its L2);
 //   * a tile cut between workgroups: each stores its raw partial tile (write-through sc1 stores), one agent-scope
 //     ticket per workgroup, and the LAST to arrive adds every segment in k order (fixed: the result does not depend
 //     on arrival order) and runs the epilogue (MI355X_MICROARCH.md, inter-workgroup hand-off: sc1 payload,
 //     vmcnt(0), barrier, one relaxed agent-scope add whose return value names the last arriver, sc1 loads);
-//   * per 32-k step: the next step's 32 KB are loaded into registers (buffer loads, 4 x 16 B per thread and
-//     operand) one step ahead and written to the other half of a double-buffered LDS ring under this step's
-//     MFMAs; fragments of half 1 are read under half 0's MFMAs, and the next step's half 0 under half 1's:
-//     one barrier per step;
-//   * LDS formats: a k-contiguous operand keeps 128-byte rows (32 k), 16-byte chunk c of row r at c ^ ((r >> 1) & 7)
+//   * per 64-k step (256 MFMAs per wave, in four quarters of 64): the next step's 64 KB sit in registers (buffer
+//     loads, 8 x 16 B per thread and operand, issued one step ahead) and are copied into the other half of a
+//     double-buffered LDS ring, one (copy, reload) pair per 12 MFMAs over the first three quarters; each quarter
+//     reads the next quarter's fragments; one barrier per step, 16 MFMAs into the last quarter. Measured on the
+//     tower shapes (tools/gemm32_cmp.sh): bursts of copies or loads between consecutive MFMAs starve the MFMA pipe
+//     (clustered: 0.87 of peak; one pair per 5 MFMAs: 0.90; per 12: 0.91-0.92);
+//   * LDS formats: a k-contiguous operand keeps 256-byte rows (64 k), 16-byte chunk c of row r at c ^ (r & 15)
 //     (the 16 rows of one ds_read_b128 quarter-wave hit 16 distinct bank groups); an m/n-contiguous operand keeps
-//     32 k-rows of 512 bytes, chunk c of k-row kk at c ^ (((kk >> 2) & 3) << 2) (the four lane groups of an MFMA
+//     64 k-rows of 512 bytes, chunk c of k-row kk at c ^ (((kk >> 2) & 3) << 2) (the four lane groups of an MFMA
 //     read four k-rows: distinct banks), read as ds_read_b32 (pairs of k-rows 512 B apart: ds_read2_b32);
-//   * both layouts feed the MFMA in one permuted k order: in half h, MFMA e takes k = 16 h + 4 lg + e in lane
+//   * both layouts feed the MFMA in one permuted k order: in quarter q, MFMA e takes k = 16 q + 4 lg + e in lane
 //     group lg.
 #include <hip/hip_runtime.h>
 
@@ -36,15 +38,17 @@ namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 128, kBN = 128, kBK = 32, kThreads = 256;
-constexpr int kStage = (kBM + kBN) * kBK;  // floats per LDS stage (32 KB)
+constexpr int kBM = 128, kBN = 128, kBK = 64, kThreads = 256;
+constexpr int kStage = (kBM + kBN) * kBK;  // floats per LDS stage (64 KB)
 constexpr int kSlot = kBM * kBN;           // floats per partial tile (64 KB)
-constexpr int kMinIters = 8;               // 32-k steps per workgroup at least (small GEMMs take fewer workgroups)
+constexpr int kMinIters = 2;               // 64-k steps per workgroup at least (small GEMMs take fewer workgroups)
 constexpr int kWgPerCu = 1;                // one 4-wave workgroup per CU: one wave per SIMD, registers to spare
 constexpr uint32_t kOOB = 0x80000000u;            // a buffer offset past every extent: the load returns zeros
 constexpr int kLdsBytes = 2 * kStage * 4 + 16;     // two stages + the last-arriver flag
 
-struct GemmArgs {
+// One GEMM of a launch (a launch runs up to kMaxProbs of them, same operand layouts: e.g. the same layer of both
+// DSSM towers); its tiles and 64-k steps continue the previous problem's in the stream-K numbering.
+struct Prob {
     const float* A;
     const float* B;
     float* C;
@@ -53,13 +57,34 @@ struct GemmArgs {
     int M, N, K;
     int act;
     int tiles_n, nk;
-    int64_t units;  // tiles * nk
-    int* cnt;       // one arrival counter per tile (zero between launches)
+    int64_t unit0;  // first stream-K unit (tile-major, 64-k steps minor) of this problem
+    int tile0;      // first global tile (arrival counter index)
+    int pad_;
+};
+constexpr int kMaxProbs = 4;
+
+struct GemmArgs {
+    Prob p[kMaxProbs];
+    int np;
     int one;        // 1 (a branch condition the compiler cannot fold)
+    int64_t units;  // all problems' units
+    int* cnt;       // one arrival counter per global tile (zero between launches)
     float* slots;   // 2 G partial tiles
 };
 
 __device__ __forceinline__ int64_t seg_lo(int64_t v, int64_t U, int G) { return v * U / G; }
+
+__device__ __forceinline__ int prob_of(const GemmArgs& g, int64_t x) {
+    int q = 0;
+    while (q + 1 < g.np && x >= g.p[q + 1].unit0) ++q;
+    return q;
+}
+
+// the global tile holding stream-K unit x
+__device__ __forceinline__ int gtile_of(const GemmArgs& g, int64_t x) {
+    const int q = prob_of(g, x);
+    return g.p[q].tile0 + (int)((x - g.p[q].unit0) / g.p[q].nk);
+}
 
 // the workgroup (virtual index) whose range holds iteration x
 __device__ __forceinline__ int seg_owner(int64_t x, int64_t U, int G) {
@@ -85,23 +110,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t b
 template <bool KC>
 struct Operand {
     __amdgpu_buffer_rsrc_t rs;
-    uint32_t voff[4];  // per chunk, at k = 0
-    uint32_t kstep;    // bytes per 32-k step
+    uint32_t voff[8];  // per chunk, at k = 0
+    uint32_t kstep;    // bytes per 64-k step
     int kcol;          // KC: this thread's k offset in a step (the K tail masks it)
-    uint32_t loff[4];  // LDS float offsets of the chunks
+    uint32_t loff[8];  // LDS float offsets of the chunks
 
     __device__ __forceinline__ void init(const float* p, int64_t ld, int rows, int row0, int K, int tid) {
         if constexpr (KC) {
-            const int ch = tid & 7, sw = (tid >> 4) & 7;
+            // 256-byte rows (64 k) = 16 chunks; 16 threads per row; chunk c of row r at c ^ (r & 15)
+            const int ch = tid & 15;
             kcol = ch * 4;
-            const int last = rows - 1 - row0;  // rows past the matrix re-read its last row (never stored)
+            const int last = rows - 1 - row0;
             rs = rsrc(p + (int64_t)row0 * ld, (int64_t)last * ld * 4 + (int64_t)K * 4);
             kstep = kBK * 4;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int r = (tid >> 3) + 32 * c;
+            for (int c = 0; c < 8; ++c) {
+                const int r = (tid >> 4) + 16 * c;
                 voff[c] = (uint32_t)(((int64_t)min(r, last) * ld + ch * 4) * 4);
-                loff[c] = r * 32 + ((ch ^ sw) << 2);
+                loff[c] = r * 64 + ((ch ^ (r & 15)) << 2);
             }
         } else {
             const int c32 = tid & 31;
@@ -109,7 +135,7 @@ struct Operand {
             rs = rsrc(p + row0, ((int64_t)(K - 1) * ld + (ld - row0)) * 4);
             kstep = (uint32_t)(kBK * ld * 4);
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < 8; ++c) {
                 const int kk = (tid >> 5) + 8 * c;
                 voff[c] = (uint32_t)(((int64_t)kk * ld + c32 * 4) * 4);
                 loff[c] = kk * 128 + ((c32 ^ (((kk >> 2) & 3) << 2)) << 2);
@@ -117,47 +143,42 @@ struct Operand {
         }
     }
 
-    // step kt's chunks into registers (kt may run past the segment: past K the loads return zeros)
-    __device__ __forceinline__ void load(f4 (&r)[4], int kt, int K) const {
+    __device__ __forceinline__ void load1(f4& r, int c, int kt, int K) const {
         const uint32_t ko = (uint32_t)kt * kstep;
         if constexpr (KC) {
             const bool ok = kt * kBK + kcol < K;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) r[c] = bload(rs, ok ? voff[c] + ko : kOOB);
+            r = bload(rs, ok ? voff[c] + ko : kOOB);
         } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) r[c] = bload(rs, voff[c] + ko);
+            r = bload(rs, voff[c] + ko);
         }
     }
-
-    __device__ __forceinline__ void store(const f4 (&r)[4], float* st) const {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) *reinterpret_cast<f4*>(st + loff[c]) = r[c];
+    __device__ __forceinline__ void store1(const f4& r, int c, float* st) const {
+        *reinterpret_cast<f4*>(st + loff[c]) = r;
     }
 };
 
-// fragments of half h: f[i][e] = X(k = 16 h + 4 lg + e, tile index t0 + 16 i + lr)
+// fragments of k-chunk q (16 k): f[i][e] = X(k = 16 q + 4 lg + e, tile index t0 + 16 i + lr)
 template <bool KC>
-__device__ __forceinline__ void read_frag(f4 (&f)[4], const float* st, int t0, int h, int lr, int lg) {
+__device__ __forceinline__ void read_frag(f4 (&f)[4], const float* st, int t0, int q, int lr, int lg) {
     if constexpr (KC) {
-        const int sw = (lr >> 1) & 7;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            f[i] = *reinterpret_cast<const f4*>(st + (t0 + 16 * i + lr) * 32 + (((4 * h + lg) ^ sw) << 2));
+            f[i] = *reinterpret_cast<const f4*>(st + (t0 + 16 * i + lr) * 64 + (((4 * q + lg) ^ lr) << 2));
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int col = t0 + 16 * i + lr;
-            const float* p = st + (((col >> 2) ^ (lg << 2)) << 2) + (col & 3) + (16 * h + 4 * lg) * 128;
+            const float* p = st + (((col >> 2) ^ (lg << 2)) << 2) + (col & 3) + (16 * q + 4 * lg) * 128;
 #pragma unroll
             for (int e = 0; e < 4; ++e) f[i][e] = p[e * 128];
         }
     }
 }
 
-__device__ __forceinline__ void mfma_half(f4 (&acc)[4][4], const f4 (&a)[4], const f4 (&b)[4]) {
+template <int E0 = 0, int E1 = 4>
+__device__ __forceinline__ void mfma_quarter(f4 (&acc)[4][4], const f4 (&a)[4], const f4 (&b)[4]) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+    for (int e = E0; e < E1; ++e)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -166,7 +187,7 @@ __device__ __forceinline__ void mfma_half(f4 (&acc)[4][4], const f4 (&a)[4], con
 
 template <bool AKC, bool BKC>
 __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
-    // DS read instructions per half-step for both operands: 4 ds_read_b128 (k-contiguous) or 8 ds_read2_b32 (else)
+    // DS read instructions per quarter-step for both operands: 4 ds_read_b128 (k-contiguous) or 8 ds_read2_b32 (else)
     constexpr int kFragReads = (AKC ? 4 : 8) + (BKC ? 4 : 8);
     extern __shared__ __attribute__((aligned(16))) float lds[];  // 2 stages + the last-arriver flag
     int& s_last = *reinterpret_cast<int*>(lds + 2 * kStage);
@@ -178,22 +199,26 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
     const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
     const int64_t U = g.units;
     const int64_t lo = seg_lo(v, U, G), hi = seg_lo(v + 1, U, G);
-    const int K = g.K;
+    const int lo_tile = gtile_of(g, lo);
 
     for (int64_t u = lo; u < hi;) {
-        const int tile = (int)(u / g.nk);
-        const int k_lo = (int)(u - (int64_t)tile * g.nk);
-        const int k_hi = (int)min<int64_t>(g.nk, hi - (int64_t)tile * g.nk);
-        u = (int64_t)tile * g.nk + k_hi;
-        const int m0 = (tile / g.tiles_n) * kBM, n0 = (tile % g.tiles_n) * kBN;
+        const Prob& P = g.p[prob_of(g, u)];
+        const int K = P.K;
+        const int tile = (int)((u - P.unit0) / P.nk);
+        const int64_t t_unit0 = P.unit0 + (int64_t)tile * P.nk;  // the tile's first unit
+        const int k_lo = (int)(u - t_unit0);
+        const int k_hi = (int)min<int64_t>(P.nk, hi - t_unit0);
+        u = t_unit0 + k_hi;
+        const int gt = P.tile0 + tile;
+        const int m0 = (tile / P.tiles_n) * kBM, n0 = (tile % P.tiles_n) * kBN;
 
         Operand<AKC> oa;
         Operand<BKC> ob;
-        oa.init(g.A, g.lda, g.M, m0, K, tid);
-        ob.init(g.B, g.ldb, g.N, n0, K, tid);
+        oa.init(P.A, P.lda, P.M, m0, K, tid);
+        ob.init(P.B, P.ldb, P.N, n0, K, tid);
         float bv[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bv[j] = g.bias ? g.bias[min(n0 + wn * 64 + 16 * j + lr, g.N - 1)] : 0.f;
+        for (int j = 0; j < 4; ++j) bv[j] = P.bias ? P.bias[min(n0 + wn * 64 + 16 * j + lr, P.N - 1)] : 0.f;
 
         f4 acc[4][4];
 #pragma unroll
@@ -202,87 +227,108 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
             for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
         __syncthreads();  // the previous segment's LDS reads and s_last are done
-        // two register sets: step j's chunks live in set j & 1 from their load (two steps ahead) to their copy into
-        // LDS (one step ahead)
-        f4 ra[2][4], rb[2][4];
-        oa.load(ra[0], k_lo, K);
-        ob.load(rb[0], k_lo, K);
-        oa.load(ra[1], k_lo + 1, K);
-        ob.load(rb[1], k_lo + 1, K);
-        oa.store(ra[0], lds);
-        ob.store(rb[0], lds + kBM * kBK);
-        oa.load(ra[0], k_lo + 2, K);
-        ob.load(rb[0], k_lo + 2, K);
+        // one register set: step kt's data is loaded during step kt - 2 ... written during step kt - 1
+        f4 ra[8], rb[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { oa.load1(ra[c], c, k_lo, K); ob.load1(rb[c], c, k_lo, K); }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { oa.store1(ra[c], c, lds); ob.store1(rb[c], c, lds + kBM * kBK); }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { oa.load1(ra[c], c, k_lo + 1, K); ob.load1(rb[c], c, k_lo + 1, K); }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
         f4 fa[2][4], fb[2][4];
         read_frag<AKC>(fa[0], lds, wm * 64, 0, lr, lg);
         read_frag<BKC>(fb[0], lds + kBM * kBK, wn * 64, 0, lr, lg);
 
-        // One step (32 k) of the tile. Branch-free: past the segment's last step the copies go to the dead stage and
-        // the loads re-read (or read zeros past K); both are unused.
-        // One step (32 k) of the tile. Branch-free: past the segment's last step the copies go to the dead stage and
-        // the loads re-read (or read zeros past K); both are unused. Every non-MFMA instruction is spread between
-        // MFMAs (a burst of LDS copies or buffer loads between consecutive MFMAs starves the MFMA pipe; measured:
-        // clustered copies cost 9 % of the loop, clustered loads 5 %).
-        auto step = [&](int kt, const float* cur, float* nxt, f4 (&rw)[4], f4 (&rwb)[4]) {
-            // phase 1, under half 0's 64 MFMAs: half 1's fragments of this step, then the next step's chunks (set
-            // rw) into the other stage
+        constexpr int G1 = kFragReads >= 16 ? 1 : 24 / kFragReads;  // reads G1 MFMAs apart
+        // One step (64 k) in four quarters of 64 MFMAs, each in a block of its own (behind branches the compiler
+        // cannot fold: MFMAs carry no chain, instruction selection would order them past the barrier):
+        //   Q0: MFMAs of chunk 0 | reads of chunk 1 | copies 0..7 of the next tile (A), loads of the tile after
+        //   Q1: MFMAs of chunk 1 | reads of chunk 2 | copies 0..7 (B), loads
+        //   Q2: MFMAs of chunk 2 | reads of chunk 3            then barrier (the next tile written, this read)
+        //   Q3: MFMAs of chunk 3 | reads of the next tile's chunk 0
+        // One step (64 k) in four quarters of 64 MFMAs, each in a block of its own (behind branches the compiler
+        // cannot fold: MFMAs carry no chain, instruction selection would order them past the barrier). The 16
+        // (copy, load) pairs of the next tile are spread over Q0..Q2 (6, 5, 5: one per 12 MFMAs); the barrier sits
+        // 16 MFMAs into Q3.
+#define RF_Q(ID, NP, PG)                                                                  \
+        do {                                                                              \
+            _Pragma("unroll") for (int q = 0; q < kFragReads; ++q) {                      \
+                __builtin_amdgcn_sched_group_barrier(0x008, G1, ID);                      \
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, ID);                       \
+            }                                                                             \
+            _Pragma("unroll") for (int q = 0; q < NP; ++q) {                              \
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, ID);                       \
+                __builtin_amdgcn_sched_group_barrier(0x008, PG / 2, ID);                  \
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, ID);                       \
+                __builtin_amdgcn_sched_group_barrier(0x008, PG - PG / 2, ID);             \
+            }                                                                             \
+            __builtin_amdgcn_sched_group_barrier(0x008, 64 - G1 * kFragReads - NP * PG, ID); \
+        } while (0)
+#define RF_SEP()                                         \
+        do {                                             \
+            __builtin_amdgcn_sched_barrier(0);           \
+            if (g.one) asm volatile("" ::: "memory");    \
+            __builtin_amdgcn_sched_barrier(0);           \
+        } while (0)
+        auto step = [&](int kt, const float* cur, float* nxt) {
+            // Q0: chunk 0's MFMAs | chunk 1's fragments | A chunks 0..5 of the next tile (copy, then reload)
             read_frag<AKC>(fa[1], cur, wm * 64, 1, lr, lg);
             read_frag<BKC>(fb[1], cur + kBM * kBK, wn * 64, 1, lr, lg);
-            oa.store(rw, nxt);
-            ob.store(rwb, nxt + kBM * kBK);
-            mfma_half(acc, fa[0], fb[0]);
-            constexpr int R1 = kFragReads, G1 = 24 / R1;  // reads spread over the first 24 MFMAs
 #pragma unroll
-            for (int q = 0; q < R1; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, G1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
+            for (int c = 0; c < 6; ++c) { oa.store1(ra[c], c, nxt); oa.load1(ra[c], c, kt + 2, K); }
+            mfma_quarter(acc, fa[0], fb[0]);
+            RF_Q(0, 6, 6);
+            RF_SEP();
+            // Q1: chunk 1 | chunk 2's fragments | A chunks 6, 7, B chunks 0..2
+            read_frag<AKC>(fa[0], cur, wm * 64, 2, lr, lg);
+            read_frag<BKC>(fb[0], cur + kBM * kBK, wn * 64, 2, lr, lg);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {  // each copy ahead of 5 MFMAs: the last one lands before the barrier's wait
-                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, (64 - G1 * R1) / 8, 0);
-            }
+            for (int c = 6; c < 8; ++c) { oa.store1(ra[c], c, nxt); oa.load1(ra[c], c, kt + 2, K); }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { ob.store1(rb[c], c, nxt + kBM * kBK); ob.load1(rb[c], c, kt + 2, K); }
+            mfma_quarter(acc, fa[1], fb[1]);
+            RF_Q(1, 5, 7);
+            RF_SEP();
+            // Q2: chunk 2 | chunk 3's fragments | B chunks 3..7
+            read_frag<AKC>(fa[1], cur, wm * 64, 3, lr, lg);
+            read_frag<BKC>(fb[1], cur + kBM * kBK, wn * 64, 3, lr, lg);
+#pragma unroll
+            for (int c = 3; c < 8; ++c) { ob.store1(rb[c], c, nxt + kBM * kBK); ob.load1(rb[c], c, kt + 2, K); }
+            mfma_quarter(acc, fa[0], fb[0]);
+            RF_Q(2, 5, 7);
+            RF_SEP();
+            // Q3: 16 MFMAs of chunk 3, the barrier, its other 48 under the next tile's chunk-0 fragments
+            mfma_quarter<0, 1>(acc, fa[1], fb[1]);
             __builtin_amdgcn_sched_barrier(0);
-            // The barrier sits in a block of its own behind a branch the compiler cannot fold (g.one == 1): MFMAs
-            // carry no chain, so within one block instruction selection may order them past it.
             if (g.one) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();  // the next stage is written; every wave is done reading this one
+                __builtin_amdgcn_s_barrier();  // the next tile is written; every wave is done reading this one
             }
             __builtin_amdgcn_sched_barrier(0);
-            // phase 2, under half 1's 64 MFMAs: the next step's half-0 fragments, then step kt + 3's chunks into the
-            // set just copied
             read_frag<AKC>(fa[0], nxt, wm * 64, 0, lr, lg);
             read_frag<BKC>(fb[0], nxt + kBM * kBK, wn * 64, 0, lr, lg);
-            oa.load(rw, kt + 3, K);
-            ob.load(rwb, kt + 3, K);
-            mfma_half(acc, fa[1], fb[1]);
+            mfma_quarter<1, 4>(acc, fa[1], fb[1]);
 #pragma unroll
-            for (int q = 0; q < R1; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, G1, 1);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, (64 - G1 * R1) / 8, 1);
-                __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+            for (int q = 0; q < kFragReads; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, G1 / 2 > 0 ? G1 / 2 : 1, 3);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 3);
             }
             __builtin_amdgcn_sched_barrier(0);
         };
         int kt = k_lo;
         for (; kt + 1 < k_hi; kt += 2) {
-            step(kt, lds, lds + kStage, ra[1], rb[1]);
-            step(kt + 1, lds + kStage, lds, ra[0], rb[0]);
+            step(kt, lds, lds + kStage);
+            step(kt + 1, lds + kStage, lds);
         }
-        if (kt < k_hi) step(kt, lds, lds + kStage, ra[1], rb[1]);
+        if (kt < k_hi) step(kt, lds, lds + kStage);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-        const bool full = k_lo == 0 && k_hi == g.nk;
+        const bool full = k_lo == 0 && k_hi == P.nk;
         if (!full) {
             // a cut tile: this segment's raw partial into its slot, one ticket; the last arriver combines in k order
-            const int slot_id = (tile == (int)(lo / g.nk)) ? 2 * v : 2 * v + 1;
+            const int slot_id = gt == lo_tile ? 2 * v : 2 * v + 1;
             float* slot = g.slots + (size_t)slot_id * kSlot;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -294,17 +340,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            const int v_first = seg_owner((int64_t)tile * g.nk, U, G);
-            const int v_last = seg_owner((int64_t)tile * g.nk + g.nk - 1, U, G);
+            const int v_first = seg_owner(t_unit0, U, G);
+            const int v_last = seg_owner(t_unit0 + P.nk - 1, U, G);
             if (tid == 0) {
-                const int old = __hip_atomic_fetch_add(g.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int old = __hip_atomic_fetch_add(g.cnt + gt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 s_last = old == v_last - v_first;
             }
             __syncthreads();
             if (!s_last) continue;
-            if (tid == 0) __hip_atomic_store(g.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) __hip_atomic_store(g.cnt + gt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (int w = v_first; w <= v_last; ++w) {
-                const int sid = (tile == (int)(seg_lo(w, U, G) / g.nk)) ? 2 * w : 2 * w + 1;
+                const int sid = gt == gtile_of(g, seg_lo(w, U, G)) ? 2 * w : 2 * w + 1;
                 const float* p = g.slots + (size_t)sid * kSlot;
                 float t[4][4][4];
 #pragma unroll
@@ -324,7 +370,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
             }
         }
         // epilogue: bias + activation, values first, stores after (unguarded on interior tiles)
-        rf_act::with_act(g.act, [&](auto F) {
+        rf_act::with_act(P.act, [&](auto F) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -333,12 +379,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
                     for (int r = 0; r < 4; ++r) acc[i][j][r] = F(acc[i][j][r] + bv[j]);
         });
         const int rbase = m0 + wm * 64 + lg * 4, cbase = n0 + wn * 64 + lr;
-        if (m0 + kBM <= g.M && n0 + kBN <= g.N) {
+        if (m0 + kBM <= P.M && n0 + kBN <= P.N) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float* yr = g.C + (int64_t)(rbase + 16 * i + r) * g.ldc + cbase;
+                    float* yr = P.C + (int64_t)(rbase + 16 * i + r) * P.ldc + cbase;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) yr[16 * j] = acc[i][j][r];
                 }
@@ -348,11 +394,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = rbase + 16 * i + r;
-                    if (row >= g.M) continue;
-                    float* yr = g.C + (int64_t)row * g.ldc + cbase;
+                    if (row >= P.M) continue;
+                    float* yr = P.C + (int64_t)row * P.ldc + cbase;
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (cbase + 16 * j < g.N) yr[16 * j] = acc[i][j][r];
+                        if (cbase + 16 * j < P.N) yr[16 * j] = acc[i][j][r];
                 }
         }
     }
@@ -378,40 +424,58 @@ extern "C" size_t rf_gemm_f32_ws_bytes(int64_t M, int64_t N, int64_t K) {
     return cnt_bytes(tiles_of(M, N)) + slot_bytes();
 }
 
-extern "C" int rf_gemm_f32(const float* A, int64_t lda, int32_t a_kc, const float* B, int64_t ldb, int32_t b_kc,
-                           int64_t M, int64_t N, int64_t K, const float* bias, int32_t act, float* C, int64_t ldc,
-                           void* ws, size_t ws_bytes, void* stream) {
-    RF_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30),
-               "rf_gemm_f32: bad shape");
-    RF_REQUIRE(act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX, "rf_gemm_f32: activation must be elementwise");
-    if (M == 0 || N == 0) return RF_OK;
-    RF_REQUIRE((K == 0 || (A && B)) && C && ws, "rf_gemm_f32: null pointer");
-    RF_REQUIRE(K == 0 || (K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0),
-               "rf_gemm_f32: K, lda, ldb must be multiples of 4 and A, B 16-byte aligned");
-    RF_REQUIRE(K == 0 || ((a_kc ? lda >= K : lda >= M) && (b_kc ? ldb >= K : ldb >= N)), "rf_gemm_f32: leading dimension too small");
-    RF_REQUIRE(ldc >= N,
-               "rf_gemm_f32: leading dimension too small");
-    // 32-bit buffer offsets: a k-contiguous operand's 128-row tile block, an m/n-contiguous operand's whole K rows
-    RF_REQUIRE((a_kc ? 128 * (__int128)lda : (K + 64) * (__int128)lda) * 4 < ((__int128)1 << 31) &&
-                   (b_kc ? 128 * (__int128)ldb : (K + 64) * (__int128)ldb) * 4 < ((__int128)1 << 31),
-               "rf_gemm_f32: operand block exceeds 2 GiB (32-bit buffer offsets)");
-    const int64_t tiles = tiles_of(M, N);
-    RF_REQUIRE(ws_bytes >= rf_gemm_f32_ws_bytes(M, N, K), "rf_gemm_f32: workspace too small");
+extern "C" size_t rf_gemm_f32_grouped_ws_bytes(const rf_gemm_f32_problem* probs, int32_t n) {
+    int64_t tiles = 0;
+    for (int i = 0; probs && i < n; ++i) tiles += tiles_of(probs[i].M, probs[i].N);
+    return cnt_bytes(tiles) + slot_bytes();
+}
+
+extern "C" int rf_gemm_f32_grouped(const rf_gemm_f32_problem* probs, int32_t n, int32_t a_kc, int32_t b_kc, void* ws,
+                                   size_t ws_bytes, void* stream) {
+    RF_REQUIRE(probs && n >= 1 && n <= kMaxProbs, "rf_gemm_f32_grouped: 1..%d problems", kMaxProbs);
+    RF_REQUIRE(ws, "rf_gemm_f32_grouped: null workspace");
     GemmArgs g{};
-    g.A = A;
-    g.B = B;
-    g.C = C;
-    g.bias = bias;
-    g.lda = lda;
-    g.ldb = ldb;
-    g.ldc = ldc;
-    g.M = (int)M;
-    g.N = (int)N;
-    g.K = (int)K;
-    g.act = act;
-    g.tiles_n = (int)((N + kBN - 1) / kBN);
-    g.nk = (int)std::max<int64_t>((K + kBK - 1) / kBK, 1);
-    g.units = tiles * g.nk;
+    int64_t units = 0, tiles = 0;
+    for (int i = 0; i < n; ++i) {
+        const rf_gemm_f32_problem& q = probs[i];
+        const int64_t M = q.M, N = q.N, K = q.K, lda = q.lda, ldb = q.ldb, ldc = q.ldc;
+        RF_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30),
+                   "rf_gemm_f32: bad shape (problem %d)", i);
+        RF_REQUIRE(q.act >= RF_ACT_NONE && q.act < RF_ACT_SOFTMAX, "rf_gemm_f32: activation must be elementwise");
+        if (M == 0 || N == 0) continue;
+        RF_REQUIRE((K == 0 || (q.A && q.B)) && q.C, "rf_gemm_f32: null pointer (problem %d)", i);
+        RF_REQUIRE(K == 0 || (K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)q.A & 15) == 0 &&
+                              ((uintptr_t)q.B & 15) == 0),
+                   "rf_gemm_f32: K, lda, ldb must be multiples of 4 and A, B 16-byte aligned");
+        RF_REQUIRE(K == 0 || ((a_kc ? lda >= K : lda >= M) && (b_kc ? ldb >= K : ldb >= N)),
+                   "rf_gemm_f32: leading dimension too small");
+        RF_REQUIRE(ldc >= N, "rf_gemm_f32: leading dimension too small");
+        // 32-bit buffer offsets: a k-contiguous operand's 128-row tile block, an m/n-contiguous operand's K + 192 rows
+        RF_REQUIRE((a_kc ? 128 * (__int128)lda : (K + 192) * (__int128)lda) * 4 < ((__int128)1 << 31) &&
+                       (b_kc ? 128 * (__int128)ldb : (K + 192) * (__int128)ldb) * 4 < ((__int128)1 << 31),
+                   "rf_gemm_f32: operand block exceeds 2 GiB (32-bit buffer offsets)");
+        Prob& P = g.p[g.np++];
+        P.A = q.A;
+        P.B = q.B;
+        P.C = q.C;
+        P.bias = q.bias;
+        P.lda = lda;
+        P.ldb = ldb;
+        P.ldc = ldc;
+        P.M = (int)M;
+        P.N = (int)N;
+        P.K = (int)K;
+        P.act = q.act;
+        P.tiles_n = (int)((N + kBN - 1) / kBN);
+        P.nk = (int)std::max<int64_t>((K + kBK - 1) / kBK, 1);
+        P.unit0 = units;
+        P.tile0 = (int)tiles;
+        tiles += tiles_of(M, N);
+        units += tiles_of(M, N) * P.nk;
+    }
+    if (g.np == 0) return RF_OK;
+    RF_REQUIRE(ws_bytes >= cnt_bytes(tiles) + slot_bytes(), "rf_gemm_f32: workspace too small");
+    g.units = units;
     g.one = 1;
     // counters at the start, partial slots at the far end: one zeroed ws serves calls of any shape it is large
     // enough for (a smaller call's slots never land on a larger call's counters)
@@ -435,4 +499,11 @@ extern "C" int rf_gemm_f32(const float* A, int64_t lda, int32_t a_kc, const floa
     }
     hipLaunchKernelGGL(kerns[which], dim3(G), dim3(kThreads), kLdsBytes, st, g);
     return rf_check_launch("gemm32_kernel");
+}
+
+extern "C" int rf_gemm_f32(const float* A, int64_t lda, int32_t a_kc, const float* B, int64_t ldb, int32_t b_kc,
+                           int64_t M, int64_t N, int64_t K, const float* bias, int32_t act, float* C, int64_t ldc,
+                           void* ws, size_t ws_bytes, void* stream) {
+    const rf_gemm_f32_problem p{A, lda, B, ldb, C, ldc, bias, M, N, K, act, 0};
+    return rf_gemm_f32_grouped(&p, 1, a_kc, b_kc, ws, ws_bytes, stream);
 }

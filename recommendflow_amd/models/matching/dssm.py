@@ -14,7 +14,7 @@ from typing import Optional
 
 import torch
 
-from ...backend.blocks.mlp import create_mlp
+from ...backend.blocks.mlp import create_mlp, forward_towers
 from ...backend.encoder.sparse_encoder import FusedSparseEncoder
 from ...backend.layers.core import BatchNormalization
 from ...runtime.batch import SparseBatch
@@ -31,10 +31,14 @@ class Dssm(torch.nn.Module):
         self.ad_dense = create_mlp(list(units), 0.3, "selu", bn, name="ad_dense_tower",
                                    in_features=ad_encoder.out_width, dtype=tower_dtype, seed=seed + 2, device=device)
 
-    def embed(self, user: SparseBatch, ad: SparseBatch):
-        u = self.user_dense(self.enc_u(user))
-        a = self.ad_dense(self.enc_a(ad))
+    def towers(self, xu: torch.Tensor, xa: torch.Tensor):
+        """l2norm(user_tower(xu)), l2norm(ad_tower(xa)) from the pooled encoder outputs: both towers layer by layer
+        (backend.blocks.mlp.forward_towers: the small layers of both towers share one launch)."""
+        u, a = forward_towers([self.user_dense, self.ad_dense], [xu, xa])
         return torch.nn.functional.normalize(u, dim=-1, eps=1e-6), torch.nn.functional.normalize(a, dim=-1, eps=1e-6)
+
+    def embed(self, user: SparseBatch, ad: SparseBatch):
+        return self.towers(self.enc_u(user), self.enc_a(ad))
 
     def forward(self, user: SparseBatch, ad: SparseBatch) -> torch.Tensor:
         u, a = self.embed(user, ad)

@@ -6,11 +6,13 @@ covers the three layouts:
     forward        y  = act(x W^T + b)   gemm_f32(x, W, trans_b=True)      A k-contiguous, B k-contiguous
     weight grad    G  = dpre^T h         gemm_f32(dpre, h, trans_a=True)   A m-contiguous, B n-contiguous
     input grad     dz = dpre W           gemm_f32(dpre, W)                 A k-contiguous, B n-contiguous
+gemm_f32_grouped runs up to 4 such GEMMs of one layout in one launch (the same layer of both towers).
 The workspace (per-tile counters that every launch leaves zero, then the stream-K partial tiles) is allocated
 zeroed once per (device, stream) and grown as needed; calls on one stream share it.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
@@ -69,3 +71,60 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: b
            L.ACT[act], L.ptr(out), out.stride(0), L.ptr(ws), ws.numel(), st)
     calls += 1
     return out
+
+
+def gemm_f32_grouped(problems, trans_a: bool = False, trans_b: bool = False, stream=None):
+    """One launch for every (a, b, bias, act, out) of `problems` (1..4, one layout for all): out = act(op(a) op(b) +
+    bias) as gemm_f32 computes it. Returns the outputs."""
+    global calls
+    if not 1 <= len(problems) <= 4:
+        raise ValueError("rf_gemm_f32_grouped: 1..4 problems")
+    arr = (L.GemmProblem * len(problems))()
+    outs = []
+    for i, (a, b, bias, act, out) in enumerate(problems):
+        M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+        N, Kb = (b.shape[0], b.shape[1]) if trans_b else (b.shape[1], b.shape[0])
+        if Kb != K:
+            raise ValueError(f"rf_gemm_f32_grouped: inner dimensions differ ({K} vs {Kb}) in problem {i}")
+        _op(a, not trans_a)
+        _op(b, trans_b)
+        if out is None:
+            out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+        arr[i] = L.GemmProblem(L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), L.ptr(out), out.stride(0), L.ptr(bias),
+                               M, N, K, L.ACT[act], 0)
+        outs.append(out)
+    st = stream if isinstance(stream, int) else L.stream_ptr(stream)
+    lib = L.load()
+    need = int(lib.rf_gemm_f32_grouped_ws_bytes(ctypes.cast(arr, ctypes.c_void_p), len(problems)))
+    ws = _workspace(problems[0][0].device, st, need)
+    L.call("rf_gemm_f32_grouped", ctypes.cast(arr, ctypes.c_void_p), len(problems), int(not trans_a), int(trans_b), L.ptr(ws), ws.numel(), st)
+    calls += 1
+    return outs
+
+
+def _tiles(M: int, N: int) -> int:
+    return ((M + 127) // 128) * ((N + 127) // 128)
+
+
+def group_pays(shapes, cus: int = None) -> bool:
+    """Whether one grouped launch beats one launch per problem for these (M, N) output shapes: grouping fills the
+    chip with problems too small to fill it alone (the towers' 512- and 256-wide layers: 0.61 -> 0.79 and 0.27 ->
+    0.45 of peak, tools/gemm32_group_probe.py), but a problem with a tile per CU already runs each CU's tile whole,
+    and sharing its grid with another problem cuts tiles between workgroups (the 1024-wide input layers: 0.915 ->
+    0.849)."""
+    if cus is None:
+        cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return len(shapes) > 1 and max(_tiles(M, N) for M, N in shapes) < cus
+
+
+def gemm_f32_layer(problems, trans_a: bool = False, trans_b: bool = False, stream=None):
+    """The same layer of several towers: one grouped launch when group_pays, else one launch per problem."""
+    shapes = []
+    for a, b, _, _, _ in problems:
+        M = a.shape[1] if trans_a else a.shape[0]
+        N = b.shape[0] if trans_b else b.shape[1]
+        shapes.append((M, N))
+    if group_pays(shapes):
+        return gemm_f32_grouped(problems, trans_a=trans_a, trans_b=trans_b, stream=stream)
+    return [gemm_f32(a, b, trans_a=trans_a, trans_b=trans_b, bias=bias, act=act, out=out, stream=stream)
+            for a, b, bias, act, out in problems]

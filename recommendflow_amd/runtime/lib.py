@@ -106,6 +106,8 @@ _SIGS = {
     "rf_adam_untouched": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp,
                                          ctypes.c_size_t, _vp]),
     "rf_gemm_f32_ws_bytes": (ctypes.c_size_t, [_i64, _i64, _i64]),
+    "rf_gemm_f32_grouped_ws_bytes": (ctypes.c_size_t, [_vp, _i32]),
+    "rf_gemm_f32_grouped": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, ctypes.c_size_t, _vp]),
     "rf_gemm_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _i32, _i64, _i64, _i64, _vp, _i32, _vp, _i64, _vp,
                                    ctypes.c_size_t, _vp]),
     "rf_tower_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
@@ -133,6 +135,12 @@ class IdsTask(ctypes.Structure):
     """include/rf_api.h rf_ids_task (rf_single_token_ids_multi_fwd)."""
     _fields_ = [("slots", _vp), ("tok_bytes", _vp), ("tok_off", _vp), ("bag_off", _vp), ("lmax", _vp), ("ids", _vp),
                 ("table_rows", _i64), ("n_slots", _i32), ("batch", _i32), ("flags", _i32), ("reserved", _i32)]
+
+
+class GemmProblem(ctypes.Structure):
+    """include/rf_api.h rf_gemm_f32_problem."""
+    _fields_ = [("A", _vp), ("lda", _i64), ("B", _vp), ("ldb", _i64), ("C", _vp), ("ldc", _i64), ("bias", _vp),
+                ("M", _i64), ("N", _i64), ("K", _i64), ("act", _i32), ("reserved", _i32)]
 
 
 class RFError(RuntimeError):

@@ -100,3 +100,41 @@ def test_output_row_stride_and_views(cuda):
     G.gemm_f32(x[:, 8704:], W, trans_b=True, out=out[:, 1024:])
     _check(out[:, 1024:], x[:, 8704:], W, False, True, None, "none")
     assert torch.isnan(out[:, :1024]).all()  # nothing written outside the view
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False)])
+def test_grouped_problems_vs_float64(cuda, ta, tb):
+    """rf_gemm_f32_grouped: the same layer of the two DSSM towers in one launch (their tiles share the stream-K grid)
+    plus a ragged third and fourth problem; every output vs float64, replays bit-identical."""
+    shapes = [(4096, 512, 1024), (4096, 512, 1024), (300, 200, 100), (132, 68, 4100)] if not ta else \
+        [(512, 1024, 4096), (512, 1024, 4096), (300, 200, 100), (132, 68, 4100)]
+    probs = []
+    for i, (M, N, K) in enumerate(shapes):
+        a, b, bias = _operands(M, N, K, ta, tb, seed=50 + i)
+        probs.append((a, b, bias, "selu" if i % 2 else "none", None))
+    outs = G.gemm_f32_grouped(probs, trans_a=ta, trans_b=tb)
+    for (a, b, bias, act, _), c in zip(probs, outs):
+        _check(c, a, b, ta, tb, bias, act)
+    outs2 = G.gemm_f32_grouped(probs, trans_a=ta, trans_b=tb)
+    assert all(torch.equal(x, y) for x, y in zip(outs, outs2))
+
+
+def test_forward_towers_matches_each_tower(cuda):
+    """backend.blocks.mlp.forward_towers (the DSSM inference towers layer by layer, one grouped launch per layer)
+    against each MLP's own forward: the same folded weights and epilogue, so equal within fp32 summation order."""
+    from recommendflow_amd.backend.blocks.mlp import create_mlp, forward_towers
+    from recommendflow_amd.backend.layers.core import BatchNormalization
+
+    bn = BatchNormalization(epsilon=1e-6)
+    mu = create_mlp([1024, 512, 256], 0.3, "selu", bn, in_features=8704, dtype=torch.float32, seed=1)
+    ma = create_mlp([1024, 512, 256], 0.3, "selu", bn, in_features=20480, dtype=torch.float32, seed=2)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randn(1024, 8704 + 20480, device="cuda", generator=g) * 0.05
+    xu, xa = x[:, :8704], x[:, 8704:]
+    n0 = G.calls
+    u, a = forward_towers([mu, ma], [xu, xa])
+    want = sum(1 if G.group_pays([(1024, u), (1024, u)]) else 2 for u in (1024, 512, 256))
+    assert G.calls - n0 == want  # grouped where it pays (layers without a tile per CU), else one launch each
+    u1, a1 = mu(xu), ma(xa)
+    torch.testing.assert_close(u, u1, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(a, a1, rtol=1e-5, atol=1e-5)
