@@ -728,7 +728,31 @@ def bench_sharded_sim(args, specs, multi, P):
     S = len(specs)
     n_bins = args.shard_rows * P // (2 * S)
     sp = [SlotSpec(s.name, n_bins, s.seeds, s.combiner, s.mask_empty) for s in specs]
-    comm = LoopbackComm(P)
+
+    class CountingLoopback(LoopbackComm):
+        """LoopbackComm that also counts the bytes each exchange sends and times its device copy."""
+
+        def __init__(self, world):
+            super().__init__(world)
+            self.reset()
+
+        def reset(self):
+            self.bytes, self.events = [], []
+
+        def exchange(self, x, send_splits, recv_splits):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            y = x.clone()
+            e1.record()
+            self.bytes.append(x.numel() * x.element_size())
+            self.events.append((e0, e1))
+            return y
+
+        def copy_ms(self):
+            torch.cuda.synchronize()
+            return sum(a.elapsed_time(b) for a, b in self.events)
+
+    comm = CountingLoopback(P)
     enc = ShardedFusedEncoder(sp, D, 0, P, comm=comm, seed=2024)
     batches = [synthetic_batch(B, multi, seed=4321 + i).to("cuda") for i in range(2)]
     out = torch.empty((B, enc.out_width), dtype=torch.float32, device="cuda")
@@ -763,7 +787,49 @@ def bench_sharded_sim(args, specs, multi, P):
     el = time.perf_counter() - t0
     stage = {n: round(sum(e[k].elapsed_time(e[k + 1]) for e in evs) / steps, 4) for k, n in enumerate(names)}
     row_b = D * 4
+    # per-step bytes each way of the row-return exchange (ids out, rows back; the own-rank share never leaves
+    # the GPU) and the owner-side partial-pooling exchange (entries out, one partial per (unit, owner) back), and
+    # each mode's predicted step at P with the all-to-alls at xGMI's 7 x 153 GB/s per GPU in place of
+    # the loopback copies (no overlap assumed: the plain forward runs them in line)
+    xgmi = 7 * 153e9
+    remote = (P - 1) / P
+    comm.reset()
+    step(0)
+    torch.cuda.synchronize()
+    row_bytes = [b * remote for b in comm.bytes]
+    row_copy_ms = comm.copy_ms()
+    el_ms = el / steps * 1e3
+    row_pred = el_ms - row_copy_ms + sum(row_bytes) / xgmi * 1e3
+    partial = {}
+    try:
+        for i in range(3):
+            enc.forward_partial(batches[i % 2], out)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            enc.forward_partial(batches[i % 2], out)
+        torch.cuda.synchronize()
+        pp_ms = (time.perf_counter() - t0) / steps * 1e3
+        comm.reset()
+        enc.forward_partial(batches[0], out)
+        torch.cuda.synchronize()
+        pp_bytes = [b * remote for b in comm.bytes]
+        pp_copy_ms = comm.copy_ms()
+        pp_pred = pp_ms - pp_copy_ms + sum(pp_bytes) / xgmi * 1e3
+        partial = {"ms_per_step": round(pp_ms, 4), "loopback_copy_ms": round(pp_copy_ms, 4),
+                   "xgmi_bytes_each_way": {"entries_out": int(pp_bytes[0]), "partials_back": int(pp_bytes[1])},
+                   "predicted_ms_at_xgmi": round(pp_pred, 4)}
+    except Exception as e:  # noqa: BLE001
+        partial = {"error": f"{type(e).__name__}: {e}"[:200]}
+    pp_pred = partial.get("predicted_ms_at_xgmi")
+    res_modes = {"row_return": {"ms_per_step": round(el_ms, 4), "loopback_copy_ms": round(row_copy_ms, 4),
+                                "xgmi_bytes_each_way": {"ids_out": int(row_bytes[0]), "rows_back": int(row_bytes[1])},
+                                "predicted_ms_at_xgmi": round(row_pred, 4)},
+                 "partial_pool": partial,
+                 "default_by_prediction": ("partial_pool" if pp_pred is not None and pp_pred < row_pred else "row_return"),
+                 "xgmi_GBs_per_gpu": xgmi / 1e9}
     res = {"ms_per_step": round(el / steps * 1e3, 4), "examples_per_s_this_rank": round(B * steps / el, 1),
+           "modes": res_modes,
            "stage_ms": stage, "rows_read_by_pool": st["logical"], "rows_requested_after_dedup": st["req"],
            "requests_local_in_place": int((st["row_map"] < 0).sum()),  # row_map bit 31: read from the own shard
            "requests_remote": int((st["row_map"] >= 0).sum()),
