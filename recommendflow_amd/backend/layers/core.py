@@ -82,9 +82,9 @@ class Dense(torch.nn.Module):
         return self._linear(x, self.weight, self.bias, out, stream)
 
     def _linear(self, x, weight, bias, out, stream):
-        """rf_linear_fwd, or its split-K form when the shape asks for one (fp32 deep-K layers at a grid of at
-        most one 128-tile per CU: rf_linear_splitk_ws_bytes > 0); the partial-sum workspace comes from the
-        caching allocator on the launch stream."""
+        """fp32: rf_gemm_f32 (stream-K, bias + activation in the epilogue; hipBLASLt only behind
+        RF_TOWER_BLASLT_WIDE=1). bf16, and fp32 shapes rf_gemm_f32 refuses: rf_linear_fwd, or its split-K form
+        when rf_linear_splitk_ws_bytes > 0 (workspace from the caching allocator on the launch stream)."""
         M, dt = x.shape[0], L.torch_dtype_code(self.dtype)
         blaslt = (_BLASLT_WIDE and self.dtype == torch.float32 and self.in_features >= _BLASLT_MIN_K
                   and out.is_contiguous() and self.activation in (None, "none", "linear", "relu", "selu"))
@@ -94,8 +94,7 @@ class Dense(torch.nn.Module):
             return G.gemm_f32(x, weight, trans_b=True, bias=bias, act=self.activation or "none", out=out,
                               stream=stream)
         if blaslt:
-            # fp32 deep-K layers (the DSSM towers' 8704 / 20480-wide inputs): hipBLASLt's kernel with its bias
-            # epilogue runs them at 146-151 TF/s against 123-130 for rf_linear_splitk_fwd
+            # A/B only: hipBLASLt's fp32 kernel with its bias epilogue, SELU / ReLU in place after
             with torch.cuda.stream(stream) if isinstance(stream, torch.cuda.Stream) else _nullctx():
                 if bias is None:
                     torch.mm(x, weight.t(), out=out)
