@@ -691,7 +691,9 @@ __device__ __forceinline__ void ln_fold_row_stats(const float2* rs2, int P, int 
 // chunks (k = 4 lg .. 4 lg + 3 and 16 + 4 lg .. 16 + 4 lg + 3) feed 8 MFMAs, A and B in the same permuted k order.
 // SPLIT (split-K, EPI plain only): blockIdx.y = s takes k in [s kspan, min(K, (s + 1) kspan)) and stores raw
 // partial sums to y + s M ldy (splitk_reduce_kernel adds them in order s = 0, 1, ... with the bias / activation).
-template <int BM, int EPI = kEpiPlain, bool F32 = false, bool SPLIT = false>
+// ST: ring depth (kLdsStages by default; launch_lds_epi takes a deeper ring when the grid holds at most one tile per
+// CU, where no second workgroup covers the load waits)
+template <int BM, int EPI = kEpiPlain, bool F32 = false, bool SPLIT = false, int ST = kLdsStages>
 __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ xv, const void* __restrict__ wv,
                                                        const float* __restrict__ bias, float* __restrict__ y, int64_t M,
                                                        int N, int K, int64_t ldx, int64_t ldy, int act, EpiArgs ea,
@@ -734,7 +736,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
     auto As = [&](int s) { return lds + s * (A_EL + B_EL); };
     auto Bs = [&](int s) { return lds + s * (A_EL + B_EL) + A_EL; };
 #pragma unroll
-    for (int p = 0; p + 1 < kLdsStages; ++p)
+    for (int p = 0; p + 1 < ST; ++p)
         if (p < nk) glds_stage<BM, (int)sizeof(T)>(x, w, M, N, ldx, ldw, m0, n0, p * kK, As(p), Bs(p), tid);
     // The epilogue's per-column parameters (bias, or the LN fold's s_c / t_c) are loaded now, under the first
     // stage's copies, instead of as dependent loads after the last MFMA (one HBM round trip off the tail).
@@ -759,7 +761,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
         }
     }
     // LN-fold row statistics (mu, rstd per tile row), in an LDS area past the ring
-    float* srow = reinterpret_cast<float*>(smem_raw + (size_t)kLdsStages * (A_EL + B_EL) * sizeof(T));
+    float* srow = reinterpret_cast<float*>(smem_raw + (size_t)ST * (A_EL + B_EL) * sizeof(T));
     // LN fold: the tile's row statistics (complete: the previous launch wrote them) are combined in a fixed order
     // (TPR threads per row, each a strided subset, then a commutative lane combine: every lane the same bits).
     // Their loads are issued here, into registers, and the combine runs after the k-loop, so the two dependent
@@ -787,15 +789,18 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
         }
     }
     for (int kt = 0; kt < nk; ++kt) {
-        const int s = kt % kLdsStages;
-        // stage kt must have landed; the stages issued after it (at most kLdsStages - 2) may stay in flight
-        if (kLdsStages >= 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+        const int s = kt % ST;
+        // stage kt must have landed; the stages issued after it (min(ST - 2, nk - 1 - kt)) may stay in flight
+        // (vmcnt retires in issue order; the epilogue parameter loads issued after the prologue only make it wait longer)
+        const int ahead = min(ST - 2, nk - 1 - kt);
+        if (ST >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+        else if (ST >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage kt landed for every wave; every wave is done reading stage kt - 1
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + kLdsStages - 1 < nk) {
-            const int s2 = (kt + kLdsStages - 1) % kLdsStages;
-            glds_stage<BM, (int)sizeof(T)>(x, w, M, N, ldx, ldw, m0, n0, (kt + kLdsStages - 1) * kK, As(s2), Bs(s2), tid);
+        if (kt + ST - 1 < nk) {
+            const int s2 = (kt + ST - 1) % ST;
+            glds_stage<BM, (int)sizeof(T)>(x, w, M, N, ldx, ldw, m0, n0, (kt + ST - 1) * kK, As(s2), Bs(s2), tid);
         }
         const T* A = As(s);
         const T* B = Bs(s);
@@ -1111,9 +1116,9 @@ __global__ __launch_bounds__(256) void head_softmax_kernel(const float* __restri
     head_finish(z, act, y + row * ldy);
 }
 
-template <int BM>
+template <int BM, int ST = kLdsStages>
 constexpr size_t gemm_lds_bytes() {
-    return (size_t)kLdsStages * (BM + kLdsBN) * kLdsK * 2 + (size_t)BM * 2 * sizeof(float);  // ring + LN-fold rows
+    return (size_t)ST * (BM + kLdsBN) * kLdsK * 2 + (size_t)BM * 2 * sizeof(float);  // ring + LN-fold rows
 }
 
 // small-N head: one wave per row, fp32 dot products, optional row softmax (N <= 64)
@@ -1666,6 +1671,15 @@ extern "C" int rf_norm_fwd(const float* x, int64_t rows, int32_t cols, int64_t l
 }
 
 namespace {
+// grids of at most this many 64-row tiles take the 4-deep ring (RF_LDS_DEEP_TILES overrides it for A/B runs; 0 = never)
+int64_t lds_deep_ring_tiles() {
+    static const int64_t v = [] {
+        const char* e = getenv("RF_LDS_DEEP_TILES");
+        return e ? (int64_t)atoll(e) : (int64_t)256;
+    }();
+    return v;
+}
+
 // Launches gemm_lds_kernel<BM, EPI> with the tile choice of rf_linear_fwd's LDS path.
 template <int EPI>
 int launch_lds_epi(const void* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t N, const float* b, int32_t act,
@@ -1679,6 +1693,14 @@ int launch_lds_epi(const void* x, int64_t M, int32_t K, int64_t ldx, const void*
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<128>());
         if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
         hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea, 0);
+    } else if (tiles <= lds_deep_ring_tiles()) {
+        // at most one 64-row tile per CU (cfg3's 4096 x 1024 -> 512 output layer): nothing shares the CU, so a
+        // 4-deep ring keeps three k-steps of loads in flight behind the MFMAs
+        auto kern = gemm_lds_kernel<64, EPI, false, false, 4>;
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64, 4>());
+        if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
+        constexpr size_t deep_lds = gemm_lds_bytes<64, 4>();
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), deep_lds, st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea, 0);
     } else {
         auto kern = gemm_lds_kernel<64, EPI>;
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64>());
