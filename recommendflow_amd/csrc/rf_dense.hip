@@ -611,6 +611,11 @@ __device__ __forceinline__ void glds_stage(const void* __restrict__ xv, const vo
 //              Dense(NH) over this tile's columns: hpart[row][tile_n][h] = sum_c y[row][c] Wh[h][c], reduced over the
 //              tile's waves in a fixed order (head_softmax_kernel adds the tiles in order, the bias, the softmax)
 enum { kEpiPlain = 0, kEpiStats = 1, kEpiLnFold = 2, kEpiLnFoldStats = 3, kEpiLnFoldHead = 4 };
+// lab ablations (tools/build_variants.sh -DRF_LAB_ABL=bits; result-changing, never in the shipped build): 1 = no head
+// partials / hand-off, 2 = no hand-off (partials stored), 4 = no LN-fold row statistics (loads and combine)
+#ifndef RF_LAB_ABL
+#define RF_LAB_ABL 0
+#endif
 constexpr int kHeadN = 2;  // kEpiLnFoldHead: head outputs (cfg3's Dense(2, softmax))
 
 struct EpiArgs {
@@ -777,7 +782,13 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
         const int64_t row = m0 + rl < M ? m0 + rl : M - 1;
         rs2 = reinterpret_cast<const float2*>(ea.stats) + row * ea.P;
         stats_late = ea.P <= NPR * TPR;
-        if (stats_late) {
+        if (RF_LAB_ABL & 4) {
+            if (part == 0) {
+                srow[2 * rl] = 0.f;
+                srow[2 * rl + 1] = 1.f;
+            }
+            stats_late = false;
+        } else if (stats_late) {
 #pragma unroll
             for (int u = 0; u < NPR; ++u) {
                 const int p = part + u * TPR;
@@ -1028,7 +1039,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                 }
             }
         }
-        if constexpr (EPI == kEpiLnFoldHead) {
+        if constexpr (EPI == kEpiLnFoldHead && !(RF_LAB_ABL & 1)) {
             // this wave's TN columns of every row it holds: sum_c y[row][c] Wh[h][c], c in fragment order, then the
             // 16 lanes of a row (row16_sum); the WN waves of a row meet in LDS (the ring is free after a barrier)
             float* hred = reinterpret_cast<float*>(smem_raw);  // [WN][BM][kHeadN]
@@ -1061,23 +1072,23 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                     else *dst = v;
                 }
             }
-            if (ea.hcnt) {
-                // the row block's last tile to finish finishes the head (MI355X_MICROARCH's hand-off row 1: every
-                // storing wave waits for its sc1 stores, a barrier, ONE agent-scope add per workgroup on the row
-                // block's counter; the workgroup whose add returned tiles_n - 1 reads every tile's partials with sc1
-                // loads, adds them in tile order (as head_softmax_kernel) and resets the counter for the next launch)
+            if (ea.hcnt && !(RF_LAB_ABL & 2)) {
+                // the row block's last tile to finish finishes the head: MI355X_MICROARCH's hand-off table, first row,
+                // in every cell: the partials are stored sc1 (relaxed agent atomic stores), every storing wave waits
+                // for them (vmcnt(0)), a workgroup barrier, then ONE lane adds to the row block's counter (agent
+                // scope); the workgroup whose add returned tiles_n - 1 reads every partial with sc1 loads after a
+                // barrier; hipMalloc'd workspace; one workgroup per CU (the launch's 99 KB of LDS). Release / acquire
+                // semantics on the add lower to an L2 write-back + L1 invalidate per workgroup and cost
+                // 7.7 us of a 21 us launch (profiles/r05/scorer_gemm_ablation.txt); the sc1 form needs neither.
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 int* s_last = reinterpret_cast<int*>(smem_raw);
                 if (tid == 0) {
-                    // release: this workgroup's partial stores (ordered before it by the barrier) happen-before the
-                    // add; acquire: the finisher sees every other tile's released partials
-                    const int old = __hip_atomic_fetch_add(ea.hcnt + tile / tiles_n, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                    const int old = __hip_atomic_fetch_add(ea.hcnt + tile / tiles_n, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     s_last[0] = old == tiles_n - 1;
                 }
                 __syncthreads();
                 if (s_last[0]) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread of the finisher, after tid 0's acquire
                     if (tid == 0) __hip_atomic_store(ea.hcnt + tile / tiles_n, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     for (int rl = tid; rl < BM; rl += 256) {
                         const int64_t row = m0 + rl;
@@ -1680,12 +1691,24 @@ int64_t lds_deep_ring_tiles() {
     return v;
 }
 
+// A/B only (default 0 = never): grids of at most this many 64-row tiles (and more than lds_deep_ring_tiles) take a
+// 3-deep ring (72 KB: two workgroups per CU still fit)
+int64_t lds_ring3_tiles() {
+    static const int64_t v = [] {
+        const char* e = getenv("RF_LDS_RING3_TILES");
+        return e ? (int64_t)atoll(e) : (int64_t)0;
+    }();
+    return v;
+}
+
 // Launches gemm_lds_kernel<BM, EPI> with the tile choice of rf_linear_fwd's LDS path.
 template <int EPI>
+// one_per_cu: 64-row tiles on the 4-deep ring whatever the grid (99 KB of LDS: one workgroup per CU), which the
+// in-kernel head hand-off needs (MI355X_MICROARCH's sc1 hand-off row: one workgroup per CU)
 int launch_lds_epi(const void* x, int64_t M, int32_t K, int64_t ldx, const void* W, int32_t N, const float* b, int32_t act,
-                   float* y, int64_t ldy, const EpiArgs& ea, hipStream_t st, const char* who) {
+                   float* y, int64_t ldy, const EpiArgs& ea, hipStream_t st, const char* who, bool one_per_cu = false) {
     const int64_t t128 = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
-    const bool big = t128 >= 512;
+    const bool big = t128 >= 512 && !one_per_cu;
     const int64_t tiles = big ? t128 : ((M + 63) / 64) * ((N + kLdsBN - 1) / kLdsBN);
     RF_REQUIRE(tiles < (int64_t)1 << 31, "%s: too many tiles", who);
     if (big) {
@@ -1693,7 +1716,7 @@ int launch_lds_epi(const void* x, int64_t M, int32_t K, int64_t ldx, const void*
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<128>());
         if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
         hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea, 0);
-    } else if (tiles <= lds_deep_ring_tiles()) {
+    } else if (one_per_cu || tiles <= lds_deep_ring_tiles()) {
         // at most one 64-row tile per CU (cfg3's 4096 x 1024 -> 512 output layer): nothing shares the CU, so a
         // 4-deep ring keeps three k-steps of loads in flight behind the MFMAs
         auto kern = gemm_lds_kernel<64, EPI, false, false, 4>;
@@ -1701,6 +1724,12 @@ int launch_lds_epi(const void* x, int64_t M, int32_t K, int64_t ldx, const void*
         if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
         constexpr size_t deep_lds = gemm_lds_bytes<64, 4>();
         hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), deep_lds, st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea, 0);
+    } else if (tiles <= lds_ring3_tiles()) {
+        auto kern = gemm_lds_kernel<64, EPI, false, false, 3>;
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64, 3>());
+        if (e != hipSuccess) return rf_set_error(RF_EHIP, "%s: %s", who, hipGetErrorString(e));
+        constexpr size_t r3_lds = gemm_lds_bytes<64, 3>();
+        hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), r3_lds, st, (const uint16_t*)x, (const uint16_t*)W, b, y, M, N, K, ldx, ldy, act, ea, 0);
     } else {
         auto kern = gemm_lds_kernel<64, EPI>;
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)gemm_lds_bytes<64>());
@@ -1820,7 +1849,8 @@ extern "C" int rf_linear_lnfold_head_fwd(const void* x, int64_t M, int32_t K, in
     const int64_t t128 = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
     const bool fused = !separate && t128 < 512;  // launch_lds_epi's choice: 64-row tiles below 512 128-row tiles
     ea.hcnt = fused ? static_cast<int*>(ws) : nullptr;
-    const int rc = launch_lds_epi<kEpiLnFoldHead>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, st, "rf_linear_lnfold_head_fwd");
+    const int rc = launch_lds_epi<kEpiLnFoldHead>(x, M, K, ldx, Wg, N, nullptr, act, y, ldy, ea, st, "rf_linear_lnfold_head_fwd",
+                                                  fused);
     if (rc != RF_OK || fused) return rc;
     hipLaunchKernelGGL(head_softmax_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, (const float*)ea.hpart,
                        (N + kLdsBN - 1) / kLdsBN, M, head_b, head_act, out, ldo);
