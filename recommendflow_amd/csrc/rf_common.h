@@ -49,7 +49,21 @@ __device__ __forceinline__ uint32_t f32_to_bf16_bits(float f) {
 // Reads the token with aligned dword loads: a dword that holds at least one byte of the token never
 // crosses a page boundary past the token, so no read faults beyond the caller's buffer.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+// 64-bit rotate by a constant as two v_alignbit_b32 (the shift-or form compiled to a 64-bit shift, two 32-bit
+// shifts and two ors per rotate: half of SipHash's VALU)
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (b == 32) return ((uint64_t)lo << 32) | hi;
+    if (b > 32) {
+        const uint32_t t = lo;
+        lo = hi;
+        hi = t;
+        b -= 32;
+    }
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - b);
+    const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - b);
+    return ((uint64_t)nhi << 32) | nlo;
+}
 
 #define RF_SIPROUND                                                          \
     do {                                                                     \
@@ -151,6 +165,61 @@ __device__ __forceinline__ void siphash24x2_dev(uint64_t s0, uint64_t s1, const 
         tail = (uint64_t)msg32(2 * nb) | ((uint64_t)msg32(2 * nb + 1) << 32);
         tail &= (~0ULL) >> (64 - 8 * r);
     }
+    const uint64_t bl = ((uint64_t)(uint32_t)n << 56) | tail;
+    a3 ^= bl; b3 ^= bl;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+    a0 ^= bl; b0 ^= bl;
+    a2 ^= 0xff; b2 ^= 0xff;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+    RF_SIPROUND2;
+#undef RF_SIPROUND2
+    h0 = a0 ^ a1 ^ a2 ^ a3;
+    h1 = b0 ^ b1 ^ b2 ^ b3;
+}
+
+// siphash24x2_dev over a token whose covering dwords were loaded ahead into registers (so the message reads are not
+// round trips inside the rounds): wv[j] = dword j of the aligned window that starts sh = (address & 3) bytes before
+// the token, 0 from dword (sh + n + 3) / 4 on; needs sh + n <= 4 kSipRegWords. Same values as siphash24x2_dev.
+constexpr int kSipRegWords = 8;
+__device__ __forceinline__ void siphash24x2_regs(uint64_t s0, uint64_t s1, const uint32_t (&wv)[kSipRegWords + 1],
+                                                 uint32_t sh, int n, uint64_t& h0, uint64_t& h1) {
+    uint64_t a0 = 0x736f6d6570736575ULL ^ s0, a1 = 0x646f72616e646f6dULL ^ s0;
+    uint64_t a2 = 0x6c7967656e657261ULL ^ s0, a3 = 0x7465646279746573ULL ^ s0;
+    uint64_t b0 = 0x736f6d6570736575ULL ^ s1, b1 = 0x646f72616e646f6dULL ^ s1;
+    uint64_t b2 = 0x6c7967656e657261ULL ^ s1, b3 = 0x7465646279746573ULL ^ s1;
+    auto msg64 = [&](int i) -> uint64_t {  // message word i (bytes 8i .. 8i + 7 of the token); i compile-time
+        const uint32_t lo = __builtin_amdgcn_alignbyte(wv[2 * i + 1], wv[2 * i], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(wv[2 * i + 2], wv[2 * i + 1], sh);
+        return (uint64_t)lo | ((uint64_t)hi << 32);
+    };
+#define RF_SIPROUND2                                                                                 \
+    do {                                                                                             \
+        uint64_t v0 = a0, v1 = a1, v2 = a2, v3 = a3;                                                 \
+        RF_SIPROUND;                                                                                 \
+        a0 = v0; a1 = v1; a2 = v2; a3 = v3;                                                          \
+        v0 = b0; v1 = b1; v2 = b2; v3 = b3;                                                          \
+        RF_SIPROUND;                                                                                 \
+        b0 = v0; b1 = v1; b2 = v2; b3 = v3;                                                          \
+    } while (0)
+    const int nb = n >> 3;
+    uint64_t tail = 0;
+#pragma unroll
+    for (int i = 0; i < kSipRegWords / 2; ++i) {
+        const uint64_t m = msg64(i);
+        if (i < nb) {
+            a3 ^= m; b3 ^= m;
+            RF_SIPROUND2;
+            RF_SIPROUND2;
+            a0 ^= m; b0 ^= m;
+        } else if (i == nb) {
+            tail = m;
+        }
+    }
+    const int r = n & 7;
+    tail = r ? tail & ((~0ULL) >> (64 - 8 * r)) : 0ull;
     const uint64_t bl = ((uint64_t)(uint32_t)n << 56) | tail;
     a3 ^= bl; b3 ^= bl;
     RF_SIPROUND2;

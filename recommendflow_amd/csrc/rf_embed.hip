@@ -321,6 +321,10 @@ __global__ __launch_bounds__(64) void single_token_ids_kernel(const rf_slot_desc
 // index arithmetic (round 4: the per-lane descriptor gathers and the 64-bit u % n_slots were a third of the
 // cfg3 id pass, profiles/r04/cfg3_*).
 constexpr int kIdsMaxSlots = 512;
+#ifndef RF_IDS_UNITS
+#define RF_IDS_UNITS 2
+#endif
+constexpr int kIdsUnits = RF_IDS_UNITS;  // units per thread (single_token_ids_em_body)
 struct IdsSlot {
     uint64_t salt0, salt1;
     BucketMod bm;
@@ -353,35 +357,72 @@ __device__ __forceinline__ void single_token_ids_em_body(const rf_slot_desc* __r
     const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
     const uint32_t ns = (uint32_t)n_slots, nu = (uint32_t)n_units;
     const uint32_t stride = (uint32_t)(n_blocks * blockDim.x);
-    for (uint32_t u = (uint32_t)(block * blockDim.x) + threadIdx.x; u < nu; u += stride) {
-        const uint32_t s = u % ns;
-        const IdsSlot& sl = ssl[s];
-        uint32_t r0 = kRowNaN, r1 = kRowNaN;
-        if (sl.live) {
-            const int t = bag_off[u];
-            if (bag_off[u + 1] > t) {
-                const int tb = tok_off[t], n = tok_off[t + 1] - tb;
-                uint64_t h0, h1;
-                siphash24x2_dev(sl.salt0, sl.salt1, tok_bytes + tb, n, h0, h1);
-                r0 = (uint32_t)(sl.rb0 + bucket_from_hash(h0, n, sl.bm));
-                r1 = (uint32_t)(sl.rb1 + bucket_from_hash(h1, n, sl.bm));
-            } else if (mask_pad) {
-                r0 = r1 = kRowZero;
-            } else {
-                int64_t pb0 = 0, pb1 = 0;
-                if (!sl.mask_empty) {
-                    pb0 = (int64_t)(siphash24_dev(sl.salt0, sl.salt0, tok_bytes, 0) % (uint64_t)sl.nbins);
-                    pb1 = (int64_t)(siphash24_dev(sl.salt1, sl.salt1, tok_bytes, 0) % (uint64_t)sl.nbins);
+    // kIdsUnits units per thread in lockstep (round 5): the CSR offsets, then the token offsets, then the token's
+    // dwords of every unit are loaded before any is hashed, so a thread waits out three round trips per
+    // kIdsUnits units instead of four per unit (the message reads of siphash24x2_dev sit inside its rounds)
+    for (uint32_t u0 = (uint32_t)(block * blockDim.x) + threadIdx.x; u0 < nu; u0 += kIdsUnits * stride) {
+        uint32_t uu[kIdsUnits], ss[kIdsUnits];
+        bool live[kIdsUnits];
+        int t0[kIdsUnits], t1[kIdsUnits];
+#pragma unroll
+        for (int k = 0; k < kIdsUnits; ++k) {
+            uu[k] = u0 + (uint32_t)k * stride;
+            ss[k] = uu[k] < nu ? uu[k] % ns : 0u;
+            live[k] = uu[k] < nu && ssl[ss[k]].live;
+            t0[k] = live[k] ? bag_off[uu[k]] : 0;
+            t1[k] = live[k] ? bag_off[uu[k] + 1] : 0;
+        }
+        int tb[kIdsUnits], n[kIdsUnits];
+#pragma unroll
+        for (int k = 0; k < kIdsUnits; ++k) {
+            const bool has = live[k] && t1[k] > t0[k];
+            tb[k] = has ? tok_off[t0[k]] : 0;
+            n[k] = has ? tok_off[t0[k] + 1] - tb[k] : -1;  // -1: empty bag or dead slot
+        }
+        uint32_t wv[kIdsUnits][kSipRegWords + 1];
+        uint32_t sh[kIdsUnits];
+#pragma unroll
+        for (int k = 0; k < kIdsUnits; ++k) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(tok_bytes + tb[k]);
+            sh[k] = (uint32_t)(a & 3);
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(a - sh[k]);
+            const int nw = n[k] > 0 && (int)sh[k] + n[k] <= 4 * kSipRegWords ? (int)((sh[k] + (uint32_t)n[k] + 3) >> 2) : 0;
+#pragma unroll
+            for (int j = 0; j < kSipRegWords; ++j) wv[k][j] = j < nw ? w[j] : 0u;
+            wv[k][kSipRegWords] = 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kIdsUnits; ++k) {
+            if (uu[k] >= nu) continue;
+            const IdsSlot& sl = ssl[ss[k]];
+            uint32_t r0 = kRowNaN, r1 = kRowNaN;
+            if (live[k]) {
+                if (n[k] >= 0) {
+                    uint64_t h0, h1;
+                    if ((int)sh[k] + n[k] <= 4 * kSipRegWords)
+                        siphash24x2_regs(sl.salt0, sl.salt1, wv[k], sh[k], n[k], h0, h1);
+                    else  // long token: the streaming form
+                        siphash24x2_dev(sl.salt0, sl.salt1, tok_bytes + tb[k], n[k], h0, h1);
+                    r0 = (uint32_t)(sl.rb0 + bucket_from_hash(h0, n[k], sl.bm));
+                    r1 = (uint32_t)(sl.rb1 + bucket_from_hash(h1, n[k], sl.bm));
+                } else if (mask_pad) {
+                    r0 = r1 = kRowZero;
+                } else {
+                    int64_t pb0 = 0, pb1 = 0;
+                    if (!sl.mask_empty) {
+                        pb0 = (int64_t)(siphash24_dev(sl.salt0, sl.salt0, tok_bytes, 0) % (uint64_t)sl.nbins);
+                        pb1 = (int64_t)(siphash24_dev(sl.salt1, sl.salt1, tok_bytes, 0) % (uint64_t)sl.nbins);
+                    }
+                    r0 = (uint32_t)(sl.rb0 + pb0);
+                    r1 = (uint32_t)(sl.rb1 + pb1);
                 }
-                r0 = (uint32_t)(sl.rb0 + pb0);
-                r1 = (uint32_t)(sl.rb1 + pb1);
             }
+            if (flags & RF_FLAG_SPEC_ROWS) {  // the NaN / zero rows at table_rows / table_rows + 1
+                r0 = r0 == kRowNaN ? (uint32_t)table_rows : r0 == kRowZero ? (uint32_t)table_rows + 1u : r0;
+                r1 = r1 == kRowNaN ? (uint32_t)table_rows : r1 == kRowZero ? (uint32_t)table_rows + 1u : r1;
+            }
+            *reinterpret_cast<uint2*>(ids + 2 * (size_t)uu[k]) = make_uint2(r0, r1);
         }
-        if (flags & RF_FLAG_SPEC_ROWS) {  // the NaN / zero rows at table_rows / table_rows + 1
-            r0 = r0 == kRowNaN ? (uint32_t)table_rows : r0 == kRowZero ? (uint32_t)table_rows + 1u : r0;
-            r1 = r1 == kRowNaN ? (uint32_t)table_rows : r1 == kRowZero ? (uint32_t)table_rows + 1u : r1;
-        }
-        *reinterpret_cast<uint2*>(ids + 2 * (size_t)u) = make_uint2(r0, r1);
     }
 }
 
@@ -434,7 +475,7 @@ extern "C" int rf_single_token_ids_multi_fwd(const rf_ids_task* tasks, int32_t n
                        "rf_single_token_ids_multi_fwd: task %d: null pointer or ids not 8-byte aligned", k);
         a.t[k] = t;
         a.first[k] = blocks;
-        blocks += std::min<int64_t>((n_units + 255) / 256, 256 * 32 / n_tasks);
+        blocks += std::min<int64_t>((n_units + 256 * kIdsUnits - 1) / (256 * kIdsUnits), 256 * 32 / n_tasks);
     }
     a.first[n_tasks] = blocks;
     if (blocks == 0) return RF_OK;
@@ -461,7 +502,7 @@ extern "C" int rf_single_token_ids_fwd(const rf_slot_desc* d_slots, int32_t n_sl
         return e && e[0] == '1';
     }();
     if (n_slots <= kIdsMaxSlots && !slot_major && n_units < ((int64_t)1 << 31)) {
-        const int64_t blocks = std::min<int64_t>((n_units + 255) / 256, 256 * 32);
+        const int64_t blocks = std::min<int64_t>((n_units + 256 * kIdsUnits - 1) / (256 * kIdsUnits), 256 * 32);
         hipLaunchKernelGGL(single_token_ids_em_kernel, dim3((unsigned)blocks), dim3(256), sizeof(IdsSlot) * n_slots,
                            rf_stream(stream), d_slots,
                            n_slots, tok_bytes, tok_off, bag_off, lmax, n_units, table_rows, ids, flags);

@@ -188,8 +188,9 @@ def test_esim_cfg3_full_shape_sampled(O, cuda):
     """cfg3 at its FULL shape (BASELINE.json configs[2]): 100 + 100 single-valued slots with num_bins = 1M per
     hash (two bf16 tables of 200M x 64 rows, 25.6 GB each), B = 4096, gather path. The token ids of the whole
     batch are checked against the oracle's hash (rf_single_token_ids_multi_fwd vs orf_hash_rows, bit-exact);
-    64 sampled examples go end to end through the oracle (their rows read from the device tables by the
-    oracle's ids, then esim_pool + MLPs in float64) at the §8d bar."""
+    64 sampled examples go end to end through the oracle (their rows from the oracle's table init at the oracle's
+    ids — and the device tables' copies of those rows bit-exact with them —, then esim_pool + MLPs in float64) at
+    the §8d bar."""
     Ls, B, NB = 100, 4096, 1_000_000
     user = [SlotSpec(f"u{i:03d}", NB, (2022, 2023)) for i in range(Ls)]
     ad = [SlotSpec(f"a{i:03d}", NB, (2022, 2023)) for i in range(Ls)]
@@ -211,7 +212,12 @@ def test_esim_cfg3_full_shape_sampled(O, cuda):
         sub = _take_examples(h, idx)
         rows = O.hash_rows(enc.host_desc, sub.tok_bytes, sub.tok_off, sub.bag_off, sub.batch)
         uniq, inv = np.unique(rows, return_inverse=True)
-        gathered = enc.table[torch.from_numpy(uniq).cuda()].float().cpu().numpy()
+        # the rows from the oracle's table init (not read back from the device: VERDICT r4), then the device's
+        # copies of the same rows checked bit for bit against them
+        init = np.stack([O.table_init_uniform(1, enc.dim, O.DT_BF16, seed=enc.seed, row0=int(r))[0] for r in uniq])
+        dev = enc.table[torch.from_numpy(uniq).cuda()].cpu().view(torch.int16).numpy().view(np.uint16)
+        np.testing.assert_array_equal(dev, init)
+        gathered = (init.astype(np.uint32) << 16).view(np.float32)
         row_map = np.concatenate([inv, np.zeros(2 * Ls, np.int64)]).astype(np.int32)  # + pad rows (unused: L = 1)
         out = O.pool_rows(enc.host_desc, sub.bag_off, sub.lmax, sub.batch, sub.n_tokens, gathered, enc.dim,
                           enc.out_width, row_map=row_map)

@@ -143,6 +143,49 @@ def test_simulated_shards_bit_exact(cuda, P, tdt, mode):
         np.testing.assert_array_equal(bits(outs[r]), bits(want))
 
 
+def _oracle_pooled(O, enc, host_batch, seed, dtype_code, lo=-0.05, hi=0.05):
+    """The pooled output of host_batch from the oracle alone: token rows by the oracle's hash (orf_hash_rows), pad
+    rows by its bucket of b"" (bin 0 under mask_value ""), each needed row by the oracle's table init (the same
+    counter-based rows rf_table_init_uniform writes), then orf_pool_rows_fwd over that compact row set."""
+    desc = enc.host_desc
+    h = host_batch
+    tok_rows = O.hash_rows(desc, h.tok_bytes, h.tok_off, h.bag_off, h.batch)
+    pad = np.zeros(2 * len(desc), np.int64)
+    for s, d in enumerate(desc):
+        for k in range(2):
+            salt = int(d["salt"][k])
+            b = 0 if d["mask_empty"] else int(O.hash_tokens(np.zeros(1, np.uint8), np.zeros(2, np.int32), salt, salt,
+                                                          int(d["num_bins"]), False)[0])
+            pad[2 * s + k] = int(d["row_base"][k]) + b
+    logical = np.concatenate([tok_rows, pad])
+    uniq, inv = np.unique(logical, return_inverse=True)
+    rows = np.stack([O.table_init_uniform(1, enc.dim, dtype_code, seed=seed, row0=int(r), row_stride=1, lo=lo, hi=hi)[0]
+                     for r in uniq])
+    if dtype_code != O.DT_F32:  # bf16 rows widen exactly
+        rows = (rows.astype(np.uint32) << 16).view(np.float32)
+    return O.pool_rows(desc, h.bag_off, h.lmax, h.batch, h.n_tokens, rows, enc.dim, enc.out_width,
+                       row_map=inv.astype(np.int32))
+
+
+@pytest.mark.parametrize("P", [2, 8])
+@pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
+def test_simulated_shards_vs_oracle(O, cuda, P, tdt):
+    """The simulated P-rank forward against the oracle alone (test_simulated_shards_bit_exact compares
+    with this repo's unsharded kernel): every rank's pooled output bit-exact with orf_pool_rows_fwd over rows from
+    the oracle's hash and table init (bf16 tables: the oracle's fp32 result rounded to nearest even)."""
+    sp = slots(48, seed=P)
+    encs = [ShardedFusedEncoder(sp, 64, r, P, table_dtype=tdt, seed=21, dedup=True, route="hash") for r in range(P)]
+    batches = [synthetic_batch(120 + 17 * r, [i % 3 == 0 for i in range(len(sp))], seed=60 + r) for r in range(P)]
+    outs = simulate_sharded_forward(encs, batches, local_fast=True)
+    ref = FusedSparseEncoder(sp, 64, table_dtype=tdt, seed=21)  # descriptors only (the oracle builds the rows)
+    code = O.DT_F32 if tdt == torch.float32 else O.DT_BF16
+    for r in range(P):
+        want = torch.from_numpy(_oracle_pooled(O, ref, batches[r], 21, code))
+        if tdt == torch.bfloat16:
+            want = want.to(torch.bfloat16)
+        np.testing.assert_array_equal(bits(outs[r]), bits(want))
+
+
 def test_sharded_cfg2_layout(cuda):
     """The 229-slot base_recall_sdpa layout, 10M x 64 fp32 fused table, 4 simulated shards, B=1024 per rank."""
     import os
