@@ -322,7 +322,7 @@ __global__ __launch_bounds__(64) void single_token_ids_kernel(const rf_slot_desc
 // cfg3 id pass, profiles/r04/cfg3_*).
 constexpr int kIdsMaxSlots = 512;
 #ifndef RF_IDS_UNITS
-#define RF_IDS_UNITS 2
+#define RF_IDS_UNITS 1
 #endif
 constexpr int kIdsUnits = RF_IDS_UNITS;  // units per thread (single_token_ids_em_body)
 struct IdsSlot {
@@ -357,9 +357,9 @@ __device__ __forceinline__ void single_token_ids_em_body(const rf_slot_desc* __r
     const bool mask_pad = (flags & RF_FLAG_MASK_PADDING) != 0;
     const uint32_t ns = (uint32_t)n_slots, nu = (uint32_t)n_units;
     const uint32_t stride = (uint32_t)(n_blocks * blockDim.x);
-    // kIdsUnits units per thread in lockstep (round 5): the CSR offsets, then the token offsets, then the token's
-    // dwords of every unit are loaded before any is hashed, so a thread waits out three round trips per
-    // kIdsUnits units instead of four per unit (the message reads of siphash24x2_dev sit inside its rounds)
+    // kIdsUnits units per thread in lockstep: the CSR offsets, then the token offsets, then the token's dwords of
+    // every unit are loaded before any is hashed (siphash24x2_dev's message reads sit inside its rounds). One unit
+    // per thread measured best (tools/ids_probe.py: 16.0 us for 1, 16.7 for 2, 21.2 for 4 units per thread)
     for (uint32_t u0 = (uint32_t)(block * blockDim.x) + threadIdx.x; u0 < nu; u0 += kIdsUnits * stride) {
         uint32_t uu[kIdsUnits], ss[kIdsUnits];
         bool live[kIdsUnits];
