@@ -250,7 +250,11 @@ static int fused_hash_embed_fwd_impl(uint32_t allowed_diag, const rf_slot_desc* 
         return launch_single_token_any(table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,
                                        table, table_rows, dim, out, out_stride, flags, grid_for(items, 1, 256 * 32 * 2), st);
     }
-    const int grid = grid_for(items, kWaves, 256 * 32 * 2);
+    static const int grid_cap = [] {  // RF_FUSED_GRID_CAP: A/B of a persistent grid (waves walk several items)
+        const char* e = getenv("RF_FUSED_GRID_CAP");
+        return e ? std::max(1, atoi(e)) : 256 * 32 * 2;
+    }();
+    const int grid = grid_for(items, kWaves, grid_cap);
     return launch_fused_any(false, table_dtype, out_dtype, d_slots, n_slots, tok_bytes, tok_off, bag_off, lmax, n_units,
                             table, table_rows, dim, out, out_stride, flags, idx_out, grid, st);
 }
