@@ -740,9 +740,15 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
 
     auto As = [&](int s) { return lds + s * (A_EL + B_EL); };
     auto Bs = [&](int s) { return lds + s * (A_EL + B_EL) + A_EL; };
+    // the ring's first ST - 1 stages. With ST >= 3 they are issued AFTER the epilogue parameter and row-statistics
+    // loads below: vmcnt retires in issue order, so the loop's first wait for stage 0 with stages 1 .. ST - 2 left in
+    // flight would otherwise also wait for every younger parameter load (and, in effect, for the whole prologue)
+    auto ring_prologue = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int p = 0; p + 1 < ST; ++p)
-        if (p < nk) glds_stage<BM, (int)sizeof(T)>(x, w, M, N, ldx, ldw, m0, n0, p * kK, As(p), Bs(p), tid);
+        for (int p = 0; p + 1 < ST; ++p)
+            if (p < nk) glds_stage<BM, (int)sizeof(T)>(x, w, M, N, ldx, ldw, m0, n0, p * kK, As(p), Bs(p), tid);
+    };
+    if constexpr (ST < 3) ring_prologue();
     // The epilogue's per-column parameters (bias, or the LN fold's s_c / t_c) are loaded now, under the first
     // stage's copies, instead of as dependent loads after the last MFMA (one HBM round trip off the tail).
     float pb[FN], pt[FN];
@@ -799,6 +805,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             __syncthreads();  // srow visible to every wave (this also retires stage 0's copies: the loop waits for them first)
         }
     }
+    if constexpr (ST >= 3) ring_prologue();
     for (int kt = 0; kt < nk; ++kt) {
         const int s = kt % ST;
         // stage kt must have landed; the stages issued after it (min(ST - 2, nk - 1 - kt)) may stay in flight
