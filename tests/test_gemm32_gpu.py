@@ -75,6 +75,20 @@ def test_ragged_shapes_every_layout(cuda, M, N, K, ta, tb):
     _check(c, a, b, ta, tb, bias, "relu")
 
 
+# few 64-k steps per tile and many tiles per workgroup: every segment boundary hands the next tile's first two
+# k-steps over from the previous segment's last two (RF_G32_XTILE), single-step tails and cut tiles included
+SHORT_K = [(4096, 2048, 128), (2048, 4096, 192), (3000, 1000, 320), (4096, 1024, 64), (1500, 3000, 100)]
+
+
+@pytest.mark.parametrize("M,N,K", SHORT_K)
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False), (False, False)])
+def test_short_k_many_tiles(cuda, M, N, K, ta, tb):
+    a, b, bias = _operands(M, N, K, ta, tb, seed=7 * M + N + K)
+    c = G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act="selu")
+    _check(c, a, b, ta, tb, bias, "selu")
+    assert torch.equal(c, G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act="selu"))
+
+
 def test_workspace_shared_across_shapes(cuda):
     """One zeroed workspace per stream serves every shape: a small call after a large one, a large one after a small
     one (the per-tile counters sit at the start, the partial tiles at the far end), the results unchanged."""
