@@ -210,7 +210,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
         const int k_hi = (int)min<int64_t>(P.nk, hi - t_unit0);
         u = t_unit0 + k_hi;
         const int gt = P.tile0 + tile;
+#if RF_G32_MFAST
+        const int tiles_m = (P.M + kBM - 1) / kBM;
+        const int m0 = (tile % tiles_m) * kBM, n0 = (tile / tiles_m) * kBN;
+#else
         const int m0 = (tile / P.tiles_n) * kBM, n0 = (tile % P.tiles_n) * kBN;
+#endif
 
         Operand<AKC> oa;
         Operand<BKC> ob;
