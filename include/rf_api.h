@@ -724,6 +724,23 @@ int rf_bucketize_ids(const float* values, const int32_t* bag_off, int32_t n_slot
 int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int32_t cols, int32_t k, int64_t col_base,
                   const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld, float* out_val,
                   int64_t* out_idx, int64_t out_ld, void* stream);
+/* rf_topk_merge with the block's item indices given per entry (col_idx[row][c], same ld as scores) instead of
+ * col_base + c: the candidate lists of rf_ip_candidates_f32 (entries past a row's count hold NaN scores). */
+int rf_topk_merge_idx(const float* scores, const uint32_t* col_idx, int64_t ld, int32_t rows, int32_t cols, int32_t k,
+                      const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld, float* out_val,
+                      int64_t* out_idx, int64_t out_ld, void* stream);
+/*
+ * FaissSearcher Flat's screen (faiss_searcher.py:141-204, exact): for M queries q [M][K] (row stride ldq) against N
+ * items [N][K] (contiguous rows), every pair with score <q_m, item_n> >= thr[m] is appended, in no particular order,
+ * to row m's list: cand_val[m][0 .. cap) and cand_idx[m][0 .. cap) (item index col_base + n); count[m] (zero
+ * before the call) counts every such pair, so count[m] > cap means entries were dropped. The scores are bit for bit
+ * those of rf_linear_fwd (fp32, the LDS-DMA MFMA kernel), and no score matrix is written. With thr[m] = the k-th best
+ * score of any subset of the items, the lists hold every item of the exact top-k (the k-th best over all items is
+ * at least thr[m]). K >= 256, K % 32 == 0, 16-byte aligned q and items.
+ */
+int rf_ip_candidates_f32(const float* q, int64_t ldq, int32_t M, const float* items, int32_t N, int32_t K,
+                         const float* thr, int32_t cap, int32_t* count, float* cand_val, uint32_t* cand_idx,
+                         int64_t col_base, void* stream);
 
 /*
  * Que2Search AttentionFusion forward (backend/layers/fusion_layers.py:35-46), fp32:

@@ -7,6 +7,15 @@ block by block with the MFMA GEMM (rf_linear_fwd: queries . items_block^T, 32768
 the running top-k is merged after every block (rf_topk_merge: radix select + bitonic merge, ties by
 smaller item index). Approximate faiss indexes (IVF / HNSW / PQ) are out of scope.
 
+Screened form (round 5; fp32 index, E >= 256, E % 32 == 0, more than one block, not inside a graph capture): the
+first block is scored and merged as above, its k-th best score per query is a threshold no item of the exact top-k
+falls below (the k-th best over all items is at least the k-th best of any subset), and ONE launch over the other
+N - 32768 items (rf_ip_candidates_f32: the same fp32 MFMA scores, no score matrix written) keeps every item at or
+above it; one rf_topk_merge_idx over those candidates and the first block's top-k gives the result. Same scores,
+same ties (item index), same top-k as the block loop; a query whose candidate list overflows `cap` sends the whole
+batch back to the block loop (one host read of the counts). It removes the [B, N] score matrix's write and re-read
+(2 x 4.3 GB at the cfg5 shapes).
+
 search() returns what the reference returns without an encoder: (item_list[indexes], directories) for
 an int topK, {k: (items, sims)} for a list of topK (:178-204).
 """
@@ -20,6 +29,7 @@ import torch
 from ...runtime import lib as L
 
 BLOCK = 32768
+SCREEN_CAP_MAX = 32768  # rf_topk_merge_idx's column limit
 
 
 class FaissSearcher:
@@ -63,6 +73,38 @@ class FaissSearcher:
         self.index = self.get_vecs(self.items)  # [N, E] resident in HBM
         return self
 
+    screen = True  # the screened search where it applies (A/B: False keeps the block loop)
+
+    def _screened(self, q: torch.Tensor, k: int):
+        """The screened search (module docstring), or None when a candidate list overflowed."""
+        B, E = q.shape
+        N = self.index.shape[0]
+        dev = self.device
+        st = L.stream_ptr()
+        scores = torch.empty((B, BLOCK), dtype=torch.float32, device=dev)
+        L.call("rf_linear_fwd", L.ptr(q), L.DT_F32, B, E, q.stride(0), L.ptr(self.index), BLOCK, None, 0, L.ptr(scores),
+               scores.stride(0), st)
+        v0 = torch.empty((B, k), dtype=torch.float32, device=dev)
+        i0 = torch.empty((B, k), dtype=torch.int64, device=dev)
+        L.call("rf_topk_merge", L.ptr(scores), scores.stride(0), B, BLOCK, k, 0, None, None, 0, k, L.ptr(v0), L.ptr(i0), k, st)
+        del scores
+        thr = v0[:, k - 1].contiguous()  # -inf where the block held fewer than k scores (then every item passes)
+        # room for ~3x the candidates a uniform score distribution gives (k per 32768 items), at most 32768
+        cap = int(min(SCREEN_CAP_MAX, max(1024, 3 * k * (N - BLOCK) // BLOCK + k)))
+        count = torch.zeros(B, dtype=torch.int32, device=dev)
+        cval = torch.full((B, cap), float("nan"), dtype=torch.float32, device=dev)
+        cidx = torch.empty((B, cap), dtype=torch.int32, device=dev)
+        rest = self.index[BLOCK:]
+        L.call("rf_ip_candidates_f32", L.ptr(q), q.stride(0), B, L.ptr(rest), N - BLOCK, E, L.ptr(thr), cap, L.ptr(count),
+               L.ptr(cval), L.ptr(cidx), BLOCK, st)
+        if int(count.max().item()) > cap:
+            return None
+        out_v = torch.empty((B, k), dtype=torch.float32, device=dev)
+        out_i = torch.empty((B, k), dtype=torch.int64, device=dev)
+        L.call("rf_topk_merge_idx", L.ptr(cval), L.ptr(cidx), cap, B, cap, k, L.ptr(v0), L.ptr(i0), k, k, L.ptr(out_v),
+               L.ptr(out_i), k, st)
+        return out_v, out_i
+
     def search_index(self, target, k: int):
         """(directories [B, k] fp32, indexes [B, k] int64) on the device — faiss index.search."""
         if self.index is None:
@@ -72,6 +114,11 @@ class FaissSearcher:
         q = self.get_vecs(target)
         B, E = q.shape
         N = self.index.shape[0]
+        if (self.screen and self.dtype == torch.float32 and N > BLOCK and E >= 256 and E % 32 == 0 and B > 0
+                and not torch.cuda.is_current_stream_capturing()):
+            res = self._screened(q, k)
+            if res is not None:
+                return res
         dev = self.device
         vals = [torch.empty((B, k), dtype=torch.float32, device=dev) for _ in range(2)]
         idxs = [torch.empty((B, k), dtype=torch.int64, device=dev) for _ in range(2)]

@@ -610,7 +610,11 @@ __device__ __forceinline__ void glds_stage(const void* __restrict__ xv, const vo
 //   kEpiLnFoldHead   kEpiLnFold's y (stored only when y is given), then the per-row partial logits of a small head
 //              Dense(NH) over this tile's columns: hpart[row][tile_n][h] = sum_c y[row][c] Wh[h][c], reduced over the
 //              tile's waves in a fixed order (head_softmax_kernel adds the tiles in order, the bias, the softmax)
-enum { kEpiPlain = 0, kEpiStats = 1, kEpiLnFold = 2, kEpiLnFoldStats = 3, kEpiLnFoldHead = 4 };
+//   kEpiCompact  no output matrix: every score y[row][col] >= thr[row] is appended, in no particular order, to
+//              row's candidate list (cval / cidx [row][0 .. cap), index cbase + col); ccount[row] counts every such
+//              score (entries past cap are dropped: the caller sees ccount > cap). The exact-search screen of
+//              FaissSearcher (rf_ip_candidates_f32): the scores are this kernel's, bit for bit, as rf_linear_fwd's
+enum { kEpiPlain = 0, kEpiStats = 1, kEpiLnFold = 2, kEpiLnFoldStats = 3, kEpiLnFoldHead = 4, kEpiCompact = 5 };
 // lab ablations (tools/build_variants.sh -DRF_LAB_ABL=bits; result-changing, never in the shipped build): 1 = no head
 // partials / hand-off, 2 = no hand-off (partials stored), 4 = no LN-fold row statistics (loads and combine)
 #ifndef RF_LAB_ABL
@@ -634,6 +638,12 @@ struct EpiArgs {
     int hact;            // head activation
     float* hout;         // [M][kHeadN] probabilities, row stride hldo
     int64_t hldo;
+    const float* thr;    // kEpiCompact: per-row threshold [M]
+    int* ccount;         // kEpiCompact: per-row candidate counts [M] (zero before the launch)
+    float* cval;         // kEpiCompact: [M][cap] scores
+    uint32_t* cidx;      // kEpiCompact: [M][cap] item indices
+    int cap;
+    int64_t cbase;       // kEpiCompact: item index of column 0
 };
 
 // the head's outputs of one row from its logits: softmax over the kHeadN values, or an elementwise activation
@@ -728,8 +738,11 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
     const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
     const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
     const int tiles_n = (N + kLdsBN - 1) / kLdsBN;
-    const int64_t m0 = (int64_t)(tile / tiles_n) * BM;
-    const int n0 = (tile % tiles_n) * kLdsBN;
+    // kEpiCompact (a few query rows against a long item matrix): the row tiles of one item tile are consecutive, so
+    // they run together on one XCD and the item tile is read from HBM once (n-fastest order re-reads it per row tile)
+    const int tiles_m = (int)((M + BM - 1) / BM);
+    const int64_t m0 = (int64_t)(EPI == kEpiCompact ? tile % tiles_m : tile / tiles_n) * BM;
+    const int n0 = (EPI == kEpiCompact ? tile / tiles_m : tile % tiles_n) * kLdsBN;
     const int nk = K / kK;
 
     f4 acc[FM][FN];
@@ -770,6 +783,17 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             pb[j] = bias ? bias[col] : 0.f;
             pt[j] = 0.f;
         }
+    }
+    // kEpiCompact: this lane's row thresholds, loaded under the k-loop like the column parameters (+inf past M)
+    float tv[EPI == kEpiCompact ? FM : 1][4];
+    if constexpr (EPI == kEpiCompact) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * TM + lg * 4 + i * 16 + r;
+                tv[i][r] = row < M ? ea.thr[row] : INFINITY;
+            }
     }
     // LN-fold row statistics (mu, rstd per tile row), in an LDS area past the ring
     float* srow = reinterpret_cast<float*>(smem_raw + (size_t)ST * (A_EL + B_EL) * sizeof(T));
@@ -939,6 +963,56 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                     }
             }
         }
+    } else if constexpr (EPI == kEpiCompact) {
+        // per (fragment row i, accumulator row r): this lane's passing columns (4 bits, one per column fragment j), a
+        // prefix count over the 16 lanes sharing the row (lane & 15) and ONE atomic add per row group and wave for
+        // the group's total — every add issued before any result is used (one round trip, not 16) — then each lane
+        // writes its entries at base + its exclusive prefix
+        uint32_t pm[FM][4];
+        int pin[FM][4], pbase[FM][4];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                uint32_t m = 0;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) m |= (cbase + j * 16 < N && acc[i][j][r] >= tv[i][r]) ? (1u << j) : 0u;
+                const int n = __builtin_popcount(m);
+                int incl = n;
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const int y = __shfl_up(incl, o, 16);
+                    if (lr >= o) incl += y;
+                }
+                const int total = __shfl(incl, 15, 16);
+                pm[i][r] = m;
+                pin[i][r] = incl - n;
+                pbase[i][r] = 0;
+                const int64_t row = rbase + i * 16 + r;
+                if (lr == 15 && total > 0) pbase[i][r] = atomicAdd(ea.ccount + row, total);
+            }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int base = __shfl(pbase[i][r], 15, 16);
+                const uint32_t m = pm[i][r];
+                if (m) {
+                    const int64_t row = rbase + i * 16 + r;
+                    int off = base + pin[i][r];
+                    float* cv = ea.cval + row * (int64_t)ea.cap;
+                    uint32_t* ci = ea.cidx + row * (int64_t)ea.cap;
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        if (m & (1u << j)) {
+                            if (off < ea.cap) {
+                                cv[off] = acc[i][j][r];
+                                ci[off] = (uint32_t)(ea.cbase + cbase + j * 16);
+                            }
+                            ++off;
+                        }
+                }
+            }
     } else if constexpr (EPI == kEpiStats || EPI == kEpiLnFoldStats) {
         // pass 1: activation, the fp32 value kept in acc (0 past N); then the bf16 stores
         with_act(act, [&](auto A) {
@@ -1928,6 +2002,21 @@ int launch_lds_f32(const void* x, const void* W, const float* b, float* y, int64
     return rf_check_launch("gemm_lds_kernel (fp32)");
 }
 
+// rf_ip_candidates_f32: the compaction form of the fp32 LDS-DMA GEMM (gemm_lds_kernel<128, kEpiCompact, F32>)
+int launch_ip_candidates(const float* q, int64_t ldq, int64_t M, const float* items, int64_t ldi, int N, int K, const EpiArgs& ea,
+                         hipStream_t st) {
+    auto kern = gemm_lds_kernel<128, kEpiCompact, true>;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)gemm_lds_bytes<128>());
+    if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel (compact): %s", hipGetErrorString(e));
+    const int64_t tiles = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
+    RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_ip_candidates_f32: too many tiles");
+    (void)ldi;
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, q, items, nullptr, nullptr, M, N,
+                       K, ldq, (int64_t)0, RF_ACT_NONE, ea, 0);
+    return rf_check_launch("gemm_lds_kernel (compact)");
+}
+
 bool lds_disabled() {  // RF_GEMM_LDS=0: the register-staged kernel everywhere (A/B measurement only)
     static const bool off = [] {
         const char* e = getenv("RF_GEMM_LDS");
@@ -1971,6 +2060,25 @@ extern "C" int rf_linear_splitk_fwd(const void* x, int32_t x_dtype, int64_t M, i
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, (const float*)ws, S, M, N, b, act, y, ldy);
     return rf_check_launch("splitk_reduce_kernel");
+}
+
+extern "C" int rf_ip_candidates_f32(const float* q, int64_t ldq, int32_t M, const float* items, int32_t N, int32_t K,
+                                    const float* thr, int32_t cap, int32_t* count, float* cand_val, uint32_t* cand_idx,
+                                    int64_t col_base, void* stream) {
+    RF_REQUIRE(M >= 0 && N >= 0 && K >= 256 && K % 32 == 0 && ldq >= K && ldq % 4 == 0 && cap >= 1,
+               "rf_ip_candidates_f32: needs K >= 256, K %% 32 == 0, ldq %% 4 == 0, cap >= 1");
+    RF_REQUIRE(col_base >= 0 && col_base + N <= ((int64_t)1 << 32) - 1, "rf_ip_candidates_f32: item index must fit 32 bits");
+    if (M == 0 || N == 0) return RF_OK;
+    RF_REQUIRE(q && items && thr && count && cand_val && cand_idx, "rf_ip_candidates_f32: null pointer");
+    RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)items & 15) == 0, "rf_ip_candidates_f32: q / items must be 16-byte aligned");
+    EpiArgs ea{};
+    ea.thr = thr;
+    ea.ccount = count;
+    ea.cval = cand_val;
+    ea.cidx = cand_idx;
+    ea.cap = cap;
+    ea.cbase = col_base;
+    return launch_ip_candidates(q, ldq, M, items, K, N, K, ea, rf_stream(stream));
 }
 
 extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,

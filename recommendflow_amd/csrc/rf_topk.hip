@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
                                                         int64_t col_base, const float* __restrict__ prev_val,
                                                         const int64_t* __restrict__ prev_idx, int k_prev, int64_t prev_ld,
                                                         float* __restrict__ out_val, int64_t* __restrict__ out_idx,
-                                                        int64_t out_ld) {
+                                                        int64_t out_ld, const uint32_t* __restrict__ col_idx) {
     __shared__ uint32_t hist[kWavesTopk][256];
     __shared__ uint32_t tot[256];
     __shared__ uint64_t cand[2 * kMaxK];
@@ -47,6 +47,7 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int64_t row = blockIdx.x;
     const float* srow = scores + row * ld;
+    const uint32_t* irow = col_idx ? col_idx + row * ld : nullptr;  // explicit item indices (rf_topk_merge_idx)
 
     // previous running top-k as keys (entries with index -1 are empty), and whether it is sorted
     if (t == 0) s_unsorted = 0;
@@ -70,7 +71,8 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     for (int j = 0; j < IPT; ++j) {
         const int c = t + kThreads * j;
         const float s = c < cols ? srow[c] : __builtin_nanf("");
-        uint64_t kv = !isnan(s) ? ((uint64_t)f2key(s) << 32) | (uint64_t)(~(uint32_t)(col_base + c)) : 0ull;
+        const uint32_t ix = irow ? (c < cols ? irow[c] : 0u) : (uint32_t)(col_base + c);
+        uint64_t kv = !isnan(s) ? ((uint64_t)f2key(s) << 32) | (uint64_t)(~ix) : 0ull;
         if (kv <= floor_key) kv = 0ull;
         key[j] = kv;
         nvalid += kv != 0ull;
@@ -220,9 +222,10 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
 
 }  // namespace
 
-extern "C" int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int32_t cols, int32_t k, int64_t col_base,
-                             const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld,
-                             float* out_val, int64_t* out_idx, int64_t out_ld, void* stream) {
+namespace {
+int topk_launch(const float* scores, const uint32_t* col_idx, int64_t ld, int32_t rows, int32_t cols, int32_t k,
+                int64_t col_base, const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld,
+                float* out_val, int64_t* out_idx, int64_t out_ld, void* stream) {
     RF_REQUIRE(rows >= 0 && cols >= 0 && cols <= 32 * kThreads, "rf_topk_merge: cols must be in [0, 32768]");
     RF_REQUIRE(k >= 1 && k <= kMaxK && k_prev >= 0 && k_prev <= kMaxK, "rf_topk_merge: k and k_prev must be in [1, 1024]");
     RF_REQUIRE(ld >= cols && out_ld >= k && (k_prev == 0 || prev_ld >= k_prev), "rf_topk_merge: bad leading dimension");
@@ -234,7 +237,7 @@ extern "C" int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int3
     hipStream_t st = rf_stream(stream);
 #define RF_TOPK(N)                                                                                                  \
     hipLaunchKernelGGL(topk_kernel<N>, dim3(rows), dim3(kThreads), 0, st, scores, ld, cols, k, col_base, prev_val, \
-                       prev_idx, k_prev, prev_ld, out_val, out_idx, out_ld)
+                       prev_idx, k_prev, prev_ld, out_val, out_idx, out_ld, col_idx)
     if (ipt <= 1) RF_TOPK(1);
     else if (ipt <= 2) RF_TOPK(2);
     else if (ipt <= 4) RF_TOPK(4);
@@ -243,4 +246,20 @@ extern "C" int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int3
     else RF_TOPK(32);
 #undef RF_TOPK
     return rf_check_launch("rf_topk_merge");
+}
+}  // namespace
+
+extern "C" int rf_topk_merge(const float* scores, int64_t ld, int32_t rows, int32_t cols, int32_t k, int64_t col_base,
+                             const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld,
+                             float* out_val, int64_t* out_idx, int64_t out_ld, void* stream) {
+    return topk_launch(scores, nullptr, ld, rows, cols, k, col_base, prev_val, prev_idx, k_prev, prev_ld, out_val, out_idx,
+                       out_ld, stream);
+}
+
+extern "C" int rf_topk_merge_idx(const float* scores, const uint32_t* col_idx, int64_t ld, int32_t rows, int32_t cols,
+                                 int32_t k, const float* prev_val, const int64_t* prev_idx, int32_t k_prev, int64_t prev_ld,
+                                 float* out_val, int64_t* out_idx, int64_t out_ld, void* stream) {
+    RF_REQUIRE(cols == 0 || col_idx, "rf_topk_merge_idx: null col_idx");
+    return topk_launch(scores, col_idx, ld, rows, cols, k, 0, prev_val, prev_idx, k_prev, prev_ld, out_val, out_idx, out_ld,
+                       stream);
 }

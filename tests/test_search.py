@@ -199,3 +199,106 @@ def test_attention_fusion_vs_oracle(cuda, C, d, norm):
     np.testing.assert_allclose(out, want, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(af.attention.cpu().numpy(), att, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(af.get_fusion_weights(), att.sum(0, keepdims=True) / att.sum(), rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cols,k", [(100, 10), (5000, 200), (20000, 1024)])
+def test_topk_merge_idx_explicit_indices(cuda, cols, k):
+    """rf_topk_merge_idx: the block's item indices come from col_idx (any order, NaN-padded tail), ties by item index."""
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    rng = np.random.default_rng(cols * 3 + k)
+    B = 11
+    s = (rng.integers(-40, 40, (B, cols)) * 0.5).astype(np.float32)  # many exact ties
+    idx = np.stack([rng.permutation(10 ** 7)[:cols] for _ in range(B)]).astype(np.uint32)
+    s[2, cols // 3:] = np.nan  # a short candidate list
+    prev_v = np.sort((rng.integers(-40, 40, (B, k)) * 0.5).astype(np.float32), axis=1)[:, ::-1].copy()
+    prev_i = (rng.permutation(10 ** 6)[: B * k].reshape(B, k) + 2 * 10 ** 7).astype(np.int64)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    ds, di = dev(s), dev(idx.view(np.int32))
+    pv, pi = dev(prev_v), dev(prev_i)
+    ov = torch.empty((B, k), device="cuda")
+    oi = torch.empty((B, k), dtype=torch.int64, device="cuda")
+    L.call("rf_topk_merge_idx", L.ptr(ds), L.ptr(di), cols, B, cols, k, L.ptr(pv), L.ptr(pi), k, k, L.ptr(ov), L.ptr(oi), k,
+           L.stream_ptr())
+    gv, gi = ov.cpu().numpy(), oi.cpu().numpy()
+    for b in range(B):
+        cand = [(float(s[b, c]), int(idx[b, c])) for c in range(cols) if not np.isnan(s[b, c])]
+        cand += [(float(prev_v[b, j]), int(prev_i[b, j])) for j in range(k)]
+        cand.sort(key=lambda x: (-x[0], x[1]))
+        assert gi[b].tolist() == [w[1] for w in cand[:k]], b
+        assert gv[b].tolist() == [w[0] for w in cand[:k]], b
+
+
+@pytest.mark.gpu
+def test_ip_candidates_exact(cuda):
+    """rf_ip_candidates_f32 keeps exactly the pairs whose rf_linear_fwd score (the same kernel's bits) is >= the row's
+    threshold, with those scores and item indices col_base + n, and counts them."""
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    B, N, E, base = 200, 50000, 256, 70000
+    q = torch.randn((B, E), device="cuda", generator=g)
+    items = torch.randn((N, E), device="cuda", generator=g)
+    full = torch.empty((B, N), device="cuda")
+    L.call("rf_linear_fwd", L.ptr(q), L.DT_F32, B, E, E, L.ptr(items), N, None, 0, L.ptr(full), N, L.stream_ptr())
+    thr = torch.quantile(full[:, :4096], 0.995, dim=1).contiguous()
+    thr[3] = float("inf")  # nothing passes
+    cap = 1024
+    count = torch.zeros(B, dtype=torch.int32, device="cuda")
+    cval = torch.full((B, cap), float("nan"), device="cuda")
+    cidx = torch.empty((B, cap), dtype=torch.int32, device="cuda")
+    L.call("rf_ip_candidates_f32", L.ptr(q), E, B, L.ptr(items), N, E, L.ptr(thr), cap, L.ptr(count), L.ptr(cval),
+           L.ptr(cidx), base, L.stream_ptr())
+    f, t = full.cpu().numpy(), thr.cpu().numpy()
+    cnt, cv, ci = count.cpu().numpy(), cval.cpu().numpy(), cidx.cpu().numpy().view(np.uint32)
+    for b in range(B):
+        want = np.nonzero(f[b] >= t[b])[0]
+        assert cnt[b] == len(want), b
+        assert cnt[b] <= cap
+        got = ci[b, : cnt[b]].astype(np.int64) - base
+        order = np.argsort(got)
+        np.testing.assert_array_equal(got[order], want)
+        np.testing.assert_array_equal(cv[b, : cnt[b]][order].view(np.uint32), f[b, want].view(np.uint32))
+        assert np.isnan(cv[b, cnt[b]:]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 50, 200, 1024])
+@pytest.mark.parametrize("dups", [False, True])
+def test_screened_search_equals_block_loop(cuda, k, dups):
+    """The screened Flat search returns the block loop's top-k bit for bit (values, indices, tie order): 3 full
+    item blocks + a tail, E = 256; with duplicated item rows every score ties with another item's."""
+    from recommendflow_amd.backend.third_party_components.faiss_searcher import FaissSearcher
+
+    rng = np.random.default_rng(k + 1000 * dups)
+    N, E, B = 3 * 32768 + 5000, 256, 300
+    items = rng.normal(size=(N, E)).astype(np.float32)
+    if dups:
+        items[1::2] = items[0::2][: N // 2]
+    q = rng.normal(size=(B, E)).astype(np.float32)
+    s = FaissSearcher(items=items, index_param="Flat", measurement="ip").train()
+    s.screen = False
+    want_v, want_i = [t.cpu().numpy() for t in s.search_index(q, k)]
+    s.screen = True
+    got_v, got_i = [t.cpu().numpy() for t in s.search_index(q, k)]
+    np.testing.assert_array_equal(got_i, want_i)
+    np.testing.assert_array_equal(got_v.view(np.uint32), want_v.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_screened_search_overflow_falls_back(cuda):
+    """Every item identical: every candidate list overflows its cap, and the block loop answers."""
+    from recommendflow_amd.backend.third_party_components.faiss_searcher import FaissSearcher
+
+    N, E, B, k = 2 * 32768 + 300, 256, 8, 10
+    items = np.ones((N, E), np.float32)
+    q = np.random.default_rng(2).normal(size=(B, E)).astype(np.float32)
+    s = FaissSearcher(items=items, index_param="Flat", measurement="ip").train()
+    v, i = [t.cpu().numpy() for t in s.search_index(q, k)]
+    assert (i == np.arange(k)[None, :]).all()  # all tie: the smallest item indices
+    assert np.allclose(v, q.sum(1, keepdims=True), rtol=1e-5, atol=1e-4)
