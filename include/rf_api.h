@@ -741,6 +741,19 @@ int rf_topk_merge_idx(const float* scores, const uint32_t* col_idx, int64_t ld, 
 int rf_ip_candidates_f32(const float* q, int64_t ldq, int32_t M, const float* items, int32_t N, int32_t K,
                          const float* thr, int32_t cap, int32_t* count, float* cand_val, uint32_t* cand_idx,
                          int64_t col_base, void* stream);
+/* The same screen on bf16 copies of q and the items (rows of K % 64 == 0 bf16, ldq % 8 == 0): a pair is kept when its
+ * bf16 score (fp32 accumulation) is >= thr[m] - qbound[m] * vnorm[n], with qbound = C ||q_m|| and vnorm the items'
+ * fp32 norms; C >= (2u + u^2 + 2 gamma_K (1 + u)^2) (u = 2^-8, gamma_K = K 2^-24 / (1 - K 2^-24)) bounds the distance
+ * between a bf16 score and the fp32 one, so every pair whose fp32 score reaches thr[m] is kept (finite inputs). The
+ * kept scores are bf16 ones: rf_ip_rescore_f32 replaces them by the exact fp32 scores. */
+int rf_ip_candidates_bf16(const void* q, int64_t ldq, int32_t M, const void* items, int32_t N, int32_t K, const float* thr,
+                          const float* qbound, const float* vnorm, int32_t cap, int32_t* count, float* cand_val,
+                          uint32_t* cand_idx, int64_t col_base, void* stream);
+/* cand_val[m][c] = the fp32 score <q_m, items[cand_idx[m][c]]> for c < min(count[m], cap), computed in the k order
+ * of rf_linear_fwd's fp32 MFMA kernel (per 32-k step, half, element, lane group ascending: an fmaf chain), i.e.
+ * the same bits as rf_linear_fwd (order = 0; 1 = lane groups descending, a diagnostic). K % 32 == 0, K <= 8192. */
+int rf_ip_rescore_f32(const float* q, int64_t ldq, int32_t M, const float* items, int32_t K, const int32_t* count,
+                      int32_t cap, float* cand_val, const uint32_t* cand_idx, int32_t order, void* stream);
 
 /*
  * Que2Search AttentionFusion forward (backend/layers/fusion_layers.py:35-46), fp32:

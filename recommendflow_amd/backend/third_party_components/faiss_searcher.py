@@ -14,7 +14,11 @@ N - 32768 items (rf_ip_candidates_f32: the same fp32 MFMA scores, no score matri
 above it; one rf_topk_merge_idx over those candidates and the first block's top-k gives the result. Same scores,
 same ties (item index), same top-k as the block loop; a query whose candidate list overflows `cap` sends the whole
 batch back to the block loop (one host read of the counts). It removes the [B, N] score matrix's write and re-read
-(2 x 4.3 GB at the cfg5 shapes).
+(2 x 4.3 GB at the cfg5 shapes). On long catalogs (more than 8 blocks, E % 64 == 0) the first 4 blocks are scored
+exactly for the threshold and the rest is screened on bf16 copies (rf_ip_candidates_bf16: a pair is kept when its
+bf16 score is within the bf16 error bound C ||q|| ||v|| of the threshold), the kept pairs rescored exactly in
+rf_linear_fwd's k order (rf_ip_rescore_f32: the same bits) before the merge: the result is still the block loop's,
+bit for bit.
 
 search() returns what the reference returns without an encoder: (item_list[indexes], directories) for
 an int topK, {k: (items, sims)} for a list of topK (:178-204).
@@ -30,6 +34,11 @@ from ...runtime import lib as L
 
 BLOCK = 32768
 SCREEN_CAP_MAX = 32768  # rf_topk_merge_idx's column limit
+# bf16 screen: |<q~, v~> - <q, v>| <= (2u + u^2 + 2 gamma_K (1 + u)^2) sum |q_i v_i| <= C ||q|| ||v|| with u = 2^-8 (bf16
+# round to nearest), gamma_K = K 2^-24 / (1 - K 2^-24) for the fp32 sums of both (K <= 1024): 0.00791 at K = 1024;
+# C = 0.008 also covers the rounding of the two norms
+SCREEN_BF16_C = 0.008
+SCREEN_EXACT_BLOCKS = 4  # leading blocks scored exactly for the threshold before a bf16 screen
 
 
 class FaissSearcher:
@@ -71,9 +80,18 @@ class FaissSearcher:
 
     def train(self):
         self.index = self.get_vecs(self.items)  # [N, E] resident in HBM
+        self.index_bf16 = None  # the bf16 screen's copy and the item norms, built on first use
         return self
 
+    def _bf16_screen_index(self):
+        if getattr(self, "index_bf16", None) is None:
+            self.index_bf16 = self.index.to(torch.bfloat16).contiguous()
+            self.index_norm = self.index.norm(dim=1).contiguous()
+        return self.index_bf16, self.index_norm
+
     screen = True  # the screened search where it applies (A/B: False keeps the block loop)
+
+    screen_bf16 = True  # the bf16 screen + exact rescoring where the catalog is long enough (A/B: False)
 
     def _screened(self, q: torch.Tensor, k: int):
         """The screened search (module docstring), or None when a candidate list overflowed."""
@@ -81,24 +99,46 @@ class FaissSearcher:
         N = self.index.shape[0]
         dev = self.device
         st = L.stream_ptr()
+        bf = self.screen_bf16 and N > 2 * SCREEN_EXACT_BLOCKS * BLOCK and E % 64 == 0 and E <= 1024
+        n0 = SCREEN_EXACT_BLOCKS * BLOCK if bf else BLOCK
+        # the leading items exactly: the block loop's scores and merges
         scores = torch.empty((B, BLOCK), dtype=torch.float32, device=dev)
-        L.call("rf_linear_fwd", L.ptr(q), L.DT_F32, B, E, q.stride(0), L.ptr(self.index), BLOCK, None, 0, L.ptr(scores),
-               scores.stride(0), st)
-        v0 = torch.empty((B, k), dtype=torch.float32, device=dev)
-        i0 = torch.empty((B, k), dtype=torch.int64, device=dev)
-        L.call("rf_topk_merge", L.ptr(scores), scores.stride(0), B, BLOCK, k, 0, None, None, 0, k, L.ptr(v0), L.ptr(i0), k, st)
+        vals = [torch.empty((B, k), dtype=torch.float32, device=dev) for _ in range(2)]
+        idxs = [torch.empty((B, k), dtype=torch.int64, device=dev) for _ in range(2)]
+        cur, k_prev = 0, 0
+        for c0 in range(0, n0, BLOCK):
+            L.call("rf_linear_fwd", L.ptr(q), L.DT_F32, B, E, q.stride(0), L.ptr(self.index[c0:]), BLOCK, None, 0,
+                   L.ptr(scores), scores.stride(0), st)
+            nxt = 1 - cur
+            L.call("rf_topk_merge", L.ptr(scores), scores.stride(0), B, BLOCK, k, c0, L.ptr(vals[cur]), L.ptr(idxs[cur]),
+                   k_prev, k, L.ptr(vals[nxt]), L.ptr(idxs[nxt]), k, st)
+            cur, k_prev = nxt, k
         del scores
-        thr = v0[:, k - 1].contiguous()  # -inf where the block held fewer than k scores (then every item passes)
-        # room for ~3x the candidates a uniform score distribution gives (k per 32768 items), at most 32768
-        cap = int(min(SCREEN_CAP_MAX, max(1024, 3 * k * (N - BLOCK) // BLOCK + k)))
+        v0, i0 = vals[cur], idxs[cur]
+        thr = v0[:, k - 1].contiguous()  # -inf where the blocks held fewer than k scores (then every item passes)
+        # room for ~3x the candidates a uniform score distribution gives (k per n0 items; x1.5 for the bf16 margin)
+        per = 3 * k * (N - n0) // n0 * (3 if bf else 2) // 2 + k
+        cap = int(min(SCREEN_CAP_MAX, max(1024, per)))
         count = torch.zeros(B, dtype=torch.int32, device=dev)
         cval = torch.full((B, cap), float("nan"), dtype=torch.float32, device=dev)
         cidx = torch.empty((B, cap), dtype=torch.int32, device=dev)
-        rest = self.index[BLOCK:]
-        L.call("rf_ip_candidates_f32", L.ptr(q), q.stride(0), B, L.ptr(rest), N - BLOCK, E, L.ptr(thr), cap, L.ptr(count),
-               L.ptr(cval), L.ptr(cidx), BLOCK, st)
-        if int(count.max().item()) > cap:
-            return None
+        if bf:
+            # candidates by bf16 scores within their error bound of the threshold, then their exact fp32 scores in
+            # rf_linear_fwd's k order (rf_ip_rescore_f32: the same bits)
+            ib, vn = self._bf16_screen_index()
+            qb = q.to(torch.bfloat16).contiguous()
+            qbound = (q.norm(dim=1) * SCREEN_BF16_C).contiguous()
+            L.call("rf_ip_candidates_bf16", L.ptr(qb), qb.stride(0), B, L.ptr(ib[n0:]), N - n0, E, L.ptr(thr),
+                   L.ptr(qbound), L.ptr(vn[n0:]), cap, L.ptr(count), L.ptr(cval), L.ptr(cidx), n0, st)
+            if int(count.max().item()) > cap:
+                return None
+            L.call("rf_ip_rescore_f32", L.ptr(q), q.stride(0), B, L.ptr(self.index), E, L.ptr(count), cap, L.ptr(cval),
+                   L.ptr(cidx), 0, st)
+        else:
+            L.call("rf_ip_candidates_f32", L.ptr(q), q.stride(0), B, L.ptr(self.index[n0:]), N - n0, E, L.ptr(thr), cap,
+                   L.ptr(count), L.ptr(cval), L.ptr(cidx), n0, st)
+            if int(count.max().item()) > cap:
+                return None
         out_v = torch.empty((B, k), dtype=torch.float32, device=dev)
         out_i = torch.empty((B, k), dtype=torch.int64, device=dev)
         L.call("rf_topk_merge_idx", L.ptr(cval), L.ptr(cidx), cap, B, cap, k, L.ptr(v0), L.ptr(i0), k, k, L.ptr(out_v),

@@ -644,6 +644,8 @@ struct EpiArgs {
     uint32_t* cidx;      // kEpiCompact: [M][cap] item indices
     int cap;
     int64_t cbase;       // kEpiCompact: item index of column 0
+    const float* qbound; // kEpiCompact, optional: the pass test is y >= thr[row] - qbound[row] * vnorm[col] (a screen
+    const float* vnorm;  //   on rounded operands with its error bound), both or neither
 };
 
 // the head's outputs of one row from its logits: softmax over the kHeadN values, or an elementwise activation
@@ -785,7 +787,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
         }
     }
     // kEpiCompact: this lane's row thresholds, loaded under the k-loop like the column parameters (+inf past M)
-    float tv[EPI == kEpiCompact ? FM : 1][4];
+    float tv[EPI == kEpiCompact ? FM : 1][4], qv[EPI == kEpiCompact ? FM : 1][4], vv[EPI == kEpiCompact ? FN : 1];
     if constexpr (EPI == kEpiCompact) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -793,7 +795,10 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             for (int r = 0; r < 4; ++r) {
                 const int64_t row = m0 + wm * TM + lg * 4 + i * 16 + r;
                 tv[i][r] = row < M ? ea.thr[row] : INFINITY;
+                qv[i][r] = ea.qbound && row < M ? ea.qbound[row] : 0.f;
             }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) vv[j] = ea.vnorm ? ea.vnorm[min(n0 + wn * TN + j * 16 + lr, N - 1)] : 0.f;
     }
     // LN-fold row statistics (mu, rstd per tile row), in an LDS area past the ring
     float* srow = reinterpret_cast<float*>(smem_raw + (size_t)ST * (A_EL + B_EL) * sizeof(T));
@@ -976,7 +981,8 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
             for (int r = 0; r < 4; ++r) {
                 uint32_t m = 0;
 #pragma unroll
-                for (int j = 0; j < FN; ++j) m |= (cbase + j * 16 < N && acc[i][j][r] >= tv[i][r]) ? (1u << j) : 0u;
+                for (int j = 0; j < FN; ++j)
+                    m |= (cbase + j * 16 < N && acc[i][j][r] >= tv[i][r] - qv[i][r] * vv[j]) ? (1u << j) : 0u;
                 const int n = __builtin_popcount(m);
                 int incl = n;
 #pragma unroll
@@ -2003,15 +2009,15 @@ int launch_lds_f32(const void* x, const void* W, const float* b, float* y, int64
 }
 
 // rf_ip_candidates_f32: the compaction form of the fp32 LDS-DMA GEMM (gemm_lds_kernel<128, kEpiCompact, F32>)
-int launch_ip_candidates(const float* q, int64_t ldq, int64_t M, const float* items, int64_t ldi, int N, int K, const EpiArgs& ea,
+template <bool F32>
+int launch_ip_candidates(const void* q, int64_t ldq, int64_t M, const void* items, int N, int K, const EpiArgs& ea,
                          hipStream_t st) {
-    auto kern = gemm_lds_kernel<128, kEpiCompact, true>;
+    auto kern = gemm_lds_kernel<128, kEpiCompact, F32>;
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)gemm_lds_bytes<128>());
     if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm_lds_kernel (compact): %s", hipGetErrorString(e));
     const int64_t tiles = ((M + 127) / 128) * ((N + kLdsBN - 1) / kLdsBN);
-    RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_ip_candidates_f32: too many tiles");
-    (void)ldi;
+    RF_REQUIRE(tiles < (int64_t)1 << 31, "rf_ip_candidates: too many tiles");
     hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), gemm_lds_bytes<128>(), st, q, items, nullptr, nullptr, M, N,
                        K, ldq, (int64_t)0, RF_ACT_NONE, ea, 0);
     return rf_check_launch("gemm_lds_kernel (compact)");
@@ -2078,7 +2084,28 @@ extern "C" int rf_ip_candidates_f32(const float* q, int64_t ldq, int32_t M, cons
     ea.cidx = cand_idx;
     ea.cap = cap;
     ea.cbase = col_base;
-    return launch_ip_candidates(q, ldq, M, items, K, N, K, ea, rf_stream(stream));
+    return launch_ip_candidates<true>(q, ldq, M, items, N, K, ea, rf_stream(stream));
+}
+
+extern "C" int rf_ip_candidates_bf16(const void* q, int64_t ldq, int32_t M, const void* items, int32_t N, int32_t K,
+                                     const float* thr, const float* qbound, const float* vnorm, int32_t cap, int32_t* count,
+                                     float* cand_val, uint32_t* cand_idx, int64_t col_base, void* stream) {
+    RF_REQUIRE(M >= 0 && N >= 0 && K >= 64 && K % 64 == 0 && ldq >= K && ldq % 8 == 0 && cap >= 1,
+               "rf_ip_candidates_bf16: needs K %% 64 == 0, ldq %% 8 == 0, cap >= 1");
+    RF_REQUIRE(col_base >= 0 && col_base + N <= ((int64_t)1 << 32) - 1, "rf_ip_candidates_bf16: item index must fit 32 bits");
+    if (M == 0 || N == 0) return RF_OK;
+    RF_REQUIRE(q && items && thr && qbound && vnorm && count && cand_val && cand_idx, "rf_ip_candidates_bf16: null pointer");
+    RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)items & 15) == 0, "rf_ip_candidates_bf16: q / items must be 16-byte aligned");
+    EpiArgs ea{};
+    ea.thr = thr;
+    ea.qbound = qbound;
+    ea.vnorm = vnorm;
+    ea.ccount = count;
+    ea.cval = cand_val;
+    ea.cidx = cand_idx;
+    ea.cap = cap;
+    ea.cbase = col_base;
+    return launch_ip_candidates<false>(q, ldq, M, items, N, K, ea, rf_stream(stream));
 }
 
 extern "C" int rf_linear_fwd(const void* x, int32_t x_dtype, int64_t M, int32_t K, int64_t ldx, const void* W,

@@ -124,6 +124,8 @@ _SIGS = {
     "rf_topk_merge": (ctypes.c_int, [_vp, _i64, _i32, _i32, _i32, _i64, _vp, _vp, _i32, _i64, _vp, _vp, _i64, _vp]),
     "rf_topk_merge_idx": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _i64, _vp, _vp, _i64, _vp]),
     "rf_ip_candidates_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _i64, _vp]),
+    "rf_ip_rescore_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _i32, _vp]),
+    "rf_ip_candidates_bf16": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _vp]),
 }
 EXPORTED = tuple(_SIGS)
 # include/rf_diag.h: tools-only entry points (not the production ABI)

@@ -302,3 +302,54 @@ def test_screened_search_overflow_falls_back(cuda):
     v, i = [t.cpu().numpy() for t in s.search_index(q, k)]
     assert (i == np.arange(k)[None, :]).all()  # all tie: the smallest item indices
     assert np.allclose(v, q.sum(1, keepdims=True), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [256, 512])
+def test_ip_rescore_matches_linear_fwd_bits(cuda, K):
+    """rf_ip_rescore_f32 (order 0) reproduces rf_linear_fwd's fp32 scores bit for bit on random candidate pairs."""
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    g = torch.Generator(device="cuda").manual_seed(K)
+    B, N, cap = 48, 30000, 1500
+    q = torch.randn((B, K), device="cuda", generator=g)
+    items = torch.randn((N, K), device="cuda", generator=g)
+    full = torch.empty((B, N), device="cuda")
+    L.call("rf_linear_fwd", L.ptr(q), L.DT_F32, B, K, K, L.ptr(items), N, None, 0, L.ptr(full), N, L.stream_ptr())
+    idx = torch.stack([torch.randperm(N, generator=torch.Generator().manual_seed(r))[:cap] for r in range(B)]).cuda()
+    cidx = idx.to(torch.int32).contiguous()
+    count = torch.full((B,), cap, dtype=torch.int32, device="cuda")
+    count[3] = 7  # short list: entries past it untouched
+    cval = torch.full((B, cap), float("nan"), device="cuda")
+    L.call("rf_ip_rescore_f32", L.ptr(q), K, B, L.ptr(items), K, L.ptr(count), cap, L.ptr(cval), L.ptr(cidx), 0,
+           L.stream_ptr())
+    want = torch.gather(full, 1, idx)
+    got = cval.clone()
+    assert torch.isnan(got[3, 7:]).all()
+    got[3, 7:] = want[3, 7:]
+    assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [50, 200])
+@pytest.mark.parametrize("dups", [False, True])
+def test_bf16_screened_search_equals_block_loop(cuda, k, dups):
+    """The bf16 screen (9 blocks + a tail: 4 exact blocks, the rest screened on bf16 copies within the bf16 error
+    bound, the kept pairs rescored exactly) returns the block loop's top-k bit for bit."""
+    from recommendflow_amd.backend.third_party_components.faiss_searcher import FaissSearcher
+
+    rng = np.random.default_rng(k + 7 * dups)
+    N, E, B = 9 * 32768 + 3000, 256, 200
+    items = rng.normal(size=(N, E)).astype(np.float32)
+    if dups:
+        items[5::7] = items[0] * 1.0  # many exact duplicates of one item: score ties across the blocks
+    q = rng.normal(size=(B, E)).astype(np.float32)
+    s = FaissSearcher(items=items, index_param="Flat", measurement="ip").train()
+    s.screen = False
+    want_v, want_i = [t.cpu().numpy() for t in s.search_index(q, k)]
+    s.screen = True
+    got_v, got_i = [t.cpu().numpy() for t in s.search_index(q, k)]
+    np.testing.assert_array_equal(got_i, want_i)
+    np.testing.assert_array_equal(got_v.view(np.uint32), want_v.view(np.uint32))

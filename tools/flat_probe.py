@@ -45,7 +45,9 @@ def ev(fn, reps=5):
 
 s.screen = False
 res = {"search_index_block_loop_ms": round(ev(lambda: s.search_index(q, K)), 3)}
-s.screen = True
+s.screen, s.screen_bf16 = True, False
+res["search_index_screened_fp32_ms"] = round(ev(lambda: s.search_index(q, K)), 3)
+s.screen_bf16 = True
 res["search_index_screened_ms"] = round(ev(lambda: s.search_index(q, K)), 3)
 a_v, a_i = s.search_index(q, K)
 s.screen = False
