@@ -166,6 +166,13 @@ int rf_table_init_uniform(void* table, int32_t dtype, int64_t rows, int32_t dim,
 int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L,
                                int32_t d, int64_t ex_stride, int64_t ld, float* out, int64_t out_stride,
                                int64_t out_off, float* att_out, void* stream);
+/* rf_esim_soft_attention_fwd over pairs built by index instead of copies (the cascade's rank stage, cfg5): pair e
+ * reads its q sequence at q + (e / q_rep) * q_stride (one user's sequence for q_rep consecutive candidates) and its
+ * a sequence at a + a_rows[e] * a_stride (a candidate item's row of a catalog of encoded sequences); rows ld apart
+ * inside an example. Same pooled values as expanding / gathering q and a first. */
+int rf_esim_soft_attention_idx_fwd(const void* q, int32_t q_rep, const void* a, const int64_t* a_rows, int64_t a_stride,
+                                   int32_t dtype, int32_t batch, int32_t L, int32_t d, int64_t q_stride, int64_t ld,
+                                   float* out, int64_t out_stride, int64_t out_off, void* stream);
 
 /*
  * Exact-fp32 GEMM of the DSSM towers, forward and training step (models/matching/dssm.py:25-26 create_mlp(...,

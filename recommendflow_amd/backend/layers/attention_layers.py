@@ -53,6 +53,25 @@ def esim_soft_attention_pool(q: torch.Tensor, a: torch.Tensor, out: Optional[tor
     return out
 
 
+def esim_soft_attention_pool_idx(q: torch.Tensor, q_rep: int, a_table: torch.Tensor, a_rows: torch.Tensor,
+                                 out: torch.Tensor, out_col: int = 0, stream=None) -> torch.Tensor:
+    """esim_soft_attention_pool over B * q_rep pairs without materialising them: pair e takes q[e // q_rep]
+    ([Bq, L, d]) and a_table[a_rows[e]] ([N, L, d]); fills out[:, out_col:out_col + 6d] (rf_esim_soft_attention_idx_fwd)."""
+    L.require_gpu()
+    if q.dtype != a_table.dtype or q.dtype not in (torch.bfloat16, torch.float16):
+        raise ValueError("q and a_table must share a bf16 / f16 dtype")
+    if q.dim() != 3 or a_table.dim() != 3 or q.shape[1:] != a_table.shape[1:] or not q.is_contiguous() or not a_table.is_contiguous():
+        raise ValueError("q [Bq, L, d] and a_table [N, L, d] must be contiguous with the same (L, d)")
+    a_rows = a_rows.reshape(-1).to(torch.int64).contiguous()
+    P = a_rows.numel()
+    if P != q.shape[0] * q_rep or out.shape[0] != P:
+        raise ValueError(f"{P} pairs need q with {P // max(q_rep, 1)} rows x q_rep {q_rep} and out with {P} rows")
+    _, Ln, d = q.shape
+    L.call("rf_esim_soft_attention_idx_fwd", L.ptr(q), int(q_rep), L.ptr(a_table), L.ptr(a_rows), Ln * d,
+           L.torch_dtype_code(q.dtype), P, Ln, d, Ln * d, d, L.ptr(out), out.stride(0), out_col, L.stream_ptr(stream))
+    return out
+
+
 class SoftAttention:
     """SoftAttention()([x0, x1]) -> (S @ x0, S @ x1), E[n,i,j] = x1[n,i] . x0[n,j], S = softmax_j(E)."""
 

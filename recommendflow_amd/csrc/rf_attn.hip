@@ -775,6 +775,11 @@ struct EsimGatherArgs {
     uint16_t* outb;        // OB only: the pooled features as bf16 (row stride out_stride, column out_off) ...
     float* ostats;         // ... and per 32-column slice (sum, squared deviations from the slice mean) of the fp32
     int oP, op0;           // values: ostats[row][op0 + slice], oP pairs per row (rf_linear_lnfold_* consume them)
+    // plain (non-GATHER) path, rf_esim_soft_attention_idx_fwd: example e reads q example e / q_rep (q_rep >= 1; 0 = 1)
+    // and a example a_rows[e] (a_stride elements apart; a_rows == nullptr: e, ex_stride apart)
+    int q_rep;
+    const int64_t* a_rows;
+    int64_t a_stride;
 };
 
 template <bool F16, int D, int NTT, int XM, bool GATHER = false, bool STAMP = false, bool OB = false>
@@ -805,8 +810,10 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     uint4 pre[NCH];
     const int img_bytes = L * (int)ld * 2;
     auto prefetch = [&](int64_t e) __attribute__((always_inline)) {
-        const auto rq = __builtin_amdgcn_make_buffer_rsrc((void*)(q + e * ex_stride), 0, img_bytes, 0x00020000);
-        const auto ra = __builtin_amdgcn_make_buffer_rsrc((void*)(a + e * ex_stride), 0, img_bytes, 0x00020000);
+        const int64_t eq = ga.q_rep > 1 ? e / ga.q_rep : e;
+        const uint16_t* ap = ga.a_rows ? a + ga.a_rows[e] * ga.a_stride : a + e * ex_stride;
+        const auto rq = __builtin_amdgcn_make_buffer_rsrc((void*)(q + eq * ex_stride), 0, img_bytes, 0x00020000);
+        const auto ra = __builtin_amdgcn_make_buffer_rsrc((void*)ap, 0, img_bytes, 0x00020000);
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int cm = tid + (i % HALF) * NTH;
@@ -1192,7 +1199,7 @@ int launch_big_lds(K kernel, int grid, size_t lds, hipStream_t st, const char* n
 
 template <bool F16, int D, int NTT>
 int launch_esim2_nt(int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L, int64_t ex_stride,
-                    int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
+                    int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimGatherArgs& ga) {
     // RF_ESIM_XM=0 keeps the v3 statistics (x read from LDS and converted on the VALU); A/B runs only
     static const int xm = [] {
         const char* e = getenv("RF_ESIM_XM");
@@ -1202,16 +1209,16 @@ int launch_esim2_nt(int grid, size_t lds, hipStream_t st, const void* q, const v
     const int rc = launch_big_lds(kern, grid, lds, st, "esim2_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kEsim2Waves * 64), lds, st, (const uint16_t*)q, (const uint16_t*)a, batch, L,
-                       ex_stride, ld, out, out_stride, out_off, EsimGatherArgs{});
+                       ex_stride, ld, out, out_stride, out_off, ga);
     return RF_OK;
 }
 
 template <bool F16, int D>
 int launch_esim2(int nt, int grid, size_t lds, hipStream_t st, const void* q, const void* a, int batch, int L,
-                 int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off) {
+                 int64_t ex_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off, const EsimGatherArgs& ga) {
     switch (nt) {
 #define RF_NT(N) \
-    case N: return launch_esim2_nt<F16, D, N>(grid, lds, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
+    case N: return launch_esim2_nt<F16, D, N>(grid, lds, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ga);
         RF_NT(1) RF_NT(2) RF_NT(3) RF_NT(4) RF_NT(5) RF_NT(6) RF_NT(7) RF_NT(8)
 #undef RF_NT
         default: return rf_set_error(RF_EINVAL, "esim2: bad tile count %d", nt);
@@ -1220,7 +1227,8 @@ int launch_esim2(int nt, int grid, size_t lds, hipStream_t st, const void* q, co
 
 // the 4-wave persistent kernel (two workgroups per CU when the images fit 80 KB)
 int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, int32_t L, int32_t d, int64_t ex_stride,
-                   int64_t ld, float* out, int64_t out_stride, int64_t out_off, hipStream_t st) {
+                   int64_t ld, float* out, int64_t out_stride, int64_t out_off, hipStream_t st,
+                   const EsimGatherArgs& ga = EsimGatherArgs{}) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int nt = (L + 15) >> 4;
@@ -1228,10 +1236,10 @@ int esim2_dispatch(const void* q, const void* a, int32_t dtype, int32_t batch, i
     const int per_cu = lds2 <= 80 * 1024 ? 2 : 1;
     const int grid2 = (int)std::min<int64_t>(batch, (int64_t)per_cu * cus);
     if (dtype == RF_DTYPE_BF16)
-        return d == 64 ? launch_esim2<false, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
-                       : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
-    return d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off)
-                   : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off);
+        return d == 64 ? launch_esim2<false, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ga)
+                       : launch_esim2<false, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ga);
+    return d == 64 ? launch_esim2<true, 64>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ga)
+                   : launch_esim2<true, 128>(nt, grid2, lds2, st, q, a, batch, L, ex_stride, ld, out, out_stride, out_off, ga);
 }
 
 // GATHER: bf16 tables, the v5 statistics, two workgroups per CU when images + id buffers fit 80 KB
@@ -1312,6 +1320,28 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
     }
 #undef RF_ESIM_LAUNCH
     return rf_check_launch("esim_kernel");
+}
+
+extern "C" int rf_esim_soft_attention_idx_fwd(const void* q, int32_t q_rep, const void* a, const int64_t* a_rows,
+                                              int64_t a_stride, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                                              int64_t q_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
+                                              void* stream) {
+    RF_REQUIRE(dtype == RF_DTYPE_BF16 || dtype == RF_DTYPE_F16, "rf_esim_soft_attention_idx_fwd: dtype must be BF16 or F16");
+    RF_REQUIRE(L >= 1 && L <= 128 && (d == 64 || d == 128) && batch >= 0 && q_rep >= 1,
+               "rf_esim_soft_attention_idx_fwd: need 1 <= L <= 128, d 64 or 128, batch >= 0, q_rep >= 1");
+    RF_REQUIRE(ld % 8 == 0 && q_stride % 8 == 0 && a_stride % 8 == 0 && ld >= d,
+               "rf_esim_soft_attention_idx_fwd: ld / q_stride / a_stride must be multiples of 8 elements");
+    RF_REQUIRE((int64_t)L * ld * 2 < ((int64_t)1 << 31), "rf_esim_soft_attention_idx_fwd: one example's rows must span < 2 GiB");
+    RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)a & 15) == 0, "rf_esim_soft_attention_idx_fwd: q/a must be 16-byte aligned");
+    if (batch == 0) return RF_OK;
+    RF_REQUIRE(q && a && a_rows && out, "rf_esim_soft_attention_idx_fwd: null pointer");
+    EsimGatherArgs ga{};
+    ga.q_rep = q_rep;
+    ga.a_rows = a_rows;
+    ga.a_stride = a_stride;
+    const int rc = esim2_dispatch(q, a, dtype, batch, L, d, q_stride, ld, out, out_stride, out_off, rf_stream(stream), ga);
+    if (rc) return rc;
+    return rf_check_launch("rf_esim_soft_attention_idx_fwd");
 }
 
 extern "C" int rf_sdpa_fwd(const void* q, const void* k, const void* v, int32_t dtype, int32_t batch, int32_t heads,

@@ -25,7 +25,7 @@ from typing import Optional, Sequence
 import torch
 
 from ..backend.encoder.sparse_encoder import FusedSparseEncoder, SlotSpec
-from ..backend.layers.attention_layers import esim_soft_attention_pool
+from ..backend.layers.attention_layers import esim_soft_attention_pool, esim_soft_attention_pool_idx
 from ..backend.layers.core import Dense
 from ..backend.third_party_components.faiss_searcher import FaissSearcher
 from ..runtime import lib as L
@@ -108,13 +108,13 @@ class Cascade(torch.nn.Module):
         cand2 = torch.gather(cand1, 1, pos2)                                                # [B, K2]
         # rank: ESIM over (user sequence, candidate item sequence) pairs, fp16 MFMA attention
         Lq, d = self.ranker.L, self.ranker.d
-        q = self.ranker.enc_q(rank_user).to(self.rank_dtype).view(B, 1, Lq * d).expand(B, self.k2, Lq * d)
-        q = q.reshape(B * self.k2, Lq, d)
-        a = gather_rows(self.a_item, cand2).view(B * self.k2, Lq, d)
+        # the (user, candidate) pairs by index: user b's sequence for its k2 candidates, the candidates' rows of the
+        # encoded catalog (rf_esim_soft_attention_idx_fwd; nothing expanded or gathered)
+        q = self.ranker.enc_q(rank_user).to(self.rank_dtype).view(B, Lq, d).contiguous()
         pooled = torch.empty((B * self.k2, self.ranker.pooled_width), dtype=torch.float32, device=u.device)
         xd = dense.repeat_interleave(self.k2, dim=0) if dense.shape[0] == B else dense
         self.ranker.input_mlp(xd, out=pooled[:, : self.ranker.d_emb])
-        esim_soft_attention_pool(q, a, out=pooled, out_col=self.ranker.d_emb)
+        esim_soft_attention_pool_idx(q, self.k2, self.a_item.view(-1, Lq, d), cand2, out=pooled, out_col=self.ranker.d_emb)
         p = self.ranker.dense_output(self.ranker.output_mlp(pooled))[:, 1].view(B, self.k2)
         s3, pos3 = topk_rows(p, self.k3)
         return CascadeResult(torch.gather(cand2, 1, pos3), s3, cand1, cand2)
