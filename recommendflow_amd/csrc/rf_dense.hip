@@ -983,6 +983,11 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
 #pragma unroll
                 for (int j = 0; j < FN; ++j)
                     m |= (cbase + j * 16 < N && acc[i][j][r] >= tv[i][r] - qv[i][r] * vv[j]) ? (1u << j) : 0u;
+                pm[i][r] = m;
+                pin[i][r] = 0;
+                pbase[i][r] = 0;
+                // most (i, r) slices of a tile (4 rows x 64 columns) hold no candidate: one wave vote skips the count
+                if (!__any(m != 0u)) continue;
                 const int n = __builtin_popcount(m);
                 int incl = n;
 #pragma unroll
@@ -991,9 +996,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
                     if (lr >= o) incl += y;
                 }
                 const int total = __shfl(incl, 15, 16);
-                pm[i][r] = m;
                 pin[i][r] = incl - n;
-                pbase[i][r] = 0;
                 const int64_t row = rbase + i * 16 + r;
                 if (lr == 15 && total > 0) pbase[i][r] = atomicAdd(ea.ccount + row, total);
             }
@@ -1001,6 +1004,7 @@ __global__ __launch_bounds__(256) void gemm_lds_kernel(const void* __restrict__ 
         for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
+                if (!__any(pm[i][r] != 0u)) continue;
                 const int base = __shfl(pbase[i][r], 15, 16);
                 const uint32_t m = pm[i][r];
                 if (m) {
