@@ -15,7 +15,7 @@ above it; one rf_topk_merge_idx over those candidates and the first block's top-
 same ties (item index), same top-k as the block loop; a query whose candidate list overflows `cap` sends the whole
 batch back to the block loop (one host read of the counts). It removes the [B, N] score matrix's write and re-read
 (2 x 4.3 GB at the cfg5 shapes). On long catalogs (more than 8 blocks, E % 64 == 0) the first 4 blocks are scored
-exactly for the threshold and the rest is screened on bf16 copies (rf_ip_candidates_bf16: a pair is kept when its
+exactly for the threshold (blocks 2-4 screened by block 1's k-th score) and the rest is screened on bf16 copies (rf_ip_candidates_bf16: a pair is kept when its
 bf16 score is within the bf16 error bound C ||q|| ||v|| of the threshold), the kept pairs rescored exactly in
 rf_linear_fwd's k order (rf_ip_rescore_f32: the same bits) before the merge: the result is still the block loop's,
 bit for bit.
@@ -101,20 +101,31 @@ class FaissSearcher:
         st = L.stream_ptr()
         bf = self.screen_bf16 and N > 2 * SCREEN_EXACT_BLOCKS * BLOCK and E % 64 == 0 and E <= 1024
         n0 = SCREEN_EXACT_BLOCKS * BLOCK if bf else BLOCK
-        # the leading items exactly: the block loop's scores and merges
+        # the first block exactly (the block loop's scores and merge)
         scores = torch.empty((B, BLOCK), dtype=torch.float32, device=dev)
-        vals = [torch.empty((B, k), dtype=torch.float32, device=dev) for _ in range(2)]
-        idxs = [torch.empty((B, k), dtype=torch.int64, device=dev) for _ in range(2)]
-        cur, k_prev = 0, 0
-        for c0 in range(0, n0, BLOCK):
-            L.call("rf_linear_fwd", L.ptr(q), L.DT_F32, B, E, q.stride(0), L.ptr(self.index[c0:]), BLOCK, None, 0,
-                   L.ptr(scores), scores.stride(0), st)
-            nxt = 1 - cur
-            L.call("rf_topk_merge", L.ptr(scores), scores.stride(0), B, BLOCK, k, c0, L.ptr(vals[cur]), L.ptr(idxs[cur]),
-                   k_prev, k, L.ptr(vals[nxt]), L.ptr(idxs[nxt]), k, st)
-            cur, k_prev = nxt, k
+        v0 = torch.empty((B, k), dtype=torch.float32, device=dev)
+        i0 = torch.empty((B, k), dtype=torch.int64, device=dev)
+        L.call("rf_linear_fwd", L.ptr(q), L.DT_F32, B, E, q.stride(0), L.ptr(self.index), BLOCK, None, 0, L.ptr(scores),
+               scores.stride(0), st)
+        L.call("rf_topk_merge", L.ptr(scores), scores.stride(0), B, BLOCK, k, 0, None, None, 0, k, L.ptr(v0), L.ptr(i0), k, st)
         del scores
-        v0, i0 = vals[cur], idxs[cur]
+        lead_counts = []
+        if n0 > BLOCK:
+            # the next leading blocks exactly as well, but screened by the first block's k-th score (one fp32
+            # compaction launch, one merge of its few candidates) instead of a score block and a merge each
+            t0 = v0[:, k - 1].contiguous()
+            cap0 = int(min(SCREEN_CAP_MAX, max(1024, 3 * k * (n0 - BLOCK) // BLOCK + k)))  # ~3x the expected count
+            cnt0 = torch.zeros(B, dtype=torch.int32, device=dev)
+            cv0 = torch.full((B, cap0), float("nan"), dtype=torch.float32, device=dev)
+            ci0 = torch.empty((B, cap0), dtype=torch.int32, device=dev)
+            L.call("rf_ip_candidates_f32", L.ptr(q), q.stride(0), B, L.ptr(self.index[BLOCK:]), n0 - BLOCK, E, L.ptr(t0),
+                   cap0, L.ptr(cnt0), L.ptr(cv0), L.ptr(ci0), BLOCK, st)
+            v1 = torch.empty_like(v0)
+            i1 = torch.empty_like(i0)
+            L.call("rf_topk_merge_idx", L.ptr(cv0), L.ptr(ci0), cap0, B, cap0, k, L.ptr(v0), L.ptr(i0), k, k, L.ptr(v1),
+                   L.ptr(i1), k, st)
+            v0, i0 = v1, i1
+            lead_counts.append((cnt0, cap0))  # checked with the later counts (one host read)
         thr = v0[:, k - 1].contiguous()  # -inf where the blocks held fewer than k scores (then every item passes)
         # room for ~3x the candidates a uniform score distribution gives (k per n0 items; x1.5 for the bf16 margin)
         per = 3 * k * (N - n0) // n0 * (3 if bf else 2) // 2 + k
@@ -130,7 +141,7 @@ class FaissSearcher:
             qbound = (q.norm(dim=1) * SCREEN_BF16_C).contiguous()
             L.call("rf_ip_candidates_bf16", L.ptr(qb), qb.stride(0), B, L.ptr(ib[n0:]), N - n0, E, L.ptr(thr),
                    L.ptr(qbound), L.ptr(vn[n0:]), cap, L.ptr(count), L.ptr(cval), L.ptr(cidx), n0, st)
-            if int(count.max().item()) > cap:
+            if int(count.max().item()) > cap or any(int(c.max().item()) > cp for c, cp in lead_counts):
                 return None
             L.call("rf_ip_rescore_f32", L.ptr(q), q.stride(0), B, L.ptr(self.index), E, L.ptr(count), cap, L.ptr(cval),
                    L.ptr(cidx), 0, st)
