@@ -2027,6 +2027,255 @@ int launch_ip_candidates(const void* q, int64_t ldq, int64_t M, const void* item
     return rf_check_launch("gemm_lds_kernel (compact)");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Query-stationary bf16 screen (rf_ip_candidates_bf16 at K = 64 / 128 / 256): the kEpiCompact test of
+// gemm_lds_kernel<128, kEpiCompact, bf16> without its per-tile operand traffic. At the cascade's shapes (1024
+// queries x ~1M items x 256) the 128 x 128 tile GEMM re-reads a 64 KB query panel for every 8.4 MFLOP tile and
+// drains its 4-step ring at every tile: 14 % of the bf16 peak (1.29 ms). Here
+//   * a workgroup owns 256 query rows (wave w: rows 64 w .. 64 w + 63) and a contiguous range of 64-item tiles;
+//     each wave keeps its 64 rows x K in registers for the whole launch (A fragments, 16 K / 4 VGPRs per 16 rows);
+//   * the item tiles stream through a 3-deep LDS-DMA ring (global_load_lds_dwordx4, 16-byte chunk c of row r stored
+//     at chunk c ^ (r & 7): conflict-free ds_read_b128 B fragments), tile t + 2 issued when tile t opens;
+//   * per tile and wave 16 accumulator tiles x K / 32 v_mfma_f32_16x16x32_bf16, then the pass test
+//     y >= thr[row] - qbound[row] * vnorm[col] (kEpiCompact's) on all 64 values; one wave vote skips the tile when
+//     nothing passes. At the cascade's pass rate (~0.06 %) most wave tiles (4096 pairs) still hold one or two
+//     passing pairs, and an atomic round trip per tile at one wave per SIMD doubled the launch: passing pairs are
+//     appended to the wave's LDS list instead (a ballot and a lane rank per slot) and the list is flushed to the
+//     rows' candidate lists (one atomic add per pair on its row's counter; counts past cap are kept: the caller's
+//     overflow test) when half full and at the end;
+//   * block b runs on XCD b % 8: the query blocks of one item range are b, b + 8, ..., so they share that XCD's L2
+//     and the items come from HBM about once.
+// One workgroup per CU (the A fragments and accumulators take ~300 registers at one wave per SIMD).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {  // the LDS byte address of a generic pointer into LDS
+    return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+constexpr int kScrTN = 64, kScrStages = 3, kScrQ = 256;  // items per tile, ring depth, query rows per workgroup
+constexpr int kScrList = 1024;                            // passing pairs listed per wave before a flush
+// lab ablations (tools/build_variants.sh -DRF_LAB_SCR=bits; wrong results, never in the shipped build): 1 = no pass
+// test / list, 2 = no MFMAs, 4 = no item copies or waits (stale LDS), 8 = the row pre-filter without the list
+#ifndef RF_LAB_SCR
+#define RF_LAB_SCR 0
+#endif
+
+template <int KT>
+__global__ __launch_bounds__(256) void ip_screen_bf16_kernel(const uint16_t* __restrict__ q, int64_t ldq, int M,
+                                                             const uint16_t* __restrict__ items, int N, EpiArgs ea) {
+    constexpr int KB = KT * 64;           // bytes per item row (K = 32 KT bf16)
+    constexpr int CPR = KB / 16;          // 16-byte chunks per row
+    constexpr int RPI = 1024 / KB;        // rows per 1 KiB DMA wave-instruction
+    constexpr int STAGE = kScrTN * KB + 1024;  // bytes per ring stage: the items, then each wave's copy of their norms
+    constexpr int DMA = kScrTN / RPI / 4; // DMA instructions per wave and stage (= KT)
+    static_assert(CPR >= 8 && RPI * CPR == 64, "K = 64, 128 or 256");
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int QB = (M + kScrQ - 1) / kScrQ;
+    const int b = blockIdx.x, qb = (b / 8) % QB, c = (b % 8) + 8 * (b / (8 * QB));
+    const int nch = gridDim.x / QB;
+    const int64_t T = (N + kScrTN - 1) / kScrTN;
+    const int t0 = (int)(T * c / nch), t1 = (int)(T * (c + 1) / nch);
+    if (t0 >= t1) return;  // workgroup-uniform
+    const int nt = t1 - t0;
+    auto dma = [&](int t, int s) __attribute__((always_inline)) {
+        char* dst = smem_raw + s * STAGE;
+        const int64_t n0 = (int64_t)t * kScrTN;
+#pragma unroll
+        for (int it = 0; it < DMA; ++it) {
+            const int g = wave + 4 * it, r = g * RPI + lane / CPR, p = lane % CPR;
+            const int64_t item = n0 + r < N ? n0 + r : N - 1;  // rows past N: any valid row (never passes)
+            const char* src = reinterpret_cast<const char*>(items) + item * KB + ((p ^ (r & 7)) << 4);
+            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + g * 1024), 16, 0, 0);
+        }
+        // the tile's item norms by LDS-DMA as well (one copy per wave, so each wave's own vmcnt covers its copy): an
+        // ordinary global load used while a DMA is in flight makes hipcc drain every DMA (vmcnt(0)) at that use
+        const float* vsrc = ea.vnorm + (n0 + lane < N ? n0 + lane : N - 1);
+        __builtin_amdgcn_global_load_lds(vsrc, (__attribute__((address_space(3))) void*)(dst + kScrTN * KB + wave * 256), 4, 0, 0);
+    };
+    dma(t0, 0);
+    if (nt > 1) dma(t0 + 1, 1);
+    // this wave's query rows: A fragments (row qrow0 + 16 i + lr, k = 32 kt + 8 lg ..) and the rows' thresholds
+    const int64_t qrow0 = (int64_t)qb * kScrQ + wave * 64;
+    bf16x8 a[4][KT];
+    float tv[4][4], qv[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t row = qrow0 + 16 * i + lr;
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+            a[i][kt] = row < M ? *reinterpret_cast<const bf16x8*>(q + row * ldq + 32 * kt + 8 * lg) : bf16x8{};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t rr = qrow0 + 16 * i + 4 * lg + r;
+            tv[i][r] = rr < M ? ea.thr[rr] : INFINITY;
+            qv[i][r] = rr < M ? ea.qbound[rr] : 0.f;
+        }
+    }
+    // retire these loads here and hand their registers on through empty asm: a use inside the loop of a load result
+    // still pending at loop entry gets a vmcnt(0) in the loop body (every tile, draining the DMAs in flight)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) asm volatile("" : "+v"(a[i][kt]));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(tv[i][r]), "+v"(qv[i][r]));
+    }
+    // this wave's list of passing pairs (score, column, row in the wave's 64) past the ring
+    char* lbase = smem_raw + kScrStages * STAGE + wave * kScrList * 9;
+    float* lv = reinterpret_cast<float*>(lbase);
+    uint32_t* lc = reinterpret_cast<uint32_t*>(lbase + kScrList * 4);
+    uint8_t* lrw = reinterpret_cast<uint8_t*>(lbase + kScrList * 8);
+    int nb = 0;  // wave-uniform
+    auto emit = [&](int rl, float v, int64_t col) __attribute__((always_inline)) {
+        const int64_t row = qrow0 + rl;
+        const int off = atomicAdd(ea.ccount + row, 1);
+        if (off < ea.cap) {
+            ea.cval[row * (int64_t)ea.cap + off] = v;
+            ea.cidx[row * (int64_t)ea.cap + off] = (uint32_t)(ea.cbase + col);
+        }
+    };
+    auto flush = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the list writes of every lane (DS ops retire in order)
+        __builtin_amdgcn_wave_barrier();
+        for (int e = lane; e < nb; e += 64) emit(lrw[e], lv[e], lc[e]);
+        __builtin_amdgcn_wave_barrier();
+        nb = 0;
+    };
+    for (int u = 0; u < nt; ++u) {
+        const int t = t0 + u;
+        const int64_t n0 = (int64_t)t * kScrTN;
+        // tile t landed (vmcnt retires in issue order: tile t + 1's copies may stay in flight)
+        if (RF_LAB_SCR & 4) {
+        } else if (u + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA + 1) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's part of tile t is in; every wave is done with tile t - 1
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 2 < nt && !(RF_LAB_SCR & 4)) dma(t + 2, (u + 2) % kScrStages);
+        // The tile's LDS reads are inline asm: hipcc cannot tell them from reads of the stage being DMA'd and would
+        // put a vmcnt(0) (drain tile t + 2's copies, just issued) in front of the first use of each; their lgkmcnt
+        // waits are explicit, and an empty asm on each fragment orders its use after its wait
+        const uint32_t bsl = lds_u32(smem_raw + (u % kScrStages) * STAGE);
+        float vv[4];  // the item norms of this lane's columns
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            asm volatile("ds_read_b32 %0, %1" : "=v"(vv[j]) : "v"(bsl + kScrTN * KB + wave * 256 + (16 * j + lr) * 4));
+        bf16x8 bfr[2][KT];
+        auto read_b = [&](int j, bf16x8(&f)[KT]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int kt = 0; kt < KT; ++kt)
+                asm volatile("ds_read_b128 %0, %1"
+                             : "=v"(f[kt])
+                             : "v"(bsl + (16 * j + lr) * KB + (((4 * kt + lg) ^ (lr & 7)) << 4)));
+        };
+        read_b(0, bfr[0]);
+        f4 acc[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j < 3) {
+                read_b(j + 1, bfr[(j + 1) & 1]);  // in flight under this column block's MFMAs
+                asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(KT));
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)");
+            }
+#pragma unroll
+            for (int kt = 0; kt < KT; ++kt) asm volatile("" : "+v"(bfr[j & 1][kt]));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                if (RF_LAB_SCR & 2) {
+                    acc[i][j] = f4{(float)bfr[j & 1][i % KT][0], (float)bfr[j & 1][(i + 1) % KT][1], (float)a[i][0][0],
+                                   (float)bfr[j & 1][j % KT][2]};
+                } else {
+#pragma unroll
+                    for (int kt = 0; kt < KT; ++kt)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kt], bfr[j & 1][kt], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(vv[j]));  // read before the last wait above
+        // C/D layout: column n0 + 16 j + lr, row qrow0 + 16 i + 4 lg + r. A row pre-filter first: the largest of the
+        // lane's four scores of a row against the row's bar at the lane's largest item norm (qbound >= 0, so no pair
+        // that passes is missed; columns past N are excluded by the exact test only)
+        const float vmax = fmaxf(fmaxf(vv[0], vv[1]), fmaxf(vv[2], vv[3]));
+        uint32_t pm = 0;  // bit 4 i + r: row (i, r) may hold a passing pair in this lane's columns
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float m = fmaxf(fmaxf(acc[i][0][r], acc[i][1][r]), fmaxf(acc[i][2][r], acc[i][3][r]));
+                pm |= m >= tv[i][r] - qv[i][r] * vmax ? 1u << (4 * i + r) : 0u;
+            }
+        if (RF_LAB_SCR & 1) {
+            float z = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) z += acc[i][j][0] + acc[i][j][3];
+            pm = z == 12345.f;
+        }
+        // most wave tiles hold a pair or two that pass: they go to the wave's LDS list (a ballot and a lane rank per
+        // passing slot, no global round trip here); the list is flushed to the rows' candidate lists when half full
+        if (RF_LAB_SCR & 8) {
+            if (__any(pm != 0u)) asm volatile("" ::"v"(pm));  // keeps the pre-filter; nb (the list) stays empty
+        } else if (__any(pm != 0u)) {
+            if (nb > kScrList / 2) flush();
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (!__any((pm >> (4 * i + r)) & 1u)) continue;  // wave-uniform: most rows of a tile
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const bool p = n0 + 16 * j + lr < N && acc[i][j][r] >= tv[i][r] - qv[i][r] * vv[j];
+                        const uint64_t bm = __ballot(p);
+                        if (bm) {
+                            if (p) {
+                                const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                                if (pos < kScrList) {  // (asm: see the tile reads)
+                                    asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %2, %3\n\tds_write_b8 %4, %5"
+                                                 :
+                                                 : "v"(lds_u32(lv + pos)), "v"(acc[i][j][r]), "v"(lds_u32(lc + pos)),
+                                                   "v"((uint32_t)(n0 + 16 * j + lr)), "v"(lds_u32(lrw + pos)),
+                                                   "v"((uint32_t)(16 * i + 4 * lg + r))
+                                                 : "memory");
+                                } else {  // a tile with more passing pairs than the list holds: straight to the rows
+                                    emit(16 * i + 4 * lg + r, acc[i][j][r], n0 + 16 * j + lr);
+                                }
+                            }
+                            nb = min(nb + __popcll(bm), kScrList);
+                        }
+                    }
+                }
+        }
+    }
+    flush();
+}
+
+template <int KT>
+int launch_ip_screen_bf16(const void* q, int64_t ldq, int M, const void* items, int N, const EpiArgs& ea, hipStream_t st) {
+    auto kern = ip_screen_bf16_kernel<KT>;
+    constexpr int lds = kScrStages * (kScrTN * KT * 64 + 1024) + 4 * kScrList * 9;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return rf_set_error(RF_EHIP, "ip_screen_bf16_kernel: %s", hipGetErrorString(e));
+    const int QB = (M + kScrQ - 1) / kScrQ;
+    const int C8 = std::max(1, 256 / (8 * QB));  // item ranges per XCD: about one workgroup per CU in all
+    const int64_t grid = 8LL * QB * C8;
+    RF_REQUIRE(grid < (int64_t)1 << 31, "rf_ip_candidates_bf16: too many query rows");
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, st, (const uint16_t*)q, ldq, M, (const uint16_t*)items, N, ea);
+    return rf_check_launch("ip_screen_bf16_kernel");
+}
+
+bool screen_gemm_forced() {  // RF_SCREEN_GEMM=1: the bf16 screen on gemm_lds_kernel<128, kEpiCompact> (A/B only)
+    static const bool on = [] {
+        const char* e = getenv("RF_SCREEN_GEMM");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 bool lds_disabled() {  // RF_GEMM_LDS=0: the register-staged kernel everywhere (A/B measurement only)
     static const bool off = [] {
         const char* e = getenv("RF_GEMM_LDS");
@@ -2109,6 +2358,11 @@ extern "C" int rf_ip_candidates_bf16(const void* q, int64_t ldq, int32_t M, cons
     ea.cidx = cand_idx;
     ea.cap = cap;
     ea.cbase = col_base;
+    if (!screen_gemm_forced()) {
+        if (K == 256) return launch_ip_screen_bf16<8>(q, ldq, M, items, N, ea, rf_stream(stream));
+        if (K == 128) return launch_ip_screen_bf16<4>(q, ldq, M, items, N, ea, rf_stream(stream));
+        if (K == 64) return launch_ip_screen_bf16<2>(q, ldq, M, items, N, ea, rf_stream(stream));
+    }
     return launch_ip_candidates<false>(q, ldq, M, items, N, K, ea, rf_stream(stream));
 }
 

@@ -268,6 +268,52 @@ def test_ip_candidates_exact(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K,M,N", [(256, 300, 50000 + 37), (128, 1024, 20000 + 5), (64, 77, 9000 + 1), (256, 300, 100)])
+def test_ip_candidates_bf16_screen(cuda, K, M, N):
+    """rf_ip_candidates_bf16 (the query-stationary kernel at K = 64 / 128 / 256) keeps every pair whose bf16-operand
+    score is >= thr[row] - qbound[row] vnorm[col] and no other: against float64 dot products of the same bf16 values,
+    within the fp32 accumulation error of unit rows (1e-4), with each kept pair's score, its index col_base + n, and
+    counts equal to the kept entries. Ragged query blocks and item tiles, a row nothing passes, a catalog shorter than
+    one tile per workgroup."""
+    import torch
+
+    from recommendflow_amd.runtime import lib as L
+
+    g = torch.Generator(device="cuda").manual_seed(K + M)
+    q = torch.randn((M, K), device="cuda", generator=g)
+    q = q / q.norm(dim=1, keepdim=True)
+    items = torch.randn((N, K), device="cuda", generator=g)
+    items = items / items.norm(dim=1, keepdim=True)
+    qb, ib = q.to(torch.bfloat16).contiguous(), items.to(torch.bfloat16).contiguous()
+    ref = qb.double() @ ib.double().t()
+    thr = torch.quantile(ref[:, : min(N, 4096)].float(), 0.99, dim=1).contiguous()
+    thr[1] = float("inf")  # nothing passes
+    qbound = (q.norm(dim=1) * 0.008).contiguous()
+    vn = items.norm(dim=1).contiguous()
+    cap, base = 2048, 123457
+    count = torch.zeros(M, dtype=torch.int32, device="cuda")
+    cval = torch.full((M, cap), float("nan"), device="cuda")
+    cidx = torch.empty((M, cap), dtype=torch.int32, device="cuda")
+    L.call("rf_ip_candidates_bf16", L.ptr(qb), K, M, L.ptr(ib), N, K, L.ptr(thr), L.ptr(qbound), L.ptr(vn), cap,
+           L.ptr(count), L.ptr(cval), L.ptr(cidx), base, L.stream_ptr())
+    t = (thr.double()[:, None] - qbound.double()[:, None] * vn.double()[None, :]).cpu().numpy()
+    r = ref.cpu().numpy()
+    cnt, cv, ci = count.cpu().numpy(), cval.cpu().numpy(), cidx.cpu().numpy().view(np.uint32)
+    eps = 1e-4
+    assert cnt[1] == 0
+    for row in range(M):
+        assert cnt[row] <= cap, row
+        got = ci[row, : cnt[row]].astype(np.int64) - base
+        assert len(np.unique(got)) == len(got) and (got >= 0).all() and (got < N).all(), row
+        must = np.nonzero(r[row] >= t[row] + eps)[0]
+        assert np.isin(must, got).all(), row
+        assert (r[row, got] >= t[row, got] - eps).all(), row
+        np.testing.assert_allclose(cv[row, : cnt[row]], r[row, got], rtol=0, atol=eps)
+        assert np.isnan(cv[row, cnt[row]:]).all()
+    assert cnt.sum() > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k", [1, 50, 200, 1024])
 @pytest.mark.parametrize("dups", [False, True])
 def test_screened_search_equals_block_loop(cuda, k, dups):
