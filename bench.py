@@ -958,7 +958,7 @@ def bench_cascade(args, enc):
     ms = (time.perf_counter() - t0) / steps * 1e3
     out = {"users_per_s": round(B / ms * 1e3, 1), "ms_per_step": round(ms, 3), "catalog_items": N,
            "catalog_index_s": round(index_s, 2), "pairs_ranked_per_s": round(B * 50 / ms * 1e3, 1),
-           "config": f"1024 users/step; recall: cfg2 towers, Flat IP top-200 over {N} items (fp32 MFMA + rf_topk_merge); "
+           "config": f"1024 users/step; recall: cfg2 towers, Flat IP top-200 over {N} items (exact: fp32 lead blocks + rf_topk_merge, the rest screened in bf16 within its error bound and rescored in fp32; bit-identical to the block loop); "
                      "prerank: u*v -> Dense(64, relu) -> Dense(1), top-50; rank: cfg3 ESIM (fp16 attention) top-10"}
     del cas, esim, dssm, rb, kb, ur, uk
     torch.cuda.empty_cache()
