@@ -2054,7 +2054,8 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {  // the LDS byte ad
 constexpr int kScrTN = 64, kScrStages = 3, kScrQ = 256;  // items per tile, ring depth, query rows per workgroup
 constexpr int kScrList = 1024;                            // passing pairs listed per wave before a flush
 // lab ablations (tools/build_variants.sh -DRF_LAB_SCR=bits; wrong results, never in the shipped build): 1 = no pass
-// test / list, 2 = no MFMAs, 4 = no item copies or waits (stale LDS), 8 = the row pre-filter without the list
+// test / list, 2 = no MFMAs, 4 = no item copies or waits (stale LDS), 8 = the row pre-filter without the list,
+// 16 = the list never flushed
 #ifndef RF_LAB_SCR
 #define RF_LAB_SCR 0
 #endif
@@ -2136,6 +2137,10 @@ __global__ __launch_bounds__(256) void ip_screen_bf16_kernel(const uint16_t* __r
         }
     };
     auto flush = [&]() __attribute__((always_inline)) {
+        if (RF_LAB_SCR & 16) {  // lab: the list is dropped
+            nb = 0;
+            return;
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the list writes of every lane (DS ops retire in order)
         __builtin_amdgcn_wave_barrier();
         for (int e = lane; e < nb; e += 64) emit(lrw[e], lv[e], lc[e]);
