@@ -169,8 +169,10 @@ int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t dtype, int3
 /* rf_esim_soft_attention_fwd over pairs built by index instead of copies (the cascade's rank stage, cfg5): pair e
  * reads its q sequence at q + (e / q_rep) * q_stride (one user's sequence for q_rep consecutive candidates) and its
  * a sequence at a + a_rows[e] * a_stride (a candidate item's row of a catalog of encoded sequences); rows ld apart
- * inside an example. Same pooled values as expanding / gathering q and a first. */
-int rf_esim_soft_attention_idx_fwd(const void* q, int32_t q_rep, const void* a, const int64_t* a_rows, int64_t a_stride,
+ * inside an example. Same pooled values as expanding / gathering q and a first. a_count = the catalog's row count:
+ * a_rows[e] outside [0, a_count) is checked on the device, reads nothing and gives pair e NaN features. */
+int rf_esim_soft_attention_idx_fwd(const void* q, int32_t q_rep, const void* a, const int64_t* a_rows, int64_t a_count,
+                                   int64_t a_stride,
                                    int32_t dtype, int32_t batch, int32_t L, int32_t d, int64_t q_stride, int64_t ld,
                                    float* out, int64_t out_stride, int64_t out_off, void* stream);
 

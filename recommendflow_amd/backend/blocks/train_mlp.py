@@ -46,10 +46,11 @@ def _linear_f32(x: torch.Tensor, W: torch.Tensor, b: torch.Tensor, act: int, out
     M, K = x.shape
     N = W.shape[0]
     if _BLASLT_WIDE and K >= _BLASLT_MIN_K and act == L.ACT["selu"] and out.is_contiguous():
+        GM.note_torch_fallback("a tower forward layer (RF_TOWER_BLASLT_WIDE=1)")
         torch.addmm(b, x, W.t(), out=out)
         torch.selu_(out)
         return
-    if GM.supported(x, W, out):
+    if GM.supported_gemm(x, W, trans_b=True, out=out):
         GM.gemm_f32(x, W, trans_b=True, bias=b, act=_ACT_NAME[act], out=out, stream=stream)
         return
     ws_bytes = int(L.load().rf_linear_splitk_ws_bytes(L.DT_F32, M, K, N))
@@ -104,6 +105,7 @@ _SMALL_MM_ROCBLAS = os.environ.get("RF_SMALL_MM_ROCBLAS", "0") == "1"
 
 
 def _mm(a: torch.Tensor, b: torch.Tensor, small: bool) -> torch.Tensor:
+    GM.note_torch_fallback("a tower backward product (RF_TOWER_BWD_BLAS=1)")
     if not (small and _SMALL_MM_ROCBLAS):
         return torch.mm(a, b)
     prev = torch.backends.cuda.preferred_blas_library()
@@ -121,8 +123,9 @@ def _ws(M: int, K: int, device) -> torch.Tensor:
 def _gemm_layer(probs, trans_a: bool, trans_b: bool, stream):
     """One layer's GEMMs of every tower: probs = [(a, b, bias, act name, out)]. librf (rf_gemm_f32, grouped into one
     launch where runtime.gemm.group_pays) when every operand qualifies; otherwise torch one by one."""
-    if all(GM.supported(a, b) and (o is None or GM.supported(o)) for a, b, _, _, o in probs):
+    if all(GM.supported_gemm(a, b, trans_a, trans_b, o) for a, b, _, _, o in probs):
         return GM.gemm_f32_layer(probs, trans_a=trans_a, trans_b=trans_b, stream=stream)
+    GM.note_torch_fallback("a tower backward layer")
     outs = []
     for a, b, bias, act, o in probs:
         A = a.t() if trans_a else a

@@ -56,7 +56,8 @@ def esim_soft_attention_pool(q: torch.Tensor, a: torch.Tensor, out: Optional[tor
 def esim_soft_attention_pool_idx(q: torch.Tensor, q_rep: int, a_table: torch.Tensor, a_rows: torch.Tensor,
                                  out: torch.Tensor, out_col: int = 0, stream=None) -> torch.Tensor:
     """esim_soft_attention_pool over B * q_rep pairs without materialising them: pair e takes q[e // q_rep]
-    ([Bq, L, d]) and a_table[a_rows[e]] ([N, L, d]); fills out[:, out_col:out_col + 6d] (rf_esim_soft_attention_idx_fwd)."""
+    ([Bq, L, d]) and a_table[a_rows[e]] ([N, L, d]); fills out[:, out_col:out_col + 6d] (rf_esim_soft_attention_idx_fwd).
+    A row id outside [0, N) is caught on the device: that pair's features are NaN (no read past the table)."""
     L.require_gpu()
     if q.dtype != a_table.dtype or q.dtype not in (torch.bfloat16, torch.float16):
         raise ValueError("q and a_table must share a bf16 / f16 dtype")
@@ -67,7 +68,7 @@ def esim_soft_attention_pool_idx(q: torch.Tensor, q_rep: int, a_table: torch.Ten
     if P != q.shape[0] * q_rep or out.shape[0] != P:
         raise ValueError(f"{P} pairs need q with {P // max(q_rep, 1)} rows x q_rep {q_rep} and out with {P} rows")
     _, Ln, d = q.shape
-    L.call("rf_esim_soft_attention_idx_fwd", L.ptr(q), int(q_rep), L.ptr(a_table), L.ptr(a_rows), Ln * d,
+    L.call("rf_esim_soft_attention_idx_fwd", L.ptr(q), int(q_rep), L.ptr(a_table), L.ptr(a_rows), a_table.shape[0], Ln * d,
            L.torch_dtype_code(q.dtype), P, Ln, d, Ln * d, d, L.ptr(out), out.stride(0), out_col, L.stream_ptr(stream))
     return out
 

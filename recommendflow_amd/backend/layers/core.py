@@ -88,13 +88,15 @@ class Dense(torch.nn.Module):
         M, dt = x.shape[0], L.torch_dtype_code(self.dtype)
         blaslt = (_BLASLT_WIDE and self.dtype == torch.float32 and self.in_features >= _BLASLT_MIN_K
                   and out.is_contiguous() and self.activation in (None, "none", "linear", "relu", "selu"))
-        if self.dtype == torch.float32 and not blaslt and self.activation != "softmax" and G.supported(x, weight, out):
+        if self.dtype == torch.float32 and not blaslt and self.activation != "softmax" and \
+                G.supported_gemm(x, weight, trans_b=True, out=out):
             # fp32 layers (the DSSM towers, dssm.py:25-26): rf_gemm_f32, stream-K exact-fp32 MFMA with the bias
             # and activation in its epilogue
             return G.gemm_f32(x, weight, trans_b=True, bias=bias, act=self.activation or "none", out=out,
                               stream=stream)
         if blaslt:
             # A/B only: hipBLASLt's fp32 kernel with its bias epilogue, SELU / ReLU in place after
+            G.note_torch_fallback("a Dense layer (RF_TOWER_BLASLT_WIDE=1)")
             with torch.cuda.stream(stream) if isinstance(stream, torch.cuda.Stream) else _nullctx():
                 if bias is None:
                     torch.mm(x, weight.t(), out=out)

@@ -80,13 +80,26 @@ class FaissSearcher:
 
     def train(self):
         self.index = self.get_vecs(self.items)  # [N, E] resident in HBM
-        self.index_bf16 = None  # the bf16 screen's copy and the item norms, built on first use
         return self
 
+    @property
+    def index(self):
+        return self._index
+
+    @index.setter
+    def index(self, value):
+        # assigning an index drops the bf16 screen's copy and the item norms derived from the old one
+        self._index = value
+        self._screen_key = None
+        self.index_bf16 = self.index_norm = None
+
     def _bf16_screen_index(self):
-        if getattr(self, "index_bf16", None) is None:
-            self.index_bf16 = self.index.to(torch.bfloat16).contiguous()
-            self.index_norm = self.index.norm(dim=1).contiguous()
+        # keyed on the index tensor's identity and version as well: an in-place write to the index rebuilds them
+        key = (self._index.data_ptr(), tuple(self._index.shape), self._index._version)
+        if self.index_bf16 is None or self._screen_key != key:
+            self.index_bf16 = self._index.to(torch.bfloat16).contiguous()
+            self.index_norm = self._index.norm(dim=1).contiguous()
+            self._screen_key = key
         return self.index_bf16, self.index_norm
 
     screen = True  # the screened search where it applies (A/B: False keeps the block loop)

@@ -776,10 +776,12 @@ struct EsimGatherArgs {
     float* ostats;         // ... and per 32-column slice (sum, squared deviations from the slice mean) of the fp32
     int oP, op0;           // values: ostats[row][op0 + slice], oP pairs per row (rf_linear_lnfold_* consume them)
     // plain (non-GATHER) path, rf_esim_soft_attention_idx_fwd: example e reads q example e / q_rep (q_rep >= 1; 0 = 1)
-    // and a example a_rows[e] (a_stride elements apart; a_rows == nullptr: e, ex_stride apart)
+    // and a example a_rows[e] (a_stride elements apart; a_rows == nullptr: e, ex_stride apart); a row outside
+    // [0, a_count) reads nothing (an empty descriptor) and its example's pooled features are NaN
     int q_rep;
     const int64_t* a_rows;
     int64_t a_stride;
+    int64_t a_count;
 };
 
 template <bool F16, int D, int NTT, int XM, bool GATHER = false, bool STAMP = false, bool OB = false>
@@ -811,9 +813,16 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
     const int img_bytes = L * (int)ld * 2;
     auto prefetch = [&](int64_t e) __attribute__((always_inline)) {
         const int64_t eq = ga.q_rep > 1 ? e / ga.q_rep : e;
-        const uint16_t* ap = ga.a_rows ? a + ga.a_rows[e] * ga.a_stride : a + e * ex_stride;
+        const uint16_t* ap = a + e * ex_stride;
+        int a_bytes = img_bytes;
+        if (ga.a_rows) {
+            const int64_t r = ga.a_rows[e];
+            const bool ok = r >= 0 && r < ga.a_count;
+            ap = a + (ok ? r : 0) * ga.a_stride;
+            a_bytes = ok ? img_bytes : 0;
+        }
         const auto rq = __builtin_amdgcn_make_buffer_rsrc((void*)(q + eq * ex_stride), 0, img_bytes, 0x00020000);
-        const auto ra = __builtin_amdgcn_make_buffer_rsrc((void*)ap, 0, img_bytes, 0x00020000);
+        const auto ra = __builtin_amdgcn_make_buffer_rsrc((void*)ap, 0, a_bytes, 0x00020000);
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
             const int cm = tid + (i % HALF) * NTH;
@@ -1047,7 +1056,13 @@ __global__ __launch_bounds__(kEsim2Waves * 64, 2) void esim2_kernel(const uint16
                     m3 = fmx(m3, ws[4 * D]);
                 }
             }
-            const float avg = (2.0f * sx + smul) / (float)(4 * L);
+            float avg = (2.0f * sx + smul) / (float)(4 * L);
+            if constexpr (!GATHER) {
+                if (ga.a_rows) {  // an a row outside the catalog: NaN features (nothing was read for it)
+                    const int64_t r = ga.a_rows[e];
+                    if (r < 0 || r >= ga.a_count) avg = m3 = __builtin_nanf("");
+                }
+            }
             const float avg_o = __shfl_xor(avg, 32, 64), mx_o = __shfl_xor(m3, 32, 64);
             {
                 static_assert(NTH / 2 >= D, "one column per thread and side: four pending values");
@@ -1323,7 +1338,7 @@ extern "C" int rf_esim_soft_attention_fwd(const void* q, const void* a, int32_t 
 }
 
 extern "C" int rf_esim_soft_attention_idx_fwd(const void* q, int32_t q_rep, const void* a, const int64_t* a_rows,
-                                              int64_t a_stride, int32_t dtype, int32_t batch, int32_t L, int32_t d,
+                                              int64_t a_count, int64_t a_stride, int32_t dtype, int32_t batch, int32_t L, int32_t d,
                                               int64_t q_stride, int64_t ld, float* out, int64_t out_stride, int64_t out_off,
                                               void* stream) {
     RF_REQUIRE(dtype == RF_DTYPE_BF16 || dtype == RF_DTYPE_F16, "rf_esim_soft_attention_idx_fwd: dtype must be BF16 or F16");
@@ -1335,10 +1350,12 @@ extern "C" int rf_esim_soft_attention_idx_fwd(const void* q, int32_t q_rep, cons
     RF_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)a & 15) == 0, "rf_esim_soft_attention_idx_fwd: q/a must be 16-byte aligned");
     if (batch == 0) return RF_OK;
     RF_REQUIRE(q && a && a_rows && out, "rf_esim_soft_attention_idx_fwd: null pointer");
+    RF_REQUIRE(a_count >= 1, "rf_esim_soft_attention_idx_fwd: a_count must be >= 1");
     EsimGatherArgs ga{};
     ga.q_rep = q_rep;
     ga.a_rows = a_rows;
     ga.a_stride = a_stride;
+    ga.a_count = a_count;
     const int rc = esim2_dispatch(q, a, dtype, batch, L, d, q_stride, ld, out, out_stride, out_off, rf_stream(stream), ga);
     if (rc) return rc;
     return rf_check_launch("rf_esim_soft_attention_idx_fwd");

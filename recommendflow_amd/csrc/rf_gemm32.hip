@@ -132,7 +132,9 @@ struct Operand {
         } else {
             const int c32 = tid & 31;
             kcol = 0;
-            rs = rsrc(p + row0, ((int64_t)(K - 1) * ld + (ld - row0)) * 4);
+            // the extent ends at the view's last column of its last k-row (rows, not ld: a trailing-column view's
+            // last k-row may end where the parent allocation does)
+            rs = rsrc(p + row0, ((int64_t)(K - 1) * ld + (rows - row0)) * 4);
             kstep = (uint32_t)(kBK * ld * 4);
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
@@ -353,6 +355,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
             }
             __syncthreads();
             if (!s_last) continue;
+            // The hand-off: every segment's slot stores are agent-scope atomics (gfx950 emits them with sc1, written
+            // through past this XCD's L2) retired by vmcnt(0) before its ticket; the last arriver's acquire fence
+            // (one L2 invalidate per cut tile, not per ticket) orders its slot loads after the ticket it read
+            // (the HIP model's happens-before edge, at the cost of one buffer_inv)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             if (tid == 0) __hip_atomic_store(g.cnt + gt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (int w = v_first; w <= v_last; ++w) {
                 const int sid = gt == gtile_of(g, seg_lo(w, U, G)) ? 2 * w : 2 * w + 1;

@@ -502,7 +502,15 @@ class FileProducer {
     std::thread th_;
 };
 
-// Fork-join pool: run(n, f) calls f(0..n-1) on the workers plus the calling thread.
+// Fork-join pool: run(n, f) calls f(0..n-1) exactly once each, on the workers plus the calling thread.
+//
+// Every run() is one Job on the caller's stack holding its own function, count and claim counter. A worker
+// takes the job pointer and registers itself (active) under the lock, and run() returns only when every index
+// is done AND no worker is registered any more, then clears the pointer under the lock. A worker that wakes
+// late therefore either finds the job gone (and touches nothing) or holds a registration that keeps the job
+// alive: no claim can cross from one run() into the next. (Round 5's pool shared one counter across runs: a
+// worker that claimed an index of run N after its end but read run N+1's count executed an index twice and
+// let run() return early, with a worker still inside the caller's lambda.)
 class Pool {
   public:
     explicit Pool(int n_threads) {
@@ -518,49 +526,65 @@ class Pool {
     }
     int size() const { return static_cast<int>(ws_.size()) + 1; }
     void run(int n, const std::function<void(int)>& f) {
-        {
+        if (n <= 0) return;
+        Job job{&f, n};
+        if (n > 1 && !ws_.empty()) {
             std::lock_guard<std::mutex> g(mu_);
-            fn_ = &f;
-            n_ = n;
-            next_.store(0);
-            pending_ = n;
+            job_ = &job;
             ++gen_;
+            cv_.notify_all();
         }
-        cv_.notify_all();
-        drain();
+        drain(job);
         std::unique_lock<std::mutex> g(mu_);
-        done_cv_.wait(g, [this] { return pending_ == 0; });
-        fn_ = nullptr;
+        done_cv_.wait(g, [&] { return job.done == job.n && job.active == 0; });
+        if (job_ == &job) job_ = nullptr;
     }
 
   private:
-    void drain() {
+    struct Job {
+        const std::function<void(int)>* fn;
+        int n;
+        std::atomic<int> next{0};
+        int done = 0;    // indices finished (under mu_)
+        int active = 0;  // workers registered on this job (under mu_)
+    };
+    // claims indices until none is left; counts the finished ones under the lock
+    void drain(Job& job) {
+        int finished = 0;
         for (;;) {
-            const int i = next_.fetch_add(1);
-            if (i >= n_) return;
-            (*fn_)(i);
+            const int i = job.next.fetch_add(1);
+            if (i >= job.n) break;
+            (*job.fn)(i);
+            ++finished;
+        }
+        if (finished) {
             std::lock_guard<std::mutex> g(mu_);
-            if (--pending_ == 0) done_cv_.notify_all();
+            job.done += finished;
+            if (job.done == job.n) done_cv_.notify_all();
         }
     }
     void work() {
         uint64_t seen = 0;
         for (;;) {
+            Job* job;
             {
                 std::unique_lock<std::mutex> g(mu_);
                 cv_.wait(g, [&] { return stop_ || gen_ != seen; });
                 if (stop_) return;
                 seen = gen_;
+                job = job_;
+                if (!job) continue;
+                ++job->active;
             }
-            drain();
+            drain(*job);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--job->active == 0) done_cv_.notify_all();
         }
     }
     std::vector<std::thread> ws_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    const std::function<void(int)>* fn_ = nullptr;
-    int n_ = 0, pending_ = 0;
-    std::atomic<int> next_{0};
+    Job* job_ = nullptr;
     uint64_t gen_ = 0;
     bool stop_ = false;
 };

@@ -33,6 +33,10 @@ def _workspace(dev: torch.device, stream_handle: int, need: int) -> torch.Tensor
         if ws is not None:
             _RETIRED.append(ws)
         ws = _WS[key] = torch.zeros(max(need, 256), dtype=torch.uint8, device=dev)
+        cur = torch.cuda.current_stream(dev)
+        if stream_handle not in (cur.cuda_stream, 0) and not torch.cuda.is_current_stream_capturing():
+            # the memset ran on torch's current stream: the launch stream waits for it
+            torch.cuda.ExternalStream(stream_handle, device=dev).wait_stream(cur)
     return ws
 
 
@@ -48,6 +52,38 @@ def supported(*ts: torch.Tensor) -> bool:
     """Operand views rf_gemm_f32 accepts: fp32, unit column stride, leading dimension % 4 == 0, 16-byte aligned."""
     return all(t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 4 == 0
                and t.data_ptr() % 16 == 0 for t in ts)
+
+
+def _block_ok(t: torch.Tensor, kc: bool, K: int) -> bool:
+    # rf_gemm_f32's 32-bit buffer offsets (rf_gemm32.hip RF_REQUIRE): a k-contiguous operand's 128-row tile block,
+    # an m/n-contiguous operand's K + 192 k-rows, each under 2 GiB
+    return (128 if kc else K + 192) * t.stride(0) * 4 < (1 << 31)
+
+
+def supported_gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+                   out: Optional[torch.Tensor] = None) -> bool:
+    """Whether rf_gemm_f32 takes this problem as laid out: supported() operands, K % 4 == 0, and every operand block
+    inside the 2 GiB limit of the C check (the tower weight gradient dpre^T h at batch x width x 4 B near
+    2 GiB must go to the fallback, not raise)."""
+    if not supported(a, b) or (out is not None and not supported(out)):
+        return False
+    K = a.shape[0] if trans_a else a.shape[1]
+    return K % 4 == 0 and _block_ok(a, not trans_a, K) and _block_ok(b, trans_b, K)
+
+
+torch_fallbacks = 0  # tower / Dense fp32 GEMMs that went to torch (hipBLASLt) instead of librf; tests assert 0
+_warned = [False]
+
+
+def note_torch_fallback(what: str):
+    """Counts (and warns once about) an fp32 tower GEMM leaving librf for torch.mm / addmm."""
+    global torch_fallbacks
+    torch_fallbacks += 1
+    if not _warned[0]:
+        _warned[0] = True
+        import warnings
+        warnings.warn(f"rf_gemm_f32 fallback to torch for {what} (operand layout or size outside librf's checks)",
+                      RuntimeWarning, stacklevel=3)
 
 
 def gemm_f32(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,

@@ -14,6 +14,7 @@ launches), so every hot-path op is capturable as-is. Inputs live in static devic
 """
 from __future__ import annotations
 
+import gc
 from typing import Callable, List, Optional, Sequence
 
 import torch
@@ -77,15 +78,32 @@ class CapturedGraph:
 
     def __init__(self, fn: Callable[[], object], warmup: int = 2):
         self.fn = fn
+        # warm-up and capture on this graph's own stream: lazy init, LDS attributes, the allocator, and the
+        # per-stream state librf's callers key on the stream (runtime/gemm.py's zeroed stream-K workspace) all
+        # exist, eagerly initialised, before the capture starts (torch's shared default capture stream would give
+        # every graph one workspace, first zeroed by a memset captured into whichever graph came first)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):  # warm-up off the capture: lazy init, LDS attributes, allocator
+        with torch.cuda.stream(side):
             for _ in range(warmup):
                 fn()
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = fn()
+        # No Python garbage collection inside the capture: a cycle collected there runs destructors (a pinned host
+        # buffer's free records and queries events) that are illegal while a stream captures, and the process
+        # aborts. torch >= 2.6 no longer collects before a capture (force_cudagraph_gc), so collect here, then hold
+        # the collector off until capture_end (GPUTEST_r05's SIGABRT: "Garbage-collecting" inside rf_gemm_f32_grouped
+        # under test_graphs_gpu's capture). thread_local: other threads' HIP calls (a FeaturePipe's producer) are
+        # not capture violations.
+        gc.collect()
+        was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
+                self.out = fn()
+        finally:
+            if was_enabled:
+                gc.enable()
 
     def replay(self):
         self.graph.replay()

@@ -31,7 +31,7 @@ _SIGS = {
     "rf_embedding_bag_fwd": (ctypes.c_int, [_vp, _i32, _i32, _i64, _vp, _i32, _i64, _i32, _i32, _vp, _i32, _i64, _i64, _vp]),
     "rf_table_init_uniform": (ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _i64, _u64, _f32, _f32, _vp]),
     "rf_esim_soft_attention_fwd": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
-    "rf_esim_soft_attention_idx_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64,
+    "rf_esim_soft_attention_idx_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i64, _i64, _vp, _i64,
                                                       _i64, _vp]),
     "rf_esim_gather_fwd": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _vp]),
     "rf_single_token_ids_fwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i32, _vp]),

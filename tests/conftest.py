@@ -1,3 +1,4 @@
+import faulthandler
 import os
 import sys
 
@@ -10,6 +11,26 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); parity tests through the C ABI")
+
+
+_FAULT_FILE = None
+
+
+def pytest_sessionstart(session):
+    """Fatal-signal tracebacks (SIGABRT / SIGSEGV) go to gpurun_out/faulthandler_<pid>.txt instead of stderr, so the
+    tail of a crashed run's output ends with the RUN line of the test that was running and the native error message
+    (glibc, HIP), not a Python stack dump of the pytest frames (GPUTEST_r05's record was cut exactly there)."""
+    global _FAULT_FILE
+    d = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, f"faulthandler_{os.getpid()}.txt")
+    _FAULT_FILE = open(path, "w")
+    faulthandler.enable(file=_FAULT_FILE, all_threads=True)
+
+
+def pytest_runtest_logstart(nodeid, location):
+    # one unbuffered line per test on stderr: a crash record names the test it happened in
+    os.write(2, f"RUN {nodeid}\n".encode())
 
 
 @pytest.fixture(scope="session")

@@ -102,3 +102,26 @@ def test_esim_pool_idx_equals_materialised_pairs(cuda, dtype, L, d):
     got = torch.empty((Bq * rep, 6 * d + 16), device="cuda")
     esim_soft_attention_pool_idx(q, rep, cat, rows, out=got, out_col=16)
     assert torch.equal(got[:, 16:], want)
+
+
+def test_esim_pool_idx_rejects_rows_outside_the_catalog(cuda):
+    """A pair whose catalog row is outside [0, N) (negative, N, far past the table) reads nothing and gets NaN
+    features; every other pair keeps its exact values (the device-side check of rf_esim_soft_attention_idx_fwd)."""
+    from recommendflow_amd.backend.layers.attention_layers import esim_soft_attention_pool_idx
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    Bq, rep, N, L, d = 5, 4, 50, 20, 64
+    q = (torch.randn((Bq, L, d), device="cuda", generator=g) * 0.5).to(torch.float16)
+    cat = (torch.randn((N, L, d), device="cuda", generator=g) * 0.5).to(torch.float16)
+    rows = torch.randint(0, N, (Bq * rep,), device="cuda", generator=g)
+    want = torch.empty((Bq * rep, 6 * d), device="cuda")
+    esim_soft_attention_pool_idx(q, rep, cat, rows, out=want)
+    bad = rows.clone()
+    bad[[1, 6, 13]] = torch.tensor([-1, N, 1 << 40], device="cuda")
+    got = torch.empty_like(want)
+    esim_soft_attention_pool_idx(q, rep, cat, bad, out=got)
+    torch.cuda.synchronize()
+    ok = torch.ones(Bq * rep, dtype=torch.bool)
+    ok[[1, 6, 13]] = False
+    assert torch.equal(got[ok.cuda()], want[ok.cuda()])
+    assert torch.isnan(got[~ok.cuda()]).all()

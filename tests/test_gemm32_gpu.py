@@ -152,3 +152,45 @@ def test_forward_towers_matches_each_tower(cuda):
     u1, a1 = mu(xu), ma(xa)
     torch.testing.assert_close(u, u1, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(a, a1, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("width", [300, 1000, 129])
+def test_trailing_column_view_operand(cuda, width):
+    """The weight-gradient layout dpre^T h with h the LAST `width` columns of a wider tensor (the towers' layer-0 view
+    of the fused encoder output), width % 128 != 0: the n-contiguous operand's buffer extent ends at the view's last
+    column, not at the parent's row end, and the result is exact."""
+    g = torch.Generator(device="cuda").manual_seed(width)
+    K, M, ld = 1000, 64, 1024 + width
+    dpre = torch.randn(K, M, device="cuda", generator=g)
+    x = torch.randn(K, ld, device="cuda", generator=g)
+    h = x[:, ld - width:]
+    c = G.gemm_f32(dpre, h, trans_a=True)
+    _check(c, dpre, h, True, False, None, "none")
+
+
+def test_oversized_operand_block_goes_to_the_fallback(cuda):
+    """An m/n-contiguous operand whose (K + 192) k-rows span >= 2 GiB is outside rf_gemm_f32's 32-bit offsets:
+    supported_gemm says so, the tower layer routes it to torch (counted), and the result is the product."""
+    from recommendflow_amd.backend.blocks.train_mlp import _gemm_layer
+
+    K, M, N = 4100, 64, 131072  # (4100 + 192) * 131072 * 4 B = 2.25 GB
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = torch.randn(K, M, device="cuda", generator=g)
+    b = torch.randn(K, N, device="cuda", generator=g)
+    assert not G.supported_gemm(a, b, trans_a=True, trans_b=False)
+    fb0 = G.torch_fallbacks
+    with pytest.warns(RuntimeWarning) if not G._warned[0] else _nowarn():
+        (c,) = _gemm_layer([(a, b, None, "none", None)], True, False, torch.cuda.current_stream().cuda_stream)
+    assert G.torch_fallbacks == fb0 + 1
+    A, B = a.t().double(), b[:, :2048].double()
+    err = ((c[:, :2048].double() - A @ B).abs() / (A.abs() @ B.abs())).max().item()
+    assert err < 1e-5, err
+    del b, c
+
+
+class _nowarn:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False

@@ -61,3 +61,24 @@ def test_product_path_has_no_oracle_import():
             if f.endswith(".py"):
                 text = open(os.path.join(dirpath, f)).read()
                 assert "from oracle" not in text and "import oracle" not in text, f
+
+
+def test_gemm_supported_applies_the_block_limit():
+    """runtime.gemm.supported_gemm mirrors rf_gemm_f32's 2 GiB operand-block check per layout (meta tensors: no
+    memory, no GPU): an m/n-contiguous operand's (K + 192) k-rows, a k-contiguous operand's 128 rows."""
+    import torch
+
+    from recommendflow_amd.runtime import gemm as G
+
+    K = 4100
+    a = torch.empty(K, 64, device="meta")
+    wide = torch.empty(K, 131072, device="meta")      # (K + 192) * 131072 * 4 B >= 2 GiB
+    narrow = torch.empty(K, 4096, device="meta")
+    assert not G.supported_gemm(a, wide, trans_a=True, trans_b=False)
+    assert not G.supported_gemm(a, wide[:, :4096], trans_a=True, trans_b=False)  # the view keeps the parent's ld
+    assert G.supported_gemm(a, narrow, trans_a=True, trans_b=False)
+    x = torch.empty(512, 1 << 22, device="meta")        # k-contiguous, 128 rows x 16 MiB = 2 GiB
+    w = torch.empty(64, 1 << 22, device="meta")
+    assert not G.supported_gemm(x, w, trans_b=True)
+    assert G.supported_gemm(x[:, : 1 << 20].contiguous(), w[:, : 1 << 20].contiguous(), trans_b=True)
+    assert not G.supported_gemm(torch.empty(64, 30, device="meta"), torch.empty(16, 30, device="meta"), trans_b=True)

@@ -54,7 +54,7 @@ def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate, off, ro
             raise AssertionError("a vendor GEMM ran on the librf route")
         monkeypatch.setattr(torch, "addmm", refuse)
         monkeypatch.setattr(torch, "mm", refuse)
-    n0 = G.calls
+    n0, fb0 = G.calls, G.torch_fallbacks
     t = _tower(in_f, units, rate)
     g = torch.Generator().manual_seed(M + in_f)
     xfull = (torch.randn(M, in_f + 8, generator=g) * 0.05 + 0.01).cuda()
@@ -65,6 +65,7 @@ def test_tower_forward_backward_vs_oracle(O, cuda, M, in_f, units, rate, off, ro
     out.backward(dout)
     if route == "librf":
         assert G.calls - n0 == 3 * len(units), G.calls - n0
+        assert G.torch_fallbacks == fb0  # no GEMM of the tower left librf
     layers = _oracle_layers(t)
     seeds = [layer_seed(t.seed, step, l) for l in range(len(units))]
     want, cache = O.tower_train_fwd(x.detach().cpu().numpy(), layers, rate, seeds)
