@@ -162,7 +162,8 @@ def main():
             for i in range(args.batches)]
     dev = [h.to("cuda") for h in host]
     out = torch.empty((args.batch, enc.out_width), dtype=torch.float32, device="cuda")
-    algo_bytes = [enc.algorithmic_bytes(h) for h in host]
+    algo_bytes = [enc.algorithmic_bytes(h) for h in host]                 # SURVEY §8d (the roofline's bytes)
+    algo_bytes_pad = [enc.algorithmic_bytes(h, pad_rows=True) for h in host]  # round-5 form, for comparison
     torch.cuda.synchronize()
 
     def step(i):
@@ -209,6 +210,7 @@ def main():
     elapsed = float(t.item())
     avg_kern_s = win0.elapsed_time(win1) / args.steps / 1e3
     bytes_per_launch = sum(algo_bytes[i % len(algo_bytes)] for i in range(args.steps)) / args.steps
+    bytes_per_launch_pad = sum(algo_bytes_pad[i % len(algo_bytes_pad)] for i in range(args.steps)) / args.steps
     achieved = bytes_per_launch / avg_kern_s / 1e9
     n_tok = sum(h.n_tokens for h in host) / len(host)
 
@@ -321,6 +323,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "algorithmic_bytes_form": "SURVEY 8d: rows 2*L*D*4 + pooled out + token bytes + 4 B per token (frac uses this)",
+            "algorithmic_bytes_per_launch_with_pad_rows": int(bytes_per_launch_pad),
+            "frac_with_pad_rows": round(bytes_per_launch_pad / avg_kern_s / 1e9 / HBM_PEAK_GBS, 4),
             "kernel_ms": round(avg_kern_s * 1e3, 4),
             "kernel_ms_timing": "HIP events around the timed window on the launch stream / steps (launches back to back)",
             "peak_measured": (probes or {}).get("stream_copy_GBs"),
@@ -1052,6 +1057,7 @@ def bench_train(args, specs, multi):
     from recommendflow_amd.backend.encoder.sparse_encoder import FusedSparseEncoder
     from recommendflow_amd.config_parser.configuration import Configuration
     from recommendflow_amd.models.matching.dssm import TrainableDssm
+    from recommendflow_amd.runtime import gemm as GM
     from recommendflow_amd.runtime.batch import synthetic_batch
 
     conf = Configuration(os.path.join(ROOT, "tests", "golden", "conf", "base_recall_sdpa.yaml"))
@@ -1187,7 +1193,8 @@ def bench_train(args, specs, multi):
                                    "line's examples_per_s keeps the bit-exact CPU order"},
            "config": "cfg2 DSSM train step: 229 slots, 9999972x64 fp32 table (+ m, v), B=4096, towers [1024,512,256] "
                      "BatchNormalization(batch stats)/selu/dropout 0.3 on librf (train_mlp.TrainTower: BN folded into "
-                     "the fp32 MFMA forward GEMM, SELU/dropout/BN backward kernels, library GEMMs for dW and dx), "
+                     "the exact-fp32 MFMA GEMM rf_gemm_f32 for forward, dW and dx, SELU/dropout/BN backward kernels; "
+                     f"torch GEMM fallbacks this run: {GM.torch_fallbacks}), "
                      "cosent_loss (HIP), Keras Adam (dense semantics, exact; deferred per row) on the table, Adam on the towers"}
     del model, enc, batches
     torch.cuda.empty_cache()

@@ -125,7 +125,7 @@ def _gemm_layer(probs, trans_a: bool, trans_b: bool, stream):
     launch where runtime.gemm.group_pays) when every operand qualifies; otherwise torch one by one."""
     if all(GM.supported_gemm(a, b, trans_a, trans_b, o) for a, b, _, _, o in probs):
         return GM.gemm_f32_layer(probs, trans_a=trans_a, trans_b=trans_b, stream=stream)
-    GM.note_torch_fallback("a tower backward layer")
+    GM.note_torch_fallback("a tower backward layer (operand layout or size outside rf_gemm_f32's checks)")
     outs = []
     for a, b, bias, act, o in probs:
         A = a.t() if trans_a else a

@@ -283,14 +283,22 @@ class FusedSparseEncoder(torch.nn.Module):
                L.ptr(grad), plan.cap, L.ptr(plan.n_uniq), L.ptr(plan.ws), plan.ws.numel(), L.stream_ptr(stream))
         return SparseGrad(plan.rows, grad, plan.n_uniq, plan.cap)
 
-    def algorithmic_bytes(self, batch: SparseBatch) -> int:
-        """HBM bytes one forward must move: rows read (every occurrence, padding positions
-        included as one pad-row read per table when Lmax > len), pooled output written, token bytes +
-        i32 offsets read."""
+    def algorithmic_bytes(self, batch: SparseBatch, pad_rows: bool = False) -> int:
+        """HBM bytes one forward must move, SURVEY §8d exactly: bytes = sum_s 2 L_s D e_T (every row occurrence, no
+        dedup credit) + sum_s 2 D e_out (pooled output) + sum_s L_s (token length + 4) (token bytes and their i32
+        offsets), summed over the batch's examples.
+
+        pad_rows=True is the round-5 form: one extra pad-row read per padded bag and table (the
+        reference gathers T[0] at every pad position; the kernel reads row 0 once per bag) plus the i32 bag
+        offsets. bench.py prints both and takes the roofline fraction from the §8d form."""
         h = batch.numpy()
         esz = torch.tensor([], dtype=self.table_dtype).element_size()
         osz = torch.tensor([], dtype=self.out_dtype).element_size()
         lens = np.diff(h.bag_off).reshape(h.batch, h.n_slots)
-        rows = int(lens.sum()) if self.mask_padding else int(lens.sum() + ((lens < h.lmax[None, :]).sum()))
-        return 2 * rows * self.dim * esz + h.batch * self.out_width * osz + int(len(h.tok_bytes)) + 4 * (h.n_tokens + 1) \
-            + 4 * (h.batch * h.n_slots + 1)
+        rows = int(lens.sum())
+        out = h.batch * self.out_width * osz
+        if not pad_rows:
+            return 2 * rows * self.dim * esz + out + int(h.tok_off[-1]) + 4 * h.n_tokens
+        if not self.mask_padding:
+            rows += int((lens < h.lmax[None, :]).sum())
+        return 2 * rows * self.dim * esz + out + int(len(h.tok_bytes)) + 4 * (h.n_tokens + 1) + 4 * (h.batch * h.n_slots + 1)

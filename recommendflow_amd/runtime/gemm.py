@@ -82,8 +82,7 @@ def note_torch_fallback(what: str):
     if not _warned[0]:
         _warned[0] = True
         import warnings
-        warnings.warn(f"rf_gemm_f32 fallback to torch for {what} (operand layout or size outside librf's checks)",
-                      RuntimeWarning, stacklevel=3)
+        warnings.warn(f"rf_gemm_f32 fallback to torch for {what}", RuntimeWarning, stacklevel=3)
 
 
 def gemm_f32(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
