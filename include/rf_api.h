@@ -683,6 +683,51 @@ int rf_cosent_loss(const float* score, const float* label, int32_t batch, float 
  */
 int rf_inbatch_ce_loss(const float* logits, int64_t ld, const float* label, int32_t batch, float scale, float* loss,
                        float* dlogits, int64_t ldd, void* ws, size_t ws_bytes, void* stream);
+/*
+ * The ESIM click head's loss (esim.py:53,88 Dense(2, 'softmax') trained by model.fit, example/ranking_search/train.py:96-104):
+ * sparse categorical cross-entropy of the softmax, computed from its logits as Keras does. logits [batch][ld] F32,
+ * label int32 [batch] in [0, n_classes): *loss = mean_b(logsumexp(z_b) - z_b[y_b]); prob (may be NULL) = softmax(z);
+ * dlogits (may be NULL) = (prob - onehot(y)) / batch. A label out of range makes that row NaN. ws: rf_loss_ws_bytes.
+ */
+int rf_softmax_ce_loss(const float* logits, int64_t ld, const int32_t* label, int32_t batch, int32_t n_classes, float* loss,
+                       float* prob, int64_t ldp, float* dlogits, int64_t ldd, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- ESIM ranking-model training (SURVEY §8f.1 for models/ranking: esim.py:45-53,69-89 under model.fit) -------
+ * The exact-fp32 training path of the ranker: Keras builds the model in float32, so every stage here computes in
+ * fp32 (the inference path above runs bf16 MFMA).
+ *
+ * rf_esim_train_fwd_f32: the ESIM attention block on fp32 q, a (example e at q + e * ex_stride, rows ld apart,
+ *   16-byte aligned; 1 <= L <= 128, d in {64, 128}): out[e][out_off ..] = [avg_q, max_q, avg_a, max_a,
+ *   avg_q - avg_a, max_q - max_a] (6d floats) and aux[e][2][d] = how many of the 4L pooled candidates equal each
+ *   max (TF's reduce_max gradient splits evenly over ties). v_mfma_f32_16x16x4_f32 products (exact fp32).
+ * rf_esim_train_bwd_f32: given the forward's pooled output and aux and dpooled (the gradient of those 6d columns),
+ *   writes dq, da (example stride g_ex_stride, rows ldg apart; every row < L overwritten). ws:
+ *   rf_esim_train_ws_bytes(batch, L, d) (per example S^T, dE^T [Lp][Lp] and G_q^T, G_a^T [d][Lp] fp32, Lp = L
+ *   rounded up to 16). Deterministic.
+ */
+size_t rf_esim_train_ws_bytes(int32_t batch, int32_t L, int32_t d);
+int rf_esim_train_fwd_f32(const float* q, const float* a, int32_t batch, int32_t L, int32_t d, int64_t ex_stride, int64_t ld,
+                          float* out, int64_t out_stride, int64_t out_off, float* aux, void* stream);
+int rf_esim_train_bwd_f32(const float* q, const float* a, int32_t batch, int32_t L, int32_t d, int64_t ex_stride, int64_t ld,
+                          const float* pooled, int64_t p_stride, int64_t p_off, const float* dpooled, int64_t dp_stride,
+                          int64_t dp_off, const float* aux, float* dq, float* da, int64_t g_ex_stride, int64_t ldg, void* ws,
+                          size_t ws_bytes, void* stream);
+/*
+ * create_mlp(units, rate, gelu, LayerNormalization(1e-6)) training stages (mlp.py:4-15; the ESIM input / output MLPs):
+ * rf_act_dropout_fwd   h = Dropout(rate)(act(pre)) with rf_dropout_fwd's keep mask (rate 0: no mask); act elementwise
+ * rf_act_dropout_bwd   dpre = dh keep / (1 - rate) act'(pre), db[N] = column sums of dpre (ws: rf_tower_ws_bytes(M, N))
+ * rf_layernorm_bwd     LayerNormalization(eps) backward over the last axis from its input x: dx, dgamma = sum(dy xhat),
+ *                      dbeta = sum(dy) (tf.nn.moments statistics; ws: rf_layernorm_bwd_ws_bytes(M, K))
+ * Column sums reduce fixed row chunks in chunk order (replay-deterministic). The forward LayerNorm is rf_norm_fwd
+ * (mode 0, F32 out) and the Dense products rf_gemm_f32.
+ */
+int rf_act_dropout_fwd(const float* pre, int64_t ldp, int64_t M, int32_t N, int32_t act, float rate, uint64_t seed, float* h,
+                       int64_t ldh, void* stream);
+int rf_act_dropout_bwd(const float* dh, int64_t lddh, const float* pre, int64_t ldp, int64_t M, int32_t N, int32_t act,
+                       float rate, uint64_t seed, float* dpre, int64_t ldd, float* db, void* ws, size_t ws_bytes, void* stream);
+size_t rf_layernorm_bwd_ws_bytes(int64_t M, int32_t K);
+int rf_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t M, int32_t K, const float* gamma,
+                     float eps, float* dx, int64_t lddx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- Lookup / Discrete embeddings: GPU index producers (rf_lookup.hip) ----------- */
 /*

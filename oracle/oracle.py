@@ -651,6 +651,121 @@ def tower_train_bwd(dout, layers, cache, rate: float, eps: float = 1e-6):
 
 
 # ----------------------------------------------------------------------------------------------
+# ESIM ranking-model training (float64): esim.py:45-53,69-89 under model.fit (example/ranking_search/train.py:96-104).
+# create_mlp(units, 0.3, gelu, LayerNormalization(1e-6)) layers (mlp.py:4-15, one norm per layer: deviation
+# D-shared-norm), the SoftAttention + combine + pooling block, Dropout(0.3) on the pooled row (esim.py:85),
+# Dense(2, softmax) and the sparse categorical cross-entropy of its logits. Dropout masks restate rf_dropout_fwd's.
+# ----------------------------------------------------------------------------------------------
+def gelu_grad(x):
+    """d/dx of the exact erf GELU: 0.5 (1 + erf(x / sqrt 2)) + x phi(x)."""
+    from scipy.special import erf
+
+    x = np.asarray(x, np.float64)
+    return 0.5 * (1.0 + erf(x / math.sqrt(2.0))) + x * np.exp(-0.5 * x * x) / math.sqrt(2.0 * math.pi)
+
+
+def ln_mlp_train_fwd(x, layers, rate: float, seeds, eps: float = 1e-6):
+    """layers: [{"W": [N][K], "b", "gamma", "beta"}] (W stored [out][in], as librf); per layer LayerNormalization
+    (tf.nn.moments: biased variance) -> Dense -> gelu -> Dropout(rate). Returns (h, cache)."""
+    h = np.asarray(x, np.float64)
+    cache = []
+    for p, seed in zip(layers, seeds):
+        W = np.asarray(p["W"], np.float64)
+        mu = h.mean(-1, keepdims=True)
+        var = ((h - mu) ** 2).mean(-1, keepdims=True)
+        rstd = 1.0 / np.sqrt(var + eps)
+        xhat = (h - mu) * rstd
+        z = xhat * p["gamma"] + p["beta"]
+        pre = z @ W.T + p["b"]
+        keep = dropout_keep(seed, h.shape[0], W.shape[0], rate) if rate > 0 else np.ones(pre.shape, bool)
+        out = np.where(keep, gelu(pre) / (1.0 - rate), 0.0)
+        cache.append({"h": h, "xhat": xhat, "rstd": rstd, "z": z, "pre": pre, "keep": keep})
+        h = out
+    return h, cache
+
+
+def ln_mlp_train_bwd(dout, layers, cache, rate: float):
+    """Backward of ln_mlp_train_fwd: (dx, [{"W", "b", "gamma", "beta"} gradients])."""
+    dh = np.asarray(dout, np.float64)
+    grads = []
+    for p, c in zip(reversed(layers), reversed(cache)):
+        W = np.asarray(p["W"], np.float64)
+        dpre = np.where(c["keep"], dh / (1.0 - rate), 0.0) * gelu_grad(c["pre"])
+        dz = dpre @ W
+        u = dz * p["gamma"]
+        xh = c["xhat"]
+        dh = c["rstd"] * (u - u.mean(-1, keepdims=True) - xh * (u * xh).mean(-1, keepdims=True))
+        grads.insert(0, {"W": dpre.T @ c["z"], "b": dpre.sum(0), "gamma": (dz * xh).sum(0), "beta": dz.sum(0)})
+    return dh, grads
+
+
+def esim_pool_bwd(q, a, dpooled):
+    """float64 backward of esim_pool: (dq, da). The max pooling's gradient follows TF's reduce_max (_MinOrMaxGrad):
+    split evenly over every candidate equal to the maximum."""
+    q = np.asarray(q, np.float64)
+    a = np.asarray(a, np.float64)
+    dp = np.asarray(dpooled, np.float64)
+    B, L, d = q.shape
+    E = np.einsum("bjk,bik->bij", q, a)
+    e = np.exp(E - E.max(axis=-1, keepdims=True))
+    S = e / e.sum(axis=-1, keepdims=True)
+    att = (S @ q, S @ a)
+    g = [dp[:, k * d:(k + 1) * d] for k in range(6)]
+    gavg = ((g[0] + g[4]) / (4 * L), (g[2] - g[4]) / (4 * L))
+    gmax = (g[1] + g[5], g[3] - g[5])
+    G, Dx = [], []
+    for x, at, ga, gm in zip((q, a), att, gavg, gmax):
+        cands = [x, at, x - at, x * at]
+        M = np.max([c.max(axis=1) for c in cands], axis=0)  # [B, d]
+        eq = [(c == M[:, None, :]).astype(np.float64) for c in cands]
+        share = gm / sum(t.sum(axis=1) for t in eq)  # [B, d]
+        G.append(x * ga[:, None, :] + share[:, None, :] * (eq[1] - eq[2] + x * eq[3]))
+        Dx.append((2.0 + at) * ga[:, None, :] + share[:, None, :] * (eq[0] + eq[2] + at * eq[3]))
+    dS = G[0] @ np.swapaxes(q, 1, 2) + G[1] @ np.swapaxes(a, 1, 2)  # [B, i, j]
+    dE = S * (dS - (S * dS).sum(axis=-1, keepdims=True))
+    St = np.swapaxes(S, 1, 2)
+    dq = Dx[0] + St @ G[0] + np.swapaxes(dE, 1, 2) @ a
+    da = Dx[1] + St @ G[1] + dE @ q
+    return dq, da
+
+
+def esim_train_loss(q, a, dense, label, input_layers, output_layers, W_out, b_out, rate: float = 0.0, seeds=None,
+                    eps: float = 1e-6, grads: bool = False):
+    """The ESIM training loss (float64) and, with grads=True, every gradient: returns (loss, probs) or (loss, probs,
+    {"q", "a", "input", "output", "W_out", "b_out"}). seeds = (input layer seeds, pooled-dropout seed, output layer
+    seeds) of the Dropout(rate) masks; W_out [2][K] stored [out][in]."""
+    nin, nout = len(input_layers), len(output_layers)
+    if seeds is None:
+        seeds = ([0] * nin, 0, [0] * nout)
+    s_in, s_pool, s_out = seeds
+    label = np.asarray(label).astype(np.int64)
+    d_emb, c_in = ln_mlp_train_fwd(dense, input_layers, rate, s_in, eps)
+    pooled = np.concatenate([d_emb, esim_pool(q, a)], axis=1)
+    keep = dropout_keep(s_pool, pooled.shape[0], pooled.shape[1], rate) if rate > 0 else np.ones(pooled.shape, bool)
+    x = np.where(keep, pooled / (1.0 - rate), 0.0)
+    h, c_out = ln_mlp_train_fwd(x, output_layers, rate, s_out, eps)
+    Wo = np.asarray(W_out, np.float64)
+    z = h @ Wo.T + b_out
+    m = z.max(axis=-1, keepdims=True)
+    lse = m[:, 0] + np.log(np.exp(z - m).sum(axis=-1))
+    B = z.shape[0]
+    loss = float((lse - z[np.arange(B), label]).mean())
+    prob = np.exp(z - lse[:, None])
+    if not grads:
+        return loss, prob
+    dz = prob.copy()
+    dz[np.arange(B), label] -= 1.0
+    dz /= B
+    gWo, gbo = dz.T @ h, dz.sum(0)
+    dx, g_out = ln_mlp_train_bwd(dz @ Wo, output_layers, c_out, rate)
+    dpooled = np.where(keep, dx / (1.0 - rate), 0.0)
+    W = d_emb.shape[1]
+    _, g_in = ln_mlp_train_bwd(dpooled[:, :W], input_layers, c_in, rate)
+    dq, da = esim_pool_bwd(q, a, dpooled[:, W:])
+    return loss, prob, {"q": dq, "a": da, "input": g_in, "output": g_out, "W_out": gWo, "b_out": gbo}
+
+
+# ----------------------------------------------------------------------------------------------
 # training losses (float64), backend/losses/match_losses.py
 # ----------------------------------------------------------------------------------------------
 def cosent_loss(y: np.ndarray, s: np.ndarray, scale: float = 20.0):

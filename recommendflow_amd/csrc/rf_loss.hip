@@ -176,6 +176,31 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ v,
     }
 }
 
+// Dense(n, softmax) + sparse categorical cross-entropy (the ESIM click head, esim.py:53,88): Keras computes the CE
+// of a softmax output from its logits, so per row loss_b = logsumexp(z_b) - z_b[y_b] and dz_b = (softmax(z_b) -
+// onehot(y_b)) / B; the mean over the batch is mean_kernel's fixed-order sum. A label outside [0, n) gives that row
+// a NaN loss and NaN gradients (never an out-of-range read).
+__global__ __launch_bounds__(256) void softmax_ce_kernel(const float* __restrict__ z, int64_t ld, const int32_t* __restrict__ y,
+                                                         int B, int N, float* __restrict__ rows, float* __restrict__ prob,
+                                                         int64_t ldp, float* __restrict__ dz, int64_t ldd) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    const float* zr = z + (int64_t)b * ld;
+    const int yb = y[b];
+    const bool ok = yb >= 0 && yb < N;
+    float m = -INFINITY;
+    for (int j = 0; j < N; ++j) m = fmaxf(m, zr[j]);
+    float s = 0.f;
+    for (int j = 0; j < N; ++j) s += expf(zr[j] - m);
+    rows[b] = ok ? m + logf(s) - zr[yb] : __builtin_nanf("");
+    const float invB = 1.0f / (float)B;
+    for (int j = 0; j < N; ++j) {
+        const float p = expf(zr[j] - m) / s;
+        if (prob) prob[(int64_t)b * ldp + j] = p;
+        if (dz) dz[(int64_t)b * ldd + j] = ok ? (p - (j == yb ? 1.f : 0.f)) * invB : __builtin_nanf("");
+    }
+}
+
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // ---- l2-normalised row cosine (the DSSM score ahead of cosent_loss) ------------------------------------------
@@ -300,4 +325,20 @@ extern "C" int rf_inbatch_ce_loss(const float* logits, int64_t ld, const float* 
     hipLaunchKernelGGL(inbatch_ce_kernel, dim3(batch), dim3(256), 0, st, logits, ld, label, batch, scale, rows, dlogits, ldd);
     hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, st, rows, batch, loss);
     return rf_check_launch("rf_inbatch_ce_loss");
+}
+
+extern "C" int rf_softmax_ce_loss(const float* logits, int64_t ld, const int32_t* label, int32_t batch, int32_t n_classes,
+                                  float* loss, float* prob, int64_t ldp, float* dlogits, int64_t ldd, void* ws, size_t ws_bytes,
+                                  void* stream) {
+    RF_REQUIRE(batch >= 1 && n_classes >= 1 && ld >= n_classes && (!prob || ldp >= n_classes) &&
+                   (!dlogits || ldd >= n_classes),
+               "rf_softmax_ce_loss: bad shape");
+    RF_REQUIRE(logits && label && loss && ws, "rf_softmax_ce_loss: null pointer");
+    RF_REQUIRE(ws_bytes >= rf_loss_ws_bytes(batch), "rf_softmax_ce_loss: workspace too small");
+    hipStream_t st = rf_stream(stream);
+    float* rows = static_cast<float*>(ws);
+    hipLaunchKernelGGL(softmax_ce_kernel, dim3((batch + 255) / 256), dim3(256), 0, st, logits, ld, label, batch, n_classes, rows,
+                       prob, ldp, dlogits, ldd);
+    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(1024), 0, st, rows, batch, loss);
+    return rf_check_launch("rf_softmax_ce_loss");
 }

@@ -428,6 +428,168 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
     st<V>(dx + r * lddx + k, o);
 }
 
+// ---- LayerNorm MLP training stages (the ESIM input / output MLPs: create_mlp(.., gelu, LayerNormalization(1e-6)),
+// esim.py:45-52, under model.fit) -----------------------------------------------------------------------------
+// activation value and derivative at the pre-activation x (exact erf GELU: tf.keras.activations.gelu)
+__device__ __forceinline__ void act_vd(int act, float x, float& y, float& dy) {
+    switch (act) {
+        case RF_ACT_GELU: {
+            const float c = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+            y = x * c;
+            dy = c + x * 0.39894228040143267794f * expf(-0.5f * x * x);
+            break;
+        }
+        case RF_ACT_RELU: y = x > 0.f ? x : 0.f; dy = x > 0.f ? 1.f : 0.f; break;
+        case RF_ACT_SELU: {
+            const float alpha = 1.6732632423543772848170429916717f, scale = 1.0507009873554804934193349852946f;
+            const float ex = expf(fminf(x, 0.f));
+            y = x > 0.f ? scale * x : scale * alpha * (ex - 1.0f);
+            dy = x > 0.f ? scale : scale * alpha * ex;
+            break;
+        }
+        default: y = x; dy = 1.f; break;
+    }
+}
+
+// h = Dropout(rate)(act(pre)): kept elements act(pre) / (1 - rate) (the rf_dropout_fwd mask), dropped 0
+template <int V>
+__global__ __launch_bounds__(256) void act_dropout_fwd_kernel(const float* __restrict__ pre, int64_t ldp, int N, int act,
+                                                              float rate, uint64_t seed, float* __restrict__ h, int64_t ldh) {
+    const int c = (blockIdx.x * 256 + threadIdx.x) * V;
+    if (c >= N) return;
+    const int64_t r = blockIdx.y;
+    typename vec_t<V>::T v = ld<V>(pre + r * ldp + c);
+    const float s = 1.0f / (1.0f - rate);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        float y, dy;
+        act_vd(act, lane<V>(v, i), y, dy);
+        lane<V>(v, i) = rate == 0.f || keep_elem(seed, r, N, c + i, rate) ? y * s : 0.f;
+    }
+    st<V>(h + r * ldh + c, v);
+}
+
+// dpre = dh keep / (1 - rate) act'(pre); bias-gradient column partials of dpre
+template <int V>
+__global__ __launch_bounds__(kColThreads) void act_dropout_bwd_kernel(const float* __restrict__ dh, int64_t lddh,
+                                                                      const float* __restrict__ pre, int64_t ldp, int64_t M,
+                                                                      int N, int act, float rate, uint64_t seed, int rows_per,
+                                                                      float* __restrict__ dpre, int64_t ldd,
+                                                                      float* __restrict__ part) {
+    const int c = (blockIdx.x * kColThreads + threadIdx.x) * V;
+    if (c >= N) return;
+    const float s = 1.0f / (1.0f - rate);
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+    const int64_t r1 = std::min<int64_t>(M, r0 + rows_per);
+    float acc[V];
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+    for (int64_t r = r0; r < r1; ++r) {
+        typename vec_t<V>::T g = ld<V>(dh + r * lddh + c), x = ld<V>(pre + r * ldp + c);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            float y, dy;
+            act_vd(act, lane<V>(x, i), y, dy);
+            const float o = rate == 0.f || keep_elem(seed, r, N, c + i, rate) ? lane<V>(g, i) * s * dy : 0.f;
+            lane<V>(g, i) = o;
+            acc[i] += o;
+        }
+        st<V>(dpre + r * ldd + c, g);
+    }
+    float* o = part + (int64_t)blockIdx.y * N + c;
+#pragma unroll
+    for (int i = 0; i < V; ++i) o[i] = acc[i];
+}
+
+// LayerNorm backward, rows: one wave per row. mean and (biased) variance as tf.nn.moments, xhat = (x - mean)
+// rsqrt(var + eps); with u = dy gamma: dx = rstd (u - mean(u) - xhat mean(u xhat)). Row (mean, rstd) to rs.
+__global__ __launch_bounds__(256) void ln_bwd_rows_kernel(const float* __restrict__ dy, int64_t lddy,
+                                                          const float* __restrict__ x, int64_t ldx, int64_t M, int K,
+                                                          const float* __restrict__ gamma, float eps, float* __restrict__ dx,
+                                                          int64_t lddx, float* __restrict__ rs) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= M) return;
+    const float* xr = x + r * ldx;
+    const float* gr = dy + r * lddy;
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s += xr[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)K;
+    float q = 0.f;
+    for (int k = lane; k < K; k += 64) {
+        const float d = xr[k] - mean;
+        q = fmaf(d, d, q);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = 1.0f / sqrtf(q / (float)K + eps);
+    float a = 0.f, b = 0.f;
+    for (int k = lane; k < K; k += 64) {
+        const float u = gr[k] * gamma[k];
+        a += u;
+        b = fmaf(u, (xr[k] - mean) * rstd, b);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+    a /= (float)K;
+    b /= (float)K;
+    float* dr = dx + r * lddx;
+    for (int k = lane; k < K; k += 64) {
+        const float xh = (xr[k] - mean) * rstd;
+        dr[k] = rstd * (gr[k] * gamma[k] - a - xh * b);
+    }
+    if (lane == 0) {
+        rs[2 * r] = mean;
+        rs[2 * r + 1] = rstd;
+    }
+}
+
+// LayerNorm backward, columns: chunk partials of dbeta = sum(dy), dgamma = sum(dy xhat) -> part[chunk][2][K]
+template <int V>
+__global__ __launch_bounds__(kColThreads) void ln_bwd_cols_kernel(const float* __restrict__ dy, int64_t lddy,
+                                                                  const float* __restrict__ x, int64_t ldx, int64_t M, int K,
+                                                                  const float* __restrict__ rs, int rows_per,
+                                                                  float* __restrict__ part) {
+    const int k0 = (blockIdx.x * kColThreads + threadIdx.x) * V;
+    if (k0 >= K) return;
+    float s1[V], s2[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) s1[i] = s2[i] = 0.f;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+    const int64_t r1 = std::min<int64_t>(M, r0 + rows_per);
+    for (int64_t r = r0; r < r1; ++r) {
+        typename vec_t<V>::T g = ld<V>(dy + r * lddy + k0), xv = ld<V>(x + r * ldx + k0);
+        const float mean = rs[2 * r], rstd = rs[2 * r + 1];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            s1[i] += lane<V>(g, i);
+            s2[i] = fmaf(lane<V>(g, i), (lane<V>(xv, i) - mean) * rstd, s2[i]);
+        }
+    }
+    float* o = part + (int64_t)blockIdx.y * 2 * K + k0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        o[i] = s1[i];
+        o[K + i] = s2[i];
+    }
+}
+
+__global__ __launch_bounds__(kFinCols * kFinGroups) void col_sum2_finish_kernel(const float* __restrict__ part, int K,
+                                                                                int chunks, float* __restrict__ out0,
+                                                                                float* __restrict__ out1) {
+    float t[2];
+    finish_sums<2>(part, K, chunks, t);
+    const int k = blockIdx.x * kFinCols + threadIdx.x;
+    if (threadIdx.x < kFinCols && k < K) {
+        out0[k] = t[0];
+        out1[k] = t[1];
+    }
+}
+
 }  // namespace
 
 // chunk partials ([chunk][2][K] floats) + rf_bn_bwd's per-column constants (3 K floats)
@@ -526,4 +688,62 @@ extern "C" int rf_bn_bwd(const float* dz, int64_t lddz, const float* x, int64_t 
     auto grid2 = [&](int v) { return dim3((K / v + 255) / 256, (unsigned)M); };
     RF_TOWER_LAUNCH(bn_bwd_apply_kernel, V, grid2, dz, lddz, x, ldx, K, mean, var, eps, (const float*)ac, dx, lddx);
     return rf_check_launch("rf_bn_bwd");
+}
+
+extern "C" int rf_act_dropout_fwd(const float* pre, int64_t ldp, int64_t M, int32_t N, int32_t act, float rate, uint64_t seed,
+                                  float* h, int64_t ldh, void* stream) {
+    RF_REQUIRE(M >= 0 && M <= 65535 && N > 0 && ldp >= N && ldh >= N && rate >= 0.f && rate < 1.f &&
+                   act >= RF_ACT_NONE && act < RF_ACT_SOFTMAX,
+               "rf_act_dropout_fwd: bad arguments");
+    if (M == 0) return RF_OK;
+    RF_REQUIRE(pre && h, "rf_act_dropout_fwd: null pointer");
+    hipStream_t st = rf_stream(stream);
+    const int V = vec4_ok(N, {{pre, ldp}, {h, ldh}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((N / v + 255) / 256, (unsigned)M); };
+    RF_TOWER_LAUNCH(act_dropout_fwd_kernel, V, grid, pre, ldp, N, act, rate, seed, h, ldh);
+    return rf_check_launch("rf_act_dropout_fwd");
+}
+
+extern "C" int rf_act_dropout_bwd(const float* dh, int64_t lddh, const float* pre, int64_t ldp, int64_t M, int32_t N,
+                                  int32_t act, float rate, uint64_t seed, float* dpre, int64_t ldd, float* db, void* ws,
+                                  size_t ws_bytes, void* stream) {
+    RF_REQUIRE(M > 0 && N > 0 && lddh >= N && ldp >= N && ldd >= N && rate >= 0.f && rate < 1.f && act >= RF_ACT_NONE &&
+                   act < RF_ACT_SOFTMAX,
+               "rf_act_dropout_bwd: bad arguments");
+    RF_REQUIRE(dh && pre && dpre && db, "rf_act_dropout_bwd: null pointer");
+    RF_REQUIRE(ws && ws_bytes >= rf_tower_ws_bytes(M, N), "rf_act_dropout_bwd: workspace too small");
+    const int chunks = tower_chunks(M, N), rows_per = (int)((M + chunks - 1) / chunks);
+    hipStream_t st = rf_stream(stream);
+    const int V = vec4_ok(N, {{dh, lddh}, {pre, ldp}, {dpre, ldd}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((N / v + kColThreads - 1) / kColThreads, chunks); };
+    RF_TOWER_LAUNCH(act_dropout_bwd_kernel, V, grid, dh, lddh, pre, ldp, M, N, act, rate, seed, rows_per, dpre, ldd,
+                    (float*)ws);
+    hipLaunchKernelGGL(col_sum_finish_kernel, dim3((N + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinGroups), 0, st,
+                       (const float*)ws, N, chunks, db);
+    return rf_check_launch("rf_act_dropout_bwd");
+}
+
+extern "C" size_t rf_layernorm_bwd_ws_bytes(int64_t M, int32_t K) {
+    const size_t rows = ((size_t)std::max<int64_t>(M, 1) * 2 * sizeof(float) + 255) & ~(size_t)255;
+    return rows + (size_t)tower_chunks(std::max<int64_t>(M, 1), std::max(K, 1)) * 2 * std::max(K, 1) * sizeof(float);
+}
+
+extern "C" int rf_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t M, int32_t K,
+                                const float* gamma, float eps, float* dx, int64_t lddx, float* dgamma, float* dbeta, void* ws,
+                                size_t ws_bytes, void* stream) {
+    RF_REQUIRE(M > 0 && M <= (1 << 26) && K > 0 && lddy >= K && ldx >= K && lddx >= K, "rf_layernorm_bwd: bad arguments");
+    RF_REQUIRE(dy && x && gamma && dx && dgamma && dbeta, "rf_layernorm_bwd: null pointer");
+    RF_REQUIRE(ws && ws_bytes >= rf_layernorm_bwd_ws_bytes(M, K), "rf_layernorm_bwd: workspace too small");
+    hipStream_t st = rf_stream(stream);
+    float* rs = static_cast<float*>(ws);
+    float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + (((size_t)M * 2 * sizeof(float) + 255) & ~(size_t)255));
+    hipLaunchKernelGGL(ln_bwd_rows_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st, dy, lddy, x, ldx, M, K, gamma, eps,
+                       dx, lddx, rs);
+    const int chunks = tower_chunks(M, K), rows_per = (int)((M + chunks - 1) / chunks);
+    const int V = vec4_ok(K, {{dy, lddy}, {x, ldx}}) ? 4 : 1;
+    auto grid = [&](int v) { return dim3((K / v + kColThreads - 1) / kColThreads, chunks); };
+    RF_TOWER_LAUNCH(ln_bwd_cols_kernel, V, grid, dy, lddy, x, ldx, M, K, (const float*)rs, rows_per, part);
+    hipLaunchKernelGGL(col_sum2_finish_kernel, dim3((K + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinGroups), 0, st,
+                       (const float*)part, K, chunks, dbeta, dgamma);
+    return rf_check_launch("rf_layernorm_bwd");
 }

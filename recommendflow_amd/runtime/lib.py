@@ -85,6 +85,17 @@ _SIGS = {
                                           _i64, _vp]),
     "rf_loss_ws_bytes": (ctypes.c_size_t, [_i32]),
     "rf_cosent_loss": (ctypes.c_int, [_vp, _vp, _i32, _f32, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "rf_softmax_ce_loss": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _vp, _vp, _i64, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
+    "rf_esim_train_ws_bytes": (ctypes.c_size_t, [_i32, _i32, _i32]),
+    "rf_esim_train_fwd_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
+    "rf_esim_train_bwd_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp,
+                                             _vp, _vp, _i64, _i64, _vp, ctypes.c_size_t, _vp]),
+    "rf_act_dropout_fwd": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i32, _f32, ctypes.c_uint64, _vp, _i64, _vp]),
+    "rf_act_dropout_bwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _f32, ctypes.c_uint64, _vp, _i64, _vp, _vp,
+                                          ctypes.c_size_t, _vp]),
+    "rf_layernorm_bwd_ws_bytes": (ctypes.c_size_t, [_i64, _i32]),
+    "rf_layernorm_bwd": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _vp, _f32, _vp, _i64, _vp, _vp, _vp, ctypes.c_size_t,
+                                        _vp]),
     "rf_inbatch_ce_loss": (ctypes.c_int, [_vp, _i64, _vp, _i32, _f32, _vp, _vp, _i64, _vp, ctypes.c_size_t, _vp]),
     "rf_vocab_capacity": (_i64, [_i64]),
     "rf_vocab_build": (ctypes.c_int, [_i32, _vp, _vp, _i64, _vp, _i64]),
