@@ -284,6 +284,8 @@ def main():
         extras = dict(extras or {}, cfg5_cascade=guarded(bench_cascade, args, enc))
     if world == 1 and not args.no_train:
         extras = dict(extras or {}, cfg2_dssm_train_step=guarded(bench_train, args, specs, multi))
+    if world == 1 and not args.no_train:
+        extras = dict(extras or {}, cfg3_esim_train_step=guarded(bench_esim_train, args))
     if world == 1 and not args.no_pipe:
         extras = dict(extras or {}, feature_pipe=guarded(bench_pipe, args, enc, specs, multi))
     if world == 1 and not args.no_extras:
@@ -1197,6 +1199,80 @@ def bench_train(args, specs, multi):
                      f"torch GEMM fallbacks this run: {GM.torch_fallbacks}), "
                      "cosent_loss (HIP), Keras Adam (dense semantics, exact; deferred per row) on the table, Adam on the towers"}
     del model, enc, batches
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_esim_train(args):
+    """SURVEY §8f.1 for the ranker: one ESIM training step (models/ranking/esim_train.TrainableEsim; esim.py:45-53,69-89
+    under model.fit, example/ranking_search/train.py:96-104) at the cfg3 shape: 100 user + 100 ad single-valued
+    slots, token dim 128 (D = 64 per hash), 16 dense features, input_mlp [256, 512], output_mlp [1024, 512],
+    Dropout 0.3, Dense(2, softmax) + sparse categorical CE, Keras Adam on the fused fp32 table (deferred, exact dense
+    semantics) and on every dense parameter, B = 4096. The table has 100K bins per hash (not cfg3's 1M): Keras
+    trains float32 tables, and 2 x 200 x 1M x 64 fp32 with Adam's m and v would be 307 GB, over one GPU's 288 GB."""
+    import numpy as np
+    import torch
+
+    from recommendflow_amd.backend.encoder.sparse_encoder import SlotSpec
+    from recommendflow_amd.models.ranking.esim_train import TrainableEsim
+    from recommendflow_amd.runtime import lib as RL
+    from recommendflow_amd.runtime.batch import synthetic_batch
+
+    B, Ls, bins = args.batch, 100, 100_000
+    user = [SlotSpec(f"u{i:03d}", bins, (2022, 2023)) for i in range(Ls)]
+    ad = [SlotSpec(f"a{i:03d}", bins, (2022, 2023)) for i in range(Ls)]
+    m = TrainableEsim(user, ad, 16, dim=64, seed=5)
+    batches = [synthetic_batch(B, [False] * (2 * Ls), seed=311 + i, slot_ids=range(2 * Ls)).to("cuda") for i in range(2)]
+    g = torch.Generator().manual_seed(4)
+    dense = [torch.randn((B, 16), generator=g).cuda() for _ in range(2)]
+    labels = [(torch.rand(B, generator=g) < 0.3).to(torch.int32).cuda() for _ in range(2)]
+    steps = max(5, args.steps // 4)
+    wi = [0]
+
+    def one():
+        i = wi[0] % 2
+        wi[0] += 1
+        return m.step(batches[i], dense[i], labels[i])
+
+    _warm(one)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = one()
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / steps * 1e3
+    # the attention block's kernels alone (HIP events on the launch stream)
+    x = m.enc(batches[0])
+    Ld = Ls * 128
+    pooled = torch.empty((B, m.pooled_width), device="cuda")
+    aux = torch.empty((B, 256), device="cuda")
+    dp = torch.randn((B, m.pooled_width), device="cuda")
+    dx = torch.empty_like(x)
+    ws = torch.empty(int(RL.load().rf_esim_train_ws_bytes(B, Ls, 128)), dtype=torch.uint8, device="cuda")
+    st = RL.stream_ptr()
+
+    def fwd():
+        RL.call("rf_esim_train_fwd_f32", RL.ptr(x), RL.ptr(x) + 4 * Ld, B, Ls, 128, x.stride(0), 128, RL.ptr(pooled),
+                pooled.stride(0), m.d_emb, RL.ptr(aux), st)
+
+    def bwd():
+        RL.call("rf_esim_train_bwd_f32", RL.ptr(x), RL.ptr(x) + 4 * Ld, B, Ls, 128, x.stride(0), 128, RL.ptr(pooled),
+                pooled.stride(0), m.d_emb, RL.ptr(dp), dp.stride(0), m.d_emb, RL.ptr(aux), RL.ptr(dx), RL.ptr(dx) + 4 * Ld,
+                dx.stride(0), 128, RL.ptr(ws), ws.numel(), st)
+
+    _, per = _time_stages([("attention_fwd", fwd), ("attention_bwd", bwd)], max(10, args.steps // 2), 3)
+    fl_f = 6.0 * Ls * Ls * 128 * B  # E, S q, S a
+    fl_b = 18.0 * Ls * Ls * 128 * B  # E, S q, S a again; dS (2); dE q; S^T G_q, S^T G_a, dE^T a
+    res = {"examples_per_s": round(B / step_ms * 1e3, 1), "ms_per_step": round(step_ms, 4), "loss": round(float(loss.item()), 4),
+           "stage_ms": {k: round(v, 4) for k, v in per.items()},
+           "attention_fwd_TFLOPs_fp32": round(fl_f / per["attention_fwd"] / 1e9, 1),
+           "attention_bwd_TFLOPs_fp32": round(fl_b / per["attention_bwd"] / 1e9, 1),
+           "attention_frac_of_157TF_fp32": round((fl_f + fl_b) / (per["attention_fwd"] + per["attention_bwd"]) / 1e9 / 157.3, 4),
+           "config": "cfg3 shape: 100 + 100 single-valued slots, 100K bins per hash (fp32 fused table 40M x 64 + Adam m, v), "
+                     "d = 128, dense 16 -> [256, 512], pooled 1280 -> [1024, 512] -> Dense(2, softmax), Dropout 0.3, "
+                     "B = 4096; exact fp32 on librf (rf_esim_train_{fwd,bwd}_f32 on v_mfma_f32_16x16x4_f32, rf_gemm_f32, "
+                     "LayerNorm / gelu+dropout / CE kernels, Keras Adam)"}
+    del m, batches, x, dx, ws
     torch.cuda.empty_cache()
     return res
 

@@ -45,11 +45,11 @@ struct Ex {
 };
 
 // stage rows [0, Lp) of one example's q and a into LDS (rows >= L zero)
-template <int D>
+template <int D, int NT = kThreads>
 __device__ __forceinline__ void stage_qa(const float* __restrict__ q, const float* __restrict__ a, int64_t ld, int L, int Lp,
                                          float* qs, float* as) {
     constexpr int RS = Ex<D>::RS, C4 = D / 4;
-    for (int t = threadIdx.x; t < 2 * Lp * C4; t += kThreads) {
+    for (int t = threadIdx.x; t < 2 * Lp * C4; t += NT) {
         const int side = t / (Lp * C4), rem = t - side * Lp * C4, r = rem / C4, c4 = rem - r * C4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (r < L) v = *reinterpret_cast<const float4*>((side ? a : q) + (int64_t)r * ld + 4 * c4);
@@ -61,29 +61,42 @@ __device__ __forceinline__ f4v lds4(const float* p) { return *reinterpret_cast<c
 
 // One strip's forward: S^T [NJ] (C layout: j = 16 jt + 4 g + r, i = ibase + li) and att_q^T, att_a^T [D/16]
 // (c = 16 ct + 4 g + r, i = ibase + li).
-template <int D, int NJ>
-__device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int L, int ibase, int li, int g, f4v (&S)[NJ],
-                                          f4v (&attq)[D / 16], f4v (&atta)[D / 16]) {
+// NJ (= Lp / 16 <= kMaxJ) is a runtime value: the j-tile loops are unrolled to kMaxJ with uniform guards, so each
+// kernel holds one copy of its code (a copy per tile count put 140K lines of ISA in the forward and thrashed the
+// instruction cache)
+constexpr int kMaxJ = 8;
+template <int D>
+__device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int L, int NJ, int ibase, int li, int g,
+                                          f4v (&S)[kMaxJ], f4v (&attq)[D / 16], f4v (&atta)[D / 16]) {
     constexpr int RS = Ex<D>::RS;
     // X = E^T strip
     f4v ar[D / 16];
 #pragma unroll
     for (int k = 0; k < D / 16; ++k) ar[k] = lds4(as + (ibase + li) * RS + 16 * k + 4 * g);
+    // two j tiles per pass: two independent accumulator chains (16x16x4 f32: 40-cycle dependent latency, 32-cycle issue)
 #pragma unroll
-    for (int jt = 0; jt < NJ; ++jt) {
-        f4v acc = zero4();
+    for (int jt = 0; jt < kMaxJ; jt += 2) {
+        f4v acc0 = zero4(), acc1 = zero4();
+        if (jt < NJ) {
+            const bool two = jt + 1 < NJ;
 #pragma unroll
-        for (int k = 0; k < D / 16; ++k) {
-            const f4v qv = lds4(qs + (16 * jt + li) * RS + 16 * k + 4 * g);
+            for (int k = 0; k < D / 16; ++k) {
+                const f4v q0 = lds4(qs + (16 * jt + li) * RS + 16 * k + 4 * g);
+                const f4v q1 = two ? lds4(qs + (16 * (jt + 1) + li) * RS + 16 * k + 4 * g) : zero4();
 #pragma unroll
-            for (int s = 0; s < 4; ++s) acc = mf(qv[s], ar[k][s], acc);
+                for (int s = 0; s < 4; ++s) {
+                    acc0 = mf(q0[s], ar[k][s], acc0);
+                    acc1 = mf(q1[s], ar[k][s], acc1);
+                }
+            }
         }
-        S[jt] = acc;
+        S[jt] = acc0;
+        S[jt + 1] = acc1;
     }
     // softmax over j (rows of X) for every column i: max, exp, sum, divide (attention_layers.py:70-72)
     float m = -INFINITY;
 #pragma unroll
-    for (int jt = 0; jt < NJ; ++jt)
+    for (int jt = 0; jt < kMaxJ; ++jt)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (16 * jt + 4 * g + r < L) m = fmaxf(m, S[jt][r]);
@@ -91,7 +104,7 @@ __device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int 
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     float sum = 0.f;
 #pragma unroll
-    for (int jt = 0; jt < NJ; ++jt)
+    for (int jt = 0; jt < kMaxJ; ++jt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float e = 16 * jt + 4 * g + r < L ? expf(S[jt][r] - m) : 0.f;
@@ -101,7 +114,7 @@ __device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int 
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
 #pragma unroll
-    for (int jt = 0; jt < NJ; ++jt)
+    for (int jt = 0; jt < kMaxJ; ++jt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) S[jt][r] = S[jt][r] / sum;
     // att^T = x^T S^T for x = q, a (A[c][j] = x[j][c], k order j = 16 jt + 4 g + r)
@@ -109,39 +122,53 @@ __device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int 
     for (int ct = 0; ct < D / 16; ++ct) {
         f4v aq = zero4(), aa = zero4();
 #pragma unroll
-        for (int jt = 0; jt < NJ; ++jt)
+        for (int jt = 0; jt < kMaxJ; ++jt)
+            if (jt < NJ) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int j = 16 * jt + 4 * g + r;
-                aq = mf(qs[j * RS + 16 * ct + li], S[jt][r], aq);
-                aa = mf(as[j * RS + 16 * ct + li], S[jt][r], aa);
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 * jt + 4 * g + r;
+                    aq = mf(qs[j * RS + 16 * ct + li], S[jt][r], aq);
+                    aa = mf(as[j * RS + 16 * ct + li], S[jt][r], aa);
+                }
             }
         attq[ct] = aq;
         atta[ct] = aa;
     }
 }
 
-// (max, count) fold of the candidates equal to the maximum (exact comparisons: any combine order gives the same pair)
-__device__ __forceinline__ void mc_add(float& m, float& c, float v) {
-    if (v > m) {
-        m = v;
-        c = 1.f;
-    } else if (v == m) {
-        c += 1.f;
-    }
-}
+// (max, count) fold of the candidates equal to the maximum (exact comparisons: any combine order gives the same pair);
+// selects, no branches
 __device__ __forceinline__ void mc_merge(float& m, float& c, float m2, float c2) {
-    if (m2 > m) {
-        m = m2;
-        c = c2;
-    } else if (m2 == m) {
-        c += c2;
-    }
+    const bool gt = m2 > m, eq = m2 == m;
+    c = gt ? c2 : (eq ? c + c2 : c);
+    m = gt ? m2 : m;
+}
+__device__ __forceinline__ void mc_add(float& m, float& c, float v) { mc_merge(m, c, v, 1.f); }
+
+// DPP moves inside a 16-lane row: quad_perm xor 1 (0xB1), xor 2 (0x4E), row_ror 4 (0x124), row_ror 8 (0x128); the four
+// steps combine disjoint groups, so every lane of the row ends with the whole row's reduction
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ void row_step(float& sum, float& m, float& c) {
+    sum += dpp<CTRL>(sum);
+    const float m2 = dpp<CTRL>(m), c2 = dpp<CTRL>(c);
+    mc_merge(m, c, m2, c2);
+}
+__device__ __forceinline__ void row16_reduce(float& sum, float& m, float& c) {
+    row_step<0xB1>(sum, m, c);
+    row_step<0x4E>(sum, m, c);
+    row_step<0x124>(sum, m, c);
+    row_step<0x128>(sum, m, c);
 }
 
-// per-wave partials of the pooled statistics in LDS: [wave][side][sum | max | count][D]
+// per-wave partials of the pooled statistics in LDS: [wave][side][sum | max | count][D]. Eight waves (two per SIMD:
+// one wave's LDS waits under the other's MFMAs; the forward needs < 256 registers), a strip per wave for L <= 128.
+constexpr int kFwdWaves = 8;
 template <int D>
-__global__ __launch_bounds__(kThreads) void esim_train_fwd_kernel(const float* __restrict__ q, const float* __restrict__ a,
+__global__ __launch_bounds__(kFwdWaves * 64) void esim_train_fwd_kernel(const float* __restrict__ q, const float* __restrict__ a,
                                                                   int L, int64_t ex_stride, int64_t ld, float* __restrict__ out,
                                                                   int64_t out_stride, int64_t out_off, float* __restrict__ aux) {
     constexpr int RS = Ex<D>::RS;
@@ -149,71 +176,52 @@ __global__ __launch_bounds__(kThreads) void esim_train_fwd_kernel(const float* _
     const int Lp = (L + 15) & ~15, NS = Lp / 16;
     float* qs = sm;
     float* as = qs + Lp * RS;
-    float* part = as + Lp * RS;  // [kWaves][2][3][D]
+    float* part = as + Lp * RS;  // [kFwdWaves][2][3][D]
     const int64_t e = blockIdx.x;
-    stage_qa<D>(q + e * ex_stride, a + e * ex_stride, ld, L, Lp, qs, as);
+    stage_qa<D, kFwdWaves * 64>(q + e * ex_stride, a + e * ex_stride, ld, L, Lp, qs, as);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
     // [wave][side][stat][D]: (sum, max, count) = (0, -inf, 0)
-    for (int t = threadIdx.x; t < kWaves * 6 * D; t += kThreads) part[t] = (t / D) % 3 == 1 ? -INFINITY : 0.f;
+    for (int t = threadIdx.x; t < kFwdWaves * 6 * D; t += kFwdWaves * 64) part[t] = (t / D) % 3 == 1 ? -INFINITY : 0.f;
     __syncthreads();
-    auto run = [&](auto nj) {
-        constexpr int NJ = decltype(nj)::value;
-        for (int s = wave; s < NS; s += kWaves) {
-            const int ibase = 16 * s, i = ibase + li;
-            f4v S[NJ], attq[D / 16], atta[D / 16];
-            strip_fwd<D, NJ>(qs, as, L, ibase, li, g, S, attq, atta);
+    for (int s = wave; s < NS; s += kFwdWaves) {
+        const int ibase = 16 * s, i = ibase + li;
+        f4v S[kMaxJ], attq[D / 16], atta[D / 16];
+        strip_fwd<D>(qs, as, L, NS, ibase, li, g, S, attq, atta);
 #pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                const float* xs = side ? as : qs;
+        for (int side = 0; side < 2; ++side) {
+            const float* xs = side ? as : qs;
 #pragma unroll
-                for (int ct = 0; ct < D / 16; ++ct) {
-                    const f4v xv = lds4(xs + i * RS + 16 * ct + 4 * g);
+            for (int ct = 0; ct < D / 16; ++ct) {
+                const f4v xv = lds4(xs + i * RS + 16 * ct + 4 * g);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float x = xv[r], at = side ? atta[ct][r] : attq[ct][r];
-                        float sum = 0.f, mx = -INFINITY, cnt = 0.f;
-                        if (i < L) {
-                            sum = 2.f * x + x * at;
-                            mc_add(mx, cnt, x);
-                            mc_add(mx, cnt, at);
-                            mc_add(mx, cnt, x - at);
-                            mc_add(mx, cnt, x * at);
-                        }
-#pragma unroll
-                        for (int o = 1; o < 16; o <<= 1) {
-                            sum += __shfl_xor(sum, o, 64);
-                            const float m2 = __shfl_xor(mx, o, 64), c2 = __shfl_xor(cnt, o, 64);
-                            mc_merge(mx, cnt, m2, c2);
-                        }
-                        if (li == 0) {
-                            float* p = part + ((wave * 2 + side) * 3) * D + 16 * ct + 4 * g + r;
-                            p[0] += sum;
-                            mc_merge(p[D], p[2 * D], mx, cnt);
-                        }
+                for (int r = 0; r < 4; ++r) {
+                    const float x = xv[r], at = side ? atta[ct][r] : attq[ct][r];
+                    const bool ok = i < L;
+                    float sum = ok ? 2.f * x + x * at : 0.f, mx = -INFINITY, cnt = 0.f;
+                    mc_add(mx, cnt, ok ? x : -INFINITY);
+                    mc_add(mx, cnt, ok ? at : -INFINITY);
+                    mc_add(mx, cnt, ok ? x - at : -INFINITY);
+                    mc_add(mx, cnt, ok ? x * at : -INFINITY);
+                    if (!ok) cnt = 0.f;
+                    row16_reduce(sum, mx, cnt);
+                    if (li == 0) {
+                        float* p = part + ((wave * 2 + side) * 3) * D + 16 * ct + 4 * g + r;
+                        p[0] += sum;
+                        mc_merge(p[D], p[2 * D], mx, cnt);
                     }
                 }
             }
         }
-    };
-    switch (NS) {
-        case 1: run(std::integral_constant<int, 1>{}); break;
-        case 2: run(std::integral_constant<int, 2>{}); break;
-        case 3: run(std::integral_constant<int, 3>{}); break;
-        case 4: run(std::integral_constant<int, 4>{}); break;
-        case 5: run(std::integral_constant<int, 5>{}); break;
-        case 6: run(std::integral_constant<int, 6>{}); break;
-        case 7: run(std::integral_constant<int, 7>{}); break;
-        default: run(std::integral_constant<int, 8>{}); break;
     }
     __syncthreads();
     // combine the waves in order; pooled = [avg_q, max_q, avg_a, max_a, avg_q - avg_a, max_q - max_a]
     const float inv = 1.0f / (float)(4 * L);
-    for (int c = threadIdx.x; c < D; c += kThreads) {
+    for (int c = threadIdx.x; c < D; c += kFwdWaves * 64) {
         float avg[2], mx[2], cn[2];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             float s = 0.f, m = -INFINITY, k = 0.f;
-            for (int w = 0; w < kWaves; ++w) {
+            for (int w = 0; w < kFwdWaves; ++w) {
                 const float* p = part + ((w * 2 + side) * 3) * D + c;
                 s += p[0];
                 mc_merge(m, k, p[D], p[2 * D]);
@@ -274,65 +282,64 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
     float* wsE = wsS + Lp * Lp;
     float* wsGq = wsE + Lp * Lp;
     float* wsGa = wsGq + D * Lp;
-    auto run = [&](auto nj) {
-        constexpr int NJ = decltype(nj)::value;
-        for (int s = wave; s < NS; s += kWaves) {
-            const int ibase = 16 * s, i = ibase + li;
-            f4v S[NJ], attq[D / 16], atta[D / 16];
-            strip_fwd<D, NJ>(qs, as, L, ibase, li, g, S, attq, atta);
-            // per 16-column tile of c: the pooled gradient's terms (G = d/d att, the direct d/d x), the direct terms
-            // stored at once, G^T to the workspace, and dS^T[j][i] += sum_c x[j][c] G^T[c][i] for x = q, a
-            // (A = x rows, k order c = 16 ct + 4 g + r); one tile's G / direct values live at a time
-            f4v dS[NJ];
+    for (int s = wave; s < NS; s += kWaves) {
+        const int ibase = 16 * s, i = ibase + li;
+        f4v S[kMaxJ], attq[D / 16], atta[D / 16];
+        strip_fwd<D>(qs, as, L, NS, ibase, li, g, S, attq, atta);
+        // per 16-column tile of c: the pooled gradient's terms (G = d/d att, the direct d/d x), the direct terms
+        // stored at once, G^T to the workspace, and dS^T[j][i] += sum_c x[j][c] G^T[c][i] for x = q, a
+        // (A = x rows, k order c = 16 ct + 4 g + r); one tile's G / direct values live at a time
+        f4v dS[kMaxJ];
 #pragma unroll
-            for (int jt = 0; jt < NJ; ++jt) dS[jt] = zero4();
+        for (int jt = 0; jt < kMaxJ; ++jt) dS[jt] = zero4();
 #pragma unroll
-            for (int ct = 0; ct < D / 16; ++ct) {
-                const f4v qv = lds4(qs + i * RS + 16 * ct + 4 * g), av = lds4(as + i * RS + 16 * ct + 4 * g);
-                f4v G[2], Dx[2];
+        for (int ct = 0; ct < D / 16; ++ct) {
+            const f4v qv = lds4(qs + i * RS + 16 * ct + 4 * g), av = lds4(as + i * RS + 16 * ct + 4 * g);
+            f4v G[2], Dx[2];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int c = 16 * ct + 4 * g + r;
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * ct + 4 * g + r;
 #pragma unroll
-                    for (int side = 0; side < 2; ++side) {
-                        const float x = side ? av[r] : qv[r], at = side ? atta[ct][r] : attq[ct][r];
-                        const float gavg = gc[3 * side * D + c], gmax = gc[(3 * side + 1) * D + c], M = gc[(3 * side + 2) * D + c];
-                        float gatt = 0.f, gx = 0.f;
-                        if (i < L) {
-                            const float dif = x - at, prd = x * at;
-                            // avg: sum(x) + sum(at) + sum(x - at) + sum(x at) over 4L rows
-                            gatt = x * gavg;
-                            gx = (2.f + at) * gavg;
-                            // max: an even share for every candidate equal to the maximum
-                            if (x == M) gx += gmax;
-                            if (at == M) gatt += gmax;
-                            if (dif == M) {
-                                gx += gmax;
-                                gatt -= gmax;
-                            }
-                            if (prd == M) {
-                                gx += gmax * at;
-                                gatt += gmax * x;
-                            }
+                for (int side = 0; side < 2; ++side) {
+                    const float x = side ? av[r] : qv[r], at = side ? atta[ct][r] : attq[ct][r];
+                    const float gavg = gc[3 * side * D + c], gmax = gc[(3 * side + 1) * D + c], M = gc[(3 * side + 2) * D + c];
+                    float gatt = 0.f, gx = 0.f;
+                    if (i < L) {
+                        const float dif = x - at, prd = x * at;
+                        // avg: sum(x) + sum(at) + sum(x - at) + sum(x at) over 4L rows
+                        gatt = x * gavg;
+                        gx = (2.f + at) * gavg;
+                        // max: an even share for every candidate equal to the maximum
+                        if (x == M) gx += gmax;
+                        if (at == M) gatt += gmax;
+                        if (dif == M) {
+                            gx += gmax;
+                            gatt -= gmax;
                         }
-                        G[side][r] = gatt;
-                        Dx[side][r] = gx;
+                        if (prd == M) {
+                            gx += gmax * at;
+                            gatt += gmax * x;
+                        }
                     }
+                    G[side][r] = gatt;
+                    Dx[side][r] = gx;
                 }
-                // direct terms of rows i < L (float4 over r: c = 16 ct + 4 g .. + 3); da gets the strip-local
-                // product added below by this same lane
-                if (i < L) {
-                    *reinterpret_cast<f4v*>(dq + e * g_ex + (int64_t)i * ldg + 16 * ct + 4 * g) = Dx[0];
-                    *reinterpret_cast<f4v*>(da + e * g_ex + (int64_t)i * ldg + 16 * ct + 4 * g) = Dx[1];
-                }
+            }
+            // direct terms of rows i < L (float4 over r: c = 16 ct + 4 g .. + 3); da gets the strip-local
+            // product added below by this same lane
+            if (i < L) {
+                *reinterpret_cast<f4v*>(dq + e * g_ex + (int64_t)i * ldg + 16 * ct + 4 * g) = Dx[0];
+                *reinterpret_cast<f4v*>(da + e * g_ex + (int64_t)i * ldg + 16 * ct + 4 * g) = Dx[1];
+            }
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int c = 16 * ct + 4 * g + r;
-                    wsGq[c * Lp + i] = G[0][r];
-                    wsGa[c * Lp + i] = G[1][r];
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * ct + 4 * g + r;
+                wsGq[c * Lp + i] = G[0][r];
+                wsGa[c * Lp + i] = G[1][r];
+            }
 #pragma unroll
-                for (int jt = 0; jt < NJ; ++jt) {
+            for (int jt = 0; jt < kMaxJ; ++jt) {
+                if (jt < NS) {
                     const f4v xq = lds4(qs + (16 * jt + li) * RS + 16 * ct + 4 * g);
                     const f4v xa = lds4(as + (16 * jt + li) * RS + 16 * ct + 4 * g);
 #pragma unroll
@@ -342,51 +349,45 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
                     }
                 }
             }
-            // softmax backward down each column i: dE = S (dS - sum_j S dS)
-            float t = 0.f;
+        }
+        // softmax backward down each column i: dE = S (dS - sum_j S dS)
+        float t = 0.f;
 #pragma unroll
-            for (int jt = 0; jt < NJ; ++jt)
+        for (int jt = 0; jt < kMaxJ; ++jt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) t += S[jt][r] * dS[jt][r];
-            t += __shfl_xor(t, 16, 64);
-            t += __shfl_xor(t, 32, 64);
+            for (int r = 0; r < 4; ++r) t += S[jt][r] * dS[jt][r];
+        t += __shfl_xor(t, 16, 64);
+        t += __shfl_xor(t, 32, 64);
 #pragma unroll
-            for (int jt = 0; jt < NJ; ++jt)
+        for (int jt = 0; jt < kMaxJ; ++jt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) dS[jt][r] = S[jt][r] * (dS[jt][r] - t);
-            // workspace: S^T[j][i], dE^T[j][i] (j = 16 jt + 4 g + r)
+            for (int r = 0; r < 4; ++r) dS[jt][r] = S[jt][r] * (dS[jt][r] - t);
+        // workspace: S^T[j][i], dE^T[j][i] (j = 16 jt + 4 g + r)
 #pragma unroll
-            for (int jt = 0; jt < NJ; ++jt)
+        for (int jt = 0; jt < kMaxJ; ++jt)
+            if (jt < NS) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int j = 16 * jt + 4 * g + r;
                     wsS[j * Lp + i] = S[jt][r];
                     wsE[j * Lp + i] = dS[jt][r];
                 }
-            // strip-local: da_i += sum_j dE^T[j][i] q_j  (da^T[c][i], A[c][j] = q[j][c])
+            }
+        // strip-local: da_i += sum_j dE^T[j][i] q_j  (da^T[c][i], A[c][j] = q[j][c])
 #pragma unroll
-            for (int ct = 0; ct < D / 16; ++ct) {
-                f4v acc = zero4();
+        for (int ct = 0; ct < D / 16; ++ct) {
+            f4v acc = zero4();
 #pragma unroll
-                for (int jt = 0; jt < NJ; ++jt)
+            for (int jt = 0; jt < kMaxJ; ++jt)
+                if (jt < NS) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc = mf(qs[(16 * jt + 4 * g + r) * RS + 16 * ct + li], dS[jt][r], acc);
-                if (i < L) {
-                    f4v* o = reinterpret_cast<f4v*>(da + e * g_ex + (int64_t)i * ldg + 16 * ct + 4 * g);
-                    *o = *o + acc;
                 }
+            if (i < L) {
+                f4v* o = reinterpret_cast<f4v*>(da + e * g_ex + (int64_t)i * ldg + 16 * ct + 4 * g);
+                *o = *o + acc;
             }
         }
-    };
-    switch (NS) {
-        case 1: run(std::integral_constant<int, 1>{}); break;
-        case 2: run(std::integral_constant<int, 2>{}); break;
-        case 3: run(std::integral_constant<int, 3>{}); break;
-        case 4: run(std::integral_constant<int, 4>{}); break;
-        case 5: run(std::integral_constant<int, 5>{}); break;
-        case 6: run(std::integral_constant<int, 6>{}); break;
-        case 7: run(std::integral_constant<int, 7>{}); break;
-        default: run(std::integral_constant<int, 8>{}); break;
     }
 }
 
@@ -480,16 +481,16 @@ extern "C" int rf_esim_train_fwd_f32(const float* q, const float* a, int32_t bat
     RF_REQUIRE(out_stride >= out_off + 6 * d, "rf_esim_train_fwd_f32: out row too short");
     if (batch == 0) return RF_OK;
     RF_REQUIRE(q && a && out && aux, "rf_esim_train_fwd_f32: null pointer");
-    const size_t lds = qa_lds_bytes(L, d) + (size_t)kWaves * 6 * d * sizeof(float);
+    const size_t lds = qa_lds_bytes(L, d) + (size_t)kFwdWaves * 6 * d * sizeof(float);
     hipStream_t st = rf_stream(stream);
     int rc;
     if (d == 64) {
         if ((rc = set_lds(esim_train_fwd_kernel<64>, lds))) return rc;
-        hipLaunchKernelGGL(esim_train_fwd_kernel<64>, dim3(batch), dim3(kThreads), lds, st, q, a, L, ex_stride, ld, out,
+        hipLaunchKernelGGL(esim_train_fwd_kernel<64>, dim3(batch), dim3(kFwdWaves * 64), lds, st, q, a, L, ex_stride, ld, out,
                            out_stride, out_off, aux);
     } else {
         if ((rc = set_lds(esim_train_fwd_kernel<128>, lds))) return rc;
-        hipLaunchKernelGGL(esim_train_fwd_kernel<128>, dim3(batch), dim3(kThreads), lds, st, q, a, L, ex_stride, ld, out,
+        hipLaunchKernelGGL(esim_train_fwd_kernel<128>, dim3(batch), dim3(kFwdWaves * 64), lds, st, q, a, L, ex_stride, ld, out,
                            out_stride, out_off, aux);
     }
     return rf_check_launch("esim_train_fwd_kernel");

@@ -59,8 +59,13 @@ class TrainableEsim:
                                      device=device)
         k = self.output_mlp.out_features
         lim = math.sqrt(6.0 / (k + 2))
-        self.W_out = ((torch.rand((2, k), generator=g) * 2 - 1) * lim).to(device).contiguous()  # [out][in]
-        self.b_out = torch.zeros(2, device=device)
+        # Dense(2, softmax): the parameters W_out [2][k], b_out [2] are the first rows of zero-padded [4][k] / [4] buffers
+        # (rf_gemm_f32 takes K and leading dimensions in multiples of 4; the padded logits are never read, their
+        # gradients stay zero)
+        self._W4 = torch.zeros((4, k), device=device)
+        self._b4 = torch.zeros(4, device=device)
+        self._W4[:2] = ((torch.rand((2, k), generator=g) * 2 - 1) * lim).to(device)
+        self.W_out, self.b_out = self._W4[:2], self._b4[:2]
         self.sparse_opt = SparseAdam(self.enc.table, learning_rate=learning_rate, deferred=True)
         self.dense_opt = KerasAdam(self.dense_parameters(), learning_rate=learning_rate)
         self.steps = 0
@@ -99,7 +104,7 @@ class TrainableEsim:
             L.call("rf_dropout_fwd", L.ptr(pooled), B, self.pooled_width, pooled.stride(0), rate, self.pooled_dropout_seed(step),
                    L.ptr(xd), xd.stride(0), st)
         h = self.output_mlp.forward(xd, step, training=training)
-        z = GM.gemm_f32(h, self.W_out, trans_b=True, bias=self.b_out, stream=st)
+        z = GM.gemm_f32(h, self._W4, trans_b=True, bias=self._b4, stream=st)  # [B, 4]: logits in columns 0, 1
         return z, (batch, x, pooled, aux, h, rate, step)
 
     def predict(self, batch: SparseBatch, dense: torch.Tensor) -> torch.Tensor:
@@ -107,7 +112,7 @@ class TrainableEsim:
         self.sparse_opt.materialize()
         z, _ = self.forward(batch, dense, training=False)
         B = z.shape[0]
-        prob = torch.empty_like(z)
+        prob = torch.empty((B, 2), device=z.device)
         ws = self._buf("loss", int(L.load().rf_loss_ws_bytes(B)), z.device)
         loss = torch.empty(1, device=z.device)
         lab = torch.zeros(B, dtype=torch.int32, device=z.device)
@@ -126,20 +131,20 @@ class TrainableEsim:
         B, dev = z.shape[0], z.device
         lab = labels.to(device=dev, dtype=torch.int32).contiguous()
         loss = torch.empty(1, device=dev)
-        prob = torch.empty_like(z)
-        dz = torch.empty_like(z)
+        prob = torch.empty((B, 2), device=dev)
+        dz = torch.zeros_like(z)  # [B, 4]: columns 2, 3 stay zero
         ws = self._buf("loss", int(lib.rf_loss_ws_bytes(B)), dev)
         L.call("rf_softmax_ce_loss", L.ptr(z), z.stride(0), L.ptr(lab), B, 2, L.ptr(loss), L.ptr(prob), prob.stride(0),
                L.ptr(dz), dz.stride(0), L.ptr(ws), ws.numel(), st)
-        # head: dW_o = dz^T h, db_o = column sums of dz, dh = dz W_o
-        self.W_out.grad = GM.gemm_f32(dz, h, trans_a=True, stream=st)
-        db = torch.empty(2, device=dev)
+        # head: dW_o = dz^T h, db_o = column sums of dz, dh = dz W_o (on the padded [B, 4] / [4, k] operands)
+        self.W_out.grad = GM.gemm_f32(dz, h, trans_a=True, stream=st)[:2]
+        db = torch.empty(4, device=dev)
         dzc = torch.empty_like(dz)
-        wst = self._buf("tower", int(lib.rf_tower_ws_bytes(B, 2)), dev)
-        L.call("rf_act_dropout_bwd", L.ptr(dz), dz.stride(0), L.ptr(dz), dz.stride(0), B, 2, L.ACT["none"], 0.0, 0, L.ptr(dzc),
+        wst = self._buf("tower", int(lib.rf_tower_ws_bytes(B, 4)), dev)
+        L.call("rf_act_dropout_bwd", L.ptr(dz), dz.stride(0), L.ptr(dz), dz.stride(0), B, 4, L.ACT["none"], 0.0, 0, L.ptr(dzc),
                dzc.stride(0), L.ptr(db), L.ptr(wst), wst.numel(), st)
-        self.b_out.grad = db
-        dh = GM.gemm_f32(dz, self.W_out, stream=st)
+        self.b_out.grad = db[:2]
+        dh = GM.gemm_f32(dz, self._W4, stream=st)
         dxd = self.output_mlp.backward(dh)
         dpooled = dxd
         if rate > 0:

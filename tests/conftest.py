@@ -28,6 +28,14 @@ def pytest_sessionstart(session):
     faulthandler.enable(file=_FAULT_FILE, all_threads=True)
 
 
+def pytest_unconfigure(config):
+    global _FAULT_FILE
+    if _FAULT_FILE is not None:
+        faulthandler.disable()
+        _FAULT_FILE.close()
+        _FAULT_FILE = None
+
+
 def pytest_runtest_logstart(nodeid, location):
     # one unbuffered line per test on stderr: a crash record names the test it happened in
     os.write(2, f"RUN {nodeid}\n".encode())
