@@ -47,9 +47,18 @@ __device__ __forceinline__ void unpack16(const uint4& v, float* f) {
 template <typename OT, int EPV>
 __device__ __forceinline__ void store_chunk(OT* dst, const float* f) {
     if constexpr (sizeof(OT) == 4) {
+        // fp32 pooled rows stream out with nontemporal stores: the 480 MB of cfg2 output per launch then does not
+        // evict the tables' Zipf-hot rows from L2 / MALL (same-box A/B, profiles/r06/headline_nt_store_ab.txt:
+        // 0.2559 -> 0.2534 ms). RF_TEMPORAL_OUT=1 at build time restores plain stores.
 #pragma unroll
-        for (int i = 0; i < EPV; i += 4)
+        for (int i = 0; i < EPV; i += 4) {
+#ifdef RF_TEMPORAL_OUT
             *reinterpret_cast<float4*>(dst + i) = make_float4(f[i], f[i + 1], f[i + 2], f[i + 3]);
+#else
+            typedef float f4nt __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(f4nt{f[i], f[i + 1], f[i + 2], f[i + 3]}, reinterpret_cast<f4nt*>(dst + i));
+#endif
+        }
     } else {
         uint32_t w[EPV / 2];
 #pragma unroll
