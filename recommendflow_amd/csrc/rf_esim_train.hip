@@ -374,8 +374,11 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
                 }
             }
         // strip-local: da_i += sum_j dE^T[j][i] q_j  (da^T[c][i], A[c][j] = q[j][c])
+        f4v* drow = reinterpret_cast<f4v*>(da + e * g_ex + (int64_t)(i < L ? i : 0) * ldg + 4 * g);
 #pragma unroll
         for (int ct = 0; ct < D / 16; ++ct) {
+            // the tile's direct terms, loaded before its 28 MFMAs (the load latency hides under the chain)
+            const f4v p0 = i < L ? drow[4 * ct] : zero4();
             f4v acc = zero4();
 #pragma unroll
             for (int jt = 0; jt < kMaxJ; ++jt)
@@ -383,73 +386,85 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc = mf(qs[(16 * jt + 4 * g + r) * RS + 16 * ct + li], dS[jt][r], acc);
                 }
-            if (i < L) {
-                f4v* o = reinterpret_cast<f4v*>(da + e * g_ex + (int64_t)i * ldg + 16 * ct + 4 * g);
-                *o = *o + acc;
-            }
+            if (i < L) drow[4 * ct] = p0 + acc;
         }
     }
 }
 
 // ---- backward, stage 2: dq_j += sum_i S_ij G_q,i + dE_ij a_i, da_j += sum_i S_ij G_a,i ---------------------------
-// D[j][c] tiles: A[j][i] = S^T / dE^T rows (float4 over i = 16 it + 4 g + s), B[i][c] = G^T[c][i] (float4) and a[i][c]
-// (LDS); a wave per 16-row tile of j
+// D[j][c] tiles: A[j][i] = S^T / dE^T rows (float4 over i = 16 it + 4 g + s, from the workspace, one tile ahead),
+// B[i][c] = G^T[c][i] and a[i][c] from LDS. The columns run in two halves: a half's G_q^T, G_a^T and a are staged in
+// LDS once and read by every j tile (the round-one kernel read G^T from L2 once per j tile: 72 % of its wave cycles
+// waited on those loads). Eight waves, a j tile each (7 at L = 100).
+constexpr int kBwd2Waves = 8;
 template <int D>
-__global__ __launch_bounds__(kThreads) void esim_train_bwd2_kernel(const float* __restrict__ a, int L, int64_t ex_stride,
-                                                                   int64_t ld, const float* __restrict__ ws,
-                                                                   float* __restrict__ dq, float* __restrict__ da, int64_t g_ex,
-                                                                   int64_t ldg) {
-    constexpr int RS = Ex<D>::RS;
+__global__ __launch_bounds__(kBwd2Waves * 64) void esim_train_bwd2_kernel(const float* __restrict__ a, int L, int64_t ex_stride,
+                                                                          int64_t ld, const float* __restrict__ ws,
+                                                                          float* __restrict__ dq, float* __restrict__ da,
+                                                                          int64_t g_ex, int64_t ldg) {
+    constexpr int H = D / 2, NT = kBwd2Waves * 64, HS = H + 4;
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int Lp = (L + 15) & ~15, NS = Lp / 16;
-    float* as = sm;
+    const int Lp = (L + 15) & ~15, NS = Lp / 16, GS = Lp + 4;  // G^T row stride in LDS
+    float* gq = sm;             // [H][GS]
+    float* ga = gq + H * GS;    // [H][GS]
+    float* as = ga + H * GS;    // [Lp][HS]
     const int64_t e = blockIdx.x;
-    {
-        constexpr int C4 = D / 4;
-        const float* ae = a + e * ex_stride;
-        for (int t = threadIdx.x; t < Lp * C4; t += kThreads) {
-            const int r = t / C4, c4 = t - r * C4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < L) v = *reinterpret_cast<const float4*>(ae + (int64_t)r * ld + 4 * c4);
-            *reinterpret_cast<float4*>(as + r * RS + 4 * c4) = v;
-        }
-    }
-    __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
     const float* wsS = ws + e * (int64_t)(2 * Lp * Lp + 2 * D * Lp);
     const float* wsE = wsS + Lp * Lp;
     const float* wsGq = wsE + Lp * Lp;
     const float* wsGa = wsGq + D * Lp;
-    for (int jt = wave; jt < NS; jt += kWaves) {
-        f4v accq[D / 16], acca[D / 16];
-#pragma unroll
-        for (int ct = 0; ct < D / 16; ++ct) accq[ct] = acca[ct] = zero4();
-        for (int it = 0; it < NS; ++it) {
-            const f4v sS = lds4(wsS + (16 * jt + li) * Lp + 16 * it + 4 * g);
-            const f4v sE = lds4(wsE + (16 * jt + li) * Lp + 16 * it + 4 * g);
-#pragma unroll
-            for (int ct = 0; ct < D / 16; ++ct) {
-                const f4v bq = lds4(wsGq + (16 * ct + li) * Lp + 16 * it + 4 * g);
-                const f4v ba = lds4(wsGa + (16 * ct + li) * Lp + 16 * it + 4 * g);
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    accq[ct] = mf(sS[s], bq[s], accq[ct]);
-                    accq[ct] = mf(sE[s], as[(16 * it + 4 * g + s) * RS + 16 * ct + li], accq[ct]);
-                    acca[ct] = mf(sS[s], ba[s], acca[ct]);
-                }
-            }
+    const float* ae = a + e * ex_stride;
+    for (int half = 0; half < 2; ++half) {
+        const int c0 = half * H;
+        if (half) __syncthreads();  // the first half's reads are done
+        for (int t = threadIdx.x; t < 2 * H * (Lp / 4); t += NT) {
+            const int side = t / (H * (Lp / 4)), rem = t - side * H * (Lp / 4), c = rem / (Lp / 4), i4 = rem - c * (Lp / 4);
+            const f4v v = lds4((side ? wsGa : wsGq) + (int64_t)(c0 + c) * Lp + 4 * i4);
+            *reinterpret_cast<f4v*>((side ? ga : gq) + c * GS + 4 * i4) = v;
         }
+        for (int t = threadIdx.x; t < Lp * (H / 4); t += NT) {
+            const int r = t / (H / 4), c4 = t - r * (H / 4);
+            f4v v = zero4();
+            if (r < L) v = lds4(ae + (int64_t)r * ld + c0 + 4 * c4);
+            *reinterpret_cast<f4v*>(as + r * HS + 4 * c4) = v;
+        }
+        __syncthreads();
+        for (int jt = wave; jt < NS; jt += kBwd2Waves) {
+            f4v accq[H / 16], acca[H / 16];
 #pragma unroll
-        for (int ct = 0; ct < D / 16; ++ct)
+            for (int ct = 0; ct < H / 16; ++ct) accq[ct] = acca[ct] = zero4();
+            f4v nS = lds4(wsS + (16 * jt + li) * Lp + 4 * g), nE = lds4(wsE + (16 * jt + li) * Lp + 4 * g);
+            for (int it = 0; it < NS; ++it) {
+                const f4v sS = nS, sE = nE;
+                if (it + 1 < NS) {
+                    nS = lds4(wsS + (16 * jt + li) * Lp + 16 * (it + 1) + 4 * g);
+                    nE = lds4(wsE + (16 * jt + li) * Lp + 16 * (it + 1) + 4 * g);
+                }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int j = 16 * jt + 4 * g + r;
-                if (j < L) {
-                    const int64_t o = e * g_ex + (int64_t)j * ldg + 16 * ct + li;
-                    dq[o] += accq[ct][r];
-                    da[o] += acca[ct][r];
+                for (int ct = 0; ct < H / 16; ++ct) {
+                    const f4v bq = lds4(gq + (16 * ct + li) * GS + 16 * it + 4 * g);
+                    const f4v ba = lds4(ga + (16 * ct + li) * GS + 16 * it + 4 * g);
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        accq[ct] = mf(sS[s], bq[s], accq[ct]);
+                        accq[ct] = mf(sE[s], as[(16 * it + 4 * g + s) * HS + 16 * ct + li], accq[ct]);
+                        acca[ct] = mf(sS[s], ba[s], acca[ct]);
+                    }
                 }
             }
+#pragma unroll
+            for (int ct = 0; ct < H / 16; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 * jt + 4 * g + r;
+                    if (j < L) {
+                        const int64_t o = e * g_ex + (int64_t)j * ldg + c0 + 16 * ct + li;
+                        dq[o] += accq[ct][r];
+                        da[o] += acca[ct][r];
+                    }
+                }
+        }
     }
 }
 
@@ -509,7 +524,9 @@ extern "C" int rf_esim_train_bwd_f32(const float* q, const float* a, int32_t bat
     RF_REQUIRE(((uintptr_t)dq & 15) == 0 && ((uintptr_t)da & 15) == 0 && ((uintptr_t)ws & 15) == 0,
                "rf_esim_train_bwd_f32: dq / da / ws must be 16-byte aligned");
     RF_REQUIRE(ws_bytes >= rf_esim_train_ws_bytes(batch, L, d), "rf_esim_train_bwd_f32: workspace too small");
-    const size_t lds1 = qa_lds_bytes(L, d) + (size_t)6 * d * sizeof(float), lds2 = qa_lds_bytes(L, d) / 2;
+    const size_t Lp = (size_t)((L + 15) & ~15);
+    const size_t lds1 = qa_lds_bytes(L, d) + (size_t)6 * d * sizeof(float),
+                 lds2 = ((size_t)d * (Lp + 4) + Lp * (d / 2 + 4)) * sizeof(float);
     hipStream_t st = rf_stream(stream);
     float* w = static_cast<float*>(ws);
     int rc;
@@ -518,14 +535,14 @@ extern "C" int rf_esim_train_bwd_f32(const float* q, const float* a, int32_t bat
         hipLaunchKernelGGL(esim_train_bwd1_kernel<64>, dim3(batch), dim3(kThreads), lds1, st, q, a, L, ex_stride, ld, pooled,
                            p_stride, p_off, dpooled, dp_stride, dp_off, aux, dq, da, g_ex_stride, ldg, w);
         if ((rc = set_lds(esim_train_bwd2_kernel<64>, lds2))) return rc;
-        hipLaunchKernelGGL(esim_train_bwd2_kernel<64>, dim3(batch), dim3(kThreads), lds2, st, a, L, ex_stride, ld,
+        hipLaunchKernelGGL(esim_train_bwd2_kernel<64>, dim3(batch), dim3(kBwd2Waves * 64), lds2, st, a, L, ex_stride, ld,
                            (const float*)w, dq, da, g_ex_stride, ldg);
     } else {
         if ((rc = set_lds(esim_train_bwd1_kernel<128>, lds1))) return rc;
         hipLaunchKernelGGL(esim_train_bwd1_kernel<128>, dim3(batch), dim3(kThreads), lds1, st, q, a, L, ex_stride, ld, pooled,
                            p_stride, p_off, dpooled, dp_stride, dp_off, aux, dq, da, g_ex_stride, ldg, w);
         if ((rc = set_lds(esim_train_bwd2_kernel<128>, lds2))) return rc;
-        hipLaunchKernelGGL(esim_train_bwd2_kernel<128>, dim3(batch), dim3(kThreads), lds2, st, a, L, ex_stride, ld,
+        hipLaunchKernelGGL(esim_train_bwd2_kernel<128>, dim3(batch), dim3(kBwd2Waves * 64), lds2, st, a, L, ex_stride, ld,
                            (const float*)w, dq, da, g_ex_stride, ldg);
     }
     return rf_check_launch("esim_train_bwd_kernels");
