@@ -12,8 +12,11 @@
 namespace rf {
 
 
+// waves per workgroup (each wave walks its own items): 4 measured 0.7-1.1 % faster than 1 on the cfg2 headline (the
+// same 12 waves per CU, a quarter of the workgroups to dispatch); 8 and 16 slower (LDS per workgroup)
+// (profiles/r06/headline_waves_per_wg_ab.txt)
 #ifndef RF_FUSED_WAVES
-#define RF_FUSED_WAVES 1
+#define RF_FUSED_WAVES 4
 #endif
 // waves per workgroup: items are wave-independent, and one-wave workgroups release their slots as soon
 // as their own item is done (a 4-wave workgroup holds its slots until the slowest of 4 items ends)
