@@ -121,7 +121,7 @@ class TrainableEsim:
         return prob
 
     def loss_and_grads(self, batch: SparseBatch, dense: torch.Tensor, labels: torch.Tensor, step: Optional[int] = None,
-                       training: bool = True, plan=None):
+                       training: bool = True, plan=None, loss_scale: float = 1.0):
         """Forward + backward without the optimizer: (loss, prob); dense parameters get .grad, the table's sparse
         gradient lands in self.enc.grad, the fused encoder output's gradient in self.dout. plan: the batch's
         backward plan when the caller made it already (step())."""
@@ -136,6 +136,8 @@ class TrainableEsim:
         ws = self._buf("loss", int(lib.rf_loss_ws_bytes(B)), dev)
         L.call("rf_softmax_ce_loss", L.ptr(z), z.stride(0), L.ptr(lab), B, 2, L.ptr(loss), L.ptr(prob), prob.stride(0),
                L.ptr(dz), dz.stride(0), L.ptr(ws), ws.numel(), st)
+        if loss_scale != 1.0:  # data parallel: the global loss is the mean over the replicas
+            dz.mul_(loss_scale)
         # head: dW_o = dz^T h, db_o = column sums of dz, dh = dz W_o (on the padded [B, 4] / [4, k] operands)
         self.W_out.grad = GM.gemm_f32(dz, h, trans_a=True, stream=st)[:2]
         db = torch.empty(4, device=dev)
@@ -163,13 +165,21 @@ class TrainableEsim:
         self.enc.grad = self.enc.backward(batch, dout, out=x) if plan is None else self.enc.backward_reduce(plan, dout, out=x)
         return loss, prob
 
-    def step(self, batch: SparseBatch, dense: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        """One training step (model.fit's train_step): forward, backward, Adam on the table and the dense parameters."""
+    def step(self, batch: SparseBatch, dense: torch.Tensor, labels: torch.Tensor, dp=None) -> torch.Tensor:
+        """One training step (model.fit's train_step): forward, backward, Adam on the table and the dense parameters.
+        `dp` (runtime.dist.DataParallel) = MirroredStrategy-style replicas, as TrainableDssm.step: the loss scaled by
+        1/P, dense gradients SUM-all-reduced in buckets, the table's sparse gradients all-gathered and summed in rank
+        order before the (identical) optimizer steps."""
         plan = self.enc.backward_plan(batch)
         self.sparse_opt.prepare(plan.rows, plan.n_uniq, plan.cap)  # the batch's rows current before the forward
         self.dense_opt.zero_grad(set_to_none=True)
-        loss, _ = self.loss_and_grads(batch, dense, labels, plan=plan)
-        self.sparse_opt.apply(self.enc.grad)
+        scale = dp.loss_scale() if dp is not None else 1.0
+        loss, _ = self.loss_and_grads(batch, dense, labels, plan=plan, loss_scale=scale)
+        sg = self.enc.grad
+        if dp is not None:
+            dp.allreduce_dense(self.dense_parameters())
+            sg = dp.allgather_sparse(sg, self.enc.table_rows)
+        self.sparse_opt.apply(sg)
         self.dense_opt.step()
         self.steps += 1
         return loss

@@ -145,7 +145,7 @@ def test_softmax_ce_loss(cuda):
     assert np.isnan(loss.item()) and torch.isnan(dz[3]).all() and not torch.isnan(dz[4]).any()
 
 
-def _esim_model(L_=8, dim=32, B=64, n_dense=16, rate=0.3, seed=0):
+def _esim_model(L_=8, dim=32, B=64, n_dense=16, rate=0.3, seed=0, multi=False):
     from recommendflow_amd.backend.encoder.sparse_encoder import SlotSpec
     from recommendflow_amd.models.ranking.esim_train import TrainableEsim
     from recommendflow_amd.runtime.batch import synthetic_batch
@@ -153,7 +153,8 @@ def _esim_model(L_=8, dim=32, B=64, n_dense=16, rate=0.3, seed=0):
     user = [SlotSpec(f"q{i}", 1000, (7, 8)) for i in range(L_)]
     ad = [SlotSpec(f"k{i}", 1000, (7, 8)) for i in range(L_)]
     m = TrainableEsim(user, ad, n_dense, dim=dim, input_units=(32, 48), output_units=(64, 32), dropout=rate, seed=seed)
-    batch = synthetic_batch(B, [False] * (2 * L_), seed=seed + 3, slot_ids=range(400, 400 + 2 * L_)).to("cuda")
+    batch = synthetic_batch(B, [multi and i % 3 == 0 for i in range(2 * L_)], seed=seed + 3,
+                            slot_ids=range(400, 400 + 2 * L_)).to("cuda")
     g = torch.Generator().manual_seed(seed + 9)
     dense = torch.randn((B, n_dense), generator=g).cuda()
     labels = torch.randint(0, 2, (B,), generator=g).cuda()
@@ -166,11 +167,12 @@ def _oracle_layers(mlp):
             for i in range(len(mlp.units))]
 
 
-@pytest.mark.parametrize("rate", [0.0, 0.3])
-def test_trainable_esim_grads_vs_oracle(cuda, rate):
+@pytest.mark.parametrize("rate,multi", [(0.0, False), (0.3, False), (0.3, True)])
+def test_trainable_esim_grads_vs_oracle(cuda, rate, multi):
     """The whole training graph: loss, every dense gradient and the fused encoder output's gradient (dq, da) vs
-    oracle.esim_train_loss on the GPU encoder's q, a (the encoder itself is bit-exact, tests/test_embed_gpu.py)."""
-    m, batch, dense, labels = _esim_model(rate=rate)
+    oracle.esim_train_loss on the GPU encoder's q, a (the encoder itself is bit-exact, tests/test_embed_gpu.py);
+    multi: every third slot multi-valued (its token sequence sum-pooled into the slot's row)."""
+    m, batch, dense, labels = _esim_model(rate=rate, multi=multi)
     step = 4
     loss, prob = m.loss_and_grads(batch, dense, labels, step=step)
     x = m.enc(batch).cpu().double().numpy()
@@ -202,3 +204,32 @@ def test_trainable_esim_steps_reduce_the_loss(cuda):
     assert losses[-1] < 0.7 * losses[0], losses
     p = m.predict(batch, dense)
     assert torch.allclose(p.sum(1), torch.ones(128, device="cuda"), atol=1e-6)
+
+
+def test_trainable_esim_data_parallel_world1_matches_single(cuda):
+    """TrainableEsim.step(dp=DataParallel) over RCCL with one rank (the bucketed dense all-reduce and the rank-ordered
+    sparse all-gather are identities at P = 1): three steps give bit-identical tables and dense parameters."""
+    import socket
+
+    import torch.distributed as dist
+
+    from recommendflow_amd.runtime.dist import DataParallel
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        dp = DataParallel(bucket_bytes=1 << 16)
+        (m0, batch, dense, labels), (m1, _, _, _) = _esim_model(rate=0.3), _esim_model(rate=0.3)
+        for _ in range(3):
+            m0.step(batch, dense, labels)
+            m1.step(batch, dense, labels, dp=dp)
+        torch.cuda.synchronize()
+        m0.sparse_opt.materialize()
+        m1.sparse_opt.materialize()
+        assert torch.equal(m0.enc.table, m1.enc.table)
+        for a, b in zip(m0.dense_parameters(), m1.dense_parameters()):
+            assert torch.equal(a, b)
+    finally:
+        dist.destroy_process_group()
