@@ -489,6 +489,18 @@ int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nranks, int32_t 
 int rf_route_hash_finish(int64_t n, int32_t nranks, int64_t table_rows, int64_t n_uniq, int64_t* local_out,
                          int32_t* row_map, void* ws, size_t ws_bytes, void* stream);
 /*
+ * rf_hash_rows fused into rf_route_hash_build: the requests are the two hashed rows of every token (j = 2 t + k, the
+ * rows rf_hash_rows would write) followed by the n_tail rows of `tail` (j = 2 n_tok + i: the slots' padding rows),
+ * hashed and inserted in one launch, with no [2 n_tok] request list in HBM. The same table, counts, row_map and
+ * workspace as rf_route_hash_build over that list (n = 2 n_tok + n_tail); rf_route_hash_finish follows unchanged.
+ * Replaces rf_hash_rows + rf_route_hash_build in the row-sharded lookup (new capability: the reference mirrors every
+ * table, gpu_utils.py:13-14). The hashing is rf_hash_rows' (preprocess_layers.py:86-97).
+ */
+int rf_route_hash_build_tokens(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                               const int32_t* tok_off, const int32_t* bag_off, int32_t batch, int64_t n_tok,
+                               const int64_t* tail, int32_t n_tail, int32_t nranks, int32_t rank, int64_t table_rows,
+                               int32_t* row_map, int32_t* counts, void* ws, size_t ws_bytes, void* stream);
+/*
  * Owner-side partial pooling, the alternative exchange of the sharded lookup (SURVEY §8e "pool partial sums at
  * the owner"; deviation D-partial-pool-order: sum / avg add the owners' partials in owner order, exact at P = 1).
  * rf_pp_plan (requester): rows = rf_hash_rows + the 2*n_slots pad rows; for every unit u = 2*(b*n_slots + s) + k

@@ -134,6 +134,20 @@ class GpuShardOps:
                ws_bytes, L.stream_ptr(None))
         return counts, (n, nranks, table_rows, row_map, ws, ws_bytes)
 
+    def route_hash_build_tokens(self, desc, n_slots: int, batch: SparseBatch, tail: torch.Tensor, nranks: int,
+                                rank: int, table_rows: int):
+        """rf_route_hash_build_tokens: hash_rows(batch, tail) + route_hash_build in one launch (no request list in
+        HBM) -> (counts, state, n requests)."""
+        n = 2 * batch.n_tokens + tail.numel()
+        counts = torch.empty(nranks, dtype=torch.int32, device=self.device)
+        row_map = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+        ws_bytes = int(L.load().rf_route_hash_ws_bytes(n, nranks, table_rows))
+        ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=self.device)
+        L.call("rf_route_hash_build_tokens", L.ptr(desc), n_slots, L.ptr(batch.tok_bytes), L.ptr(batch.tok_off),
+               L.ptr(batch.bag_off), batch.batch, batch.n_tokens, L.ptr(tail), tail.numel(), nranks, rank, table_rows,
+               L.ptr(row_map), L.ptr(counts), L.ptr(ws), ws_bytes, L.stream_ptr(None))
+        return counts, (n, nranks, table_rows, row_map, ws, ws_bytes), n
+
     def route_hash_finish(self, state, n_uniq: int):
         """rf_route_hash_finish -> (local int64 [n_uniq], row_map int32 [n])."""
         n, nranks, table_rows, row_map, ws, ws_bytes = state
@@ -436,8 +450,14 @@ class ShardedFusedEncoder(torch.nn.Module):
     def _route_hash(self, batch: SparseBatch, local_fast: bool, exchange: bool):
         """hash route: build (device counts) -> [counts all-to-all] -> ONE host read of send (+ receive) counts
         -> finish. local_fast: this rank's own rows stay out of the exchange (row_map bit 31)."""
-        req = self.ops.hash_rows(self.desc, len(self.slots), batch, tail=self.pad_rows)
-        counts, state = self.ops.route_hash_build(req, self.nranks, self.rank if local_fast else -1, self.table_rows)
+        rank = self.rank if local_fast else -1
+        if hasattr(self.ops, "route_hash_build_tokens"):  # the hash fused into the insert (GpuShardOps)
+            counts, state, n_req = self.ops.route_hash_build_tokens(self.desc, len(self.slots), batch, self.pad_rows,
+                                                                    self.nranks, rank, self.table_rows)
+        else:
+            req = self.ops.hash_rows(self.desc, len(self.slots), batch, tail=self.pad_rows)
+            counts, state = self.ops.route_hash_build(req, self.nranks, rank, self.table_rows)
+            n_req = req.numel()
         counts = counts.to(torch.int64)
         P = counts.numel()
         if exchange:
@@ -447,7 +467,7 @@ class ShardedFusedEncoder(torch.nn.Module):
         else:
             send, recv_l = [int(c) for c in counts.cpu().tolist()], None
         local, row_map = self.ops.route_hash_finish(state, sum(send))
-        return RouteState(send, local, row_map, int(local.numel()), req.numel()), recv_l
+        return RouteState(send, local, row_map, int(local.numel()), n_req), recv_l
 
     def route_exchange(self, batch: SparseBatch, local_fast: bool = False):
         """route() plus the all-to-all of the per-owner counts with ONE host synchronisation: the counts

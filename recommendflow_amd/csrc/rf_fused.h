@@ -259,8 +259,9 @@ __global__ __launch_bounds__(kWaves * 64, RF_FUSED_MIN_WAVES) void fused_hash_em
         const int ntok = __shfl(incl, 63, 64);
         // single-token items (Lmax = 1, every bag 0 or 1 token): phase 2 is one row pair per bag, so the
         // lean path below issues every team's loads up front instead of running the pooling pipeline
-        const bool lean = !no_lean && lm == 1 && comb != RF_COMB_NULL && !emit && !pregathered && !abl_nohash &&
-                          !abl_nopad && __all(len <= 1);
+        // (PRE too: the bucket then holds the row-mapped rows of the pre-gathered buffer or, bit 31, the local shard)
+        const bool lean = !no_lean && lm == 1 && comb != RF_COMB_NULL && !emit && !abl_nohash && !abl_nopad &&
+                          __all(len <= 1);
         wave_lds_sync();
 
         // ---- phase 1b: lane-per-token double hashing into the LDS bucket ----

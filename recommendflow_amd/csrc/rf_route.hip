@@ -182,32 +182,79 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t k, int log_cap) {
 // race on the CAS; its cost is the memory-side atomics, not load latency.)
 constexpr int kIlp = 4;
 
+// request j for logical row g: rank-local rows -> row_map (bit 31), others -> the key's table slot (inserted once)
+__device__ __forceinline__ void rh_insert_one(int64_t g, int64_t j, int P, int rank, int64_t lp, int64_t table_rows,
+                                              uint32_t* __restrict__ table, int log_cap, uint32_t* __restrict__ slot,
+                                              int32_t* __restrict__ row_map) {
+    const uint32_t mask = (1u << log_cap) - 1u;
+    const bool ok = g >= 0 && g < table_rows;
+    const uint32_t g32 = (uint32_t)g, p32 = (uint32_t)P;  // valid rows < 2^32: 32-bit division
+    const uint32_t gl = g32 / p32;
+    const int owner = ok ? (int)(g32 - gl * p32) : P - 1;
+    if (ok && owner == rank) {  // rank-local: read in place by the pooling, never routed
+        row_map[j] = (int32_t)(0x80000000u | gl);
+        slot[j] = kEmpty;
+        return;
+    }
+    const uint32_t key = ok ? (uint32_t)owner * (uint32_t)lp + gl : (uint32_t)((int64_t)P * lp);
+    uint32_t h = key_hash(key, log_cap);
+    while (true) {
+        uint32_t cur = table[h];
+        if (cur == kEmpty) cur = atomicCAS(table + h, kEmpty, key);
+        if (cur == kEmpty || cur == key) break;
+        h = (h + 1) & mask;
+    }
+    slot[j] = h;
+}
+
 __global__ __launch_bounds__(256) void rh_insert_kernel(const int64_t* __restrict__ rows, int64_t n, int P, int rank,
                                                         int64_t lp, int64_t table_rows, uint32_t* __restrict__ table,
                                                         int log_cap, uint32_t* __restrict__ slot,
                                                         int32_t* __restrict__ row_map) {
-    const uint32_t mask = (1u << log_cap) - 1u;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t g = rows[j];
-        const bool ok = g >= 0 && g < table_rows;
-        const uint32_t g32 = (uint32_t)g, p32 = (uint32_t)P;  // valid rows < 2^32: 32-bit division
-        const uint32_t gl = g32 / p32;
-        const int owner = ok ? (int)(g32 - gl * p32) : P - 1;
-        if (ok && owner == rank) {  // rank-local: read in place by the pooling, never routed
-            row_map[j] = (int32_t)(0x80000000u | gl);
-            slot[j] = kEmpty;
-            continue;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        rh_insert_one(rows[j], j, P, rank, lp, table_rows, table, log_cap, slot, row_map);
+}
+
+// rf_hash_rows fused into the insert (rf_route_hash_build_tokens): thread per token of a block's 256 units (its unit by
+// binary search over the bag offsets in LDS, as hash_rows_kernel), both hashes, both requests j = 2t, 2t + 1 inserted;
+// then the n_tail pre-hashed pad rows as requests 2 n_tok + i. The 16 bytes per token of the [2 n_tok] int64 request
+// list are neither written nor read back.
+constexpr int kTokUnits = 256;
+__global__ __launch_bounds__(kTokUnits) void rh_insert_tok_kernel(const rf_slot_desc* __restrict__ slots, int n_slots,
+                                                                  const uint8_t* __restrict__ tok_bytes,
+                                                                  const int32_t* __restrict__ tok_off,
+                                                                  const int32_t* __restrict__ bag_off, int64_t n_units,
+                                                                  const int64_t* __restrict__ tail, int n_tail, int64_t n_tok,
+                                                                  int P, int rank, int64_t lp, int64_t table_rows,
+                                                                  uint32_t* __restrict__ table, int log_cap,
+                                                                  uint32_t* __restrict__ slot, int32_t* __restrict__ row_map) {
+    __shared__ int32_t s_off[kTokUnits + 1];
+    for (int64_t u0 = (int64_t)blockIdx.x * kTokUnits; u0 < n_units; u0 += (int64_t)gridDim.x * kTokUnits) {
+        const int nu = (int)min<int64_t>(kTokUnits, n_units - u0);
+        __syncthreads();
+        for (int j = threadIdx.x; j <= nu; j += kTokUnits) s_off[j] = bag_off[u0 + j];
+        __syncthreads();
+        const int t0 = s_off[0], t1 = s_off[nu];
+        const uint32_t s_first = (uint32_t)(u0 % n_slots);
+        for (int t = t0 + (int)threadIdx.x; t < t1; t += kTokUnits) {
+            int lo = 0, hi = nu - 1;  // last unit j with s_off[j] <= t
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_off[mid] <= t) lo = mid; else hi = mid - 1;
+            }
+            const rf_slot_desc* sd = slots + (int)((s_first + (uint32_t)lo) % (uint32_t)n_slots);
+            const int b0 = tok_off[t], n = tok_off[t + 1] - b0;
+            uint64_t h0, h1;
+            siphash24x2_dev(sd->salt[0], sd->salt[1], tok_bytes + b0, n, h0, h1);
+            const BucketMod bm = bucket_mod_init(sd->num_bins, sd->mask_empty);
+            const int64_t g0 = sd->row_base[0] + bucket_from_hash(h0, n, bm);
+            const int64_t g1 = sd->row_base[1] + bucket_from_hash(h1, n, bm);
+            rh_insert_one(g0, 2 * (int64_t)t, P, rank, lp, table_rows, table, log_cap, slot, row_map);
+            rh_insert_one(g1, 2 * (int64_t)t + 1, P, rank, lp, table_rows, table, log_cap, slot, row_map);
         }
-        const uint32_t key = ok ? (uint32_t)owner * (uint32_t)lp + gl : (uint32_t)((int64_t)P * lp);
-        uint32_t h = key_hash(key, log_cap);
-        while (true) {
-            uint32_t cur = table[h];
-            if (cur == kEmpty) cur = atomicCAS(table + h, kEmpty, key);
-            if (cur == kEmpty || cur == key) break;
-            h = (h + 1) & mask;
-        }
-        slot[j] = h;
     }
+    for (int64_t i = (int64_t)blockIdx.x * kTokUnits + threadIdx.x; i < n_tail; i += (int64_t)gridDim.x * kTokUnits)
+        rh_insert_one(tail[i], 2 * n_tok + i, P, rank, lp, table_rows, table, log_cap, slot, row_map);
 }
 
 // Compaction of the table's live slots into (key, slot) pairs, in slot order, in three launches with no
@@ -619,30 +666,31 @@ extern "C" size_t rf_route_hash_ws_bytes(int64_t n, int32_t nranks, int64_t tabl
     return hash_layout(n, nranks, table_rows).total;
 }
 
-extern "C" int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nranks, int32_t rank, int64_t table_rows,
-                                   int32_t* row_map, int32_t* counts, void* ws, size_t ws_bytes, void* stream) {
-    RF_REQUIRE(nranks >= 1 && nranks <= 4096, "rf_route_hash_build: nranks must be in [1, 4096]");
-    RF_REQUIRE(rank >= -1 && rank < nranks, "rf_route_hash_build: rank must be -1 (no local rows) or in [0, nranks)");
-    RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 32) - 4096,
-               "rf_route_hash_build: table_rows must be in [1, 2^32 - 4096)");
-    RF_REQUIRE((table_rows + nranks - 1) / nranks < ((int64_t)1 << 31), "rf_route_hash_build: shard rows must be < 2^31");
-    RF_REQUIRE(n >= 0 && n < ((int64_t)1 << 30), "rf_route_hash_build: n must be in [0, 2^30)");
-    RF_REQUIRE(counts && ws, "rf_route_hash_build: null pointer");
+namespace {
+// the build after the insert launch (or, tokens form, the fused hash + insert): compaction of the table owner-major
+template <typename Insert>
+int route_hash_build_impl(const char* name, int64_t n, int32_t nranks, int32_t rank, int64_t table_rows, int32_t* row_map,
+                          int32_t* counts, void* ws, size_t ws_bytes, void* stream, Insert&& insert) {
+    RF_REQUIRE(nranks >= 1 && nranks <= 4096, "%s: nranks must be in [1, 4096]", name);
+    RF_REQUIRE(rank >= -1 && rank < nranks, "%s: rank must be -1 (no local rows) or in [0, nranks)", name);
+    RF_REQUIRE(table_rows >= 1 && table_rows < ((int64_t)1 << 32) - 4096, "%s: table_rows must be in [1, 2^32 - 4096)", name);
+    RF_REQUIRE((table_rows + nranks - 1) / nranks < ((int64_t)1 << 31), "%s: shard rows must be < 2^31", name);
+    RF_REQUIRE(n >= 0 && n < ((int64_t)1 << 30), "%s: n must be in [0, 2^30)", name);
+    RF_REQUIRE(counts && ws, "%s: null pointer", name);
     const HashLayout lay = hash_layout(n, nranks, table_rows);
-    RF_REQUIRE(ws_bytes >= lay.total, "rf_route_hash_build: workspace too small (%zu < %zu)", ws_bytes, lay.total);
+    RF_REQUIRE(ws_bytes >= lay.total, "%s: workspace too small (%zu < %zu)", name, ws_bytes, lay.total);
     hipStream_t st = rf_stream(stream);
     char* w = static_cast<char*>(ws);
     int32_t* cnt = reinterpret_cast<int32_t*>(w + lay.off_cnt);
     if (hipMemsetAsync(cnt, 0, sizeof(int32_t) * (nranks + 2), st) != hipSuccess)
-        return rf_set_error(RF_EHIP, "rf_route_hash_build: memset failed");
+        return rf_set_error(RF_EHIP, "%s: memset failed", name);
     if (n > 0) {
-        RF_REQUIRE(rows && row_map, "rf_route_hash_build: null pointer");
+        RF_REQUIRE(row_map, "%s: null pointer", name);
         auto* table = reinterpret_cast<uint32_t*>(w + lay.off_table);
         if (hipMemsetAsync(table, 0xff, (size_t)lay.cap * 4, st) != hipSuccess)
-            return rf_set_error(RF_EHIP, "rf_route_hash_build: memset failed");
+            return rf_set_error(RF_EHIP, "%s: memset failed", name);
         const int64_t lp = (table_rows + nranks - 1) / nranks;
-        hipLaunchKernelGGL(rh_insert_kernel, dim3(grid_of(n)), dim3(256), 0, st, rows, n, nranks, rank, lp, table_rows,
-                           table, lay.log_cap, reinterpret_cast<uint32_t*>(w + lay.off_slot), row_map);
+        insert(st, lp, table, lay.log_cap, reinterpret_cast<uint32_t*>(w + lay.off_slot));
         auto* blk = reinterpret_cast<int32_t*>(w + lay.off_blk);
         const dim3 gb((unsigned)lay.n_blk);
         auto* blk_own = reinterpret_cast<int32_t*>(w + lay.off_blk_own);
@@ -660,8 +708,40 @@ extern "C" int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nrank
         }
     }
     if (hipMemcpyAsync(counts, cnt, sizeof(int32_t) * nranks, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return rf_set_error(RF_EHIP, "rf_route_hash_build: copy failed");
-    return rf_check_launch("rf_route_hash_build");
+        return rf_set_error(RF_EHIP, "%s: copy failed", name);
+    return rf_check_launch(name);
+}
+}  // namespace
+
+extern "C" int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nranks, int32_t rank, int64_t table_rows,
+                                   int32_t* row_map, int32_t* counts, void* ws, size_t ws_bytes, void* stream) {
+    RF_REQUIRE(n == 0 || rows, "rf_route_hash_build: null pointer");
+    return route_hash_build_impl("rf_route_hash_build", n, nranks, rank, table_rows, row_map, counts, ws, ws_bytes, stream,
+                                 [&](hipStream_t st, int64_t lp, uint32_t* table, int log_cap, uint32_t* slot) {
+                                     hipLaunchKernelGGL(rh_insert_kernel, dim3(grid_of(n)), dim3(256), 0, st, rows, n, nranks,
+                                                        rank, lp, table_rows, table, log_cap, slot, row_map);
+                                 });
+}
+
+extern "C" int rf_route_hash_build_tokens(const rf_slot_desc* d_slots, int32_t n_slots, const uint8_t* tok_bytes,
+                                          const int32_t* tok_off, const int32_t* bag_off, int32_t batch, int64_t n_tok,
+                                          const int64_t* tail, int32_t n_tail, int32_t nranks, int32_t rank,
+                                          int64_t table_rows, int32_t* row_map, int32_t* counts, void* ws, size_t ws_bytes,
+                                          void* stream) {
+    RF_REQUIRE(n_slots >= 1 && batch >= 0 && n_tok >= 0 && n_tail >= 0,
+               "rf_route_hash_build_tokens: need n_slots >= 1, batch, n_tok, n_tail >= 0");
+    RF_REQUIRE(n_tok == 0 || (d_slots && tok_bytes && tok_off && bag_off), "rf_route_hash_build_tokens: null pointer");
+    RF_REQUIRE(n_tail == 0 || tail, "rf_route_hash_build_tokens: null tail");
+    const int64_t n_units = (int64_t)batch * n_slots;
+    const int64_t n = 2 * n_tok + n_tail;
+    return route_hash_build_impl(
+        "rf_route_hash_build_tokens", n, nranks, rank, table_rows, row_map, counts, ws, ws_bytes, stream,
+        [&](hipStream_t st, int64_t lp, uint32_t* table, int log_cap, uint32_t* slot) {
+            const int64_t g = std::max<int64_t>((n_units + kTokUnits - 1) / kTokUnits, (n_tail + kTokUnits - 1) / kTokUnits);
+            hipLaunchKernelGGL(rh_insert_tok_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 256 * 64))),
+                               dim3(kTokUnits), 0, st, d_slots, n_slots, tok_bytes, tok_off, bag_off, n_tok ? n_units : 0,
+                               tail, n_tail, n_tok, nranks, rank, lp, table_rows, table, log_cap, slot, row_map);
+        });
 }
 
 extern "C" int rf_route_hash_finish(int64_t n, int32_t nranks, int64_t table_rows, int64_t n_uniq, int64_t* local_out,

@@ -70,6 +70,8 @@ _SIGS = {
     "rf_route_hash_ws_bytes": (ctypes.c_size_t, [_i64, _i32, _i64]),
     "rf_route_hash_build": (ctypes.c_int, [_vp, _i64, _i32, _i32, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_route_hash_finish": (ctypes.c_int, [_i64, _i32, _i64, _i64, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "rf_route_hash_build_tokens": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _i32, _i32, _i32, _i64, _vp,
+                                                  _vp, _vp, ctypes.c_size_t, _vp]),
     "rf_embed_bwd_ws_bytes": (ctypes.c_size_t, [_i64, _i32, _i64]),
     "rf_fused_hash_embed_bwd": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64, _i32, _vp, _vp, _i64,
                                                _i32, _vp, _vp, _vp, _i64, _vp, _vp, ctypes.c_size_t, _vp]),

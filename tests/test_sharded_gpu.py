@@ -107,6 +107,10 @@ def test_route_hash_matches_oracle(O, cuda, P, rank, n):
         rows[7] = R + 11
     ops = GpuShardOps()
     c, state = ops.route_hash_build(torch.from_numpy(rows).cuda(), P, rank, R)
+    _check_route_hash(O, ops, rows, P, rank, R, c, state)
+
+
+def _check_route_hash(O, ops, rows, P, rank, R, c, state):
     wc, wl, wm = O.route_rows_local(rows, P, rank, R)
     np.testing.assert_array_equal(c.cpu().numpy(), wc)
     l, m = ops.route_hash_finish(state, int(wc.sum()))
@@ -126,6 +130,26 @@ def test_route_hash_matches_oracle(O, cuda, P, rank, n):
     loc = wm < 0  # rank-local rows: 0x80000000 | local, exact
     np.testing.assert_array_equal(m[loc], wm[loc])
     np.testing.assert_array_equal(l[m[~loc]], wl[wm[~loc]])
+
+
+@pytest.mark.parametrize("P", [1, 2, 8, 1000])
+@pytest.mark.parametrize("rank", [-1, 0])
+@pytest.mark.parametrize("B", [0, 1, 300])
+def test_route_hash_tokens_matches_oracle(O, cuda, P, rank, B):
+    """rf_route_hash_build_tokens (rf_hash_rows fused into the insert) == oracle.route_rows_local over the oracle's
+    hashed request list [2 n_tok token rows | the slots' pad rows]: the counts, the distinct rows per owner and every
+    request's row."""
+    sp = slots(30, seed=P + 1)
+    enc = FusedSparseEncoder(sp, 16, seed=1)
+    hb = synthetic_batch(B, [i % 3 == 0 for i in range(len(sp))], seed=P + B)
+    ops = GpuShardOps()
+    sh = ShardedFusedEncoder(sp, 16, 0, P, ops=ops, seed=1)
+    R = sh.table_rows
+    rows = np.concatenate([O.hash_rows(enc.host_desc, hb.tok_bytes, hb.tok_off, hb.bag_off, hb.batch).reshape(-1),
+                           sh.pad_rows.cpu().numpy()]).astype(np.int64)
+    c, state, n = ops.route_hash_build_tokens(enc.desc, len(sp), hb.to("cuda"), sh.pad_rows, P, rank, R)
+    assert n == rows.size
+    _check_route_hash(O, ops, rows, P, rank, R, c, state)
 
 
 @pytest.mark.parametrize("P", [1, 2, 4, 8])
