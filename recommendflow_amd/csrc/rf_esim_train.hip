@@ -65,9 +65,10 @@ __device__ __forceinline__ f4v lds4(const float* p) { return *reinterpret_cast<c
 // kernel holds one copy of its code (a copy per tile count put 140K lines of ISA in the forward and thrashed the
 // instruction cache)
 constexpr int kMaxJ = 8;
+// the scores half of strip_fwd: S^T [NJ] of strip ibase (X = E^T strip, softmax down j)
 template <int D>
-__device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int L, int NJ, int ibase, int li, int g,
-                                          f4v (&S)[kMaxJ], f4v (&attq)[D / 16], f4v (&atta)[D / 16]) {
+__device__ __forceinline__ void strip_scores(const float* qs, const float* as, int L, int NJ, int ibase, int li, int g,
+                                             f4v (&S)[kMaxJ]) {
     constexpr int RS = Ex<D>::RS;
     // X = E^T strip
     f4v ar[D / 16];
@@ -117,23 +118,33 @@ __device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int 
     for (int jt = 0; jt < kMaxJ; ++jt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) S[jt][r] = S[jt][r] / sum;
-    // att^T = x^T S^T for x = q, a (A[c][j] = x[j][c], k order j = 16 jt + 4 g + r)
+}
+
+// column tile ct of att^T = x^T S^T for x = q and a (A[c][j] = x[j][c], k order j = 16 jt + 4 g + r): two chains
+template <int D>
+__device__ __forceinline__ void att_tile(const float* qs, const float* as, int NJ, int ct, int li, int g,
+                                         const f4v (&S)[kMaxJ], f4v& aq, f4v& aa) {
+    constexpr int RS = Ex<D>::RS;
+    aq = zero4();
+    aa = zero4();
 #pragma unroll
-    for (int ct = 0; ct < D / 16; ++ct) {
-        f4v aq = zero4(), aa = zero4();
+    for (int jt = 0; jt < kMaxJ; ++jt)
+        if (jt < NJ) {
 #pragma unroll
-        for (int jt = 0; jt < kMaxJ; ++jt)
-            if (jt < NJ) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int j = 16 * jt + 4 * g + r;
-                    aq = mf(qs[j * RS + 16 * ct + li], S[jt][r], aq);
-                    aa = mf(as[j * RS + 16 * ct + li], S[jt][r], aa);
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int j = 16 * jt + 4 * g + r;
+                aq = mf(qs[j * RS + 16 * ct + li], S[jt][r], aq);
+                aa = mf(as[j * RS + 16 * ct + li], S[jt][r], aa);
             }
-        attq[ct] = aq;
-        atta[ct] = aa;
-    }
+        }
+}
+
+template <int D>
+__device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int L, int NJ, int ibase, int li, int g,
+                                          f4v (&S)[kMaxJ], f4v (&attq)[D / 16], f4v (&atta)[D / 16]) {
+    strip_scores<D>(qs, as, L, NJ, ibase, li, g, S);
+#pragma unroll
+    for (int ct = 0; ct < D / 16; ++ct) att_tile<D>(qs, as, NJ, ct, li, g, S, attq[ct], atta[ct]);
 }
 
 // (max, count) fold of the candidates equal to the maximum (exact comparisons: any combine order gives the same pair);
@@ -244,8 +255,15 @@ __global__ __launch_bounds__(kFwdWaves * 64) void esim_train_fwd_kernel(const fl
 
 // ---- backward, stage 1 -----------------------------------------------------------------------------------------
 // workspace per example: S^T [Lp][Lp] ([j][i]), dE^T [Lp][Lp], G_q^T [D][Lp] ([c][i]), G_a^T [D][Lp]
+// Eight waves (two per SIMD; the q / a images cap the kernel at one workgroup per CU), a strip each for L <= 128: the
+// attention output is produced one 16-column tile at a time inside the gradient loop, so a wave holds S^T, dS^T and
+// one tile of att instead of all of att (the four-wave form held att whole and ran one wave per SIMD)
+#ifndef RF_BWD1_WAVES
+#define RF_BWD1_WAVES 8
+#endif
+constexpr int kBwd1Waves = RF_BWD1_WAVES;
 template <int D>
-__global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* __restrict__ q, const float* __restrict__ a,
+__global__ __launch_bounds__(kBwd1Waves * 64) void esim_train_bwd1_kernel(const float* __restrict__ q, const float* __restrict__ a,
                                                                    int L, int64_t ex_stride, int64_t ld,
                                                                    const float* __restrict__ pooled, int64_t p_stride,
                                                                    int64_t p_off, const float* __restrict__ dpooled,
@@ -260,13 +278,13 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
     float* as = qs + Lp * RS;
     float* gc = as + Lp * RS;  // per column: gavg_q, gmax_q, M_q, gavg_a, gmax_a, M_a  [6][D]
     const int64_t e = blockIdx.x;
-    stage_qa<D>(q + e * ex_stride, a + e * ex_stride, ld, L, Lp, qs, as);
+    stage_qa<D, kBwd1Waves * 64>(q + e * ex_stride, a + e * ex_stride, ld, L, Lp, qs, as);
     {
         const float inv = 1.0f / (float)(4 * L);
         const float* dp = dpooled + e * dp_stride + dp_off;
         const float* pp = pooled + e * p_stride + p_off;
         const float* cn = aux + e * 2 * D;
-        for (int c = threadIdx.x; c < D; c += kThreads) {
+        for (int c = threadIdx.x; c < D; c += kBwd1Waves * 64) {
             const float d0 = dp[c], d1 = dp[D + c], d2 = dp[2 * D + c], d3 = dp[3 * D + c], d4 = dp[4 * D + c], d5 = dp[5 * D + c];
             gc[c] = (d0 + d4) * inv;
             gc[D + c] = (d1 + d5) / cn[c];
@@ -282,11 +300,11 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
     float* wsE = wsS + Lp * Lp;
     float* wsGq = wsE + Lp * Lp;
     float* wsGa = wsGq + D * Lp;
-    for (int s = wave; s < NS; s += kWaves) {
+    for (int s = wave; s < NS; s += kBwd1Waves) {
         const int ibase = 16 * s, i = ibase + li;
-        f4v S[kMaxJ], attq[D / 16], atta[D / 16];
-        strip_fwd<D>(qs, as, L, NS, ibase, li, g, S, attq, atta);
-        // per 16-column tile of c: the pooled gradient's terms (G = d/d att, the direct d/d x), the direct terms
+        f4v S[kMaxJ];
+        strip_scores<D>(qs, as, L, NS, ibase, li, g, S);
+        // per 16-column tile of c: the tile of att, the pooled gradient's terms (G = d/d att, the direct d/d x), the direct terms
         // stored at once, G^T to the workspace, and dS^T[j][i] += sum_c x[j][c] G^T[c][i] for x = q, a
         // (A = x rows, k order c = 16 ct + 4 g + r); one tile's G / direct values live at a time
         f4v dS[kMaxJ];
@@ -294,6 +312,8 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
         for (int jt = 0; jt < kMaxJ; ++jt) dS[jt] = zero4();
 #pragma unroll
         for (int ct = 0; ct < D / 16; ++ct) {
+            f4v attq, atta;
+            att_tile<D>(qs, as, NS, ct, li, g, S, attq, atta);
             const f4v qv = lds4(qs + i * RS + 16 * ct + 4 * g), av = lds4(as + i * RS + 16 * ct + 4 * g);
             f4v G[2], Dx[2];
 #pragma unroll
@@ -301,7 +321,7 @@ __global__ __launch_bounds__(kThreads) void esim_train_bwd1_kernel(const float* 
                 const int c = 16 * ct + 4 * g + r;
 #pragma unroll
                 for (int side = 0; side < 2; ++side) {
-                    const float x = side ? av[r] : qv[r], at = side ? atta[ct][r] : attq[ct][r];
+                    const float x = side ? av[r] : qv[r], at = side ? atta[r] : attq[r];
                     const float gavg = gc[3 * side * D + c], gmax = gc[(3 * side + 1) * D + c], M = gc[(3 * side + 2) * D + c];
                     float gatt = 0.f, gx = 0.f;
                     if (i < L) {
@@ -532,14 +552,14 @@ extern "C" int rf_esim_train_bwd_f32(const float* q, const float* a, int32_t bat
     int rc;
     if (d == 64) {
         if ((rc = set_lds(esim_train_bwd1_kernel<64>, lds1))) return rc;
-        hipLaunchKernelGGL(esim_train_bwd1_kernel<64>, dim3(batch), dim3(kThreads), lds1, st, q, a, L, ex_stride, ld, pooled,
+        hipLaunchKernelGGL(esim_train_bwd1_kernel<64>, dim3(batch), dim3(kBwd1Waves * 64), lds1, st, q, a, L, ex_stride, ld, pooled,
                            p_stride, p_off, dpooled, dp_stride, dp_off, aux, dq, da, g_ex_stride, ldg, w);
         if ((rc = set_lds(esim_train_bwd2_kernel<64>, lds2))) return rc;
         hipLaunchKernelGGL(esim_train_bwd2_kernel<64>, dim3(batch), dim3(kBwd2Waves * 64), lds2, st, a, L, ex_stride, ld,
                            (const float*)w, dq, da, g_ex_stride, ldg);
     } else {
         if ((rc = set_lds(esim_train_bwd1_kernel<128>, lds1))) return rc;
-        hipLaunchKernelGGL(esim_train_bwd1_kernel<128>, dim3(batch), dim3(kThreads), lds1, st, q, a, L, ex_stride, ld, pooled,
+        hipLaunchKernelGGL(esim_train_bwd1_kernel<128>, dim3(batch), dim3(kBwd1Waves * 64), lds1, st, q, a, L, ex_stride, ld, pooled,
                            p_stride, p_off, dpooled, dp_stride, dp_off, aux, dq, da, g_ex_stride, ldg, w);
         if ((rc = set_lds(esim_train_bwd2_kernel<128>, lds2))) return rc;
         hipLaunchKernelGGL(esim_train_bwd2_kernel<128>, dim3(batch), dim3(kBwd2Waves * 64), lds2, st, a, L, ex_stride, ld,
