@@ -70,6 +70,7 @@ struct GemmArgs {
     int64_t units;  // all problems' units
     int* cnt;       // one arrival counter per global tile (zero between launches)
     float* slots;   // 2 G partial tiles
+    int defer;      // cut tiles: partials only, gemm32_fixup_kernel combines them (many segments per tile)
 };
 
 __device__ __forceinline__ int64_t seg_lo(int64_t v, int64_t U, int G) { return v * U / G; }
@@ -345,6 +346,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
                     for (int r = 0; r < 4; ++r)
                         __hip_atomic_store(slot + ((wave * 64 + (i * 4 + j) * 4 + r) * 64 + lane), acc[i][j][r],
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (g.defer) continue;  // gemm32_fixup_kernel adds the segments (same order) after this launch
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             const int v_first = seg_owner(t_unit0, U, G);
@@ -414,6 +416,68 @@ __global__ __launch_bounds__(kThreads, 1) void gemm32_kernel(GemmArgs g) {
                 }
         }
     }
+}
+
+// The cut tiles' combine as a launch of its own (GemmArgs::defer: a few tiles over a long K, e.g. a weight gradient
+// [4 x 512] or [256 x 16] over K = 4096, cut into 32 segments each). The in-kernel last arriver reads its tile's
+// segments one after the other (32 dependent 64 KB rounds: 59-66 us for those shapes); here kFixParts workgroups
+// per tile each take 1024 of its elements and issue every segment's loads together. The sum runs in the same order
+// (segment v_first, + v_first + 1, ...) and the epilogue is the same, so the result is bit-identical to the
+// in-kernel hand-off.
+constexpr int kFixParts = 32, kFixPer = kSlot / kFixParts / kThreads;  // 2 elements per thread
+constexpr int kFixBatch = 8;                                             // segments whose loads are issued together
+__global__ __launch_bounds__(kThreads) void gemm32_fixup_kernel(GemmArgs g, int G) {
+    const int b = blockIdx.x, part = b % kFixParts;
+    const int gt = b / kFixParts;
+    int q = 0;
+    while (q + 1 < g.np && gt >= g.p[q + 1].tile0) ++q;
+    const Prob& P = g.p[q];
+    const int tile = gt - P.tile0;
+    const int64_t U = g.units, t_unit0 = P.unit0 + (int64_t)tile * P.nk;
+    const int v_first = seg_owner(t_unit0, U, G), v_last = seg_owner(t_unit0 + P.nk - 1, U, G);
+    if (v_first == v_last) return;  // a whole tile: the GEMM launch stored it
+#if RF_G32_MFAST
+    const int tiles_m = (P.M + kBM - 1) / kBM;
+    const int m0 = (tile % tiles_m) * kBM, n0 = (tile / tiles_m) * kBN;
+#else
+    const int m0 = (tile / P.tiles_n) * kBM, n0 = (tile % P.tiles_n) * kBN;
+#endif
+    float acc[kFixPer];
+    int row[kFixPer], col[kFixPer];
+    int e0 = part * (kSlot / kFixParts) + threadIdx.x;
+#pragma unroll
+    for (int s = 0; s < kFixPer; ++s) {
+        const int e = e0 + s * kThreads;  // = ((wave * 64 + (i * 4 + j) * 4 + r) * 64 + lane), as the slot stores
+        const int wave = e >> 12, ijr = (e >> 6) & 63, lane = e & 63;
+        const int i = ijr >> 4, j = (ijr >> 2) & 3, r = ijr & 3;
+        row[s] = m0 + (wave >> 1) * 64 + (lane >> 4) * 4 + 16 * i + r;
+        col[s] = n0 + (wave & 1) * 64 + (lane & 15) + 16 * j;
+    }
+    for (int w0 = v_first; w0 <= v_last; w0 += kFixBatch) {
+        float t[kFixBatch][kFixPer];
+#pragma unroll
+        for (int b = 0; b < kFixBatch; ++b) {
+            const int w = min(w0 + b, v_last);  // past the last segment: a valid slot, not added
+            const int sid = gt == gtile_of(g, seg_lo(w, U, G)) ? 2 * w : 2 * w + 1;
+            const float* p = g.slots + (size_t)sid * kSlot;
+#pragma unroll
+            for (int s = 0; s < kFixPer; ++s) t[b][s] = p[e0 + s * kThreads];
+        }
+#pragma unroll
+        for (int b = 0; b < kFixBatch; ++b)
+            if (w0 + b <= v_last) {
+#pragma unroll
+                for (int s = 0; s < kFixPer; ++s) acc[s] = w0 + b == v_first ? t[b][s] : acc[s] + t[b][s];
+            }
+    }
+    rf_act::with_act(P.act, [&](auto F) {
+#pragma unroll
+        for (int s = 0; s < kFixPer; ++s) {
+            if (row[s] >= P.M || col[s] >= P.N) continue;
+            const float bv = P.bias ? P.bias[col[s]] : 0.f;
+            P.C[(int64_t)row[s] * P.ldc + col[s]] = F(acc[s] + bv);
+        }
+    });
 }
 
 int cu_count() {
@@ -509,7 +573,12 @@ extern "C" int rf_gemm_f32_grouped(const rf_gemm_f32_problem* probs, int32_t n, 
         if (e != hipSuccess) return rf_set_error(RF_EHIP, "gemm32_kernel: %s", hipGetErrorString(e));
         attr_set[which] = true;
     }
+    // many segments per cut tile (a WG's range under a quarter of some problem's k steps): defer the combine
+    g.defer = 0;
+    for (int i = 0; i < g.np; ++i)
+        if ((int64_t)g.p[i].nk * G > 4 * g.units) g.defer = 1;
     hipLaunchKernelGGL(kerns[which], dim3(G), dim3(kThreads), kLdsBytes, st, g);
+    if (g.defer) hipLaunchKernelGGL(gemm32_fixup_kernel, dim3((unsigned)(tiles * kFixParts)), dim3(kThreads), 0, st, g, G);
     return rf_check_launch("gemm32_kernel");
 }
 

@@ -89,6 +89,27 @@ def test_short_k_many_tiles(cuda, M, N, K, ta, tb):
     assert torch.equal(c, G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act="selu"))
 
 
+# few tiles over a long K (the ESIM training step's small weight gradients and head): every tile is cut into many
+# segments, which gemm32_fixup_kernel combines in a launch of its own (GemmArgs::defer), ragged edges and bias / act
+FEW_TILES_LONG_K = [(4, 512, 4096, True, False, "none"), (256, 16, 4096, True, False, "none"),
+                    (512, 256, 4096, True, False, "none"), (130, 200, 8192, False, True, "selu"),
+                    (4, 4, 2048, False, False, "relu"), (1, 129, 4100, True, True, "none")]
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb,act", FEW_TILES_LONG_K)
+def test_few_tiles_long_k_deferred_combine(cuda, M, N, K, ta, tb, act):
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    pad = lambda n: (n + 3) // 4 * 4
+    a_full = torch.randn((K, pad(M)) if ta else (M, pad(K)), device="cuda", generator=g)
+    b_full = torch.randn((N, pad(K)) if tb else (K, pad(N)), device="cuda", generator=g)
+    a = a_full[:, :M] if ta else a_full[:, :K]
+    b = b_full[:, :K] if tb else b_full[:, :N]
+    bias = torch.randn(N, device="cuda", generator=g) if act != "none" else None
+    c = G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act=act)
+    _check(c, a, b, ta, tb, bias, act)
+    assert torch.equal(c, G.gemm_f32(a, b, trans_a=ta, trans_b=tb, bias=bias, act=act))
+
+
 def test_workspace_shared_across_shapes(cuda):
     """One zeroed workspace per stream serves every shape: a small call after a large one, a large one after a small
     one (the per-tile counters sit at the start, the partial tiles at the far end), the results unchanged."""
