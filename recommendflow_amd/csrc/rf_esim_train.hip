@@ -59,13 +59,12 @@ __device__ __forceinline__ void stage_qa(const float* __restrict__ q, const floa
 
 __device__ __forceinline__ f4v lds4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
 
-// One strip's forward: S^T [NJ] (C layout: j = 16 jt + 4 g + r, i = ibase + li) and att_q^T, att_a^T [D/16]
-// (c = 16 ct + 4 g + r, i = ibase + li).
+// One strip's scores: S^T [NJ] (C layout: j = 16 jt + 4 g + r, i = ibase + li); the attention output is taken per
+// 16-column tile from them (att_tile, or the forward's transposed tile).
 // NJ (= Lp / 16 <= kMaxJ) is a runtime value: the j-tile loops are unrolled to kMaxJ with uniform guards, so each
 // kernel holds one copy of its code (a copy per tile count put 140K lines of ISA in the forward and thrashed the
 // instruction cache)
 constexpr int kMaxJ = 8;
-// the scores half of strip_fwd: S^T [NJ] of strip ibase (X = E^T strip, softmax down j)
 template <int D>
 __device__ __forceinline__ void strip_scores(const float* qs, const float* as, int L, int NJ, int ibase, int li, int g,
                                              f4v (&S)[kMaxJ]) {
@@ -139,40 +138,12 @@ __device__ __forceinline__ void att_tile(const float* qs, const float* as, int N
         }
 }
 
-template <int D>
-__device__ __forceinline__ void strip_fwd(const float* qs, const float* as, int L, int NJ, int ibase, int li, int g,
-                                          f4v (&S)[kMaxJ], f4v (&attq)[D / 16], f4v (&atta)[D / 16]) {
-    strip_scores<D>(qs, as, L, NJ, ibase, li, g, S);
-#pragma unroll
-    for (int ct = 0; ct < D / 16; ++ct) att_tile<D>(qs, as, NJ, ct, li, g, S, attq[ct], atta[ct]);
-}
-
 // (max, count) fold of the candidates equal to the maximum (exact comparisons: any combine order gives the same pair);
 // selects, no branches
 __device__ __forceinline__ void mc_merge(float& m, float& c, float m2, float c2) {
     const bool gt = m2 > m, eq = m2 == m;
     c = gt ? c2 : (eq ? c + c2 : c);
     m = gt ? m2 : m;
-}
-__device__ __forceinline__ void mc_add(float& m, float& c, float v) { mc_merge(m, c, v, 1.f); }
-
-// DPP moves inside a 16-lane row: quad_perm xor 1 (0xB1), xor 2 (0x4E), row_ror 4 (0x124), row_ror 8 (0x128); the four
-// steps combine disjoint groups, so every lane of the row ends with the whole row's reduction
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
-template <int CTRL>
-__device__ __forceinline__ void row_step(float& sum, float& m, float& c) {
-    sum += dpp<CTRL>(sum);
-    const float m2 = dpp<CTRL>(m), c2 = dpp<CTRL>(c);
-    mc_merge(m, c, m2, c2);
-}
-__device__ __forceinline__ void row16_reduce(float& sum, float& m, float& c) {
-    row_step<0xB1>(sum, m, c);
-    row_step<0x4E>(sum, m, c);
-    row_step<0x124>(sum, m, c);
-    row_step<0x128>(sum, m, c);
 }
 
 // per-wave partials of the pooled statistics in LDS: [wave][side][sum | max | count][D]. Eight waves (two per SIMD:
@@ -195,31 +166,58 @@ __global__ __launch_bounds__(kFwdWaves * 64) void esim_train_fwd_kernel(const fl
     for (int t = threadIdx.x; t < kFwdWaves * 6 * D; t += kFwdWaves * 64) part[t] = (t / D) % 3 == 1 ? -INFINITY : 0.f;
     __syncthreads();
     for (int s = wave; s < NS; s += kFwdWaves) {
-        const int ibase = 16 * s, i = ibase + li;
-        f4v S[kMaxJ], attq[D / 16], atta[D / 16];
-        strip_fwd<D>(qs, as, L, NS, ibase, li, g, S, attq, atta);
+        const int ibase = 16 * s;
+        f4v S[kMaxJ];
+        strip_scores<D>(qs, as, L, NS, ibase, li, g, S);
 #pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            const float* xs = side ? as : qs;
+        for (int ct = 0; ct < D / 16; ++ct) {
+            // att[i][c] (not att^T): S^T's C layout is the A operand of att = S x (k order j = 16 jt + 4 g + r), x the
+            // B operand, so this lane holds rows i = ibase + 4 g + r of column c = 16 ct + li: the pooling over i is
+            // four rows in the lane and two lane swaps, instead of a 16-lane reduction per (row, column) value
+            f4v aq = zero4(), aa = zero4();
 #pragma unroll
-            for (int ct = 0; ct < D / 16; ++ct) {
-                const f4v xv = lds4(xs + i * RS + 16 * ct + 4 * g);
+            for (int jt = 0; jt < kMaxJ; ++jt)
+                if (jt < NS) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int j = 16 * jt + 4 * g + r;
+                        aq = mf(S[jt][r], qs[j * RS + 16 * ct + li], aq);
+                        aa = mf(S[jt][r], as[j * RS + 16 * ct + li], aa);
+                    }
+                }
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const float* xs = side ? as : qs;
+                const f4v at = side ? aa : aq;
+                float sum = 0.f, cand[16];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float x = xv[r], at = side ? atta[ct][r] : attq[ct][r];
+                    const int i = ibase + 4 * g + r;
                     const bool ok = i < L;
-                    float sum = ok ? 2.f * x + x * at : 0.f, mx = -INFINITY, cnt = 0.f;
-                    mc_add(mx, cnt, ok ? x : -INFINITY);
-                    mc_add(mx, cnt, ok ? at : -INFINITY);
-                    mc_add(mx, cnt, ok ? x - at : -INFINITY);
-                    mc_add(mx, cnt, ok ? x * at : -INFINITY);
-                    if (!ok) cnt = 0.f;
-                    row16_reduce(sum, mx, cnt);
-                    if (li == 0) {
-                        float* p = part + ((wave * 2 + side) * 3) * D + 16 * ct + 4 * g + r;
-                        p[0] += sum;
-                        mc_merge(p[D], p[2 * D], mx, cnt);
-                    }
+                    const float x = xs[i * RS + 16 * ct + li];
+                    if (ok) sum += 2.f * x + x * at[r];
+                    cand[4 * r] = ok ? x : -INFINITY;
+                    cand[4 * r + 1] = ok ? at[r] : -INFINITY;
+                    cand[4 * r + 2] = ok ? x - at[r] : -INFINITY;
+                    cand[4 * r + 3] = ok ? x * at[r] : -INFINITY;
+                }
+                float mx = cand[0];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) mx = fmaxf(mx, cand[k]);
+                mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+                mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+                // the candidates equal to the strip's maximum (masked rows are -inf: never equal to a finite maximum)
+                float cnt = 0.f;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) cnt += (cand[k] == mx && cand[k] != -INFINITY) ? 1.f : 0.f;
+                cnt += __shfl_xor(cnt, 16, 64);
+                cnt += __shfl_xor(cnt, 32, 64);
+                sum += __shfl_xor(sum, 16, 64);
+                sum += __shfl_xor(sum, 32, 64);
+                if (g == 0) {
+                    float* p = part + ((wave * 2 + side) * 3) * D + 16 * ct + li;
+                    p[0] += sum;
+                    mc_merge(p[D], p[2 * D], mx, cnt);
                 }
             }
         }
