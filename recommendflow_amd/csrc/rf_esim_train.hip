@@ -45,15 +45,29 @@ struct Ex {
 };
 
 // stage rows [0, Lp) of one example's q and a into LDS (rows >= L zero)
+// kStageBatch chunks per thread are loaded before any is written to LDS: a load -> write loop waits out one HBM round
+// trip per chunk (14 of them per example at 112 x 128 with 512 threads)
+constexpr int kStageBatch = 8;
 template <int D, int NT = kThreads>
 __device__ __forceinline__ void stage_qa(const float* __restrict__ q, const float* __restrict__ a, int64_t ld, int L, int Lp,
                                          float* qs, float* as) {
     constexpr int RS = Ex<D>::RS, C4 = D / 4;
-    for (int t = threadIdx.x; t < 2 * Lp * C4; t += NT) {
-        const int side = t / (Lp * C4), rem = t - side * Lp * C4, r = rem / C4, c4 = rem - r * C4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < L) v = *reinterpret_cast<const float4*>((side ? a : q) + (int64_t)r * ld + 4 * c4);
-        *reinterpret_cast<float4*>((side ? as : qs) + r * RS + 4 * c4) = v;
+    const int n = 2 * Lp * C4;
+    for (int t0 = threadIdx.x; t0 < n; t0 += kStageBatch * NT) {
+        float4 v[kStageBatch];
+#pragma unroll
+        for (int b = 0; b < kStageBatch; ++b) {
+            const int t = t0 + b * NT;
+            const int side = t / (Lp * C4), rem = t - side * Lp * C4, r = rem / C4, c4 = rem - r * C4;
+            v[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t < n && r < L) v[b] = *reinterpret_cast<const float4*>((side ? a : q) + (int64_t)r * ld + 4 * c4);
+        }
+#pragma unroll
+        for (int b = 0; b < kStageBatch; ++b) {
+            const int t = t0 + b * NT;
+            const int side = t / (Lp * C4), rem = t - side * Lp * C4, r = rem / C4, c4 = rem - r * C4;
+            if (t < n) *reinterpret_cast<float4*>((side ? as : qs) + r * RS + 4 * c4) = v[b];
+        }
     }
 }
 
@@ -436,16 +450,33 @@ __global__ __launch_bounds__(kBwd2Waves * 64) void esim_train_bwd2_kernel(const 
     for (int half = 0; half < 2; ++half) {
         const int c0 = half * H;
         if (half) __syncthreads();  // the first half's reads are done
-        for (int t = threadIdx.x; t < 2 * H * (Lp / 4); t += NT) {
-            const int side = t / (H * (Lp / 4)), rem = t - side * H * (Lp / 4), c = rem / (Lp / 4), i4 = rem - c * (Lp / 4);
-            const f4v v = lds4((side ? wsGa : wsGq) + (int64_t)(c0 + c) * Lp + 4 * i4);
-            *reinterpret_cast<f4v*>((side ? ga : gq) + c * GS + 4 * i4) = v;
-        }
-        for (int t = threadIdx.x; t < Lp * (H / 4); t += NT) {
-            const int r = t / (H / 4), c4 = t - r * (H / 4);
-            f4v v = zero4();
-            if (r < L) v = lds4(ae + (int64_t)r * ld + c0 + 4 * c4);
-            *reinterpret_cast<f4v*>(as + r * HS + 4 * c4) = v;
+        // G_q^T, G_a^T and a of this half: every chunk of a batch loaded before any LDS write (see stage_qa)
+        const int ng = 2 * H * (Lp / 4), na = Lp * (H / 4);
+        for (int t0 = threadIdx.x; t0 < ng + na; t0 += kStageBatch * NT) {
+            f4v v[kStageBatch];
+#pragma unroll
+            for (int b = 0; b < kStageBatch; ++b) {
+                const int t = t0 + b * NT;
+                v[b] = zero4();
+                if (t < ng) {
+                    const int side = t / (H * (Lp / 4)), rem = t - side * H * (Lp / 4), c = rem / (Lp / 4), i4 = rem - c * (Lp / 4);
+                    v[b] = lds4((side ? wsGa : wsGq) + (int64_t)(c0 + c) * Lp + 4 * i4);
+                } else if (t < ng + na) {
+                    const int r = (t - ng) / (H / 4), c4 = (t - ng) - r * (H / 4);
+                    if (r < L) v[b] = lds4(ae + (int64_t)r * ld + c0 + 4 * c4);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < kStageBatch; ++b) {
+                const int t = t0 + b * NT;
+                if (t < ng) {
+                    const int side = t / (H * (Lp / 4)), rem = t - side * H * (Lp / 4), c = rem / (Lp / 4), i4 = rem - c * (Lp / 4);
+                    *reinterpret_cast<f4v*>((side ? ga : gq) + c * GS + 4 * i4) = v[b];
+                } else if (t < ng + na) {
+                    const int r = (t - ng) / (H / 4), c4 = (t - ng) - r * (H / 4);
+                    *reinterpret_cast<f4v*>(as + r * HS + 4 * c4) = v[b];
+                }
+            }
         }
         __syncthreads();
         for (int jt = wave; jt < NS; jt += kBwd2Waves) {
