@@ -502,6 +502,17 @@ __global__ __launch_bounds__(kBwd2Waves * 64) void esim_train_bwd2_kernel(const 
                     }
                 }
             }
+            // stage 1's values of this lane's 2 x H / 16 x 4 outputs loaded together, then the adds and stores
+            float oq[H / 16][4], oa[H / 16][4];
+#pragma unroll
+            for (int ct = 0; ct < H / 16; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = 16 * jt + 4 * g + r;
+                    const int64_t o = e * g_ex + (int64_t)min(j, L - 1) * ldg + c0 + 16 * ct + li;
+                    oq[ct][r] = dq[o];
+                    oa[ct][r] = da[o];
+                }
 #pragma unroll
             for (int ct = 0; ct < H / 16; ++ct)
 #pragma unroll
@@ -509,8 +520,8 @@ __global__ __launch_bounds__(kBwd2Waves * 64) void esim_train_bwd2_kernel(const 
                     const int j = 16 * jt + 4 * g + r;
                     if (j < L) {
                         const int64_t o = e * g_ex + (int64_t)j * ldg + c0 + 16 * ct + li;
-                        dq[o] += accq[ct][r];
-                        da[o] += acca[ct][r];
+                        dq[o] = oq[ct][r] + accq[ct][r];
+                        da[o] = oa[ct][r] + acca[ct][r];
                     }
                 }
         }
