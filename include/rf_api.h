@@ -482,6 +482,8 @@ size_t rf_route_ws_bytes(int64_t n, int32_t nranks, int64_t table_rows);
  * (n_uniq = the sum of counts, from the host) sorts the distinct keys (radix over the key bits of the distinct
  * set only) and writes local_out[0 .. n_uniq) in (owner, local) order and the remaining row_map entries, exactly
  * as rf_route_rows would for the routed rows. Same ws for both calls: rf_route_hash_ws_bytes(n, P, table_rows).
+ * n_uniq = -1 (P <= 64): the distinct total is read from the workspace on the device, so the finish can be enqueued
+ * before the host has read the counts (local_out then needs n entries; its first sum(counts) are the rows).
  */
 size_t rf_route_hash_ws_bytes(int64_t n, int32_t nranks, int64_t table_rows);
 int rf_route_hash_build(const int64_t* rows, int64_t n, int32_t nranks, int32_t rank, int64_t table_rows,

@@ -149,12 +149,14 @@ class GpuShardOps:
         return counts, (n, nranks, table_rows, row_map, ws, ws_bytes), n
 
     def route_hash_finish(self, state, n_uniq: int):
-        """rf_route_hash_finish -> (local int64 [n_uniq], row_map int32 [n])."""
+        """rf_route_hash_finish -> (local int64 [n_uniq], row_map int32 [n]). n_uniq = -1 (nranks <= 64): the
+        distinct total is read on the device, so this can be enqueued before the host reads the counts; local then
+        has n entries, of which the first sum(counts) are the distinct rows."""
         n, nranks, table_rows, row_map, ws, ws_bytes = state
-        local = torch.empty(max(n_uniq, 1), dtype=torch.int64, device=self.device)
+        local = torch.empty(max(n if n_uniq < 0 else n_uniq, 1), dtype=torch.int64, device=self.device)
         L.call("rf_route_hash_finish", n, nranks, table_rows, n_uniq, L.ptr(local), L.ptr(row_map), L.ptr(ws), ws_bytes,
                L.stream_ptr(None))
-        return local[:n_uniq], row_map[:n]
+        return (local if n_uniq < 0 else local[:n_uniq]), row_map[:n]
 
     # -- owner-side partial pooling (rf_partial.hip) ---------------------------------------------------
     def pp_plan(self, desc, n_slots: int, batch: SparseBatch, rows: torch.Tensor, flags: int, nranks: int):
@@ -460,13 +462,31 @@ class ShardedFusedEncoder(torch.nn.Module):
             n_req = req.numel()
         counts = counts.to(torch.int64)
         P = counts.numel()
-        if exchange:
-            recv = self.comm.exchange_counts(counts)
-            both = [int(c) for c in torch.cat([counts, recv.to(counts.device)]).cpu().tolist()]
-            send, recv_l = both[:P], both[P:]
+        recv = self.comm.exchange_counts(counts) if exchange else None
+        if isinstance(self.ops, GpuShardOps) and P <= 64:
+            # the counts go to pinned host memory first, then the finish (row map + send ids) is enqueued with the
+            # distinct total read on the device, and the host waits only for the copies: the finish kernel runs
+            # while the host turns the counts into split sizes
+            pin = getattr(self, "_counts_pin", None)
+            if pin is None or pin.numel() != 2 * P:
+                pin = self._counts_pin = torch.empty(2 * P, dtype=torch.int64, pin_memory=True)
+            pin[:P].copy_(counts, non_blocking=True)
+            if recv is not None:
+                pin[P:].copy_(recv.to(counts.device), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            local, row_map = self.ops.route_hash_finish(state, -1)
+            ev.synchronize()
+            both = [int(c) for c in pin.tolist()]
+            send, recv_l = both[:P], (both[P:] if recv is not None else None)
+            local = local[: sum(send)]
         else:
-            send, recv_l = [int(c) for c in counts.cpu().tolist()], None
-        local, row_map = self.ops.route_hash_finish(state, sum(send))
+            if recv is not None:
+                both = [int(c) for c in torch.cat([counts, recv.to(counts.device)]).cpu().tolist()]
+                send, recv_l = both[:P], both[P:]
+            else:
+                send, recv_l = [int(c) for c in counts.cpu().tolist()], None
+            local, row_map = self.ops.route_hash_finish(state, sum(send))
         return RouteState(send, local, row_map, int(local.numel()), n_req), recv_l
 
     def route_exchange(self, batch: SparseBatch, local_fast: bool = False):

@@ -566,7 +566,8 @@ __global__ __launch_bounds__(256) void rh_scatter_owner_kernel(uint32_t* table, 
 __global__ __launch_bounds__(256) void rh_finish_kernel(const uint32_t* __restrict__ keys, int64_t u, int P, int64_t lp,
                                                         int64_t* __restrict__ local_out, const uint32_t* __restrict__ slot,
                                                         int64_t n, const uint32_t* __restrict__ uid_of_slot,
-                                                        int32_t* __restrict__ row_map) {
+                                                        int32_t* __restrict__ row_map, const int32_t* __restrict__ u_dev) {
+    if (u_dev) u = *u_dev;  // the build's distinct total, read on the device (no host round trip before this launch)
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < u; i += stride) {
         const uint32_t k = keys[i];
@@ -747,7 +748,10 @@ extern "C" int rf_route_hash_build_tokens(const rf_slot_desc* d_slots, int32_t n
 extern "C" int rf_route_hash_finish(int64_t n, int32_t nranks, int64_t table_rows, int64_t n_uniq, int64_t* local_out,
                                     int32_t* row_map, void* ws, size_t ws_bytes, void* stream) {
     RF_REQUIRE(nranks >= 1 && nranks <= 4096 && table_rows >= 1, "rf_route_hash_finish: bad nranks / table_rows");
-    RF_REQUIRE(n >= 0 && n_uniq >= 0 && n_uniq <= n, "rf_route_hash_finish: need 0 <= n_uniq <= n");
+    RF_REQUIRE(n >= 0 && n_uniq >= -1 && n_uniq <= n, "rf_route_hash_finish: need -1 <= n_uniq <= n");
+    // n_uniq = -1 (P <= 64 only): the distinct total is read from the workspace on the device, so the launch can be
+    // enqueued before the host has read the counts; local_out must then hold n entries (the distinct total's bound)
+    RF_REQUIRE(n_uniq >= 0 || nranks <= kOwnerMajorMaxP, "rf_route_hash_finish: n_uniq = -1 needs nranks <= %d", kOwnerMajorMaxP);
     const HashLayout lay = hash_layout(n, nranks, table_rows);
     RF_REQUIRE(ws && ws_bytes >= lay.total, "rf_route_hash_finish: workspace too small");
     if (n == 0 || n_uniq == 0) return RF_OK;
@@ -761,8 +765,10 @@ extern "C" int rf_route_hash_finish(int64_t n, int32_t nranks, int64_t table_row
     auto* table = reinterpret_cast<uint32_t*>(w + lay.off_table);
     const int64_t lp = (table_rows + nranks - 1) / nranks;
     if (nranks <= kOwnerMajorMaxP) {  // keys already owner-major (rh_scatter_owner_kernel), table = slot -> uid
-        hipLaunchKernelGGL(rh_finish_kernel, dim3(grid_of((n + kIlp - 1) / kIlp)), dim3(256), 0, st, kin, n_uniq, nranks,
-                           lp, local_out, reinterpret_cast<const uint32_t*>(w + lay.off_slot), n, table, row_map);
+        const int32_t* u_dev = n_uniq < 0 ? reinterpret_cast<const int32_t*>(w + lay.off_cnt) + nranks : nullptr;
+        hipLaunchKernelGGL(rh_finish_kernel, dim3(grid_of((n + kIlp - 1) / kIlp)), dim3(256), 0, st, kin, n_uniq < 0 ? n : n_uniq,
+                           nranks, lp, local_out, reinterpret_cast<const uint32_t*>(w + lay.off_slot), n, table, row_map,
+                           u_dev);
         return rf_check_launch("rf_route_hash_finish");
     }
     size_t sb = lay.sort_bytes;
