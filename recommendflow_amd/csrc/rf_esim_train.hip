@@ -8,7 +8,7 @@
 // TF's reduce_max gradient splits the gradient evenly over the elements equal to the maximum (_MinOrMaxGrad), so the
 // forward also writes, per (example, side, column), how many of the 4L candidates equal the maximum (aux).
 //
-// Layout of the work: one 256-thread workgroup per example; q and a staged in LDS (fp32, rows padded to 16, row
+// Layout of the work: one eight-wave workgroup per example; q and a staged in LDS (fp32, rows padded to 16, row
 // stride D + 4 floats); a wave owns a 16-column strip of i (rows of a) at a time and every product is a
 // v_mfma_f32_16x16x4_f32 (exact fp32 products and accumulation, no xf32 on gfx950):
 //   X = E^T strip [j][i] = q a^T       (A = q rows, B = a rows of the strip: both k-contiguous, float4 LDS reads)
@@ -33,8 +33,6 @@
 namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
-constexpr int kWaves = 4;
-constexpr int kThreads = kWaves * 64;
 
 __device__ __forceinline__ f4v mf(float a, float b, f4v c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 __device__ __forceinline__ f4v zero4() { return f4v{0.f, 0.f, 0.f, 0.f}; }
@@ -48,7 +46,7 @@ struct Ex {
 // kStageBatch chunks per thread are loaded before any is written to LDS: a load -> write loop waits out one HBM round
 // trip per chunk (14 of them per example at 112 x 128 with 512 threads)
 constexpr int kStageBatch = 8;
-template <int D, int NT = kThreads>
+template <int D, int NT>
 __device__ __forceinline__ void stage_qa(const float* __restrict__ q, const float* __restrict__ a, int64_t ld, int L, int Lp,
                                          float* qs, float* as) {
     constexpr int RS = Ex<D>::RS, C4 = D / 4;
