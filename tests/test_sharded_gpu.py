@@ -149,6 +149,11 @@ def test_route_hash_tokens_matches_oracle(O, cuda, P, rank, B):
                            sh.pad_rows.cpu().numpy()]).astype(np.int64)
     c, state, n = ops.route_hash_build_tokens(enc.desc, len(sp), hb.to("cuda"), sh.pad_rows, P, rank, R)
     assert n == rows.size
+    if P <= 64:  # the device-count finish (n_uniq = -1, enqueued before the host read) writes the same ids and map
+        l_dev, m_dev = ops.route_hash_finish(state, -1)
+        l_dev, m_dev = l_dev.clone(), m_dev.clone()
+        l_host, m_host = ops.route_hash_finish(state, int(c.sum()))
+        assert torch.equal(l_dev[: l_host.numel()], l_host) and torch.equal(m_dev, m_host)
     _check_route_hash(O, ops, rows, P, rank, R, c, state)
 
 
