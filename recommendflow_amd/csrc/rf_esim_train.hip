@@ -406,17 +406,25 @@ __global__ __launch_bounds__(kBwd1Waves * 64) void esim_train_bwd1_kernel(const 
         // strip-local: da_i += sum_j dE^T[j][i] q_j  (da^T[c][i], A[c][j] = q[j][c])
         f4v* drow = reinterpret_cast<f4v*>(da + e * g_ex + (int64_t)(i < L ? i : 0) * ldg + 4 * g);
 #pragma unroll
-        for (int ct = 0; ct < D / 16; ++ct) {
-            // the tile's direct terms, loaded before its 28 MFMAs (the load latency hides under the chain)
+        for (int ct = 0; ct < D / 16; ct += 2) {
+            // two tiles at a time (two independent accumulator chains); their direct terms loaded before the MFMAs
             const f4v p0 = i < L ? drow[4 * ct] : zero4();
-            f4v acc = zero4();
+            const f4v p1 = i < L ? drow[4 * ct + 4] : zero4();
+            f4v acc0 = zero4(), acc1 = zero4();
 #pragma unroll
             for (int jt = 0; jt < kMaxJ; ++jt)
                 if (jt < NS) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc = mf(qs[(16 * jt + 4 * g + r) * RS + 16 * ct + li], dS[jt][r], acc);
+                    for (int r = 0; r < 4; ++r) {
+                        const float* qr = qs + (16 * jt + 4 * g + r) * RS + li;
+                        acc0 = mf(qr[16 * ct], dS[jt][r], acc0);
+                        acc1 = mf(qr[16 * ct + 16], dS[jt][r], acc1);
+                    }
                 }
-            if (i < L) drow[4 * ct] = p0 + acc;
+            if (i < L) {
+                drow[4 * ct] = p0 + acc0;
+                drow[4 * ct + 4] = p1 + acc1;
+            }
         }
     }
 }
