@@ -182,25 +182,34 @@ __global__ __launch_bounds__(kFwdWaves * 64) void esim_train_fwd_kernel(const fl
         f4v S[kMaxJ];
         strip_scores<D>(qs, as, L, NS, ibase, li, g, S);
 #pragma unroll
-        for (int ct = 0; ct < D / 16; ++ct) {
+        for (int ct2 = 0; ct2 < D / 16; ct2 += 2) {
             // att[i][c] (not att^T): S^T's C layout is the A operand of att = S x (k order j = 16 jt + 4 g + r), x the
             // B operand, so this lane holds rows i = ibase + 4 g + r of column c = 16 ct + li: the pooling over i is
-            // four rows in the lane and two lane swaps, instead of a 16-lane reduction per (row, column) value
-            f4v aq = zero4(), aa = zero4();
+            // four rows in the lane and two lane swaps, instead of a 16-lane reduction per (row, column) value.
+            // Two column tiles at a time: four independent accumulator chains
+            f4v at4[2][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) at4[h][0] = at4[h][1] = zero4();
 #pragma unroll
             for (int jt = 0; jt < kMaxJ; ++jt)
                 if (jt < NS) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int j = 16 * jt + 4 * g + r;
-                        aq = mf(S[jt][r], qs[j * RS + 16 * ct + li], aq);
-                        aa = mf(S[jt][r], as[j * RS + 16 * ct + li], aa);
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            at4[h][0] = mf(S[jt][r], qs[j * RS + 16 * (ct2 + h) + li], at4[h][0]);
+                            at4[h][1] = mf(S[jt][r], as[j * RS + 16 * (ct2 + h) + li], at4[h][1]);
+                        }
                     }
                 }
 #pragma unroll
+            for (int h = 0; h < 2; ++h) {
+            const int ct = ct2 + h;
+#pragma unroll
             for (int side = 0; side < 2; ++side) {
                 const float* xs = side ? as : qs;
-                const f4v at = side ? aa : aq;
+                const f4v at = at4[h][side];
                 float sum = 0.f, cand[16];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -231,6 +240,7 @@ __global__ __launch_bounds__(kFwdWaves * 64) void esim_train_fwd_kernel(const fl
                     p[0] += sum;
                     mc_merge(p[D], p[2 * D], mx, cnt);
                 }
+            }
             }
         }
     }
